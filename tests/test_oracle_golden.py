@@ -1,0 +1,161 @@
+"""Pin the CPU oracle to golden vectors captured from the reference itself.
+
+Tolerances: the reference runs in fp32 (pocketfft), the oracle in float64 with
+explicit DFT sums, so agreement is at fp32 rounding: forward rel-L2 <= 1e-5,
+gradients rel-L2 <= 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import load_golden, rel_l2
+from recipe import make_array, make_state
+
+FWD_TOL = 1e-5
+GRAD_TOL = 1e-4
+
+
+def _params(g, prefix="p."):
+    return {k[len(prefix):]: torch.from_numpy(v) for k, v in g.items() if k.startswith(prefix)}
+
+
+def _check(g, out, params, inputs, skip_missing=()):
+    assert rel_l2(out.detach().numpy(), g["out"]) <= FWD_TOL
+    cot = torch.from_numpy(g["cot"]).double()
+    (out * cot).sum().backward()
+    n = 0
+    for k, v in g.items():
+        if k.startswith("g."):
+            name = k[2:]
+            p = params[name]
+            assert p.grad is not None, name
+            assert rel_l2(p.grad.numpy(), v) <= GRAD_TOL, (name, rel_l2(p.grad.numpy(), v))
+            n += 1
+        elif k.startswith("gin."):
+            name = k[4:]
+            assert rel_l2(inputs[name].grad.numpy(), v) <= GRAD_TOL, name
+            n += 1
+    assert n > 0
+
+
+def _leaf(g, prefix="p."):
+    out = {}
+    for k, v in _params(g, prefix).items():
+        t = v.to(torch.complex128 if v.is_complex() else torch.float64)
+        if t.is_floating_point() or t.is_complex():
+            t.requires_grad_(True)
+        out[k] = t
+    return out
+
+
+@pytest.mark.parametrize("case", ["sc2d_a", "sc2d_overlap", "sc2d_nyq"])
+def test_spectral_conv2d(case):
+    g = load_golden(case)
+    p = _leaf(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    y = oracle.spectral_conv2d(x, p["weights1"], p["weights2"])
+    _check(g, y, p, {"x": x})
+
+
+@pytest.mark.parametrize("case", ["sc1d", "sc1d_nyq"])
+def test_spectral_conv1d(case):
+    g = load_golden(case)
+    p = _leaf(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    y = oracle.spectral_conv1d(x, p["weights1"])
+    _check(g, y, p, {"x": x})
+
+
+@pytest.mark.parametrize("case", ["fno2d", "fno2d_input61", "fno2d_head61"])
+def test_fno2d(case):
+    g = load_golden(case)
+    p = _leaf(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    _check(g, oracle.fno2d(p, x), p, {"x": x})
+
+
+@pytest.mark.parametrize("case", ["fno1d", "fno1d_input64"])
+def test_fno1d(case):
+    g = load_golden(case)
+    p = _leaf(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    _check(g, oracle.fno1d(p, x), p, {"x": x})
+
+
+@pytest.mark.parametrize("case,heads", [("nio2d_fno_train", ("fno_drift", "fno_diffusion")),
+                                        ("nio2d_fno_eval", ("fno_drift", "fno_diffusion")),
+                                        ("nc_nio2d_fno_eval", ("fno_Fx", "fno_Fy"))])
+def test_niofp2d_fno(case, heads):
+    g = load_golden(case)
+    p = _leaf(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    grid = torch.from_numpy(g["in.grid"]).double().requires_grad_(True)
+    idx = g["idx"].tolist() if "idx" in g else None
+    if idx is not None:
+        assert len(idx) == int(g["L"])
+    y = oracle.niofp2d_fno(p, x, grid, idx=idx, heads=heads)
+    _check(g, y, p, {"x": x, "grid": grid})
+
+
+@pytest.mark.parametrize("case,heads", [("nio1d_fno_train", ("fno_drift", "fno_diffusion")),
+                                        ("nio1d_fno_eval", ("fno_drift", "fno_diffusion")),
+                                        ("gpe_nio_fno_train", ("fno_V",))])
+def test_niofp_fno_1d(case, heads):
+    g = load_golden(case)
+    p = _leaf(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    grid = torch.from_numpy(g["in.grid"]).double().requires_grad_(True)
+    idx = g["idx"].tolist() if "idx" in g else None
+    y = oracle.niofp_fno(p, x, grid, idx=idx, heads=heads)
+    _check(g, y, p, {"x": x, "grid": grid})
+
+
+def test_niofp2d_nio_branch_trunk():
+    """NIOFP2D (config D's model) at the reference grid 80^2; parameters from the
+    shared numpy recipe (the 11M-parameter encoder cannot be a fixture)."""
+    import json
+    g = load_golden("nio2d_nc_train")
+    shapes = [(k, tuple(s)) for k, s in json.loads(str(g["layout_json"]))]
+    st = make_state(shapes, seed=int(g["recipe_seed"]))
+    p = {k: torch.from_numpy(v).double().requires_grad_(v.dtype.kind == "f") for k, v in st.items()}
+    x = torch.from_numpy(g["in.x"]).double()
+    assert np.array_equal(g["in.x"], make_array((1, 51, 80, 80), 401, "nio2d_nc.x"))
+    grid = torch.from_numpy(g["in.grid"]).double()
+    y = oracle.niofp2d(p, x, grid, idx=g["idx"].tolist(), heads=("fno_Fx", "fno_Fy"))
+    assert rel_l2(y.detach().numpy(), g["out"]) <= 1e-4   # BN over 50 images in fp32
+    (y * torch.from_numpy(g["cot"]).double()).sum().backward()
+    gmax = max(float(v) for k, v in g.items() if k.startswith("gnorm."))
+    for k, v in g.items():
+        if k.startswith("g."):
+            assert rel_l2(p[k[2:]].grad.numpy(), v) <= 1e-3, k
+        if k.startswith("gnorm."):
+            # conv biases ahead of train-mode BatchNorm have exactly zero gradient; the fp32
+            # reference leaves ~1e-8 noise there, hence the absolute term
+            got = float(p[k[6:]].grad.norm())
+            assert abs(got - float(v)) <= 1e-3 * abs(float(v)) + 1e-5 * gmax, k
+
+
+def test_adam_two_steps():
+    g = load_golden("adam_fno2d")
+    names = [k[3:] for k in g if k.startswith("p0.")]
+    for name in names:
+        p = torch.from_numpy(g["p0." + name]).double()
+        m = torch.zeros_like(p)
+        v = torch.zeros_like(p)
+        for step in (1, 2):
+            p, m, v = oracle.adam_step(p, torch.from_numpy(g[f"g{step}." + name]), m, v, step, lr=0.0005)
+            assert rel_l2(p.numpy(), g[f"p{step}." + name]) <= 1e-6, (name, step)
+
+
+def test_metrics():
+    g = load_golden("metric_train_rel_l2")
+    e0, e1 = oracle.train_rel_l2_2ch(torch.from_numpy(g["pred"]), torch.from_numpy(g["out"]))
+    assert rel_l2(e0.numpy(), g["e_drift"]) <= 1e-6 and rel_l2(e1.numpy(), g["e_diffusion"]) <= 1e-6
+    g = load_golden("metric_rel_l2")
+    assert abs(oracle.rel_l2(g["a"], g["b"]) - float(g["val"])) <= 1e-6 * float(g["val"])
+    g = load_golden("metric_time_avg_rel_l2_2d")
+    assert abs(oracle.time_averaged_relative_l2(g["pt_pred"], g["pt_ref"]) - float(g["val"])) <= 1e-12
+    g = load_golden("metric_time_avg_L2_1d")
+    v = oracle.time_averaged_L2_error(g["t"], g["rho_ref"], g["t"], g["rho_pred"], g["x"])
+    assert abs(v - float(g["val"])) <= 1e-12
