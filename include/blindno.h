@@ -1,0 +1,182 @@
+/*
+ * blindno.h -- C ABI of the MI355X-native BlinDNO FNO/NIO hot path (libblindno.so).
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t (passed as
+ * void* so the header needs no HIP include), enqueues work on that stream and
+ * returns a hipError_t value (0 = hipSuccess).  No entry point allocates device
+ * memory, synchronises, or calls exit/abort: callers own all buffers (the Python
+ * host layer uses PyTorch's caching allocator) and check the return code.
+ *
+ * All tensors are fp32, C-contiguous, on the current device.  Complex values are
+ * interleaved (re, im) float pairs.
+ *
+ * Layout vocabulary (see DESIGN.md "Data layout in HBM"):
+ *   field   x[n][c][h][w]    n < Bn snapshots/samples, c < C channels,
+ *                            h < P1 (rows, 1 for 1D), w < P2 (padded grid)
+ *   rowspec At[n][k][c][h]   row-DFT coefficients, k < m2 (column-major per mode)
+ *   colspec X[n][k][c][j]    2D spectrum at the K1 kept frequency rows j
+ *   rowcoef Z[n][c][h][k]    row coefficients feeding the inverse row transform
+ *   wpack   Wt[k][j][ci][co] complex mixing weights, one block per kept mode
+ * Kept rows: K1 = min(2*m1, P1); row j -> frequency r_j = j (j < m1 or K1 == P1)
+ * else P1 - 2*m1 + j.  Rows r >= P1 - m1 are owned by weights2 (weights2 wins on
+ * overlap, as the reference's second slice assignment does).
+ *
+ * Each declaration names the reference operation it replaces (file:line in
+ * yl602019618/Reconstruction-of-PDE-without-Time-Label).
+ */
+#ifndef BLINDNO_H
+#define BLINDNO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* blindno_stream_t; /* hipStream_t */
+
+/* ABI version: bump on any signature change. */
+int blindno_abi_version(void);
+/* Human-readable text of a returned error code (hipGetErrorString). */
+const char* blindno_error_string(int code);
+
+/* --- lift / projection ------------------------------------------------------------ */
+
+/* fc0 + permute + F.pad: 2d_FPE/FNOModules.py:219-224, 1d_FPE/FNOModules.py:103-106.
+ * in (Bn, N1, N2, Cin) channels-last -> x0 (Bn, C, P1, P2), zero outside h<N1, w<N2. */
+int blindno_lift_fwd(const float* in, const float* w0, const float* b0, float* x0,
+                     int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
+                     blindno_stream_t stream);
+
+/* Backward of the lift: optional d_in (may be NULL) and per-chunk partial sums of
+ * dW0 (C*Cin) then db0 (C) into partial[nchunk][C*Cin + C]. */
+int blindno_lift_bwd(const float* dx0, const float* in, const float* w0, float* d_in,
+                     float* partial, int nchunk,
+                     int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
+                     blindno_stream_t stream);
+
+/* crop + permute + fc1 + GELU + fc2: 2d_FPE/FNOModules.py:234-239, 1d_FPE/FNOModules.py:116-121.
+ * z (Bn, C, P1, P2) -> out[(n*Ho + h)*Wo + w)*ostride + ooff + co] for h<Ho, w<Wo. */
+int blindno_project_fwd(const float* z, const float* w1, const float* b1, const float* w2,
+                        const float* b2, float* out, int Bn, int C, int P1, int P2, int Ho,
+                        int Wo, int Hd, int Cout, int ostride, int ooff,
+                        blindno_stream_t stream);
+
+/* Backward of the projection: dz (Bn, C, P1, P2) (written only on the crop; caller
+ * zero-fills the rest), per-chunk partials of [dW1 (Hd*C), db1 (Hd), dW2 (Cout*Hd),
+ * db2 (Cout)].  dout is addressed like out in blindno_project_fwd, except that the
+ * sample index n is divided by dout_div (snapshot-bag broadcast; 1 = none). */
+int blindno_project_bwd(const float* z, const float* w1, const float* b1, const float* w2,
+                        const float* dout, float* dz, float* partial, int nchunk,
+                        int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout,
+                        int ostride, int ooff, int dout_div, blindno_stream_t stream);
+
+/* --- truncated spectral transforms --------------------------------------------------- */
+
+/* Row (last-axis) forward DFT of the first m2 modes: torch.fft.rfft2/rfft first stage
+ * (2d_FPE/FNOModules.py:163, 1d_FPE/FNOModules.py:50).  act: 0 = identity,
+ * 1 = GELU applied to x on load (x holds pre-activations).  x (Bn,C,P1,P2) -> At. */
+int blindno_rowdft(const float* x, float* At, const float* tw2, int Bn, int C, int P1,
+                   int P2, int m2, int act, blindno_stream_t stream);
+
+/* Column DFT at the kept rows (second stage of rfft2): At -> X (Bn, m2, C, K1).
+ * scale_mode 0: none; 1: multiply mode k by c_k/(P1*P2) (adjoint of irfft2). */
+int blindno_coldft(const float* At, float* X, const float* tw1, int Bn, int C, int P1,
+                   int m1, int m2, int P2, int scale_mode, blindno_stream_t stream);
+
+/* Per-mode complex channel mix (compl_mul2d, 2d_FPE/FNOModules.py:141-154,170-173).
+ * dir 0: Y[n,k,o,j] = sum_i X[n,k,i,j] Wt[k,j,i,o];
+ * dir 1: Y[n,k,i,j] = sum_o conj(Wt[k,j,i,o]) X[n,k,o,j]  (input-gradient). */
+int blindno_mix(const float* X, const float* Wt, float* Y, int Bn, int Ci, int Co,
+                int K1, int m2, int dir, blindno_stream_t stream);
+
+/* dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]  (weight gradient of the mix). */
+int blindno_mix_wgrad(const float* X, const float* G, float* dWt, int Bn, int Ci, int Co,
+                      int K1, int m2, blindno_stream_t stream);
+
+/* Column inverse at the kept rows: Z[n,c,h,k] = s_k * sum_j Y[n,k,c,j] e^{+2pi i r_j h/P1}.
+ * scale_mode 0: s_k = 1; 1: s_k = c_k/(P1*P2) (forward irfft2 normalisation). */
+int blindno_colidft(const float* Y, float* Z, const float* tw1, int Bn, int C, int P1,
+                    int m1, int m2, int P2, int scale_mode, blindno_stream_t stream);
+
+/* 1D mode mix (compl_mul1d + DC halving, 1d_FPE/FNOModules.py:43-58).
+ * dir 0 (forward):  X = At with X[.,0] *= 0.5 saved to Xs; Z[n,o,0,k] = c_k/P2 * sum_i X W.
+ * dir 1 (backward): G = c_k/P2 * At (= DFT of dz) saved to Xs; Z[n,i,0,k] = h_k sum_o conj(W) G
+ *                    with h_0 = 0.5, h_k = 1.   W packed as Wt[k][ci][co] complex. */
+int blindno_mix1d(const float* At, const float* Wt, float* Xs, float* Z, int Bn, int Ci,
+                  int Co, int m, int P2, int dir, blindno_stream_t stream);
+
+/* Inverse row transform + 1x1 conv + bias epilogue (irfft2 second stage, nn.Conv2d(k=1),
+ * x1 + x2; 2d_FPE/FNOModules.py:177,226-230):
+ *   z[n,o,h,w] = sum_k Re(Z[n,o,h,k] e^{+2pi i k w/P2}) + sum_i Wc[o,i] f(x[n,i,h,w]) + bc[o]
+ * f = identity (act 0) or GELU (act 1: x holds pre-activations).  wc == NULL drops the
+ * conv/bias term (bare SpectralConv2d/1d; x, bc unused). */
+int blindno_rowidft_epi(const float* Z, const float* x, const float* wc, const float* bc,
+                        float* z, const float* tw2, int Bn, int C, int P1, int P2, int m2,
+                        int act, blindno_stream_t stream);
+
+/* Backward of rowidft_epi w.r.t. its input field:
+ *   dx[n,i,h,w] = sum_k Re(G[n,i,h,k] e^{+2pi i k w/P2}) + sum_o Wc[o,i] dz[n,o,h,w]
+ * then, if act == 1, dx *= GELU'(xpre[n,i,h,w]) (xpre = stored pre-activation).
+ * wc == NULL drops the conv term (dz unused). */
+int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc, const float* xpre,
+                        float* dx, const float* tw2, int Bn, int C, int P1, int P2, int m2,
+                        int act, blindno_stream_t stream);
+
+/* 1x1-conv weight/bias gradient partials: partial[chunk][C*C + C] with
+ * dWc[o,i] = sum dz[n,o,.] f(x[n,i,.]),  dbc[o] = sum dz[n,o,.]. */
+int blindno_conv_wgrad(const float* dz, const float* x, float* partial, int nchunk, int Bn,
+                       int C, int P1, int P2, int act, blindno_stream_t stream);
+
+/* out[p] = sum_{c < nchunk} partial[c][p] (fixed order: deterministic). */
+int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np,
+                            blindno_stream_t stream);
+
+/* Pack reference-layout 2D weights (Ci,Co,m1,m2,2) x2 into Wt (m2,K1,Ci,Co) complex. */
+int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, int Ci, int Co, int m1,
+                     int m2, int P1, blindno_stream_t stream);
+/* Scatter dWt back to dW1/dW2 (Ci,Co,m1,m2,2); entries of weights1 shadowed by
+ * weights2 (overlapping rows) receive 0. */
+int blindno_unpack_w2d(const float* dWt, float* dw1, float* dw2, int Ci, int Co, int m1,
+                       int m2, int P1, blindno_stream_t stream);
+/* 1D: (Ci,Co,m) complex <-> Wt (m,Ci,Co) complex; dir 0 pack, 1 unpack. */
+int blindno_pack_w1d(const float* w, float* Wt, int Ci, int Co, int m, int dir,
+                     blindno_stream_t stream);
+
+/* --- snapshot-bag aggregation (2d_FPE/NIOModules.py:565-575; 1d_FPE/NIOModules.py:140-149) */
+
+/* y[b,s,c] = sum_{e<d} W[c,e] grid[s,e] + (W[c,d]/L) sum_l u[b,l,s] + bias[c]
+ * u (B, L, S), grid (S, d) channels-last, W (width, d+1), y (B, S, width). */
+int blindno_bagmean_fwd(const float* u, const float* grid, const float* w, const float* bias,
+                        float* y, int B, int L, int S, int d, int width,
+                        blindno_stream_t stream);
+/* s[b,s] = sum_c (W[c,d]/L) dy[b,s,c]   (the gradient of every u[b,l,s]). */
+int blindno_bagmean_bwd(const float* dy, const float* w, float* s, int B, int S, int d,
+                        int width, int L, blindno_stream_t stream);
+
+/* --- loss / metrics / optimiser -------------------------------------------------------- */
+
+/* nn.MSELoss (2d_FPE/train_fno.py:116,142): partial sums of (p-t)^2 per block into
+ * partial[nblk] and grad = gscale * 2 (p - t) / n (grad may be NULL). */
+int blindno_mse(const float* p, const float* t, float* partial, float* grad, int64_t n,
+                int nblk, const float* gscale, blindno_stream_t stream);
+
+/* Per-row sums of squares in fp64 for relative-L2 metrics (2d_FPE/train_fno.py:160-163,
+ * eval_fno.py:124-128, 2d_Non_conservative_FPE/compute_time_error.py:321-333).
+ * Row r holds n points of `stride` floats: out[2r] = sum (a[.+off_a] - b[.+off_b])^2,
+ * out[2r+1] = sum b[.+off_b]^2, or (den_all = 1) the sum over all `stride` channels of b
+ * (the train loop's denominator quirk). */
+int blindno_rowsq(const float* a, const float* b, double* out, int rows, int n, int stride,
+                  int off_a, int off_b, int den_all, blindno_stream_t stream);
+
+/* Fused Adam over a flat fp32 buffer (torch.optim.Adam, no weight decay / amsgrad):
+ * step_size = lr / (1 - beta1^t), bc2s = sqrt(1 - beta2^t). grad is scaled by gscale. */
+int blindno_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1,
+                 float beta2, float eps, float step_size, float bc2s, float gscale,
+                 blindno_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BLINDNO_H */

@@ -1,0 +1,99 @@
+"""ctypes binding of libblindno.so (the C ABI declared in include/blindno.h).
+
+The library is loaded AFTER torch so that its HIP runtime dependency
+(``libamdhip64.so.7``) resolves to the runtime torch already loaded: device
+pointers and streams are then shared with PyTorch.  There is no fallback: if the
+library or a GPU is missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BLINDNO_LIB", os.path.join(_HERE, "libblindno.so"))
+
+# argument codes: p pointer, i int32, l int64, f float, s stream
+SIGNATURES = {
+    "blindno_abi_version": "",
+    "blindno_lift_fwd": "ppppiiiiiiis",
+    "blindno_lift_bwd": "pppppiiiiiiiis",
+    "blindno_project_fwd": "ppppppiiiiiiiiiis",
+    "blindno_project_bwd": "pppppppiiiiiiiiiiiis",
+    "blindno_rowdft": "pppiiiiiis",
+    "blindno_coldft": "pppiiiiiiis",
+    "blindno_mix": "pppiiiiiis",
+    "blindno_mix_wgrad": "pppiiiiis",
+    "blindno_colidft": "pppiiiiiiis",
+    "blindno_mix1d": "ppppiiiiiis",
+    "blindno_rowidft_epi": "ppppppiiiiiis",
+    "blindno_rowidft_bwd": "ppppppiiiiiis",
+    "blindno_conv_wgrad": "pppiiiiiis",
+    "blindno_reduce_partials": "ppiis",
+    "blindno_pack_w2d": "pppiiiiis",
+    "blindno_unpack_w2d": "pppiiiiis",
+    "blindno_pack_w1d": "ppiiiis",
+    "blindno_bagmean_fwd": "pppppiiiiis",
+    "blindno_bagmean_bwd": "pppiiiiis",
+    "blindno_mse": "pppplips",
+    "blindno_rowsq": "pppiiiiiis",
+    "blindno_adam": "pppplffffffs",
+}
+
+_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,
+       "s": ctypes.c_void_p}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class BlindnoError(RuntimeError):
+    pass
+
+
+def load():
+    """Load and type the library (idempotent).  Raises BlindnoError if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise BlindnoError(
+                f"libblindno.so not found at {LIB_PATH}; build it with "
+                "`python reconstruction-of-pde-without-time-label_amd/build.py` "
+                "(there is no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, sig in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = [_CT[c] for c in sig]
+            fn.restype = ctypes.c_int
+        lib.blindno_error_string.argtypes = [ctypes.c_int]
+        lib.blindno_error_string.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES) + ["blindno_error_string"]
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.blindno_error_string(rc).decode(errors="replace")
+        raise BlindnoError(f"{name} failed: hip error {rc} ({msg})")
+    return rc

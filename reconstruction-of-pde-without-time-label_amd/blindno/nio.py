@@ -1,0 +1,185 @@
+"""Snapshot-bag (time-label-free) models: NIOFP2D_FNO, NIOFP_FNO, NIOFP2D, NIOFP,
+NIOFP_schrodinger -- drop-in for the reference's NIOModules.
+
+Same constructor signatures, attribute names and initialisation order as
+2d_FPE/NIOModules.py:14-83,508-581, 2d_Non_conservative_FPE/NIOModules.py:13-82,503-577,
+1d_FPE/NIOModules.py:15-155 and 1d_GPE/NIOModules.py:160-289.
+
+Train mode draws the bag exactly like the reference -- ``L = np.random.randint(50, T)``,
+``idx = np.random.choice(T, L)`` (with replacement) from numpy's global RNG -- so a
+seeded run sees the same bags.  ``bag_idx=`` overrides the draw (parity harness).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .deeponet import FFN, DeepOnetNoBiasOrg
+from .encoders import Encoder, Encoder2D
+from .fno import FNO1d, FNO2d
+
+
+def draw_bag(T: int):
+    """The reference's train-mode bag draw (2d_FPE/NIOModules.py:548-553)."""
+    L = np.random.randint(50, T)
+    idx = np.random.choice(T, L)
+    return L, idx
+
+
+def _select(module, x, bag_idx):
+    if bag_idx is not None:
+        idx = np.asarray(bag_idx)
+        return x[:, torch.as_tensor(idx, device=x.device)], len(idx)
+    if module.training:
+        L, idx = draw_bag(x.shape[1])
+        return x[:, torch.as_tensor(idx, device=x.device)], L
+    return x, x.shape[1]
+
+
+def _bag_mean_2d(module, u, grid, B, L, nx, ny):
+    g = grid.reshape(nx * ny, 2)
+    h = ops.BagMeanFn.apply(u.reshape(B, L, nx * ny), g, module.fc0.weight.data,
+                            module.fc0.bias.data)
+    return h.view(B, nx, ny, -1)
+
+
+def _bag_mean_1d(module, u, grid, B, L, nx):
+    h = ops.BagMeanFn.apply(u.reshape(B, L, nx), grid.reshape(nx, 1), module.fc0.weight.data,
+                            module.fc0.bias.data)
+    return h
+
+
+class NIOFP2D_FNO(nn.Module):
+    """FNO-NIO, 2d_FPE/NIOModules.py:508-581.  ``heads`` selects the head attribute names
+    (("fno_drift", "fno_diffusion") for 2d_FPE, ("fno_Fx", "fno_Fy") for the
+    non-conservative copy); ``branch_last_kernel`` is the unused Encoder2D's final kernel
+    (part of the checkpoint layout)."""
+
+    def __init__(self, input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                 width, modes, output_dim, heads: Sequence[str] = ("fno_drift", "fno_diffusion"),
+                 branch_last_kernel=(2, 1)):
+        super().__init__()
+        output_dimensions = n_basis
+        self.fno_layers = fno_layers
+        self.branch = Encoder2D(output_dimensions, last_kernel=branch_last_kernel)
+        self.fc0 = nn.Linear(3, width)
+        self.FNO_input = FNO2d(modes=12, width=4, n_layers=2, input_dim=3, output_dim=1)
+        self._heads = tuple(heads)
+        for name in self._heads:
+            setattr(self, name, FNO2d(modes=modes, width=width, n_layers=self.fno_layers,
+                                      input_dim=width, output_dim=1))
+
+    def forward(self, x, grid, bag_idx=None):
+        """x (B, T, Nx, Ny) standardised snapshots, grid (Nx, Ny, 2) -> (B, Nx, Ny, 2)."""
+        x, L = _select(self, x, bag_idx)
+        B, _, nx, ny = x.shape
+        x_in = x.reshape(B * L, 1, nx, ny)
+        grid_r = grid.permute(2, 0, 1).unsqueeze(0).expand(B * L, 2, nx, ny)
+        inp = torch.cat((x_in, grid_r), dim=1).permute(0, 2, 3, 1).contiguous()
+        u = self.FNO_input(inp)                       # (B*L, nx, ny, 1)
+        h = _bag_mean_2d(self, u, grid, B, L, nx, ny)
+        return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
+
+
+class NIOFP_FNO(nn.Module):
+    """1D FNO-NIO: 1d_FPE/NIOModules.py:87-155 (heads fno_drift/fno_diffusion) or
+    1d_GPE/NIOModules.py:228-289 (single head ``fno_V``: ``heads=("fno_V",)``)."""
+
+    def __init__(self, fno_layers, width, modes, output_dim, device,
+                 heads: Sequence[str] = ("fno_drift", "fno_diffusion")):
+        super().__init__()
+        self.device = device
+        self.fno_layers = fno_layers
+        self.FNO_input = FNO1d(modes=12, width=4, n_layers=2, input_dim=2, output_dim=1,
+                               device=self.device)
+        self.fc0 = nn.Linear(2, width)
+        self._heads = tuple(heads)
+        for name in self._heads:
+            setattr(self, name, FNO1d(modes=modes, width=width, n_layers=self.fno_layers,
+                                      input_dim=width, output_dim=1, device=self.device))
+
+    def forward(self, x, grid, bag_idx=None):
+        """x (B, T, Nx), grid (Nx, 1) -> (B, Nx, n_heads)."""
+        x, L = _select(self, x, bag_idx)
+        B, _, nx = x.shape
+        x_in = x.reshape(B * L, nx, 1)
+        grid_r = grid.unsqueeze(0).expand(B * L, nx, 1)
+        inp = torch.cat((x_in, grid_r), dim=2).contiguous()
+        u = self.FNO_input(inp)                       # (B*L, nx, 1)
+        h = _bag_mean_1d(self, u, grid, B, L, nx)
+        outs = [getattr(self, n)(h) for n in self._heads]
+        return torch.cat(outs, dim=-1) if len(outs) > 1 else outs[0]
+
+
+class NIOFP2D(nn.Module):
+    """NIO (DeepONet branch/trunk + FNO heads), 2d_FPE/NIOModules.py:14-83 and
+    2d_Non_conservative_FPE/NIOModules.py:13-82 (heads fno_Fx/fno_Fy)."""
+
+    def __init__(self, input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                 width, modes, output_dim, heads: Sequence[str] = ("fno_drift", "fno_diffusion"),
+                 branch_last_kernel=(2, 1)):
+        super().__init__()
+        output_dimensions = n_basis
+        self.trunk = FFN(input_dimensions_trunk, output_dimensions, n_hidden_layers, neurons,
+                         "leaky_relu", 0.0)
+        self.fno_layers = fno_layers
+        self.branch = Encoder2D(output_dimensions, last_kernel=branch_last_kernel)
+        self.deeponet = DeepOnetNoBiasOrg(self.branch, self.trunk)
+        self.fc0 = nn.Linear(3, width)
+        self._heads = tuple(heads)
+        for name in self._heads:
+            setattr(self, name, FNO2d(modes=modes, width=width, n_layers=self.fno_layers,
+                                      input_dim=width, output_dim=1))
+
+    def forward(self, x, grid, bag_idx=None):
+        ops.require_device(x, grid)
+        x, L = _select(self, x, bag_idx)
+        B, _, nx, ny = x.shape
+        u = self.deeponet(x.unsqueeze(2), grid.reshape(-1, 2))     # (B, L, nx*ny)
+        h = _bag_mean_2d(self, u, grid, B, L, nx, ny)
+        return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
+
+
+class NIOFP(nn.Module):
+    """1D NIO, 1d_FPE/NIOModules.py:15-84 (``heads=("fno_V",)`` + GPE encoder kernels
+    give NIOFP_schrodinger, 1d_GPE/NIOModules.py:160-223)."""
+
+    def __init__(self, input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                 width, modes, output_dim, device,
+                 heads: Sequence[str] = ("fno_drift", "fno_diffusion"),
+                 encoder_kernels=(5, 4, 15), encoder_conv4=False):
+        super().__init__()
+        output_dimensions = n_basis
+        self.trunk = FFN(input_dimensions_trunk, output_dimensions, n_hidden_layers, neurons,
+                         "leaky_relu", 0.0)
+        self.fno_layers = fno_layers
+        self.branch = Encoder(output_dimensions, final_kernels=encoder_kernels,
+                              apply_conv4=encoder_conv4)
+        self.deeponet = DeepOnetNoBiasOrg(self.branch, self.trunk)
+        self.fc0 = nn.Linear(2, width)
+        self.device = device
+        self._heads = tuple(heads)
+        for name in self._heads:
+            setattr(self, name, FNO1d(modes=modes, width=width, n_layers=self.fno_layers,
+                                      input_dim=width, output_dim=1, device=self.device))
+
+    def forward(self, x, grid, bag_idx=None):
+        ops.require_device(x, grid)
+        x, L = _select(self, x, bag_idx)
+        B, _, nx = x.shape
+        u = self.deeponet(x, grid)                                   # (B, L, nx)
+        h = _bag_mean_1d(self, u, grid, B, L, nx)
+        outs = [getattr(self, n)(h) for n in self._heads]
+        return torch.cat(outs, dim=-1) if len(outs) > 1 else outs[0]
+
+
+class NIOFP_schrodinger(NIOFP):
+    def __init__(self, input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                 width, modes, output_dim, device):
+        super().__init__(input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                         width, modes, output_dim, device, heads=("fno_V",),
+                         encoder_kernels=(5, 7, 4), encoder_conv4=True)

@@ -1,0 +1,514 @@
+"""Host orchestration of the HIP kernels: spectral convolutions, FNO bodies, bag mean,
+loss -- each wrapped as a torch.autograd.Function whose forward and backward enqueue
+only libblindno kernels on the current HIP stream.
+
+Reference semantics followed (yl602019618/Reconstruction-of-PDE-without-Time-Label):
+  SpectralConv2d  2d_FPE/FNOModules.py:124-178     SpectralConv1d 1d_FPE/FNOModules.py:27-59
+  FNO2d           2d_FPE/FNOModules.py:181-240     FNO1d          1d_FPE/FNOModules.py:62-122
+  bag mean        2d_FPE/NIOModules.py:565-575     1d_FPE/NIOModules.py:140-149
+  MSELoss         2d_FPE/train_fno.py:116,142
+There is no CPU path: CPU tensors raise.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ._lib import BlindnoError, call, ptr, stream_ptr
+
+F32 = torch.float32
+
+# ---------------------------------------------------------------------------- helpers
+
+
+def pad_amount(n: int) -> int:
+    """int(round(n/4)) with round-half-even (2d_FPE/FNOModules.py:222-223)."""
+    return int(round(n * 0.25))
+
+
+def kept_rows_count(m1: int, P1: int) -> int:
+    return 2 * m1 if 2 * m1 < P1 else P1
+
+
+_TW = {}
+
+
+def twiddle(P: int, device) -> torch.Tensor:
+    """Device table tw[j] = (cos 2 pi j/P, sin 2 pi j/P), built in double."""
+    dev = torch.device(device)
+    key = (P, dev.index)
+    t = _TW.get(key)
+    if t is None:
+        j = torch.arange(P, dtype=torch.float64) * (2.0 * torch.pi / P)
+        t = torch.stack([torch.cos(j), torch.sin(j)], 1).to(F32).to(dev).contiguous()
+        _TW[key] = t
+    return t
+
+
+def require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise BlindnoError("blindno ops need HIP device tensors; there is no CPU path "
+                               "(move the model and inputs to 'cuda')")
+
+
+def _c(t):
+    if t is None:
+        return None
+    if t.dtype not in (F32, torch.complex64):
+        raise BlindnoError(f"blindno ops are fp32: got {t.dtype}")
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _nchunk(npts: int, np_: int, target_threads: int = 1 << 18, min_pts: int = 32) -> int:
+    n = max(1, target_threads // max(1, np_))
+    n = min(n, max(1, npts // min_pts))
+    return int(n)
+
+
+def _empty(*shape, like):
+    return torch.empty(*shape, dtype=F32, device=like.device)
+
+
+def reduce_partials(partial: torch.Tensor, nchunk: int, np_: int) -> torch.Tensor:
+    out = _empty(np_, like=partial)
+    call("blindno_reduce_partials", ptr(partial), ptr(out), nchunk, np_, stream_ptr())
+    return out
+
+
+# ---------------------------------------------------------------------------- kernel wrappers
+
+
+def k_rowdft(x, Bn, C, P1, P2, m2, act):
+    At = _empty(Bn, m2, C, P1, 2, like=x)
+    call("blindno_rowdft", ptr(x), ptr(At), ptr(twiddle(P2, x.device)), Bn, C, P1, P2, m2, act,
+         stream_ptr())
+    return At
+
+
+def k_coldft(At, Bn, C, P1, m1, m2, P2, scale):
+    K1 = kept_rows_count(m1, P1)
+    X = _empty(Bn, m2, C, K1, 2, like=At)
+    call("blindno_coldft", ptr(At), ptr(X), ptr(twiddle(P1, At.device)), Bn, C, P1, m1, m2, P2,
+         scale, stream_ptr())
+    return X
+
+
+def k_colidft(Y, Bn, C, P1, m1, m2, P2, scale):
+    Z = _empty(Bn, C, P1, m2, 2, like=Y)
+    call("blindno_colidft", ptr(Y), ptr(Z), ptr(twiddle(P1, Y.device)), Bn, C, P1, m1, m2, P2,
+         scale, stream_ptr())
+    return Z
+
+
+def k_mix(X, Wt, Bn, Ci, Co, K1, m2, direction):
+    Y = _empty(Bn, m2, Co if direction == 0 else Ci, K1, 2, like=X)
+    call("blindno_mix", ptr(X), ptr(Wt), ptr(Y), Bn, Ci, Co, K1, m2, direction, stream_ptr())
+    return Y
+
+
+def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2):
+    dWt = _empty(m2, K1, Ci, Co, 2, like=X)
+    call("blindno_mix_wgrad", ptr(X), ptr(G), ptr(dWt), Bn, Ci, Co, K1, m2, stream_ptr())
+    return dWt
+
+
+def k_pack_w2d(w1, w2, P1):
+    Ci, Co, m1, m2 = w1.shape[:4]
+    K1 = kept_rows_count(m1, P1)
+    Wt = _empty(m2, K1, Ci, Co, 2, like=w1)
+    call("blindno_pack_w2d", ptr(w1), ptr(w2), ptr(Wt), Ci, Co, m1, m2, P1, stream_ptr())
+    return Wt
+
+
+def k_unpack_w2d(dWt, w1, P1):
+    Ci, Co, m1, m2 = w1.shape[:4]
+    dw1 = torch.empty_like(w1)
+    dw2 = torch.empty_like(w1)
+    call("blindno_unpack_w2d", ptr(dWt), ptr(dw1), ptr(dw2), Ci, Co, m1, m2, P1, stream_ptr())
+    return dw1, dw2
+
+
+def k_pack_w1d(w):
+    Ci, Co, m = w.shape
+    Wt = _empty(m, 1, Ci, Co, 2, like=torch.view_as_real(w))
+    call("blindno_pack_w1d", ptr(w), ptr(Wt), Ci, Co, m, 0, stream_ptr())
+    return Wt
+
+
+def k_unpack_w1d(dWt, w):
+    Ci, Co, m = w.shape
+    dw = torch.empty_like(w)
+    call("blindno_pack_w1d", ptr(dWt), ptr(dw), Ci, Co, m, 1, stream_ptr())
+    return dw
+
+
+def k_mix1d(At, Wt, Bn, Ci, Co, m, P2, direction):
+    cin = Ci if direction == 0 else Co
+    cout = Co if direction == 0 else Ci
+    Xs = _empty(Bn, m, cin, 1, 2, like=At)
+    Z = _empty(Bn, cout, 1, m, 2, like=At)
+    call("blindno_mix1d", ptr(At), ptr(Wt), ptr(Xs), ptr(Z), Bn, Ci, Co, m, P2, direction,
+         stream_ptr())
+    return Xs, Z
+
+
+def k_rowidft_epi(Z, x, wc, bc, Bn, C, P1, P2, m2, act):
+    z = _empty(Bn, C, P1, P2, like=Z)
+    call("blindno_rowidft_epi", ptr(Z), ptr(x), ptr(wc), ptr(bc), ptr(z),
+         ptr(twiddle(P2, Z.device)), Bn, C, P1, P2, m2, act, stream_ptr())
+    return z
+
+
+def k_rowidft_bwd(G, dz, wc, xpre, Bn, C, P1, P2, m2, act):
+    dx = _empty(Bn, C, P1, P2, like=G)
+    call("blindno_rowidft_bwd", ptr(G), ptr(dz), ptr(wc), ptr(xpre), ptr(dx),
+         ptr(twiddle(P2, G.device)), Bn, C, P1, P2, m2, act, stream_ptr())
+    return dx
+
+
+def k_conv_wgrad(dz, x, Bn, C, P1, P2, act):
+    np_ = C * C + C
+    nchunk = _nchunk(Bn * P1 * P2, np_)
+    partial = _empty(nchunk, np_, like=dz)
+    call("blindno_conv_wgrad", ptr(dz), ptr(x), ptr(partial), nchunk, Bn, C, P1, P2, act,
+         stream_ptr())
+    g = reduce_partials(partial, nchunk, np_)
+    return g[: C * C], g[C * C:]
+
+
+# ---------------------------------------------------------------------------- spectral layer
+
+
+class SpecShape:
+    """Geometry of one spectral layer over a padded field (P1 = 1 for 1D)."""
+
+    def __init__(self, Bn, Ci, Co, P1, P2, m1, m2, dim):
+        self.Bn, self.Ci, self.Co, self.P1, self.P2 = Bn, Ci, Co, P1, P2
+        self.m1, self.m2, self.dim = m1, m2, dim
+        self.K1 = kept_rows_count(m1, P1) if dim == 2 else 1
+        if m2 > P2 // 2 + 1:
+            raise BlindnoError(f"modes {m2} exceed P2//2+1 = {P2 // 2 + 1}")
+        if dim == 2 and m1 > P1:
+            raise BlindnoError(f"modes1 {m1} exceed P1 = {P1}")
+
+
+def spec_forward(x, act, Wt, sh: SpecShape):
+    """Forward spectrum of layer input f(x) -> (saved colspec X, rowcoef Z)."""
+    if sh.dim == 2:
+        At = k_rowdft(x, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, act)
+        X = k_coldft(At, sh.Bn, sh.Ci, sh.P1, sh.m1, sh.m2, sh.P2, 0)
+        Y = k_mix(X, Wt, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2, 0)
+        Z = k_colidft(Y, sh.Bn, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
+        return X, Z
+    At = k_rowdft(x, sh.Bn, sh.Ci, 1, sh.P2, sh.m2, act)
+    X, Z = k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 0)
+    return X, Z
+
+
+def spec_backward(dz, X, Wt, sh: SpecShape):
+    """Adjoint of spec_forward: returns (dWt, GZ) for the layer's output gradient dz."""
+    if sh.dim == 2:
+        At = k_rowdft(dz, sh.Bn, sh.Co, sh.P1, sh.P2, sh.m2, 0)
+        G = k_coldft(At, sh.Bn, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
+        dWt = k_mix_wgrad(X, G, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2)
+        GX = k_mix(G, Wt, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2, 1)
+        GZ = k_colidft(GX, sh.Bn, sh.Ci, sh.P1, sh.m1, sh.m2, sh.P2, 0)
+        return dWt, GZ
+    At = k_rowdft(dz, sh.Bn, sh.Co, 1, sh.P2, sh.m2, 0)
+    G, GZ = k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 1)
+    dWt = k_mix_wgrad(X, G, sh.Bn, sh.Ci, sh.Co, 1, sh.m2)
+    return dWt, GZ
+
+
+def pack_weights(ws, P1, dim):
+    if dim == 2:
+        return k_pack_w2d(_c(ws[0]), _c(ws[1]), P1)
+    return k_pack_w1d(_c(ws[0]))
+
+
+def unpack_weights(dWt, ws, P1, dim):
+    if dim == 2:
+        return k_unpack_w2d(dWt, ws[0], P1)
+    return (k_unpack_w1d(dWt, ws[0]),)
+
+
+class SpectralConvFn(torch.autograd.Function):
+    """Bare SpectralConv1d/2d (no 1x1 conv): x (Bn, Ci, [P1,] P2) -> (Bn, Co, [P1,] P2)."""
+
+    @staticmethod
+    def forward(ctx, x, *ws):
+        require_device(x, *ws)
+        x = _c(x)
+        dim = 2 if len(ws) == 2 else 1
+        Bn, Ci = x.shape[:2]
+        P1, P2 = (x.shape[2], x.shape[3]) if dim == 2 else (1, x.shape[2])
+        w0 = ws[0]
+        Co = w0.shape[1]
+        m1 = w0.shape[2]
+        m2 = w0.shape[3] if dim == 2 else w0.shape[2]
+        sh = SpecShape(Bn, Ci, Co, P1, P2, m1, m2, dim)
+        Wt = pack_weights(ws, P1, dim)
+        X, Z = spec_forward(x, 0, Wt, sh)
+        y = k_rowidft_epi(Z, None, None, None, Bn, Co, P1, P2, m2, 0)
+        ctx.sh, ctx.dim, ctx.P1 = sh, dim, P1
+        ctx.save_for_backward(X, Wt, *ws)
+        return y.view(Bn, Co, P2) if dim == 1 else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        X, Wt, *ws = ctx.saved_tensors
+        sh = ctx.sh
+        gy = _c(gy)
+        dWt, GZ = spec_backward(gy, X, Wt, sh)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = k_rowidft_bwd(GZ, None, None, None, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, 0)
+            if ctx.dim == 1:
+                dx = dx.view(sh.Bn, sh.Ci, sh.P2)
+        dws = unpack_weights(dWt, ws, ctx.P1, ctx.dim)
+        return (dx, *dws)
+
+
+# ---------------------------------------------------------------------------- FNO body
+
+
+class FNOMeta:
+    def __init__(self, dim, n_layers, width, modes1, modes2, hidden, cout, cin):
+        self.dim, self.n_layers, self.width = dim, n_layers, width
+        self.m1, self.m2, self.hidden, self.cout, self.cin = modes1, modes2, hidden, cout, cin
+
+
+def _fno_geometry(inp, meta: FNOMeta):
+    if meta.dim == 2:
+        Bn, N1, N2, Cin = inp.shape
+        pH, pW = pad_amount(N1), pad_amount(N2)   # x2_padding (H), x1_padding (W)
+        P1, P2 = N1 + pH, N2 + pW
+        Ho, Wo = P1 - pW, P2 - pH                 # x[..., :-x1_padding, :-x2_padding]
+    else:
+        Bn, N2, Cin = inp.shape
+        N1 = 1
+        pW = pad_amount(N2)
+        P1, P2 = 1, N2 + pW
+        Ho, Wo = 1, P2 - pW
+        pH = 0
+    if Ho <= 0 or Wo <= 0 or (meta.dim == 2 and (pH == 0 or pW == 0)) or pW == 0:
+        raise BlindnoError("grid too small: the reference's crop x[..., :-pad] needs pad > 0")
+    return Bn, N1, N2, Cin, P1, P2, Ho, Wo
+
+
+def fno_forward(meta: FNOMeta, inp, prm, save=True):
+    """prm = [fc0w, fc0b, (w1, [w2], cw, cb) * n, fc1w, fc1b, fc2w, fc2b]."""
+    Bn, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
+    C, n, dim = meta.width, meta.n_layers, meta.dim
+    nw = 2 if dim == 2 else 1
+    fc0w, fc0b = prm[0], prm[1]
+    x0 = _empty(Bn, C, P1, P2, like=inp)
+    call("blindno_lift_fwd", ptr(inp), ptr(fc0w), ptr(fc0b), ptr(x0), Bn, N1, N2, Cin, C, P1, P2,
+         stream_ptr())
+    sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, dim)
+    src, act = x0, 0
+    Xs, Wts, zs = [], [], []
+    off = 2
+    for k in range(n):
+        ws = prm[off:off + nw]
+        cw, cb = prm[off + nw], prm[off + nw + 1]
+        off += nw + 2
+        Wt = pack_weights(ws, P1, dim)
+        X, Z = spec_forward(src, act, Wt, sh)
+        z = k_rowidft_epi(Z, src, cw, cb, Bn, C, P1, P2, meta.m2, act)
+        Xs.append(X)
+        Wts.append(Wt)
+        zs.append(z)
+        src, act = z, 1
+    fc1w, fc1b, fc2w, fc2b = prm[off:off + 4]
+    Hd, Cout = fc1w.shape[0], fc2w.shape[0]
+    out = _empty(Bn, Ho, Wo, Cout, like=inp)
+    call("blindno_project_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b), ptr(out),
+         Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, stream_ptr())
+    if dim == 1:
+        out = out.view(Bn, Wo, Cout)
+    saved = (x0, Xs, Wts, zs) if save else None
+    return out, saved
+
+
+def fno_backward(meta: FNOMeta, inp, prm, saved, gout, need_inp_grad, dout_div=1):
+    Bn, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
+    C, n, dim = meta.width, meta.n_layers, meta.dim
+    nw = 2 if dim == 2 else 1
+    x0, Xs, Wts, zs = saved
+    off_fc1 = 2 + n * (nw + 2)
+    fc1w, fc1b, fc2w, fc2b = prm[off_fc1:off_fc1 + 4]
+    Hd, Cout = fc1w.shape[0], fc2w.shape[0]
+    gout = _c(gout)
+    grads: List[Optional[torch.Tensor]] = [None] * len(prm)
+    # projection
+    dz = torch.zeros(Bn, C, P1, P2, dtype=F32, device=inp.device)
+    np_p = Hd * C + Hd + Cout * Hd + Cout
+    nchunk = _nchunk(Bn * Ho * Wo, Hd, target_threads=1 << 17)
+    partial = _empty(nchunk, np_p, like=inp)
+    call("blindno_project_bwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(gout), ptr(dz),
+         ptr(partial), nchunk, Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, dout_div, stream_ptr())
+    gp = reduce_partials(partial, nchunk, np_p)
+    o = 0
+    grads[off_fc1] = gp[o:o + Hd * C].view(Hd, C); o += Hd * C
+    grads[off_fc1 + 1] = gp[o:o + Hd]; o += Hd
+    grads[off_fc1 + 2] = gp[o:o + Cout * Hd].view(Cout, Hd); o += Cout * Hd
+    grads[off_fc1 + 3] = gp[o:o + Cout]
+    sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, dim)
+    for k in reversed(range(n)):
+        off = 2 + k * (nw + 2)
+        ws = prm[off:off + nw]
+        cw = prm[off + nw]
+        src, act = (x0, 0) if k == 0 else (zs[k - 1], 1)
+        dWt, GZ = spec_backward(dz, Xs[k], Wts[k], sh)
+        for j, g in enumerate(unpack_weights(dWt, ws, P1, dim)):
+            grads[off + j] = g
+        gw, gb = k_conv_wgrad(dz, src, Bn, C, P1, P2, act)
+        grads[off + nw] = gw.view_as(cw)
+        grads[off + nw + 1] = gb
+        dz = k_rowidft_bwd(GZ, dz, cw, src if act else None, Bn, C, P1, P2, meta.m2, act)
+    # lift
+    fc0w = prm[0]
+    np_l = C * Cin + C
+    nchunk = _nchunk(Bn * N1 * N2, np_l)
+    partial = _empty(nchunk, np_l, like=inp)
+    d_inp = torch.empty_like(inp) if need_inp_grad else None
+    call("blindno_lift_bwd", ptr(dz), ptr(inp), ptr(fc0w), ptr(d_inp), ptr(partial), nchunk, Bn,
+         N1, N2, Cin, C, P1, P2, stream_ptr())
+    gl = reduce_partials(partial, nchunk, np_l)
+    grads[0] = gl[:C * Cin].view(C, Cin)
+    grads[1] = gl[C * Cin:]
+    return d_inp, grads
+
+
+class FNOFn(torch.autograd.Function):
+    """Whole FNO1d/FNO2d forward as one autograd node (keeps the reference's parameters,
+    runs only HIP kernels)."""
+
+    @staticmethod
+    def forward(ctx, meta, inp, *prm):
+        require_device(inp, *prm)
+        inp = _c(inp)
+        prm = [_c(p) for p in prm]
+        out, saved = fno_forward(meta, inp, prm, save=True)
+        ctx.meta = meta
+        x0, Xs, Wts, zs = saved
+        ctx.n = len(Xs)
+        ctx.save_for_backward(inp, x0, *Xs, *Wts, *zs, *prm)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        meta, n = ctx.meta, ctx.n
+        t = ctx.saved_tensors
+        inp, x0 = t[0], t[1]
+        Xs, Wts, zs = list(t[2:2 + n]), list(t[2 + n:2 + 2 * n]), list(t[2 + 2 * n:2 + 3 * n])
+        prm = list(t[2 + 3 * n:])
+        d_inp, grads = fno_backward(meta, inp, prm, (x0, Xs, Wts, zs), gout,
+                                    ctx.needs_input_grad[1])
+        grads = [g if ctx.needs_input_grad[2 + i] else None for i, g in enumerate(grads)]
+        return (None, d_inp, *grads)
+
+
+# ---------------------------------------------------------------------------- bag mean
+
+
+class BagMeanFn(torch.autograd.Function):
+    """Fixed-weight snapshot-bag aggregation: u (B, L, S), grid (S, d) -> (B, S, width).
+    ``w``/``bias`` are ``fc0.weight.data``/``.bias.data`` (never trained, as in the
+    reference, 2d_FPE/NIOModules.py:569-570)."""
+
+    @staticmethod
+    def forward(ctx, u, grid, w, bias):
+        require_device(u, grid, w, bias)
+        u, grid = _c(u), _c(grid)
+        w, bias = _c(w.detach()), _c(bias.detach())
+        B, L, S = u.shape
+        d = grid.shape[1]
+        width = w.shape[0]
+        y = _empty(B, S, width, like=u)
+        call("blindno_bagmean_fwd", ptr(u), ptr(grid), ptr(w), ptr(bias), ptr(y), B, L, S, d,
+             width, stream_ptr())
+        ctx.save_for_backward(w)
+        ctx.dims = (B, L, S, d, width)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (w,) = ctx.saved_tensors
+        B, L, S, d, width = ctx.dims
+        gy = _c(gy)
+        gu = ggrid = None
+        if ctx.needs_input_grad[0]:
+            s = _empty(B, S, like=gy)
+            call("blindno_bagmean_bwd", ptr(gy), ptr(w), ptr(s), B, S, d, width, L, stream_ptr())
+            gu = s.unsqueeze(1).expand(B, L, S)
+        if ctx.needs_input_grad[1]:
+            ggrid = torch.einsum("bsc,ce->se", gy, w[:, :d])
+        return gu, ggrid, None, None
+
+
+# ---------------------------------------------------------------------------- loss
+
+
+class MSEFn(torch.autograd.Function):
+    """nn.MSELoss() (mean reduction) with a fused gradient kernel."""
+
+    @staticmethod
+    def forward(ctx, pred, target):
+        require_device(pred, target)
+        pred, target = _c(pred), _c(target)
+        n = pred.numel()
+        nblk = max(1, min(1024, (n + 4095) // 4096))
+        partial = _empty(nblk, like=pred)
+        call("blindno_mse", ptr(pred), ptr(target), ptr(partial), None, n, nblk, None,
+             stream_ptr())
+        ctx.save_for_backward(pred, target)
+        return partial.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, target = ctx.saved_tensors
+        n = pred.numel()
+        nblk = max(1, min(1024, (n + 4095) // 4096))
+        partial = _empty(nblk, like=pred)
+        grad = torch.empty_like(pred)
+        g = _c(g.reshape(1))
+        call("blindno_mse", ptr(pred), ptr(target), ptr(partial), ptr(grad), n, nblk, ptr(g),
+             stream_ptr())
+        return grad, None
+
+
+def mse_loss(pred, target):
+    return MSEFn.apply(pred, target)
+
+
+# ---------------------------------------------------------------------------- metrics
+
+
+def rowsq(a, b, rows, n, stride, off_a, off_b, den_all):
+    out = torch.empty(rows, 2, dtype=torch.float64, device=a.device)
+    call("blindno_rowsq", ptr(_c(a)), ptr(_c(b)), ptr(out), rows, n, stride, off_a, off_b,
+         den_all, stream_ptr())
+    return out
+
+
+def train_rel_l2_2ch(pred, out):
+    """Per-sample train-loop metric of 2d_FPE/train_fno.py:160-163 (denominator = norm of
+    BOTH output channels).  pred/out (B, ..., 2).  Returns (e_ch0, e_ch1) fp64 (B,)."""
+    B = pred.shape[0]
+    n = pred[0].numel() // pred.shape[-1]
+    s0 = rowsq(pred, out, B, n, pred.shape[-1], 0, 0, 1)
+    s1 = rowsq(pred, out, B, n, pred.shape[-1], 1, 1, 1)
+    return s0[:, 0].sqrt() / s0[:, 1].sqrt(), s1[:, 0].sqrt() / s1[:, 1].sqrt()
+
+
+def time_averaged_relative_l2(pt_pred, pt_ref, eps=1e-12):
+    """mean_t ||P_pred[t]-P_ref[t]|| / (||P_ref[t]|| + eps)
+    (2d_Non_conservative_FPE/compute_time_error.py:321-333), fp64 accumulation on device."""
+    nt = pt_pred.shape[0]
+    n = pt_pred[0].numel()
+    s = rowsq(pt_pred.float(), pt_ref.float(), nt, n, 1, 0, 0, 0)
+    return float((s[:, 0].sqrt() / (s[:, 1].sqrt() + eps)).mean())
