@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""BlinDNO FNO-NIO training throughput on MI355X (BASELINE.json config C).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (one "step"): NIOFP2D_FNO(2,3,100,25,3,12,32,2) train step on a 128x128 grid,
+per-GPU batch B=4 snapshot bags of T=100 frames, random bag size L = randint(50, T) with
+replacement (numpy RNG seeded 1234+rank), MSE loss, backward, gradient all-reduce over
+ranks (N>1), fused Adam (lr 5e-4).  Synthetic standardised bags live in HBM (each rank
+owns its shard of a 4096-bag set).  value = world * B * K / max-over-ranks(time of K steps)
+snapshot-bags/s.
+
+Extra fields: "roofline" for the dominant kernel (algorithmic bytes or flops per launch /
+average launch time, measured with HIP events on the launch stream during the timed
+region) and "cpu_baseline" (the float32 CPU oracle timed on this host on a bounded
+sample of the same workload, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "reconstruction-of-pde-without-time-label_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP32_PEAK_TFLOPS = 157.3       # fp32 vector = fp32 MFMA dense peak (same table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--grid", type=int, default=128)
+    ap.add_argument("--T", type=int, default=100)
+    ap.add_argument("--bags", type=int, default=4096, help="dataset size (all ranks)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="cpu baseline budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-kernel-timer", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import blindno
+    from blindno import timing
+    from blindno.train import DataParallel, FlatAdam, grid2d, synthetic_bags, trained_parameters
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    blindno.load_library()
+
+    seed = 1234
+    np.random.seed(seed + rank)
+    torch.manual_seed(seed + rank)
+    N, T, B = a.grid, a.T, a.batch
+    model = blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2,
+                                branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N)).to(dev)
+    model.train()
+    opt = FlatAdam(trained_parameters(model), lr=5e-4)
+    dp = DataParallel(opt)
+    dp.broadcast_parameters(0)
+
+    n_local = max(B, a.bags // world)
+    X, Y = synthetic_bags(n_local, T, (N, N), 2, seed=seed + 7919 * rank, device=dev)
+    grid = grid2d(N, N, dev)
+    order = torch.randperm(n_local, device=dev, generator=torch.Generator(device=dev).manual_seed(seed + rank))
+    loss_acc = torch.zeros((), device=dev)
+
+    def step(i):
+        j = (i * B) % (n_local - B + 1)
+        ids = order[j:j + B]
+        x = X.index_select(0, ids)
+        y = Y.index_select(0, ids)
+        out = model(x, grid)
+        loss = blindno.mse_loss(out, y)
+        loss.backward()
+        dp.step()
+        opt.zero_grad()
+        loss_acc.add_(loss.detach())
+
+    for i in range(a.warmup):
+        step(i)
+    timer = None
+    if not a.no_kernel_timer:
+        timer = timing.KernelTimer(timing.DOMINANT)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if timer:
+        timer.start()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if timer:
+        timer.stop()
+    dtt = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(dtt, op=dist.ReduceOp.MAX)
+    dt = float(dtt)
+    value = world * B * a.steps / dt
+
+    if rank == 0:
+        res = {
+            "metric": "snapshot-bags/sec (train step), 2D FPE 128^2 FNO-NIO",
+            "value": round(value, 3),
+            "unit": "snapshot-bags/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (standardised N(0,1) bags resident in HBM; reference datasets not shipped)",
+            "config": {"workload": f"2d_FPE train_fno.py NIOFP2D_FNO(2,3,100,25,3,12,32,2) {N}x{N}",
+                       "per_gpu_batch": B, "global_batch": B * world, "T": T,
+                       "bag_size": "L=randint(50,T) with replacement", "dataset_bags": a.bags,
+                       "parallelism": f"dp{world}", "optimizer": "Adam lr 5e-4 (fused flat)"},
+        }
+        if timer:
+            res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS)
+        if world == 1 and not a.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(a, budget=a.cpu_seconds)
+        res["loss_mean"] = float(loss_acc) / (a.warmup + a.steps)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, budget):
+    """float32 CPU oracle (oracle/ restates the reference's algorithm) timed on this host:
+    forward + backward of one bag per step (L = 75, the mean bag size), until ~budget s."""
+    import oracle
+    import blindno
+    oracle.set_precision("fp32")
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    N, T = a.grid, a.T
+    m = blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2,
+                            branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N))
+    p = {k: v.detach().float().requires_grad_(True) for k, v in m.state_dict().items()
+         if not k.startswith("branch.")}
+    from blindno.train import grid2d
+    grid = grid2d(N, N, "cpu")
+    x = torch.randn(1, T, N, N)
+    y = torch.randn(1, N, N, 2)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        idx = np.random.RandomState(n).choice(T, 75)
+        out = oracle.niofp2d_fno(p, x, grid, idx=idx.tolist())
+        oracle.mse(out, y).backward()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget or n >= 50:
+            break
+    oracle.set_precision("fp64")
+    return {"value": round(n / el, 4), "unit": "snapshot-bags/s", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps of 1 bag (L=75, {N}x{N}, fp32 oracle fwd+bwd) in {el:.1f}s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -15,7 +15,8 @@
  *                            h < P1 (rows, 1 for 1D), w < P2 (padded grid)
  *   rowspec At[n][k][c][h]   row-DFT coefficients, k < m2 (column-major per mode)
  *   colspec X[n][k][c][j]    2D spectrum at the K1 kept frequency rows j
- *   rowcoef Z[n][c][h][k]    row coefficients feeding the inverse row transform
+ *   rowcoef Z[n][h][k][c]    row coefficients feeding the inverse row transform
+ *                            (all channels of one (row, mode) contiguous)
  *   wpack   Wt[k][j][ci][co] complex mixing weights, one block per kept mode
  * Kept rows: K1 = min(2*m1, P1); row j -> frequency r_j = j (j < m1 or K1 == P1)
  * else P1 - 2*m1 + j.  Rows r >= P1 - m1 are owned by weights2 (weights2 wins on
@@ -49,11 +50,13 @@ int blindno_lift_fwd(const float* in, const float* w0, const float* b0, float* x
                      blindno_stream_t stream);
 
 /* Backward of the lift: optional d_in (may be NULL) and per-chunk partial sums of
- * dW0 (C*Cin) then db0 (C) into partial[nchunk][C*Cin + C]. */
+ * dW0 (C*Cin) then db0 (C) into partial[nchunk][C*Cin + C], nchunk =
+ * blindno_lift_bwd_nchunk(Bn, N1, N2). */
 int blindno_lift_bwd(const float* dx0, const float* in, const float* w0, float* d_in,
                      float* partial, int nchunk,
                      int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
                      blindno_stream_t stream);
+int blindno_lift_bwd_nchunk(int Bn, int N1, int N2);
 
 /* crop + permute + fc1 + GELU + fc2: 2d_FPE/FNOModules.py:234-239, 1d_FPE/FNOModules.py:116-121.
  * z (Bn, C, P1, P2) -> out[(n*Ho + h)*Wo + w)*ostride + ooff + co] for h<Ho, w<Wo. */
@@ -63,70 +66,79 @@ int blindno_project_fwd(const float* z, const float* w1, const float* b1, const 
                         blindno_stream_t stream);
 
 /* Backward of the projection: dz (Bn, C, P1, P2) (written only on the crop; caller
- * zero-fills the rest), per-chunk partials of [dW1 (Hd*C), db1 (Hd), dW2 (Cout*Hd),
- * db2 (Cout)].  dout is addressed like out in blindno_project_fwd, except that the
- * sample index n is divided by dout_div (snapshot-bag broadcast; 1 = none). */
+ * zero-fills the rest), per-workgroup partials of [dW1 (Hd*C), db1 (Hd), dW2 (Cout*Hd),
+ * db2 (Cout)] into partial[nchunk][...], nchunk = blindno_project_bwd_nchunk(Bn, Ho, Wo)
+ * (any value >= 1 is accepted).  dout is addressed like out in blindno_project_fwd, except
+ * that the sample index n is divided by dout_div (snapshot-bag broadcast; 1 = none).
+ * Hd must be a multiple of 64 (the reference's fc1 is Linear(width, 128)). */
 int blindno_project_bwd(const float* z, const float* w1, const float* b1, const float* w2,
                         const float* dout, float* dz, float* partial, int nchunk,
                         int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout,
                         int ostride, int ooff, int dout_div, blindno_stream_t stream);
+int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo);
 
 /* --- truncated spectral transforms --------------------------------------------------- */
 
 /* Row (last-axis) forward DFT of the first m2 modes: torch.fft.rfft2/rfft first stage
- * (2d_FPE/FNOModules.py:163, 1d_FPE/FNOModules.py:50).  act: 0 = identity,
- * 1 = GELU applied to x on load (x holds pre-activations).  x (Bn,C,P1,P2) -> At. */
-int blindno_rowdft(const float* x, float* At, const float* tw2, int Bn, int C, int P1,
+ * (2d_FPE/FNOModules.py:163, 1d_FPE/FNOModules.py:50).  act: 0 = identity, 1 = GELU
+ * applied to x on load (x holds pre-activations).  x (Bn,C,P1,P2) -> At (rowspec).
+ * Runs on the f32 matrix cores.  Tp: B-operand image of T (P2 x 2*m2, T[w][2k] = cos,
+ * T[w][2k+1] = -sin of 2 pi k w/P2): Tp[kb][kq][n][s] = T[16 kb + 4 kq + s][n], KB =
+ * ceil(P2/16), n < Npad = 16*ceil(2*m2/16), zero padded. */
+int blindno_rowdft(const float* x, float* At, const float* Tp, int Bn, int C, int P1,
                    int P2, int m2, int act, blindno_stream_t stream);
 
-/* Column DFT at the kept rows (second stage of rfft2): At -> X (Bn, m2, C, K1).
- * scale_mode 0: none; 1: multiply mode k by c_k/(P1*P2) (adjoint of irfft2). */
-int blindno_coldft(const float* At, float* X, const float* tw1, int Bn, int C, int P1,
-                   int m1, int m2, int P2, int scale_mode, blindno_stream_t stream);
-
-/* Per-mode complex channel mix (compl_mul2d, 2d_FPE/FNOModules.py:141-154,170-173).
- * dir 0: Y[n,k,o,j] = sum_i X[n,k,i,j] Wt[k,j,i,o];
- * dir 1: Y[n,k,i,j] = sum_o conj(Wt[k,j,i,o]) X[n,k,o,j]  (input-gradient). */
-int blindno_mix(const float* X, const float* Wt, float* Y, int Bn, int Ci, int Co,
-                int K1, int m2, int dir, blindno_stream_t stream);
+/* Column pass of SpectralConv2d, one workgroup per (sample, column mode): column DFT at
+ * the K1 kept rows, per-mode complex channel mix (compl_mul2d, 2d_FPE/FNOModules.py:141-154,
+ * 170-173), column inverse.  tw1: P1-entry table (cos, sin)(2 pi j / P1).
+ * dir 0 (forward): Xs = colDFT(At) (Bn,m2,Ci,K1) saved for the weight gradient;
+ *                  Z[n][h][k][o] = c_k/(P1 P2) colIDFT(sum_i Xs W)   (rowcoef, Co channels).
+ * dir 1 (adjoint): At holds the row DFT of the output gradient (Co channels);
+ *                  Xs = c_k/(P1 P2) colDFT(At) = spectrum gradient G (Bn,m2,Co,K1);
+ *                  Z[n][h][k][i] = colIDFT(sum_o conj(W) G)             (Ci channels). */
+int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Z, const float* tw1,
+                    int Bn, int Ci, int Co, int P1, int m1, int m2, int P2, int dir,
+                    blindno_stream_t stream);
 
 /* dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]  (weight gradient of the mix). */
 int blindno_mix_wgrad(const float* X, const float* G, float* dWt, int Bn, int Ci, int Co,
                       int K1, int m2, blindno_stream_t stream);
 
-/* Column inverse at the kept rows: Z[n,c,h,k] = s_k * sum_j Y[n,k,c,j] e^{+2pi i r_j h/P1}.
- * scale_mode 0: s_k = 1; 1: s_k = c_k/(P1*P2) (forward irfft2 normalisation). */
-int blindno_colidft(const float* Y, float* Z, const float* tw1, int Bn, int C, int P1,
-                    int m1, int m2, int P2, int scale_mode, blindno_stream_t stream);
-
-/* 1D mode mix (compl_mul1d + DC halving, 1d_FPE/FNOModules.py:43-58).
- * dir 0 (forward):  X = At with X[.,0] *= 0.5 saved to Xs; Z[n,o,0,k] = c_k/P2 * sum_i X W.
- * dir 1 (backward): G = c_k/P2 * At (= DFT of dz) saved to Xs; Z[n,i,0,k] = h_k sum_o conj(W) G
- *                    with h_0 = 0.5, h_k = 1.   W packed as Wt[k][ci][co] complex. */
+/* 1D mode mix (compl_mul1d + DC halving, 1d_FPE/FNOModules.py:43-58).  At (Bn,m,C,1).
+ * dir 0 (forward):  Xs = At with X[.,0] *= 0.5 (saved); Z[n][0][k][o] = c_k/P2 sum_i Xs W.
+ * dir 1 (adjoint):  Xs = c_k/P2 At (spectrum gradient); Z[n][0][k][i] = h_k sum_o conj(W) Xs
+ *                   with h_0 = 0.5, h_k = 1.   W packed as Wt[k][ci][co] complex. */
 int blindno_mix1d(const float* At, const float* Wt, float* Xs, float* Z, int Bn, int Ci,
                   int Co, int m, int P2, int dir, blindno_stream_t stream);
 
 /* Inverse row transform + 1x1 conv + bias epilogue (irfft2 second stage, nn.Conv2d(k=1),
  * x1 + x2; 2d_FPE/FNOModules.py:177,226-230):
- *   z[n,o,h,w] = sum_k Re(Z[n,o,h,k] e^{+2pi i k w/P2}) + sum_i Wc[o,i] f(x[n,i,h,w]) + bc[o]
+ *   z[n,o,h,w] = sum_k Re(Z[n,h,k,o] e^{+2pi i k w/P2}) + sum_i Wc[o,i] f(x[n,i,h,w]) + bc[o]
  * f = identity (act 0) or GELU (act 1: x holds pre-activations).  wc == NULL drops the
- * conv/bias term (bare SpectralConv2d/1d; x, bc unused). */
+ * conv/bias term (bare SpectralConv2d/1d; x, bc unused).  twk: (P2*m2 + 16) complex table
+ * twk[w*m2 + k] = e^{+2 pi i k w/P2} (16 zero pads).  C <= 32, P2 <= 320, (m2*P2 + 4*m2*C) complex must fit in 160 KiB LDS. */
 int blindno_rowidft_epi(const float* Z, const float* x, const float* wc, const float* bc,
                         float* z, const float* tw2, int Bn, int C, int P1, int P2, int m2,
                         int act, blindno_stream_t stream);
 
-/* Backward of rowidft_epi w.r.t. its input field:
- *   dx[n,i,h,w] = sum_k Re(G[n,i,h,k] e^{+2pi i k w/P2}) + sum_o Wc[o,i] dz[n,o,h,w]
- * then, if act == 1, dx *= GELU'(xpre[n,i,h,w]) (xpre = stored pre-activation).
- * wc == NULL drops the conv term (dz unused). */
-int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc, const float* xpre,
-                        float* dx, const float* tw2, int Bn, int C, int P1, int P2, int m2,
-                        int act, blindno_stream_t stream);
+/* Adjoint of rowidft_epi w.r.t. its input field:
+ *   dx[n,i,h,w] = sum_k Re(G[n,h,k,i] e^{+2pi i k w/P2}) + sum_o Wc[o,i] dz[n,o,h,w]
+ * then, if act == 1, dx *= GELU'(xsrc[n,i,h,w]) (xsrc = the layer input's pre-activation).
+ * wc == NULL drops the conv term.  twk as in blindno_rowidft_epi.
+ * If partial != NULL (requires C <= 8 and wc), the 1x1-conv
+ * gradients are reduced in the same pass into partial[blindno_rowidft_bwd_nchunk()][C*C + C]
+ * = [dWc[o][i] = sum dz_o f(xsrc_i) | dbc[o] = sum dz_o]. */
+int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc, const float* xsrc,
+                        float* dx, const float* tw2, float* partial, int Bn, int C, int P1,
+                        int P2, int m2, int act, blindno_stream_t stream);
+int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1);
 
-/* 1x1-conv weight/bias gradient partials: partial[chunk][C*C + C] with
- * dWc[o,i] = sum dz[n,o,.] f(x[n,i,.]),  dbc[o] = sum dz[n,o,.]. */
+/* 1x1-conv weight/bias gradient partials (for C > 8): partial[nchunk][C*C + C] with
+ * dWc[o,i] = sum dz[n,o,.] f(x[n,i,.]),  dbc[o] = sum dz[n,o,.];
+ * nchunk must equal blindno_conv_wgrad_nchunk(Bn, P1, P2). */
 int blindno_conv_wgrad(const float* dz, const float* x, float* partial, int nchunk, int Bn,
                        int C, int P1, int P2, int act, blindno_stream_t stream);
+int blindno_conv_wgrad_nchunk(int Bn, int P1, int P2);
 
 /* out[p] = sum_{c < nchunk} partial[c][p] (fixed order: deterministic). */
 int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np,

@@ -21,7 +21,14 @@ import torch.nn.functional as F
 DT = torch.float64
 CDT = torch.complex128
 
-__all__ = [
+def set_precision(name: str = "fp64") -> None:
+    """Switch the oracle's arithmetic type ("fp64" for parity checks, "fp32" to time it as
+    the CPU baseline in the reference's own precision)."""
+    global DT, CDT
+    DT, CDT = (torch.float32, torch.complex64) if name == "fp32" else (torch.float64, torch.complex128)
+
+
+__all__ = ["set_precision", 
     "pad_amount", "gelu", "c2r_weights", "spectral_conv2d", "spectral_conv1d",
     "fno2d", "fno1d", "bag_mean", "niofp2d_fno", "niofp_fno", "encoder2d",
     "ffn", "deeponet_nobias", "niofp2d", "mse", "train_rel_l2_2ch", "rel_l2",

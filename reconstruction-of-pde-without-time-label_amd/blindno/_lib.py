@@ -24,13 +24,11 @@ SIGNATURES = {
     "blindno_project_fwd": "ppppppiiiiiiiiiis",
     "blindno_project_bwd": "pppppppiiiiiiiiiiiis",
     "blindno_rowdft": "pppiiiiiis",
-    "blindno_coldft": "pppiiiiiiis",
-    "blindno_mix": "pppiiiiiis",
+    "blindno_colpass": "pppppiiiiiiiis",
     "blindno_mix_wgrad": "pppiiiiis",
-    "blindno_colidft": "pppiiiiiiis",
     "blindno_mix1d": "ppppiiiiiis",
     "blindno_rowidft_epi": "ppppppiiiiiis",
-    "blindno_rowidft_bwd": "ppppppiiiiiis",
+    "blindno_rowidft_bwd": "pppppppiiiiiis",
     "blindno_conv_wgrad": "pppiiiiiis",
     "blindno_reduce_partials": "ppiis",
     "blindno_pack_w2d": "pppiiiiis",
@@ -41,6 +39,11 @@ SIGNATURES = {
     "blindno_mse": "pppplips",
     "blindno_rowsq": "pppiiiiiis",
     "blindno_adam": "pppplffffffs",
+    # size queries (return a count, not an error code)
+    "blindno_lift_bwd_nchunk": "iii",
+    "blindno_conv_wgrad_nchunk": "iii",
+    "blindno_rowidft_bwd_nchunk": "iii",
+    "blindno_project_bwd_nchunk": "iii",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,
@@ -90,9 +93,22 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+_HOOKS = {}   # kernel name -> object with before(args) / after(args) (blindno.timing)
+
+
+def query(name, *args) -> int:
+    """Call a size-query entry point (returns a count)."""
+    return int(getattr(load(), name)(*args))
+
+
 def call(name, *args):
     lib = load()
+    hook = _HOOKS.get(name)
+    if hook is not None:
+        hook.before(args)
     rc = getattr(lib, name)(*args)
+    if hook is not None:
+        hook.after(args)
     if rc != 0:
         msg = lib.blindno_error_string(rc).decode(errors="replace")
         raise BlindnoError(f"{name} failed: hip error {rc} ({msg})")

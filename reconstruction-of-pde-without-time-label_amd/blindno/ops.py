@@ -15,7 +15,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import BlindnoError, call, ptr, stream_ptr
+from ._lib import BlindnoError, call, ptr, query, stream_ptr
 
 F32 = torch.float32
 
@@ -46,6 +46,52 @@ def twiddle(P: int, device) -> torch.Tensor:
     return t
 
 
+_TWR = {}
+
+
+def twiddle_rows(P2: int, m2: int, device) -> torch.Tensor:
+    """Device table twk[w][k] = (cos 2 pi k w/P2, sin 2 pi k w/P2), padded by 16 entries
+    (the row-DFT kernel reads whole mode chunks)."""
+    dev = torch.device(device)
+    key = (P2, m2, dev.index)
+    t = _TWR.get(key)
+    if t is None:
+        w = torch.arange(P2, dtype=torch.int64)[:, None]
+        k = torch.arange(m2, dtype=torch.int64)[None, :]
+        ph = ((w * k) % P2).to(torch.float64) * (2.0 * torch.pi / P2)
+        tab = torch.stack([torch.cos(ph), torch.sin(ph)], -1).reshape(-1, 2)
+        tab = torch.cat([tab, torch.zeros(16, 2, dtype=torch.float64)], 0)
+        t = tab.to(F32).to(dev).contiguous()
+        _TWR[key] = t
+    return t
+
+
+_TWM = {}
+
+
+def twiddle_mfma(P2: int, m2: int, device) -> torch.Tensor:
+    """B-operand image of the row-DFT matrix T (P2 x 2*m2; T[w][2k] = cos, T[w][2k+1] = -sin
+    of 2 pi k w / P2) for the MFMA row DFT: Tp[kb][kq][n][s] = T[16 kb + 4 kq + s][n], zero
+    padded to KB = ceil(P2/16) blocks and Npad = 16*ceil(2*m2/16) columns."""
+    dev = torch.device(device)
+    key = (P2, m2, dev.index)
+    t = _TWM.get(key)
+    if t is None:
+        KB = (P2 + 15) // 16
+        Npad = ((2 * m2 + 15) // 16) * 16
+        w = torch.arange(KB * 16, dtype=torch.int64)[:, None]
+        k = torch.arange(m2, dtype=torch.int64)[None, :]
+        ph = ((w * k) % P2).to(torch.float64) * (2.0 * torch.pi / P2)
+        T = torch.zeros(KB * 16, Npad, dtype=torch.float64)
+        T[:, 0:2 * m2:2] = torch.cos(ph)
+        T[:, 1:2 * m2:2] = -torch.sin(ph)
+        T[P2:] = 0.0
+        Tp = T.view(KB, 4, 4, Npad).permute(0, 1, 3, 2).contiguous()   # [kb][kq][n][s]
+        t = Tp.to(F32).to(dev).reshape(-1).contiguous()
+        _TWM[key] = t
+    return t
+
+
 def require_device(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -59,12 +105,6 @@ def _c(t):
     if t.dtype not in (F32, torch.complex64):
         raise BlindnoError(f"blindno ops are fp32: got {t.dtype}")
     return t if t.is_contiguous() else t.contiguous()
-
-
-def _nchunk(npts: int, np_: int, target_threads: int = 1 << 18, min_pts: int = 32) -> int:
-    n = max(1, target_threads // max(1, np_))
-    n = min(n, max(1, npts // min_pts))
-    return int(n)
 
 
 def _empty(*shape, like):
@@ -82,30 +122,21 @@ def reduce_partials(partial: torch.Tensor, nchunk: int, np_: int) -> torch.Tenso
 
 def k_rowdft(x, Bn, C, P1, P2, m2, act):
     At = _empty(Bn, m2, C, P1, 2, like=x)
-    call("blindno_rowdft", ptr(x), ptr(At), ptr(twiddle(P2, x.device)), Bn, C, P1, P2, m2, act,
-         stream_ptr())
+    call("blindno_rowdft", ptr(x), ptr(At), ptr(twiddle_mfma(P2, m2, x.device)), Bn, C, P1, P2,
+         m2, act, stream_ptr())
     return At
 
 
-def k_coldft(At, Bn, C, P1, m1, m2, P2, scale):
+def k_colpass(At, Wt, Bn, Ci, Co, P1, m1, m2, P2, direction):
+    """Column DFT at the kept rows + per-mode mix + column inverse (one launch).
+    Returns (saved spectrum (Bn, m2, Cin, K1), row coefficients Z (Bn, P1, m2, Cout))."""
     K1 = kept_rows_count(m1, P1)
-    X = _empty(Bn, m2, C, K1, 2, like=At)
-    call("blindno_coldft", ptr(At), ptr(X), ptr(twiddle(P1, At.device)), Bn, C, P1, m1, m2, P2,
-         scale, stream_ptr())
-    return X
-
-
-def k_colidft(Y, Bn, C, P1, m1, m2, P2, scale):
-    Z = _empty(Bn, C, P1, m2, 2, like=Y)
-    call("blindno_colidft", ptr(Y), ptr(Z), ptr(twiddle(P1, Y.device)), Bn, C, P1, m1, m2, P2,
-         scale, stream_ptr())
-    return Z
-
-
-def k_mix(X, Wt, Bn, Ci, Co, K1, m2, direction):
-    Y = _empty(Bn, m2, Co if direction == 0 else Ci, K1, 2, like=X)
-    call("blindno_mix", ptr(X), ptr(Wt), ptr(Y), Bn, Ci, Co, K1, m2, direction, stream_ptr())
-    return Y
+    cin, cout = (Ci, Co) if direction == 0 else (Co, Ci)
+    Xs = _empty(Bn, m2, cin, K1, 2, like=At)
+    Z = _empty(Bn, P1, m2, cout, 2, like=At)
+    call("blindno_colpass", ptr(At), ptr(Wt), ptr(Xs), ptr(Z), ptr(twiddle(P1, At.device)), Bn,
+         Ci, Co, P1, m1, m2, P2, direction, stream_ptr())
+    return Xs, Z
 
 
 def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2):
@@ -148,7 +179,7 @@ def k_mix1d(At, Wt, Bn, Ci, Co, m, P2, direction):
     cin = Ci if direction == 0 else Co
     cout = Co if direction == 0 else Ci
     Xs = _empty(Bn, m, cin, 1, 2, like=At)
-    Z = _empty(Bn, cout, 1, m, 2, like=At)
+    Z = _empty(Bn, 1, m, cout, 2, like=At)
     call("blindno_mix1d", ptr(At), ptr(Wt), ptr(Xs), ptr(Z), Bn, Ci, Co, m, P2, direction,
          stream_ptr())
     return Xs, Z
@@ -157,20 +188,29 @@ def k_mix1d(At, Wt, Bn, Ci, Co, m, P2, direction):
 def k_rowidft_epi(Z, x, wc, bc, Bn, C, P1, P2, m2, act):
     z = _empty(Bn, C, P1, P2, like=Z)
     call("blindno_rowidft_epi", ptr(Z), ptr(x), ptr(wc), ptr(bc), ptr(z),
-         ptr(twiddle(P2, Z.device)), Bn, C, P1, P2, m2, act, stream_ptr())
+         ptr(twiddle_rows(P2, m2, Z.device)), Bn, C, P1, P2, m2, act, stream_ptr())
     return z
 
 
-def k_rowidft_bwd(G, dz, wc, xpre, Bn, C, P1, P2, m2, act):
+def k_rowidft_bwd(G, dz, wc, xsrc, Bn, C, P1, P2, m2, act, want_wgrad=False):
+    """dx = irow^H(G) + Wc^T dz, times GELU'(xsrc) if act.  With want_wgrad (C <= 8) the
+    1x1-conv weight/bias gradients are reduced in the same pass: returns (dx, gw, gb)."""
     dx = _empty(Bn, C, P1, P2, like=G)
-    call("blindno_rowidft_bwd", ptr(G), ptr(dz), ptr(wc), ptr(xpre), ptr(dx),
-         ptr(twiddle(P2, G.device)), Bn, C, P1, P2, m2, act, stream_ptr())
-    return dx
+    partial, nchunk = None, 0
+    if want_wgrad:
+        nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1)
+        partial = _empty(nchunk, C * C + C, like=G)
+    call("blindno_rowidft_bwd", ptr(G), ptr(dz), ptr(wc), ptr(xsrc), ptr(dx),
+         ptr(twiddle_rows(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, stream_ptr())
+    if not want_wgrad:
+        return dx, None, None
+    g = reduce_partials(partial, nchunk, C * C + C)
+    return dx, g[: C * C], g[C * C:]
 
 
 def k_conv_wgrad(dz, x, Bn, C, P1, P2, act):
     np_ = C * C + C
-    nchunk = _nchunk(Bn * P1 * P2, np_)
+    nchunk = query("blindno_conv_wgrad_nchunk", Bn, P1, P2)
     partial = _empty(nchunk, np_, like=dz)
     call("blindno_conv_wgrad", ptr(dz), ptr(x), ptr(partial), nchunk, Bn, C, P1, P2, act,
          stream_ptr())
@@ -195,30 +235,21 @@ class SpecShape:
 
 
 def spec_forward(x, act, Wt, sh: SpecShape):
-    """Forward spectrum of layer input f(x) -> (saved colspec X, rowcoef Z)."""
+    """Forward spectrum of layer input f(x) -> (saved spectrum X, row coefficients Z)."""
+    At = k_rowdft(x, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, act)
     if sh.dim == 2:
-        At = k_rowdft(x, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, act)
-        X = k_coldft(At, sh.Bn, sh.Ci, sh.P1, sh.m1, sh.m2, sh.P2, 0)
-        Y = k_mix(X, Wt, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2, 0)
-        Z = k_colidft(Y, sh.Bn, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
-        return X, Z
-    At = k_rowdft(x, sh.Bn, sh.Ci, 1, sh.P2, sh.m2, act)
-    X, Z = k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 0)
-    return X, Z
+        return k_colpass(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 0)
+    return k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 0)
 
 
 def spec_backward(dz, X, Wt, sh: SpecShape):
     """Adjoint of spec_forward: returns (dWt, GZ) for the layer's output gradient dz."""
+    At = k_rowdft(dz, sh.Bn, sh.Co, sh.P1, sh.P2, sh.m2, 0)
     if sh.dim == 2:
-        At = k_rowdft(dz, sh.Bn, sh.Co, sh.P1, sh.P2, sh.m2, 0)
-        G = k_coldft(At, sh.Bn, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
-        dWt = k_mix_wgrad(X, G, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2)
-        GX = k_mix(G, Wt, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2, 1)
-        GZ = k_colidft(GX, sh.Bn, sh.Ci, sh.P1, sh.m1, sh.m2, sh.P2, 0)
-        return dWt, GZ
-    At = k_rowdft(dz, sh.Bn, sh.Co, 1, sh.P2, sh.m2, 0)
-    G, GZ = k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 1)
-    dWt = k_mix_wgrad(X, G, sh.Bn, sh.Ci, sh.Co, 1, sh.m2)
+        G, GZ = k_colpass(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
+    else:
+        G, GZ = k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 1)
+    dWt = k_mix_wgrad(X, G, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2)
     return dWt, GZ
 
 
@@ -264,7 +295,7 @@ class SpectralConvFn(torch.autograd.Function):
         dWt, GZ = spec_backward(gy, X, Wt, sh)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = k_rowidft_bwd(GZ, None, None, None, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, 0)
+            dx, _, _ = k_rowidft_bwd(GZ, None, None, None, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, 0)
             if ctx.dim == 1:
                 dx = dx.view(sh.Bn, sh.Ci, sh.P2)
         dws = unpack_weights(dWt, ws, ctx.P1, ctx.dim)
@@ -346,7 +377,7 @@ def fno_backward(meta: FNOMeta, inp, prm, saved, gout, need_inp_grad, dout_div=1
     # projection
     dz = torch.zeros(Bn, C, P1, P2, dtype=F32, device=inp.device)
     np_p = Hd * C + Hd + Cout * Hd + Cout
-    nchunk = _nchunk(Bn * Ho * Wo, Hd, target_threads=1 << 17)
+    nchunk = query("blindno_project_bwd_nchunk", Bn, Ho, Wo)
     partial = _empty(nchunk, np_p, like=inp)
     call("blindno_project_bwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(gout), ptr(dz),
          ptr(partial), nchunk, Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, dout_div, stream_ptr())
@@ -365,14 +396,18 @@ def fno_backward(meta: FNOMeta, inp, prm, saved, gout, need_inp_grad, dout_div=1
         dWt, GZ = spec_backward(dz, Xs[k], Wts[k], sh)
         for j, g in enumerate(unpack_weights(dWt, ws, P1, dim)):
             grads[off + j] = g
-        gw, gb = k_conv_wgrad(dz, src, Bn, C, P1, P2, act)
+        if C <= 4:
+            dz_new, gw, gb = k_rowidft_bwd(GZ, dz, cw, src, Bn, C, P1, P2, meta.m2, act, True)
+        else:
+            gw, gb = k_conv_wgrad(dz, src, Bn, C, P1, P2, act)
+            dz_new, _, _ = k_rowidft_bwd(GZ, dz, cw, src, Bn, C, P1, P2, meta.m2, act)
         grads[off + nw] = gw.view_as(cw)
         grads[off + nw + 1] = gb
-        dz = k_rowidft_bwd(GZ, dz, cw, src if act else None, Bn, C, P1, P2, meta.m2, act)
+        dz = dz_new
     # lift
     fc0w = prm[0]
     np_l = C * Cin + C
-    nchunk = _nchunk(Bn * N1 * N2, np_l)
+    nchunk = query("blindno_lift_bwd_nchunk", Bn, N1, N2)
     partial = _empty(nchunk, np_l, like=inp)
     d_inp = torch.empty_like(inp) if need_inp_grad else None
     call("blindno_lift_bwd", ptr(dz), ptr(inp), ptr(fc0w), ptr(d_inp), ptr(partial), nchunk, Bn,

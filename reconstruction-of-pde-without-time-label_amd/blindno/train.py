@@ -1,0 +1,175 @@
+"""Training-step runtime: flat-buffer Adam, data-parallel gradient all-reduce, StepLR
+semantics and on-device synthetic snapshot-bag data.
+
+Reference loop: 2d_FPE/train_fno.py:116-146 (MSE, Adam(lr), StepLR(100, 0.5), accelerate
+DDP with one NCCL all-reduce of gradients per step).  Here one process drives one GPU
+(torchrun), gradients of the TRAINED parameters are flattened into one fp32 buffer,
+all-reduced (RCCL over xGMI, backend "nccl") and averaged, and a single fused Adam kernel
+updates the flat parameter buffer that every parameter is a view of.
+
+Parameters that the reference never trains (the unused ``branch`` encoder and the
+``fc0`` of the bag mean, whose ``.data`` is read) receive no gradient and are left out
+of the flat buffers -- numerically identical to the reference, where DDP's zero-filled
+gradients give Adam updates of exactly zero.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ._lib import call, ptr, stream_ptr
+
+
+def _real(t: torch.Tensor) -> torch.Tensor:
+    return torch.view_as_real(t) if t.is_complex() else t
+
+
+class FlatAdam:
+    """torch.optim.Adam (no weight decay, no amsgrad) over one flat fp32 buffer.
+
+    The listed parameters are re-pointed to views of ``self.flat`` (complex parameters
+    through ``view_as_complex``), so one kernel updates all of them."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], lr: float, betas=(0.9, 0.999),
+                 eps: float = 1e-8):
+        self.params: List[torch.nn.Parameter] = [p for p in params]
+        if not self.params:
+            raise ValueError("FlatAdam: empty parameter list")
+        dev = self.params[0].device
+        self.sizes = [_real(p).numel() for p in self.params]
+        # complex parameters need an even (8-byte aligned) offset for view_as_complex
+        offs, off = [], 0
+        for p, sz in zip(self.params, self.sizes):
+            if p.is_complex() and off % 2:
+                off += 1
+            offs.append(off)
+            off += sz
+        n = off + (off % 2)
+        self.n = n
+        self.offsets = offs
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._gviews = []
+        for p, sz, o in zip(self.params, self.sizes, offs):
+            rv = _real(p.data)
+            self.flat[o:o + sz].copy_(rv.reshape(-1))
+            view = self.flat[o:o + sz].view(rv.shape)
+            p.data = torch.view_as_complex(view) if p.is_complex() else view
+            self._gviews.append(self.grad[o:o + sz])
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.t = 0
+
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+
+    def gather_grads(self):
+        """Copy every parameter's .grad into the flat grad buffer (one multi-tensor copy;
+        alignment pads stay zero)."""
+        gs = []
+        for p in self.params:
+            if p.grad is None:
+                raise RuntimeError("FlatAdam: a trained parameter received no gradient")
+            gs.append(_real(p.grad).reshape(-1))
+        torch._foreach_copy_(self._gviews, gs)
+        return self.grad
+
+    def step(self, grad_scale: float = 1.0, gather: bool = True):
+        if gather:
+            self.gather_grads()
+        self.t += 1
+        b1, b2 = self.betas
+        step_size = self.lr / (1.0 - b1 ** self.t)
+        bc2s = math.sqrt(1.0 - b2 ** self.t)
+        call("blindno_adam", ptr(self.flat), ptr(self.grad), ptr(self.m), ptr(self.v), self.n,
+             b1, b2, self.eps, step_size, bc2s, grad_scale, stream_ptr())
+
+    def state_dict(self):
+        return {"t": self.t, "m": self.m.clone(), "v": self.v.clone(), "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.t = int(sd["t"])
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.lr = float(sd["lr"])
+
+
+def trained_parameters(model: torch.nn.Module, exclude_prefixes=("branch.", "fc0.")):
+    """Parameters the reference actually trains for the FNO-NIO models (no gradient ever
+    reaches ``branch.*``; ``fc0`` is read through ``.data``)."""
+    return [p for n, p in model.named_parameters()
+            if p.requires_grad and not n.startswith(tuple(exclude_prefixes))]
+
+
+class StepLR:
+    """StepLR(step_size, gamma) stepped once per epoch.  ``world_steps`` reproduces the
+    accelerate quirk of stepping the scheduler once per process per call
+    (accelerate/scheduler.py:69-76)."""
+
+    def __init__(self, opt: FlatAdam, step_size=100, gamma=0.5, world_steps: int = 1):
+        self.opt, self.step_size, self.gamma = opt, step_size, gamma
+        self.base_lr = opt.lr
+        self.world_steps = max(1, int(world_steps))
+        self.count = 0
+
+    def step(self):
+        self.count += self.world_steps
+        self.opt.lr = self.base_lr * self.gamma ** (self.count // self.step_size)
+
+
+class DataParallel:
+    """Gradient averaging across ranks for a FlatAdam (one bucketed all-reduce of the
+    flat gradient; no other collective on the data path)."""
+
+    def __init__(self, opt: FlatAdam, group=None, bucket_bytes: int = 64 << 20):
+        self.opt = opt
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.bucket = max(1, bucket_bytes // 4)
+
+    def broadcast_parameters(self, src: int = 0):
+        if self.world > 1:
+            dist.broadcast(self.opt.flat, src, group=self.group)
+
+    def step(self):
+        g = self.opt.gather_grads()
+        if self.world > 1:
+            for off in range(0, g.numel(), self.bucket):
+                dist.all_reduce(g[off:off + self.bucket], group=self.group)
+        self.opt.step(grad_scale=1.0 / self.world, gather=False)
+
+
+def synthetic_bags(n_bags: int, T: int, grid_shape, out_ch: int, seed: int, device,
+                   chunk: int = 64):
+    """Standardised synthetic snapshot bags x ~ N(0,1) (n, T, *grid) and targets
+    (n, *grid, out_ch), generated on the device from a seeded generator (the real
+    datasets are not shipped with the reference)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = torch.empty(n_bags, T, *grid_shape, dtype=torch.float32, device=device)
+    y = torch.empty(n_bags, *grid_shape, out_ch, dtype=torch.float32, device=device)
+    for s in range(0, n_bags, chunk):
+        e = min(n_bags, s + chunk)
+        x[s:e].normal_(generator=g)
+        y[s:e].normal_(generator=g)
+    return x, y
+
+
+def grid2d(nx: int, ny: int, device):
+    """meshgrid(linspace(-1,1,nx), linspace(-1,1,ny), 'ij') stacked (2d_FPE/train_fno.py:109-114)."""
+    gx, gy = np.meshgrid(np.linspace(-1, 1, nx, dtype=np.float32),
+                         np.linspace(-1, 1, ny, dtype=np.float32), indexing="ij")
+    return torch.tensor(np.stack([gx, gy], axis=2), device=device)
+
+
+def grid1d(nx: int, device):
+    """linspace(0,1,nx)[:, None] (1d_FPE/train_fno.py:98)."""
+    return torch.linspace(0, 1, nx, device=device).unsqueeze(-1)

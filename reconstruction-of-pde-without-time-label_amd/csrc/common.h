@@ -9,24 +9,48 @@ namespace blindno {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ float gelu_f(float z) {
-  // exact-erf GELU (F.gelu default): 0.5 z (1 + erf(z / sqrt 2))
-  return 0.5f * z * (1.0f + erff(z * 0.70710678118654752f));
+// Standard normal CDF Phi(x) = 0.5 erfc(-x/sqrt2), branch-free: erfc(u) for u >= 0 from
+// the Chebyshev-fitted form erfc(u) = t exp(-u^2 + P(t)), t = 1/(1 + u/2), fractional
+// error < 1.2e-7 for all u >= 0 (Numerical Recipes "erfcc").  Exact-erf GELU semantics
+// (F.gelu default) within fp32 rounding, at ~1 rcp + 2 exp + 10 FMA.
+__device__ __forceinline__ float norm_cdf(float x) {
+  float u = fabsf(x) * 0.70710678118654752f;
+  float t = __builtin_amdgcn_rcpf(fmaf(0.5f, u, 1.0f));
+  float p = fmaf(t, 0.17087277f, -0.82215223f);
+  p = fmaf(t, p, 1.48851587f);
+  p = fmaf(t, p, -1.13520398f);
+  p = fmaf(t, p, 0.27886807f);
+  p = fmaf(t, p, -0.18628806f);
+  p = fmaf(t, p, 0.09678418f);
+  p = fmaf(t, p, 0.37409196f);
+  p = fmaf(t, p, 1.00002368f);
+  p = fmaf(t, p, -1.26551223f);
+  float half_erfc = 0.5f * t * __expf(fmaf(-u, u, p));
+  return x >= 0.f ? 1.0f - half_erfc : half_erfc;
 }
+
+__device__ __forceinline__ float gelu_f(float z) { return z * norm_cdf(z); }
 
 // GELU'(z) = Phi(z) + z phi(z)
 __device__ __forceinline__ float gelu_grad_f(float z) {
-  float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
   float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
-  return cdf + z * pdf;
+  return fmaf(z, pdf, norm_cdf(z));
 }
 
 __device__ __forceinline__ void gelu_both(float z, float& g, float& dg) {
-  float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
+  float cdf = norm_cdf(z);
   float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
   g = z * cdf;
-  dg = cdf + z * pdf;
+  dg = fmaf(z, pdf, cdf);
 }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Hermitian weight of a complex-to-real inverse of length n at bin k (< n/2+1):
 // bin 0 and the Nyquist bin (even n) count once, every other bin twice.

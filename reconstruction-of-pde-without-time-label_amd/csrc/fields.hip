@@ -1,15 +1,23 @@
-// Point-wise field kernels of the FNO body: lift (fc0 + pad), inverse row transform with
-// the fused 1x1-conv/bias epilogue, its backward, weight-gradient partial reductions,
-// the projection MLP (fc1 -> GELU -> fc2), the snapshot-bag mean, loss, metrics and Adam.
+// Field kernels of the FNO body: lift (fc0 + pad), inverse row transform with the fused
+// 1x1-conv / bias / GELU epilogue and its adjoint (with the fused 1x1-conv weight-gradient
+// reduction), weight-gradient partial reductions, the projection MLP (fc1 -> GELU -> fc2)
+// forward and backward, the snapshot-bag mean, loss, metrics and Adam.
 //
 // Reference: FNO2d.forward 2d_FPE/FNOModules.py:218-240, FNO1d.forward
 // 1d_FPE/FNOModules.py:99-122, NIOFP2D_FNO bag mean 2d_FPE/NIOModules.py:565-575,
 // train loop 2d_FPE/train_fno.py:116-146.
+//
+// Mapping rules: row kernels put one wave on one grid row (lanes = w,
+// NQ = ceil(P2/64) points per lane) and keep ALL channels of a point in registers, so the
+// 1x1 conv and GELU happen once per point; per-row spectral coefficients are wave-uniform
+// and come through scalar loads.
 #include "common.h"
 
 using namespace blindno;
 
 namespace {
+
+constexpr int kWaves = kBlock / 64;
 
 // ---------------------------------------------------------------- lift
 __global__ __launch_bounds__(kBlock) void lift_fwd_kernel(const float* __restrict__ in,
@@ -21,12 +29,12 @@ __global__ __launch_bounds__(kBlock) void lift_fwd_kernel(const float* __restric
   const int64_t total = (int64_t)Bn * C * P1 * P2;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int w = (int)(idx % P2);
+    const int w = (int)(idx % P2);
     int64_t t = idx / P2;
-    int h = (int)(t % P1);
+    const int h = (int)(t % P1);
     t /= P1;
-    int c = (int)(t % C);
-    int n = (int)(t / C);
+    const int c = (int)(t % C);
+    const int n = (int)(t / C);
     float v = 0.f;
     if (h < N1 && w < N2) {
       const float* ip = in + (((int64_t)n * N1 + h) * N2 + w) * Cin;
@@ -45,12 +53,12 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_kernel(const float* __rest
   const int64_t total = (int64_t)Bn * N1 * N2 * Cin;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int j = (int)(idx % Cin);
+    const int j = (int)(idx % Cin);
     int64_t t = idx / Cin;
-    int w = (int)(t % N2);
+    const int w = (int)(t % N2);
     t /= N2;
-    int h = (int)(t % N1);
-    int n = (int)(t / N1);
+    const int h = (int)(t % N1);
+    const int n = (int)(t / N1);
     float v = 0.f;
     for (int c = 0; c < C; ++c)
       v = fmaf(w0[c * Cin + j], dx0[(((int64_t)n * C + c) * P1 + h) * P2 + w], v);
@@ -58,186 +66,332 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_kernel(const float* __rest
   }
 }
 
-// partial[chunk][c*Cin + j] = sum dx0[n,c,h,w] in[n,h,w,j];  partial[chunk][C*Cin + c] = sum dx0
+// Tiled outer-product reductions: partial[block][a*Cb + b] = sum_p A[a][p] B[b][p] and
+// partial[block][Ca*Cb + a] = sum_p A[a][p] over the block's tile of TP points, staged in
+// LDS with coalesced loads (rows padded by one float: conflict-free column sweeps).
+constexpr int TP = 256;
+
+// lift: A = dx0 on the N1 x N2 domain (NCHW, padded strides), B = in (channels-last).
+// Workgroups sweep tiles grid-stride and keep their sums in registers (<= 4 parameters
+// per thread), so the partial count is the (bounded) grid size.
+constexpr int PPT = 4;
+
 __global__ __launch_bounds__(kBlock) void lift_bwd_w_kernel(const float* __restrict__ dx0,
                                                             const float* __restrict__ in,
-                                                            float* __restrict__ partial,
-                                                            int nchunk, int Bn, int N1, int N2,
-                                                            int Cin, int C, int P1, int P2) {
-  const int np = C * Cin + C;
+                                                            float* __restrict__ partial, int Bn,
+                                                            int N1, int N2, int Cin, int C,
+                                                            int P1, int P2) {
+  extern __shared__ float sm[];
+  float* sa = sm;                       // [C][TP+1]
+  float* sb = sa + C * (TP + 1);        // [Cin][TP+1]
   const int64_t npts = (int64_t)Bn * N1 * N2;
-  const int64_t per = (npts + nchunk - 1) / nchunk;
-  const int64_t total = (int64_t)nchunk * np;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int p = (int)(idx % np);
-    int chunk = (int)(idx / np);
-    int c, j;
-    if (p < C * Cin) {
-      c = p / Cin;
-      j = p % Cin;
-    } else {
-      c = p - C * Cin;
-      j = -1;
-    }
-    int64_t beg = chunk * per, end = beg + per < npts ? beg + per : npts;
-    float acc = 0.f;
-    for (int64_t q = beg; q < end; ++q) {
-      int w = (int)(q % N2);
-      int64_t t = q / N2;
-      int h = (int)(t % N1);
-      int n = (int)(t / N1);
-      float d = dx0[(((int64_t)n * C + c) * P1 + h) * P2 + w];
-      acc = j >= 0 ? fmaf(d, in[q * Cin + j], acc) : acc + d;
-    }
-    partial[idx] = acc;
-  }
-}
-
-// ---------------------------------------------------------------- inverse row transform + epilogue
-template <int ACT>
-__global__ __launch_bounds__(kBlock) void rowidft_epi_kernel(
-    const float2* __restrict__ Z, const float* __restrict__ x, const float* __restrict__ wc,
-    const float* __restrict__ bc, float* __restrict__ z, const float2* __restrict__ tw2, int Bn,
-    int C, int P1, int P2, int m2) {
-  extern __shared__ float2 s_tw[];
-  for (int i = threadIdx.x; i < P2; i += blockDim.x) s_tw[i] = tw2[i];
-  __syncthreads();
-  const int64_t HW = (int64_t)P1 * P2;
-  const int64_t total = (int64_t)Bn * C * HW;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int w = (int)(idx % P2);
-    int64_t t = idx / P2;
-    int h = (int)(t % P1);
-    t /= P1;
-    int o = (int)(t % C);
-    int n = (int)(t / C);
-    const float2* zc = Z + (((int64_t)n * C + o) * P1 + h) * m2;
-    float acc = 0.f;
-    int ph = 0;
-    for (int k = 0; k < m2; ++k) {
-      float2 a = zc[k];
-      float2 e = s_tw[ph];
-      acc = fmaf(a.x, e.x, fmaf(-a.y, e.y, acc));
-      ph += w;
-      if (ph >= P2) ph -= P2;
-    }
-    float cv = 0.f;
-    if (wc) {
-      cv = bc[o];
-      const float* xp = x + (int64_t)n * C * HW + (int64_t)h * P2 + w;
-      for (int i = 0; i < C; ++i) {
-        float v = xp[i * HW];
-        if (ACT) v = gelu_f(v);
-        cv = fmaf(wc[o * C + i], v, cv);
+  const int64_t ntiles = (npts + TP - 1) / TP;
+  const int t = threadIdx.x;
+  const int np = C * Cin + C;
+  float acc[PPT];
+#pragma unroll
+  for (int e = 0; e < PPT; ++e) acc[e] = 0.f;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t p0 = tile * TP;
+    {
+      const int64_t q = p0 + t;
+      const bool ok = q < npts;
+      int n = 0, h = 0, w = 0;
+      if (ok) {
+        w = (int)(q % N2);
+        const int64_t r = q / N2;
+        h = (int)(r % N1);
+        n = (int)(r / N1);
       }
+      for (int c = 0; c < C; ++c)
+        sa[c * (TP + 1) + t] = ok ? dx0[(((int64_t)n * C + c) * P1 + h) * P2 + w] : 0.f;
     }
-    z[idx] = acc + cv;
+    for (int e = t; e < TP * Cin; e += blockDim.x) {
+      const int p = e / Cin, j = e % Cin;
+      const int64_t q = p0 + p;
+      sb[j * (TP + 1) + p] = q < npts ? in[q * Cin + j] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < PPT; ++e) {
+      const int pr = t + e * kBlock;
+      if (pr >= np) continue;
+      float a2 = acc[e];
+      if (pr < C * Cin) {
+        const float* a = sa + (pr / Cin) * (TP + 1);
+        const float* b = sb + (pr % Cin) * (TP + 1);
+        for (int p = 0; p < TP; ++p) a2 = fmaf(a[p], b[p], a2);
+      } else {
+        const float* a = sa + (pr - C * Cin) * (TP + 1);
+        for (int p = 0; p < TP; ++p) a2 += a[p];
+      }
+      acc[e] = a2;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < PPT; ++e) {
+    const int pr = t + e * kBlock;
+    if (pr < np) partial[(int64_t)blockIdx.x * np + pr] = acc[e];
   }
 }
 
-template <int ACT>
-__global__ __launch_bounds__(kBlock) void rowidft_bwd_kernel(
-    const float2* __restrict__ G, const float* __restrict__ dz, const float* __restrict__ wc,
-    const float* __restrict__ xpre, float* __restrict__ dx, const float2* __restrict__ tw2,
-    int Bn, int C, int P1, int P2, int m2) {
-  extern __shared__ float2 s_tw[];
-  for (int i = threadIdx.x; i < P2; i += blockDim.x) s_tw[i] = tw2[i];
-  __syncthreads();
-  const int64_t HW = (int64_t)P1 * P2;
-  const int64_t total = (int64_t)Bn * C * HW;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int w = (int)(idx % P2);
-    int64_t t = idx / P2;
-    int h = (int)(t % P1);
-    t /= P1;
-    int i = (int)(t % C);
-    int n = (int)(t / C);
-    const float2* gc = G + (((int64_t)n * C + i) * P1 + h) * m2;
-    float acc = 0.f;
-    int ph = 0;
-    for (int k = 0; k < m2; ++k) {
-      float2 a = gc[k];
-      float2 e = s_tw[ph];
-      acc = fmaf(a.x, e.x, fmaf(-a.y, e.y, acc));
-      ph += w;
-      if (ph >= P2) ph -= P2;
-    }
-    if (wc) {
-      const float* dzp = dz + (int64_t)n * C * HW + (int64_t)h * P2 + w;
-      for (int o = 0; o < C; ++o) acc = fmaf(wc[o * C + i], dzp[o * HW], acc);
-    }
-    if (ACT) acc *= gelu_grad_f(xpre[idx]);
-    dx[idx] = acc;
-  }
-}
-
-// partial[chunk][o*C + i] = sum dz[n,o,p] f(x[n,i,p]);  partial[chunk][C*C + o] = sum dz[n,o,p]
+// conv: A = dz, B = f(x) (NCHW, HW points per sample); tiles never straddle samples
 template <int ACT>
 __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restrict__ dz,
                                                             const float* __restrict__ x,
-                                                            float* __restrict__ partial,
-                                                            int nchunk, int Bn, int C,
-                                                            int64_t HW) {
+                                                            float* __restrict__ partial, int C,
+                                                            int64_t HW, int tiles_per_n,
+                                                            int64_t ntiles) {
+  extern __shared__ float sm[];
+  float* sa = sm;
+  float* sb = sa + C * (TP + 1);
+  const int t = threadIdx.x;
   const int np = C * C + C;
-  const int64_t npts = (int64_t)Bn * HW;
-  const int64_t per = (npts + nchunk - 1) / nchunk;
-  const int64_t total = (int64_t)nchunk * np;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int p = (int)(idx % np);
-    int chunk = (int)(idx / np);
-    int o, i;
-    if (p < C * C) {
-      o = p / C;
-      i = p % C;
-    } else {
-      o = p - C * C;
-      i = -1;
-    }
-    int64_t beg = chunk * per, end = beg + per < npts ? beg + per : npts;
-    float acc = 0.f;
-    for (int64_t q = beg; q < end; ++q) {
-      int64_t n = q / HW, s = q % HW;
-      float d = dz[(n * C + o) * HW + s];
-      if (i >= 0) {
-        float v = x[(n * C + i) * HW + s];
-        if (ACT) v = gelu_f(v);
-        acc = fmaf(d, v, acc);
-      } else {
-        acc += d;
+  float acc[PPT];
+#pragma unroll
+  for (int e = 0; e < PPT; ++e) acc[e] = 0.f;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t n = tile / tiles_per_n;
+    const int64_t s0 = (tile % tiles_per_n) * TP;
+    const bool ok = s0 + t < HW;
+    for (int c = 0; c < C; ++c) {
+      const int64_t off = (n * C + c) * HW + s0 + t;
+      float a = 0.f, b = 0.f;
+      if (ok) {
+        a = dz[off];
+        b = x[off];
+        if (ACT) b = gelu_f(b);
       }
+      sa[c * (TP + 1) + t] = a;
+      sb[c * (TP + 1) + t] = b;
     }
-    partial[idx] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < PPT; ++e) {
+      const int pr = t + e * kBlock;
+      if (pr >= np) continue;
+      float a2 = acc[e];
+      if (pr < C * C) {
+        const float* a = sa + (pr / C) * (TP + 1);
+        const float* b = sb + (pr % C) * (TP + 1);
+        for (int p = 0; p < TP; ++p) a2 = fmaf(a[p], b[p], a2);
+      } else {
+        const float* a = sa + (pr - C * C) * (TP + 1);
+        for (int p = 0; p < TP; ++p) a2 += a[p];
+      }
+      acc[e] = a2;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < PPT; ++e) {
+    const int pr = t + e * kBlock;
+    if (pr < np) partial[(int64_t)blockIdx.x * np + pr] = acc[e];
   }
 }
 
-__global__ __launch_bounds__(kBlock) void reduce_partials_kernel(const float* __restrict__ partial,
-                                                                 float* __restrict__ out,
-                                                                 int nchunk, int np) {
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < np; p += gridDim.x * blockDim.x) {
-    float acc = 0.f;
-    for (int c = 0; c < nchunk; ++c) acc += partial[(int64_t)c * np + p];
-    out[p] = acc;
+// out[p] = sum_c partial[c][p]: 64 consecutive parameters per wave (coalesced), the 16
+// waves of a workgroup split the chunks, combined in fixed order (deterministic).
+constexpr int kRedWaves = 16;
+__global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __restrict__ partial,
+                                                               float* __restrict__ out,
+                                                               int nchunk, int np) {
+  __shared__ float red[kRedWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + lane;
+  float acc = 0.f;
+  if (p < np)
+    for (int c = wv; c < nchunk; c += kRedWaves) acc += partial[(int64_t)c * np + p];
+  red[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && p < np) {
+    float s = red[0][lane];
+    for (int w = 1; w < kRedWaves; ++w) s += red[w][lane];
+    out[p] = s;
+  }
+}
+
+// ---------------------------------------------------------------- inverse row transform
+// One wave per grid row (n, h); lane owns w = lane + 64 q (q < NQ) and all channels.
+//   acc[q][c] = sum_k Re(Z[n][h][k][c] e^{+2 pi i k w / P2})
+// The workgroup keeps the (m2 x P2) twiddle table T[k][w] in LDS (lane-contiguous reads) and
+// each wave stages its row's m2*C coefficients in LDS (broadcast reads).
+// MODE 0 (forward epilogue): z = acc + bc + Wc f(x)            (f = GELU if ACT)
+// MODE 1 (adjoint):          dx = (acc + Wc^T dz) * (ACT ? GELU'(xsrc) : 1)
+//                            and, with WG, per-lane sums of dz (x) f(xsrc) for dWc / dbc.
+template <int CM, int NQ, int MODE, int ACT, int WG>
+__global__ __launch_bounds__(kBlock) void rowinv_kernel(
+    const float2* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
+    const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
+    const float2* __restrict__ twk, float* __restrict__ partial, int Bn, int C, int P1, int P2,
+    int m2) {
+  extern __shared__ float2 sm2[];
+  float2* T = sm2;                                  // [m2][P2]
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int mc = m2 * C;
+  float2* zrow = T + m2 * P2 + wave * mc;           // [m2][C] of the wave's current row
+  for (int e = threadIdx.x; e < m2 * P2; e += blockDim.x) {
+    const int k = e / P2, w = e % P2;
+    T[e] = twk[(int64_t)w * m2 + k];
+  }
+  __syncthreads();
+  constexpr int NW = WG ? CM * CM + CM : 1;
+  const int nrows = Bn * P1;
+  const int64_t HW = (int64_t)P1 * P2;
+  float wacc[NW];
+#pragma unroll
+  for (int e = 0; e < NW; ++e) wacc[e] = 0.f;
+  const bool has_wc = wc != nullptr;
+  for (int row = blockIdx.x * kWaves + wave; row < nrows; row += gridDim.x * kWaves) {
+    const int n = row / P1, h = row % P1;
+    const float2* zr = Z + (int64_t)row * mc;
+    for (int e = lane; e < mc; e += 64) zrow[e] = zr[e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float acc[NQ][CM];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int c = 0; c < CM; ++c) acc[q][c] = 0.f;
+    for (int k = 0; k < m2; ++k) {
+      float2 zc[CM];
+#pragma unroll
+      for (int c = 0; c < CM; ++c) zc[c] = c < C ? zrow[k * C + c] : make_float2(0.f, 0.f);
+      const float2* Tk = T + k * P2;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int w = lane + 64 * q;
+        const float2 e = Tk[w < P2 ? w : 0];
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          acc[q][c] = fmaf(zc[c].x, e.x, fmaf(-zc[c].y, e.y, acc[q][c]));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int w = lane + 64 * q;
+      if (w >= P2) continue;
+      const int64_t base = (int64_t)n * C * HW + (int64_t)h * P2 + w;
+      if (MODE == 0) {
+        if (has_wc) {
+          float xv[CM];
+#pragma unroll
+          for (int i = 0; i < CM; ++i) {
+            float v = i < C ? xs[base + i * HW] : 0.f;
+            if (ACT) v = gelu_f(v);
+            xv[i] = v;
+          }
+#pragma unroll
+          for (int o = 0; o < CM; ++o) {
+            if (o >= C) continue;
+            float v = acc[q][o] + bc[o];
+#pragma unroll
+            for (int i = 0; i < CM; ++i)
+              if (i < C) v = fmaf(wc[o * C + i], xv[i], v);
+            out[base + o * HW] = v;
+          }
+        } else {
+#pragma unroll
+          for (int o = 0; o < CM; ++o)
+            if (o < C) out[base + o * HW] = acc[q][o];
+        }
+      } else {
+        if (has_wc) {
+          float dv[CM], xv[CM], g[CM];
+#pragma unroll
+          for (int o = 0; o < CM; ++o) dv[o] = o < C ? dz[base + o * HW] : 0.f;
+#pragma unroll
+          for (int i = 0; i < CM; ++i) {
+            g[i] = acc[q][i];
+#pragma unroll
+            for (int o = 0; o < CM; ++o) g[i] = fmaf(o < C ? wc[o * C + i] : 0.f, dv[o], g[i]);
+            xv[i] = ((WG || ACT) && i < C) ? xs[base + i * HW] : 0.f;
+            if (ACT) {
+              float a, dg;
+              gelu_both(xv[i], a, dg);
+              g[i] *= dg;
+              xv[i] = a;
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < CM; ++i)
+            if (i < C) out[base + i * HW] = g[i];
+          if constexpr (WG != 0) {
+#pragma unroll
+            for (int o = 0; o < CM; ++o) {
+#pragma unroll
+              for (int i = 0; i < CM; ++i) wacc[o * CM + i] = fmaf(dv[o], xv[i], wacc[o * CM + i]);
+              wacc[CM * CM + o] += dv[o];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < CM; ++i)
+            if (i < C) out[base + i * HW] = acc[q][i];
+        }
+      }
+    }
+  }
+  if (WG) {
+    // block reduction of the per-lane conv-weight partials -> partial[blockIdx.x][C*C + C]
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(sm2);   // reuse LDS (sized by the launcher)
+    const int np = C * C + C;
+#pragma unroll
+    for (int e = 0; e < NW; ++e) {
+      const int o = e < CM * CM ? e / CM : e - CM * CM;
+      const int i = e < CM * CM ? e % CM : -1;
+      if (o >= C || i >= C) continue;
+      const float s = wave_sum(wacc[e]);
+      const int pidx = i >= 0 ? o * C + i : C * C + o;
+      if (lane == 0) red[wave * np + pidx] = s;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+      float s = 0.f;
+      for (int w = 0; w < kWaves; ++w) s += red[w * np + p];
+      partial[(int64_t)blockIdx.x * np + p] = s;
+    }
   }
 }
 
 // ---------------------------------------------------------------- projection MLP
+// Forward: one lane per crop point, all hidden units looped; the MLP weights are staged in
+// LDS once per workgroup and read as wave-wide broadcasts.
 template <int CM, int COM>
 __global__ __launch_bounds__(kBlock) void project_fwd_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ out, int Bn,
     int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout, int ostride, int ooff) {
+  extern __shared__ float smp[];
+  float* sw1 = smp;                 // [Hd][CM] (zero padded)
+  float* sb1 = sw1 + Hd * CM;       // [Hd]
+  float* sw2 = sb1 + Hd;            // [Hd][COM]
+  for (int e = threadIdx.x; e < Hd * CM; e += blockDim.x) {
+    const int j = e / CM, i = e % CM;
+    sw1[e] = i < C ? w1[j * C + i] : 0.f;
+  }
+  for (int e = threadIdx.x; e < Hd; e += blockDim.x) sb1[e] = b1[e];
+  for (int e = threadIdx.x; e < Hd * COM; e += blockDim.x) {
+    const int j = e / COM, c = e % COM;
+    sw2[e] = c < Cout ? w2[c * Hd + j] : 0.f;
+  }
+  __syncthreads();
   const int64_t HW = (int64_t)P1 * P2;
   const int64_t total = (int64_t)Bn * Ho * Wo;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int w = (int)(idx % Wo);
-    int64_t t = idx / Wo;
-    int h = (int)(t % Ho);
-    int n = (int)(t / Ho);
+    const int w = (int)(idx % Wo);
+    const int64_t t = idx / Wo;
+    const int h = (int)(t % Ho);
+    const int n = (int)(t / Ho);
     float zi[CM];
     const float* zp = z + (int64_t)n * C * HW + (int64_t)h * P2 + w;
 #pragma unroll
@@ -246,14 +400,12 @@ __global__ __launch_bounds__(kBlock) void project_fwd_kernel(
 #pragma unroll
     for (int c = 0; c < COM; ++c) acc[c] = c < Cout ? b2[c] : 0.f;
     for (int j = 0; j < Hd; ++j) {
-      float hv = b1[j];
+      float hv = sb1[j];
 #pragma unroll
-      for (int i = 0; i < CM; ++i)
-        if (i < C) hv = fmaf(w1[j * C + i], zi[i], hv);
-      float a = gelu_f(hv);
+      for (int i = 0; i < CM; ++i) hv = fmaf(sw1[j * CM + i], zi[i], hv);
+      const float a = gelu_f(hv);
 #pragma unroll
-      for (int c = 0; c < COM; ++c)
-        if (c < Cout) acc[c] = fmaf(w2[c * Hd + j], a, acc[c]);
+      for (int c = 0; c < COM; ++c) acc[c] = fmaf(sw2[j * COM + c], a, acc[c]);
     }
     float* op = out + idx * ostride + ooff;
 #pragma unroll
@@ -262,129 +414,297 @@ __global__ __launch_bounds__(kBlock) void project_fwd_kernel(
   }
 }
 
-template <int CM, int COM>
-__global__ __launch_bounds__(kBlock) void project_bwd_dz_kernel(
+// Backward for narrow fields (C <= 4): lanes = crop points (64-point tiles, coalesced), the
+// 16 waves of a 1024-thread workgroup split the hidden units (JW = Hd/16 each), so every lane
+// keeps its wave's weight gradients in registers for the whole kernel; dz of a tile is summed
+// over the waves through LDS.  The next tile's z / dout are prefetched into registers while
+// the current tile computes (double-buffered LDS).  One workgroup partial per parameter.
+template <int CM, int JW, int COM>
+__global__ __launch_bounds__(1024) void project_bwd_split_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
-    const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz, int Bn,
-    int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout, int ostride, int ooff,
-    int dout_div) {
+    const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
+    float* __restrict__ partial, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd,
+    int Cout, int ostride, int ooff, int dout_div) {
+  constexpr int NWV = 16;
+  __shared__ float sz[2][CM][64], sg[2][COM][64], red[NWV][CM][64];
+  __shared__ float sw1[NWV * JW][CM], sb1[NWV * JW], sw2[NWV * JW][COM];
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int j0 = wave * JW;
+  for (int e = threadIdx.x; e < Hd * CM; e += blockDim.x) {
+    const int j = e / CM, i = e % CM;
+    sw1[j][i] = i < C ? w1[j * C + i] : 0.f;
+  }
+  for (int e = threadIdx.x; e < Hd; e += blockDim.x) sb1[e] = b1[e];
+  for (int e = threadIdx.x; e < Hd * COM; e += blockDim.x) {
+    const int j = e / COM, c = e % COM;
+    sw2[j][c] = c < Cout ? w2[c * Hd + j] : 0.f;
+  }
+  float gW1[JW][CM], gb1[JW], gW2[JW][COM], gb2[COM];
+#pragma unroll
+  for (int q = 0; q < JW; ++q) {
+    gb1[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < CM; ++i) gW1[q][i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < COM; ++c) gW2[q][c] = 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
   const int64_t HW = (int64_t)P1 * P2;
-  const int64_t total = (int64_t)Bn * Ho * Wo;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int w = (int)(idx % Wo);
-    int64_t t = idx / Wo;
-    int h = (int)(t % Ho);
-    int n = (int)(t / Ho);
-    float zi[CM], gz[CM], go[COM];
-    const float* zp = z + (int64_t)n * C * HW + (int64_t)h * P2 + w;
+  const int64_t npts = (int64_t)Bn * Ho * Wo;
+  const int64_t ntiles = (npts + 63) / 64;
+
+  // loader role: waves [0, CM) fetch one z channel, waves [CM, CM+COM) one dout channel
+  auto fetch = [&](int64_t tile) -> float {
+    const int64_t p = tile * 64 + lane;
+    if (tile >= ntiles || p >= npts || wave >= CM + COM) return 0.f;
+    const int w = (int)(p % Wo);
+    const int64_t r = p / Wo;
+    const int h = (int)(r % Ho);
+    const int n = (int)(r / Ho);
+    if (wave < CM) return wave < C ? z[(int64_t)n * C * HW + wave * HW + (int64_t)h * P2 + w] : 0.f;
+    const int c = wave - CM;
+    return c < Cout ? dout[((((int64_t)(n / dout_div)) * Ho + h) * Wo + w) * ostride + ooff + c] : 0.f;
+  };
+  auto stash = [&](int buf, float v) {
+    if (wave < CM) sz[buf][wave][lane] = v;
+    else if (wave < CM + COM) sg[buf][wave - CM][lane] = v;
+  };
+  int64_t tile = blockIdx.x;
+  stash(0, fetch(tile));
+  int buf = 0;
+  for (; tile < ntiles; tile += gridDim.x, buf ^= 1) {
+    __syncthreads();
+    const float pre = fetch(tile + gridDim.x);
+    float zi[CM], gv[COM], dzp[CM];
 #pragma unroll
     for (int i = 0; i < CM; ++i) {
-      zi[i] = i < C ? zp[i * HW] : 0.f;
-      gz[i] = 0.f;
+      zi[i] = sz[buf][i][lane];
+      dzp[i] = 0.f;
     }
-    const float* dp = dout + ((((int64_t)(n / dout_div)) * Ho + h) * Wo + w) * ostride + ooff;
 #pragma unroll
-    for (int c = 0; c < COM; ++c) go[c] = c < Cout ? dp[c] : 0.f;
-    for (int j = 0; j < Hd; ++j) {
-      float hv = b1[j];
+    for (int c = 0; c < COM; ++c) gv[c] = sg[buf][c][lane];
 #pragma unroll
-      for (int i = 0; i < CM; ++i)
-        if (i < C) hv = fmaf(w1[j * C + i], zi[i], hv);
+    for (int q = 0; q < JW; ++q) {
+      const int j = j0 + q;
+      float hv = sb1[j];
+#pragma unroll
+      for (int i = 0; i < CM; ++i) hv = fmaf(sw1[j][i], zi[i], hv);
+      float a, dg;
+      gelu_both(hv, a, dg);
       float da = 0.f;
 #pragma unroll
-      for (int c = 0; c < COM; ++c)
-        if (c < Cout) da = fmaf(w2[c * Hd + j], go[c], da);
-      float dh = da * gelu_grad_f(hv);
+      for (int c = 0; c < COM; ++c) da = fmaf(sw2[j][c], gv[c], da);
+      const float dh = da * dg;
 #pragma unroll
-      for (int i = 0; i < CM; ++i)
-        if (i < C) gz[i] = fmaf(w1[j * C + i], dh, gz[i]);
+      for (int i = 0; i < CM; ++i) {
+        dzp[i] = fmaf(sw1[j][i], dh, dzp[i]);
+        gW1[q][i] = fmaf(dh, zi[i], gW1[q][i]);
+      }
+      gb1[q] += dh;
+#pragma unroll
+      for (int c = 0; c < COM; ++c) gW2[q][c] = fmaf(gv[c], a, gW2[q][c]);
     }
-    float* dzp = dz + (int64_t)n * C * HW + (int64_t)h * P2 + w;
+    if (wave == 0) {
 #pragma unroll
-    for (int i = 0; i < CM; ++i)
-      if (i < C) dzp[i * HW] = gz[i];
+      for (int c = 0; c < COM; ++c) gb2[c] += gv[c];
+    }
+#pragma unroll
+    for (int i = 0; i < CM; ++i) red[wave][i][lane] = dzp[i];
+    stash(buf ^ 1, pre);
+    __syncthreads();
+    if (wave < C) {
+      const int64_t p = tile * 64 + lane;
+      if (p < npts) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < NWV; ++wv) s2 += red[wv][wave][lane];
+        const int w = (int)(p % Wo);
+        const int64_t r = p / Wo;
+        const int h = (int)(r % Ho);
+        const int n = (int)(r / Ho);
+        dz[(int64_t)n * C * HW + wave * HW + (int64_t)h * P2 + w] = s2;
+      }
+    }
+  }
+  // per-wave lane sums -> this workgroup's partial (each wave owns its hidden units)
+  const int np = Hd * C + Hd + Cout * Hd + Cout;
+  float* pp = partial + (int64_t)blockIdx.x * np;
+#pragma unroll
+  for (int q = 0; q < JW; ++q) {
+    const int j = j0 + q;
+#pragma unroll
+    for (int i = 0; i < CM; ++i) {
+      if (i >= C) continue;
+      const float s2 = wave_sum(gW1[q][i]);
+      if (lane == 0) pp[j * C + i] = s2;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const float sb = wave_sum(gb1[q]);
+    if (lane == 0) pp[Hd * C + j] = sb;
+#pragma unroll
+    for (int c = 0; c < COM; ++c) {
+      if (c >= Cout) continue;
+      const float s2 = wave_sum(gW2[q][c]);
+      if (lane == 0) pp[Hd * C + Hd + c * Hd + j] = s2;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int c = 0; c < COM; ++c) {
+      if (c >= Cout) continue;
+      const float s2 = wave_sum(gb2[c]);
+      if (lane == 0) pp[Hd * C + Hd + Cout * Hd + c] = s2;
+    }
   }
 }
 
-// partial[chunk][...] = [dW1 (Hd*C) | db1 (Hd) | dW2 (Cout*Hd) | db2 (Cout)]
-// One thread per (chunk, hidden unit j); thread j == 0 also accumulates db2.
-template <int CM, int COM>
-__global__ __launch_bounds__(kBlock) void project_bwd_w_kernel(
+// Backward: lanes = hidden units (j = lane + 64 q), one batch of PB consecutive crop points
+// (wave-uniform, their z / dout in scalar registers) at a time.  Weight gradients accumulate
+// in each lane's registers for the whole kernel; dz of the batch is a sum over hidden units
+// = over lanes, done by a transpose through the wave's LDS slice.
+template <int CM, int JPL, int PB, int COM>
+__global__ __launch_bounds__(kBlock) void project_bwd_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
-    const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ partial,
-    int nchunk, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout, int ostride,
-    int ooff, int dout_div) {
-  const int np = Hd * C + Hd + Cout * Hd + Cout;
+    const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
+    float* __restrict__ partial, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout,
+    int ostride, int ooff, int dout_div) {
+  extern __shared__ float sm[];
+  constexpr int NCOL = PB * CM;
+  constexpr int LD = NCOL + 1;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  float* red = sm + wave * 64 * LD;
   const int64_t HW = (int64_t)P1 * P2;
-  const int64_t npts = (int64_t)Bn * Ho * Wo;
-  const int64_t per = (npts + nchunk - 1) / nchunk;
-  const int64_t total = (int64_t)nchunk * Hd;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int j = (int)(idx % Hd);
-    int chunk = (int)(idx / Hd);
-    float wj[CM], gw1[CM], gw2[COM], gb2[COM];
+
+  float w1r[JPL][CM], b1r[JPL], w2r[JPL][COM];
+  float gW1[JPL][CM], gb1[JPL], gW2[JPL][COM], gb2[COM];
+#pragma unroll
+  for (int q = 0; q < JPL; ++q) {
+    const int j = lane + 64 * q;
+    b1r[q] = b1[j];
+    gb1[q] = 0.f;
 #pragma unroll
     for (int i = 0; i < CM; ++i) {
-      wj[i] = i < C ? w1[j * C + i] : 0.f;
-      gw1[i] = 0.f;
+      w1r[q][i] = i < C ? w1[j * C + i] : 0.f;
+      gW1[q][i] = 0.f;
     }
-    float w2j[COM];
 #pragma unroll
     for (int c = 0; c < COM; ++c) {
-      w2j[c] = c < Cout ? w2[c * Hd + j] : 0.f;
-      gw2[c] = 0.f;
-      gb2[c] = 0.f;
+      w2r[q][c] = c < Cout ? w2[c * Hd + j] : 0.f;
+      gW2[q][c] = 0.f;
     }
-    float gb1 = 0.f, bj = b1[j];
-    int64_t beg = chunk * per, end = beg + per < npts ? beg + per : npts;
-    for (int64_t q = beg; q < end; ++q) {
-      int w = (int)(q % Wo);
-      int64_t t = q / Wo;
-      int h = (int)(t % Ho);
-      int n = (int)(t / Ho);
-      const float* zp = z + (int64_t)n * C * HW + (int64_t)h * P2 + w;
-      float zi[CM];
-      float hv = bj;
+  }
 #pragma unroll
-      for (int i = 0; i < CM; ++i) {
-        zi[i] = i < C ? zp[i * HW] : 0.f;
-        hv = fmaf(wj[i], zi[i], hv);
-      }
-      const float* dp = dout + ((((int64_t)(n / dout_div)) * Ho + h) * Wo + w) * ostride + ooff;
-      float go[COM];
-      float da = 0.f;
+  for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
+
+  const int nbr = (Wo + PB - 1) / PB;
+  const int64_t NB = (int64_t)Bn * Ho * nbr;
+  for (int64_t b = (int64_t)blockIdx.x * kWaves + wave; b < NB; b += (int64_t)gridDim.x * kWaves) {
+    const int n = (int)(b / ((int64_t)Ho * nbr));
+    const int rem = (int)(b % ((int64_t)Ho * nbr));
+    const int h = rem / nbr;
+    const int w0 = (rem % nbr) * PB;
+    float zv[PB][CM], gv[PB][COM];
+    const float* zp = z + (int64_t)n * C * HW + (int64_t)h * P2 + w0;
+    const float* dp = dout + ((((int64_t)(n / dout_div)) * Ho + h) * Wo + w0) * ostride + ooff;
 #pragma unroll
-      for (int c = 0; c < COM; ++c) {
-        go[c] = c < Cout ? dp[c] : 0.f;
-        da = fmaf(w2j[c], go[c], da);
-      }
-      float a, g;
-      gelu_both(hv, a, g);
-      float dh = da * g;
+    for (int p = 0; p < PB; ++p) {
+      const bool ok = w0 + p < Wo;
 #pragma unroll
-      for (int i = 0; i < CM; ++i) gw1[i] = fmaf(dh, zi[i], gw1[i]);
-      gb1 += dh;
+      for (int i = 0; i < CM; ++i) zv[p][i] = (ok && i < C) ? zp[i * HW + p] : 0.f;
 #pragma unroll
-      for (int c = 0; c < COM; ++c) {
-        gw2[c] = fmaf(go[c], a, gw2[c]);
-        gb2[c] += go[c];
+      for (int c = 0; c < COM; ++c) gv[p][c] = (ok && c < Cout) ? dp[p * ostride + c] : 0.f;
+    }
+    float dzp[PB][CM];
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+#pragma unroll
+      for (int i = 0; i < CM; ++i) dzp[p][i] = 0.f;
+#pragma unroll
+    for (int q = 0; q < JPL; ++q) {
+#pragma unroll
+      for (int p = 0; p < PB; ++p) {
+        float hv = b1r[q];
+#pragma unroll
+        for (int i = 0; i < CM; ++i) hv = fmaf(w1r[q][i], zv[p][i], hv);
+        float a, dg;
+        gelu_both(hv, a, dg);
+        float da = 0.f;
+#pragma unroll
+        for (int c = 0; c < COM; ++c) da = fmaf(w2r[q][c], gv[p][c], da);
+        const float dh = da * dg;
+#pragma unroll
+        for (int i = 0; i < CM; ++i) {
+          dzp[p][i] = fmaf(w1r[q][i], dh, dzp[p][i]);
+          gW1[q][i] = fmaf(dh, zv[p][i], gW1[q][i]);
+        }
+        gb1[q] += dh;
+#pragma unroll
+        for (int c = 0; c < COM; ++c) gW2[q][c] = fmaf(gv[p][c], a, gW2[q][c]);
       }
     }
-    float* pp = partial + (int64_t)chunk * np;
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+#pragma unroll
+      for (int c = 0; c < COM; ++c) gb2[c] += gv[p][c];
+    // dz for the batch: column sums of the 64 x NCOL lane partials
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+#pragma unroll
+      for (int i = 0; i < CM; ++i) red[lane * LD + p * CM + i] = dzp[p][i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (NCOL <= 32) {
+      const int col = lane & 31, half = lane >> 5;
+      float s = 0.f;
+      if (col < NCOL)
+        for (int r = half * 32; r < half * 32 + 32; ++r) s += red[r * LD + col];
+      s += __shfl_xor(s, 32, 64);
+      if (half == 0 && col < NCOL) {
+        const int p = col / CM, i = col % CM;
+        if (i < C && w0 + p < Wo) dz[(int64_t)n * C * HW + i * HW + (int64_t)h * P2 + w0 + p] = s;
+      }
+    } else {
+      for (int col = lane; col < NCOL; col += 64) {
+        float s = 0.f;
+        for (int r = 0; r < 64; ++r) s += red[r * LD + col];
+        const int p = col / CM, i = col % CM;
+        if (i < C && w0 + p < Wo) dz[(int64_t)n * C * HW + i * HW + (int64_t)h * P2 + w0 + p] = s;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // block reduction of the per-lane weight-gradient registers
+  __syncthreads();
+  const int np = Hd * C + Hd + Cout * Hd + Cout;
+  float* slot = sm + wave * np;
+#pragma unroll
+  for (int q = 0; q < JPL; ++q) {
+    const int j = lane + 64 * q;
 #pragma unroll
     for (int i = 0; i < CM; ++i)
-      if (i < C) pp[j * C + i] = gw1[i];
-    pp[Hd * C + j] = gb1;
+      if (i < C) slot[j * C + i] = gW1[q][i];
+    slot[Hd * C + j] = gb1[q];
 #pragma unroll
     for (int c = 0; c < COM; ++c)
-      if (c < Cout) pp[Hd * C + Hd + c * Hd + j] = gw2[c];
-    if (j == 0) {
+      if (c < Cout) slot[Hd * C + Hd + c * Hd + j] = gW2[q][c];
+  }
+  if (lane == 0) {
 #pragma unroll
-      for (int c = 0; c < COM; ++c)
-        if (c < Cout) pp[Hd * C + Hd + Cout * Hd + c] = gb2[c];
-    }
+    for (int c = 0; c < COM; ++c)
+      if (c < Cout) slot[Hd * C + Hd + Cout * Hd + c] = gb2[c];
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    float s = 0.f;
+    for (int w = 0; w < kWaves; ++w) s += sm[w * np + p];
+    partial[(int64_t)blockIdx.x * np + p] = s;
   }
 }
 
@@ -396,17 +716,17 @@ __global__ __launch_bounds__(kBlock) void bagmean_fwd_kernel(const float* __rest
                                                              float* __restrict__ y, int B, int L,
                                                              int S, int d, int width) {
   const int64_t total = (int64_t)B * S;
+  const float invL = 1.0f / (float)L;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int s = (int)(idx % S);
-    int b = (int)(idx / S);
+    const int s = (int)(idx % S);
+    const int b = (int)(idx / S);
     float sum = 0.f;
     for (int l = 0; l < L; ++l) sum += u[((int64_t)b * L + l) * S + s];
     for (int c = 0; c < width; ++c) {
       float v = bias[c];
       for (int e = 0; e < d; ++e) v = fmaf(w[c * (d + 1) + e], grid[(int64_t)s * d + e], v);
-      float wl = w[c * (d + 1) + d] / (float)L;
-      v = fmaf(wl, sum, v);
+      v = fmaf(w[c * (d + 1) + d] * invL, sum, v);
       y[idx * width + c] = v;
     }
   }
@@ -417,10 +737,11 @@ __global__ __launch_bounds__(kBlock) void bagmean_bwd_kernel(const float* __rest
                                                              float* __restrict__ s, int B, int S,
                                                              int d, int width, int L) {
   const int64_t total = (int64_t)B * S;
+  const float invL = 1.0f / (float)L;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     float v = 0.f;
-    for (int c = 0; c < width; ++c) v = fmaf(w[c * (d + 1) + d] / (float)L, dy[idx * width + c], v);
+    for (int c = 0; c < width; ++c) v = fmaf(w[c * (d + 1) + d] * invL, dy[idx * width + c], v);
     s[idx] = v;
   }
 }
@@ -436,7 +757,7 @@ __global__ __launch_bounds__(kBlock) void mse_kernel(const float* __restrict__ p
   const float gs = grad ? (gscale ? gscale[0] : 1.0f) * 2.0f / (float)n : 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    float d = p[i] - t[i];
+    const float d = p[i] - t[i];
     acc = fmaf(d, d, acc);
     if (grad) grad[i] = gs * d;
   }
@@ -449,23 +770,23 @@ __global__ __launch_bounds__(kBlock) void mse_kernel(const float* __restrict__ p
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-// Row r of a/b holds n points with `stride` floats each; a point's value is at offset
-// off_a / off_b.  den_all = 1 takes the denominator over all `stride` channels of b
-// (the train-loop quirk of 2d_FPE/train_fno.py:161,163).
+// Row r holds n points of `stride` floats: out[2r] = sum (a[.+off_a] - b[.+off_b])^2,
+// out[2r+1] = sum b[.+off_b]^2 or, with den_all, over all `stride` channels of b (the train
+// loop's denominator quirk, 2d_FPE/train_fno.py:161,163).  fp64 accumulation.
 __global__ __launch_bounds__(kBlock) void rowsq_kernel(const float* __restrict__ a,
                                                        const float* __restrict__ b,
                                                        double* __restrict__ out, int rows, int n,
                                                        int stride, int off_a, int off_b,
                                                        int den_all) {
   __shared__ double ra[kBlock], rb[kBlock];
-  int r = blockIdx.x;
+  const int r = blockIdx.x;
   if (r >= rows) return;
   double sa = 0.0, sb = 0.0;
   const float* ap = a + (int64_t)r * n * stride;
   const float* bp = b + (int64_t)r * n * stride;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const float* bq = bp + (int64_t)i * stride;
-    double d = (double)ap[(int64_t)i * stride + off_a] - (double)bq[off_b];
+    const double d = (double)ap[(int64_t)i * stride + off_a] - (double)bq[off_b];
     sa += d * d;
     if (den_all) {
       for (int e = 0; e < stride; ++e) sb += (double)bq[e] * (double)bq[e];
@@ -497,29 +818,88 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ p,
                                                       float gscale) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    float gi = g[i] * gscale;
-    float mi = fmaf(1.0f - beta1, gi - m[i], m[i]);   // exp_avg.lerp_(grad, 1-beta1)
-    float vi = fmaf((1.0f - beta2) * gi, gi, v[i] * beta2);
+    const float gi = g[i] * gscale;
+    const float mi = fmaf(1.0f - beta1, gi - m[i], m[i]);   // exp_avg.lerp_(grad, 1-beta1)
+    const float vi = fmaf((1.0f - beta2) * gi, gi, v[i] * beta2);
     m[i] = mi;
     v[i] = vi;
-    float denom = sqrtf(vi) / bc2s + eps;
+    const float denom = sqrtf(vi) / bc2s + eps;
     p[i] = p[i] - step_size * (mi / denom);
   }
+}
+
+int rowinv_blocks(int Bn, int P1) {
+  const int64_t rows = (int64_t)Bn * P1;
+  const int64_t b = (rows + kWaves - 1) / kWaves;
+  return (int)(b < 2048 ? b : 2048);
+}
+
+template <int MODE, int ACT, int WG>
+int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
+                  const float* bc, float* out, const float* tw, float* partial, int nblocks,
+                  int Bn, int C, int P1, int P2, int m2, hipStream_t st) {
+  const int nq = (P2 + 63) / 64;
+  const int cm = C <= 4 ? 4 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
+  if (C > 32 || nq > 5) return (int)hipErrorInvalidValue;
+  if (WG && cm > 8) return (int)hipErrorInvalidValue;
+  size_t sh = sizeof(float2) * ((size_t)m2 * P2 + (size_t)kWaves * m2 * C);
+  if (WG) {
+    const size_t need = sizeof(float) * (size_t)kWaves * (C * C + C);
+    if (need > sh) sh = need;
+  }
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+  const dim3 g(nblocks), b(kBlock);
+  const float2* z2 = (const float2*)Z;
+  const float2* t2 = (const float2*)tw;
+#define RI(CM_, NQ_)                                                                        \
+  rowinv_kernel<CM_, NQ_, MODE, ACT, WG><<<g, b, sh, st>>>(z2, xs, dz, wc, bc, out, t2,      \
+                                                           partial, Bn, C, P1, P2, m2)
+#define RI_NQ(CM_)             \
+  switch (nq) {                \
+    case 1: RI(CM_, 1); break; \
+    case 2: RI(CM_, 2); break; \
+    case 3: RI(CM_, 3); break; \
+    case 4: RI(CM_, 4); break; \
+    default: RI(CM_, 5); break; \
+  }
+  if (cm == 4) {
+    RI_NQ(4)
+  } else if (cm == 8) {
+    RI_NQ(8)
+  } else if constexpr (!WG) {
+    if (cm == 16) {
+      RI_NQ(16)
+    } else {
+      RI_NQ(32)
+    }
+  }
+#undef RI_NQ
+#undef RI
+  return (int)hipGetLastError();
 }
 
 }  // namespace
 
 // ------------------------------------------------------------------------------ C ABI
-BLINDNO_API int blindno_abi_version(void) { return 1; }
+BLINDNO_API int blindno_abi_version(void) { return 2; }
+
+BLINDNO_API const char* blindno_error_string(int code) {
+  return hipGetErrorString((hipError_t)code);
+}
 
 BLINDNO_API int blindno_lift_fwd(const float* in, const float* w0, const float* b0, float* x0,
                                  int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
                                  void* stream) {
   if (N1 > P1 || N2 > P2) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)Bn * C * P1 * P2;
+  const int64_t total = (int64_t)Bn * C * P1 * P2;
   lift_fwd_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, (hipStream_t)stream>>>(
       in, w0, b0, x0, Bn, N1, N2, Cin, C, P1, P2);
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_lift_bwd_nchunk(int Bn, int N1, int N2) {
+  const int nt = cdiv((int64_t)Bn * N1 * N2, TP);
+  return nt < 1024 ? nt : 1024;
 }
 
 BLINDNO_API int blindno_lift_bwd(const float* dx0, const float* in, const float* w0,
@@ -527,100 +907,104 @@ BLINDNO_API int blindno_lift_bwd(const float* dx0, const float* in, const float*
                                  int N2, int Cin, int C, int P1, int P2, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (d_in) {
-    int64_t total = (int64_t)Bn * N1 * N2 * Cin;
+    const int64_t total = (int64_t)Bn * N1 * N2 * Cin;
     lift_bwd_in_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(dx0, w0, d_in, Bn, N1,
                                                                           N2, Cin, C, P1, P2);
   }
   if (partial) {
-    int64_t total = (int64_t)nchunk * (C * Cin + C);
-    lift_bwd_w_kernel<<<grid_for(total), kBlock, 0, st>>>(dx0, in, partial, nchunk, Bn, N1, N2,
-                                                          Cin, C, P1, P2);
+    if (nchunk != blindno_lift_bwd_nchunk(Bn, N1, N2) || C * Cin + C > PPT * kBlock)
+      return (int)hipErrorInvalidValue;
+    const size_t sh = sizeof(float) * (size_t)(C + Cin) * (TP + 1);
+    lift_bwd_w_kernel<<<nchunk, kBlock, sh, st>>>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2);
   }
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_conv_wgrad_nchunk(int Bn, int P1, int P2) {
+  const int64_t nt = (int64_t)Bn * cdiv((int64_t)P1 * P2, TP);
+  return (int)(nt < 1024 ? nt : 1024);
+}
+
+BLINDNO_API int blindno_conv_wgrad(const float* dz, const float* x, float* partial, int nchunk,
+                                   int Bn, int C, int P1, int P2, int act, void* stream) {
+  if (nchunk != blindno_conv_wgrad_nchunk(Bn, P1, P2) || C * C + C > PPT * kBlock)
+    return (int)hipErrorInvalidValue;
+  const int64_t HW = (int64_t)P1 * P2;
+  const int tpn = cdiv(HW, TP);
+  const int64_t ntiles = (int64_t)Bn * tpn;
+  const size_t sh = sizeof(float) * 2 * (size_t)C * (TP + 1);
+  if (act)
+    conv_wgrad_kernel<1><<<nchunk, kBlock, sh, (hipStream_t)stream>>>(dz, x, partial, C, HW, tpn, ntiles);
+  else
+    conv_wgrad_kernel<0><<<nchunk, kBlock, sh, (hipStream_t)stream>>>(dz, x, partial, C, HW, tpn, ntiles);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np,
+                                        void* stream) {
+  reduce_partials_kernel<<<cdiv(np, 64), 1024, 0, (hipStream_t)stream>>>(partial, out, nchunk, np);
   return (int)hipGetLastError();
 }
 
 BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float* wc,
                                     const float* bc, float* z, const float* tw2, int Bn, int C,
                                     int P1, int P2, int m2, int act, void* stream) {
-  int64_t total = (int64_t)Bn * C * P1 * P2;
-  dim3 g(grid_for(total, kBlock, 65536));
-  size_t sh = sizeof(float2) * P2;
+  const int nb = rowinv_blocks(Bn, P1);
+  hipStream_t st = (hipStream_t)stream;
   if (act)
-    rowidft_epi_kernel<1><<<g, kBlock, sh, (hipStream_t)stream>>>(
-        (const float2*)Z, x, wc, bc, z, (const float2*)tw2, Bn, C, P1, P2, m2);
-  else
-    rowidft_epi_kernel<0><<<g, kBlock, sh, (hipStream_t)stream>>>(
-        (const float2*)Z, x, wc, bc, z, (const float2*)tw2, Bn, C, P1, P2, m2);
-  return (int)hipGetLastError();
+    return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
+  return rowinv_launch<0, 0, 0>(Z, x, nullptr, wc, bc, z, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
+}
+
+BLINDNO_API int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1) {
+  return C <= 8 ? rowinv_blocks(Bn, P1) : 0;
 }
 
 BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc,
-                                    const float* xpre, float* dx, const float* tw2, int Bn,
-                                    int C, int P1, int P2, int m2, int act, void* stream) {
-  int64_t total = (int64_t)Bn * C * P1 * P2;
-  dim3 g(grid_for(total, kBlock, 65536));
-  size_t sh = sizeof(float2) * P2;
+                                    const float* xsrc, float* dx, const float* tw2,
+                                    float* partial, int Bn, int C, int P1, int P2, int m2,
+                                    int act, void* stream) {
+  const int nb = rowinv_blocks(Bn, P1);
+  hipStream_t st = (hipStream_t)stream;
+  if (partial) {
+    if (C > 8 || !wc) return (int)hipErrorInvalidValue;
+    if (act)
+      return rowinv_launch<1, 1, 1>(G, xsrc, dz, wc, nullptr, dx, tw2, partial, nb, Bn, C, P1, P2, m2, st);
+    return rowinv_launch<1, 0, 1>(G, xsrc, dz, wc, nullptr, dx, tw2, partial, nb, Bn, C, P1, P2, m2, st);
+  }
   if (act)
-    rowidft_bwd_kernel<1><<<g, kBlock, sh, (hipStream_t)stream>>>(
-        (const float2*)G, dz, wc, xpre, dx, (const float2*)tw2, Bn, C, P1, P2, m2);
-  else
-    rowidft_bwd_kernel<0><<<g, kBlock, sh, (hipStream_t)stream>>>(
-        (const float2*)G, dz, wc, xpre, dx, (const float2*)tw2, Bn, C, P1, P2, m2);
-  return (int)hipGetLastError();
+    return rowinv_launch<1, 1, 0>(G, xsrc, dz, wc, nullptr, dx, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
+  return rowinv_launch<1, 0, 0>(G, xsrc, dz, wc, nullptr, dx, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
 }
-
-BLINDNO_API int blindno_conv_wgrad(const float* dz, const float* x, float* partial, int nchunk,
-                                   int Bn, int C, int P1, int P2, int act, void* stream) {
-  int64_t total = (int64_t)nchunk * (C * C + C);
-  int64_t HW = (int64_t)P1 * P2;
-  if (act)
-    conv_wgrad_kernel<1><<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(dz, x, partial,
-                                                                               nchunk, Bn, C, HW);
-  else
-    conv_wgrad_kernel<0><<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(dz, x, partial,
-                                                                               nchunk, Bn, C, HW);
-  return (int)hipGetLastError();
-}
-
-BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np,
-                                        void* stream) {
-  reduce_partials_kernel<<<grid_for(np), kBlock, 0, (hipStream_t)stream>>>(partial, out, nchunk,
-                                                                           np);
-  return (int)hipGetLastError();
-}
-
-#define BLINDNO_PROJ_DISPATCH(KERNEL, GRID, ...)                                        \
-  do {                                                                                 \
-    if (Cout > 4 || C > 64) return (int)hipErrorInvalidValue;                          \
-    hipStream_t st_ = (hipStream_t)stream;                                             \
-    if (C <= 4) {                                                                      \
-      if (Cout <= 1) KERNEL<4, 1><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);              \
-      else KERNEL<4, 4><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);                        \
-    } else if (C <= 8) {                                                               \
-      if (Cout <= 1) KERNEL<8, 1><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);              \
-      else KERNEL<8, 4><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);                        \
-    } else if (C <= 16) {                                                              \
-      if (Cout <= 1) KERNEL<16, 1><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);             \
-      else KERNEL<16, 4><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);                       \
-    } else if (C <= 32) {                                                              \
-      if (Cout <= 1) KERNEL<32, 1><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);             \
-      else KERNEL<32, 4><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);                       \
-    } else {                                                                           \
-      if (Cout <= 1) KERNEL<64, 1><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);             \
-      else KERNEL<64, 4><<<GRID, kBlock, 0, st_>>>(__VA_ARGS__);                       \
-    }                                                                                  \
-  } while (0)
 
 BLINDNO_API int blindno_project_fwd(const float* z, const float* w1, const float* b1,
                                     const float* w2, const float* b2, float* out, int Bn, int C,
                                     int P1, int P2, int Ho, int Wo, int Hd, int Cout,
                                     int ostride, int ooff, void* stream) {
-  if (Ho > P1 || Wo > P2) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)Bn * Ho * Wo;
-  dim3 g(grid_for(total, kBlock, 65536));
-  BLINDNO_PROJ_DISPATCH(project_fwd_kernel, g, z, w1, b1, w2, b2, out, Bn, C, P1, P2, Ho, Wo, Hd,
-                        Cout, ostride, ooff);
+  if (Ho > P1 || Wo > P2 || C > 32 || Cout > 4) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)Bn * Ho * Wo;
+  const dim3 g(grid_for(total, kBlock, 2048));
+  hipStream_t st = (hipStream_t)stream;
+#define PF(CM_, CO_)                                                                          \
+  project_fwd_kernel<CM_, CO_><<<g, kBlock, sizeof(float) * (size_t)Hd * (CM_ + 1 + CO_), st>>>( \
+      z, w1, b1, w2, b2, out, Bn, C, P1, P2, Ho, Wo, Hd, Cout, ostride, ooff)
+  if (C <= 4) {
+    if (Cout == 1) PF(4, 1); else PF(4, 4);
+  } else if (C <= 8) {
+    if (Cout == 1) PF(8, 1); else PF(8, 4);
+  } else if (C <= 16) {
+    if (Cout == 1) PF(16, 1); else PF(16, 4);
+  } else {
+    if (Cout == 1) PF(32, 1); else PF(32, 4);
+  }
+#undef PF
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo) {
+  const int64_t pts = (int64_t)Bn * Ho * Wo;
+  const int64_t b = (pts / 8 + 4 * 16 - 1) / (4 * 16);     // >= ~16 point batches per wave
+  return (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
 }
 
 BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float* b1,
@@ -628,18 +1012,53 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
                                     float* partial, int nchunk, int Bn, int C, int P1, int P2,
                                     int Ho, int Wo, int Hd, int Cout, int ostride, int ooff,
                                     int dout_div, void* stream) {
-  if (Ho > P1 || Wo > P2 || dout_div < 1) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)Bn * Ho * Wo;
-  if (dz) {
-    dim3 g(grid_for(total, kBlock, 65536));
-    BLINDNO_PROJ_DISPATCH(project_bwd_dz_kernel, g, z, w1, b1, w2, dout, dz, Bn, C, P1, P2, Ho,
-                          Wo, Hd, Cout, ostride, ooff, dout_div);
+  if (Ho > P1 || Wo > P2 || dout_div < 1 || Hd % 64 != 0 || C > 32 || Cout > 4 || !dz ||
+      !partial || nchunk < 1)
+    return (int)hipErrorInvalidValue;
+  const int jpl = Hd / 64;
+  if (jpl != 1 && jpl != 2 && jpl != 4) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int np = Hd * C + Hd + Cout * Hd + Cout;
+  const dim3 g(nchunk);
+  if (C <= 4 && Hd == 128) {
+    if (Cout == 1)
+      project_bwd_split_kernel<4, 8, 1><<<g, 1024, 0, st>>>(z, w1, b1, w2, dout, dz, partial, Bn, C,
+                                                            P1, P2, Ho, Wo, Hd, Cout, ostride,
+                                                            ooff, dout_div);
+    else
+      project_bwd_split_kernel<4, 8, 4><<<g, 1024, 0, st>>>(z, w1, b1, w2, dout, dz, partial, Bn, C,
+                                                            P1, P2, Ho, Wo, Hd, Cout, ostride,
+                                                            ooff, dout_div);
+    return (int)hipGetLastError();
   }
-  if (partial) {
-    dim3 g(grid_for((int64_t)nchunk * Hd));
-    BLINDNO_PROJ_DISPATCH(project_bwd_w_kernel, g, z, w1, b1, w2, dout, partial, nchunk, Bn, C,
-                          P1, P2, Ho, Wo, Hd, Cout, ostride, ooff, dout_div);
+#define PB_LAUNCH(CM_, JPL_, PB_, CO_)                                                        \
+  {                                                                                           \
+    size_t sh = sizeof(float) * (size_t)kWaves * 64 * (PB_ * CM_ + 1);                        \
+    const size_t need = sizeof(float) * (size_t)kWaves * np;                                  \
+    if (need > sh) sh = need;                                                                 \
+    project_bwd_kernel<CM_, JPL_, PB_, CO_><<<g, kBlock, sh, st>>>(                           \
+        z, w1, b1, w2, dout, dz, partial, Bn, C, P1, P2, Ho, Wo, Hd, Cout, ostride, ooff,     \
+        dout_div);                                                                            \
   }
+#define PB_CO(CM_, JPL_, PB_)                    \
+  if (Cout == 1) PB_LAUNCH(CM_, JPL_, PB_, 1)    \
+  else PB_LAUNCH(CM_, JPL_, PB_, 4)
+#define PB_JPL(CM_, PB_)                      \
+  if (jpl == 2) { PB_CO(CM_, 2, PB_) }        \
+  else if (jpl == 1) { PB_CO(CM_, 1, PB_) }   \
+  else { PB_CO(CM_, 4, PB_) }
+  if (C <= 4) {
+    PB_JPL(4, 8)
+  } else if (C <= 8) {
+    PB_JPL(8, 4)
+  } else if (C <= 16) {
+    PB_JPL(16, 4)
+  } else {
+    PB_JPL(32, 2)
+  }
+#undef PB_JPL
+#undef PB_CO
+#undef PB_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -677,8 +1096,4 @@ BLINDNO_API int blindno_adam(float* p, const float* g, float* m, float* v, int64
   adam_kernel<<<grid_for(n, kBlock, 16384), kBlock, 0, (hipStream_t)stream>>>(
       p, g, m, v, n, beta1, beta2, eps, step_size, bc2s, gscale);
   return (int)hipGetLastError();
-}
-
-BLINDNO_API const char* blindno_error_string(int code) {
-  return hipGetErrorString((hipError_t)code);
 }

@@ -1,170 +1,211 @@
 // Truncated spectral transforms and per-mode channel mixing for SpectralConv1d/2d.
 //
 // Reference operation (yl602019618/Reconstruction-of-PDE-without-Time-Label):
-//   SpectralConv2d.forward  2d_FPE/FNOModules.py:156-178  (rfft2 -> compl_mul2d on the
-//   two kept corner blocks -> irfft2(s=(H,W)));  SpectralConv1d.forward
-//   1d_FPE/FNOModules.py:47-59 (rfft -> DC*0.5 -> einsum -> irfft).
-// The FFTs are evaluated as truncated DFTs: only m2 column modes and K1 kept rows are
-// ever formed, so the full spectrum is never materialised.  Twiddles come from a
-// per-length table tw[j] = (cos 2pi j/P, sin 2pi j/P) built on the host in double.
+//   SpectralConv2d.forward  2d_FPE/FNOModules.py:156-178  (rfft2 -> compl_mul2d on the two
+//   kept corner blocks -> irfft2(s=(H,W)));  SpectralConv1d.forward 1d_FPE/FNOModules.py:47-59
+//   (rfft -> DC*0.5 -> einsum bix,iox->box -> irfft).
+// The FFTs are evaluated as truncated DFTs: only m2 column modes and K1 kept rows are ever
+// formed.  The big, HBM-streaming stages are the row transforms (this file: forward row DFT;
+// fields.hip: inverse row DFT + epilogue); the column transforms and the mix work on the
+// m2/P2-sized row spectra and run one workgroup per (sample, column mode).
 #include "common.h"
 
 using namespace blindno;
 
 namespace {
 
-// ---------------------------------------------------------------- row DFT
-// At[n][k][c][h] = sum_w f(x[n][c][h][w]) e^{-2 pi i k w / P2}
-// One thread per output coefficient; the x row is swept from L1/L2.  The twiddle
-// table is staged in LDS.
-template <int ACT>
-__global__ __launch_bounds__(kBlock) void rowdft_kernel(const float* __restrict__ x,
-                                                        float2* __restrict__ At,
-                                                        const float2* __restrict__ tw2, int Bn,
-                                                        int C, int P1, int P2, int m2) {
-  extern __shared__ float2 s_tw[];
-  for (int i = threadIdx.x; i < P2; i += blockDim.x) s_tw[i] = tw2[i];
+// ------------------------------------------------------------------------------ row DFT
+// At[n][k][c][h] = sum_w f(x[n][c][h][w]) e^{-2 pi i k w / P2} as a skinny GEMM on the f32
+// matrix cores: out (rows x 2*m2, re/im interleaved) = X (rows x P2) . T (P2 x 2*m2), with
+// T[w][2k] = cos(2 pi k w/P2), T[w][2k+1] = -sin(2 pi k w/P2).
+// v_mfma_f32_16x16x4f32: one wave owns a 16-row tile and NT 16-column tiles.  The A operand
+// streams straight from HBM: lane l loads float4 x[row l&15][16 kb + 4 (l>>4) .. +3] and uses
+// component s in MFMA step s, i.e. the k-order inside each 16-block is permuted
+// (k = 16 kb + 4 (l>>4) + s); the B operand follows the same permutation from an LDS image
+// Tp[kb][kq][n][s] so that one ds_read_b128 returns the four steps' twiddles of one column.
+// f = GELU (act) is applied once per loaded element (VALU, beside the matrix pipe).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int NT, int ALIGNED>
+__global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
+                                                          float* __restrict__ At,
+                                                          const float* __restrict__ Tp,
+                                                          int nrows, int C, int P1, int P2,
+                                                          int m2, int KB, int Npad, int ntile_groups,
+                                                          int act) {
+  extern __shared__ float smT[];                 // [KB][4][Npad][4]
+  const int nT = KB * 16 * Npad;
+  for (int e = threadIdx.x; e < nT; e += blockDim.x) smT[e] = Tp[e];
   __syncthreads();
-  const int64_t total = (int64_t)Bn * m2 * C * P1;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int h = (int)(idx % P1);
-    int64_t t = idx / P1;
-    int c = (int)(t % C);
-    t /= C;
-    int k = (int)(t % m2);
-    int n = (int)(t / m2);
-    const float* row = x + (((int64_t)n * C + c) * P1 + h) * P2;
-    float re = 0.f, im = 0.f;
-    int ph = 0;
-    for (int w = 0; w < P2; ++w) {
-      float v = row[w];
-      if (ACT) v = gelu_f(v);
-      float2 e = s_tw[ph];
-      re = fmaf(v, e.x, re);
-      im = fmaf(-v, e.y, im);
-      ph += k;
-      if (ph >= P2) ph -= P2;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int nrt = (nrows + 15) >> 4;
+  const int64_t nwork = (int64_t)nrt * ntile_groups;
+  for (int64_t wk = (int64_t)blockIdx.x * 4 + wave; wk < nwork; wk += (int64_t)gridDim.x * 4) {
+    const int rt = (int)(wk / ntile_groups);
+    const int tg = (int)(wk % ntile_groups);
+    const int t0 = tg * NT;                       // first 16-column tile of this wave
+    const int row = rt * 16 + r16;
+    const bool rok = row < nrows;
+    const float* xr = x + (int64_t)(rok ? row : 0) * P2;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < KB; ++kb) {
+      const int w0 = kb * 16 + kq * 4;
+      float a[4];
+      if (ALIGNED && w0 + 3 < P2) {
+        const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < P2) ? xr[w0 + s] : 0.f;
+      }
+      if (act) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[s] = gelu_f(a[s]);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(
+            smT + (((kb * 4 + kq) * Npad) + (t0 + t) * 16 + r16) * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc[t], 0, 0, 0);
+      }
     }
-    At[idx] = make_float2(re, im);
+    // D layout: lane holds rows 4*(l>>4) + r (r < 4), column l & 15
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = (t0 + t) * 16 + r16;
+      const int k = col >> 1, part = col & 1;
+      if (k >= m2) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int orow = rt * 16 + kq * 4 + r;
+        if (orow >= nrows) continue;
+        const int h = orow % P1;
+        const int nc = orow / P1;
+        const int c = nc % C;
+        const int n = nc / C;
+        At[((((int64_t)n * m2 + k) * C + c) * P1 + h) * 2 + part] = acc[t][r];
+      }
+    }
   }
 }
 
-// ---------------------------------------------------------------- column DFT at kept rows
-// X[n][k][c][j] = s_k * sum_h At[n][k][c][h] e^{-2 pi i r_j h / P1}
-__global__ __launch_bounds__(kBlock) void coldft_kernel(const float2* __restrict__ At,
-                                                        float2* __restrict__ X,
-                                                        const float2* __restrict__ tw1, int Bn,
-                                                        int C, int P1, int m1, int m2, int P2,
-                                                        int scale_mode) {
-  extern __shared__ float2 s_tw[];
-  for (int i = threadIdx.x; i < P1; i += blockDim.x) s_tw[i] = tw1[i];
-  __syncthreads();
+// ------------------------------------------------------------------------------ column pass
+// One workgroup per (n, k).  DIR 0 (forward):  X = coldft(At) (saved), Y = mix(X, W),
+//   Z[n][h][k][c] = c_k/(P1 P2) * colidft(Y).
+// DIR 1 (adjoint):  G = c_k/(P1 P2) * coldft(At) (saved, the gradient of the spectrum),
+//   GX = mix^H(G, W), Z = colidft(GX).
+// colidft/coldft run over the K1 kept frequency rows r_j (kept_row); the phase r h mod P1
+// is advanced incrementally, twiddles come from an LDS copy of tw1[P1].
+template <int DIR>
+__global__ __launch_bounds__(kBlock) void colpass_kernel(const float2* __restrict__ At,
+                                                         const float2* __restrict__ Wt,
+                                                         float2* __restrict__ Xs,
+                                                         float2* __restrict__ Z,
+                                                         const float2* __restrict__ tw1, int Ci,
+                                                         int Co, int P1, int m1, int m2, int P2) {
+  extern __shared__ float2 sm[];
   const int K1 = kept_rows_count(m1, P1);
-  const int64_t total = (int64_t)Bn * m2 * C * K1;
-  const float inv = 1.0f / ((float)P1 * (float)P2);
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int j = (int)(idx % K1);
-    int64_t t = idx / K1;  // (n, k, c)
-    int k = (int)((t / C) % m2);
-    const float2* col = At + t * P1;
-    int r = kept_row(j, K1, m1, P1);
+  const int Cin = DIR == 0 ? Ci : Co;
+  const int Cout = DIR == 0 ? Co : Ci;
+  float2* stw = sm;
+  float2* sA = stw + P1;
+  float2* sX = sA + Cin * P1;
+  float2* sY = sX + Cin * K1;
+  const int n = blockIdx.x / m2, k = blockIdx.x % m2;
+  const int t = threadIdx.x;
+  const float ck = c2r_weight(k, P2) / ((float)P1 * (float)P2);
+
+  for (int i = t; i < P1; i += blockDim.x) stw[i] = tw1[i];
+  const float2* src = At + ((int64_t)n * m2 + k) * Cin * P1;
+  for (int i = t; i < Cin * P1; i += blockDim.x) sA[i] = src[i];
+  __syncthreads();
+
+  // column DFT at the kept rows
+  float2* xs = Xs + ((int64_t)n * m2 + k) * Cin * K1;
+  for (int o = t; o < Cin * K1; o += blockDim.x) {
+    const int c = o / K1, j = o % K1;
+    const int r = kept_row(j, K1, m1, P1);
+    const float2* a = sA + c * P1;
     float re = 0.f, im = 0.f;
     int ph = 0;
     for (int h = 0; h < P1; ++h) {
-      float2 a = col[h];
-      float2 e = s_tw[ph];
-      // (a.x + i a.y)(e.x - i e.y)
-      re = fmaf(a.x, e.x, fmaf(a.y, e.y, re));
-      im = fmaf(a.y, e.x, fmaf(-a.x, e.y, im));
+      const float2 v = a[h];
+      const float2 e = stw[ph];
+      re = fmaf(v.x, e.x, fmaf(v.y, e.y, re));    // v * conj(e)
+      im = fmaf(v.y, e.x, fmaf(-v.x, e.y, im));
       ph += r;
       if (ph >= P1) ph -= P1;
     }
-    if (scale_mode == 1) {
-      float s = c2r_weight(k, P2) * inv;
-      re *= s;
-      im *= s;
+    if (DIR == 1) {
+      re *= ck;
+      im *= ck;
     }
-    X[idx] = make_float2(re, im);
+    const float2 v = make_float2(re, im);
+    sX[o] = v;
+    xs[o] = v;
   }
-}
-
-// ---------------------------------------------------------------- column inverse at kept rows
-// Z[n][c][h][k] = s_k * sum_j Y[n][k][c][j] e^{+2 pi i r_j h / P1}
-__global__ __launch_bounds__(kBlock) void colidft_kernel(const float2* __restrict__ Y,
-                                                         float2* __restrict__ Z,
-                                                         const float2* __restrict__ tw1, int Bn,
-                                                         int C, int P1, int m1, int m2, int P2,
-                                                         int scale_mode) {
-  extern __shared__ float2 s_tw[];
-  for (int i = threadIdx.x; i < P1; i += blockDim.x) s_tw[i] = tw1[i];
   __syncthreads();
-  const int K1 = kept_rows_count(m1, P1);
-  const int64_t total = (int64_t)Bn * C * P1 * m2;
-  const float inv = 1.0f / ((float)P1 * (float)P2);
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int k = (int)(idx % m2);
-    int64_t t = idx / m2;
-    int h = (int)(t % P1);
-    t /= P1;
-    int c = (int)(t % C);
-    int n = (int)(t / C);
-    const float2* yv = Y + (((int64_t)n * m2 + k) * C + c) * K1;
-    float re = 0.f, im = 0.f;
-    for (int j = 0; j < K1; ++j) {
-      int r = kept_row(j, K1, m1, P1);
-      int ph = (int)(((int64_t)r * h) % P1);
-      float2 e = s_tw[ph];
-      float2 a = yv[j];
-      // (a.x + i a.y)(e.x + i e.y)
-      re = fmaf(a.x, e.x, fmaf(-a.y, e.y, re));
-      im = fmaf(a.x, e.y, fmaf(a.y, e.x, im));
-    }
-    float s = scale_mode == 1 ? c2r_weight(k, P2) * inv : 1.0f;
-    Z[idx] = make_float2(re * s, im * s);
-  }
-}
 
-// ---------------------------------------------------------------- per-mode channel mix
-template <int DIR>
-__global__ __launch_bounds__(kBlock) void mix_kernel(const float2* __restrict__ X,
-                                                     const float2* __restrict__ Wt,
-                                                     float2* __restrict__ Y, int Bn, int Ci,
-                                                     int Co, int K1, int m2) {
-  // DIR 0: Y[n,k,o,j] = sum_i X[n,k,i,j] W[k,j,i,o]
-  // DIR 1: Y[n,k,i,j] = sum_o conj(W[k,j,i,o]) X[n,k,o,j]
-  const int Cout = DIR == 0 ? Co : Ci;
-  const int Cin = DIR == 0 ? Ci : Co;
-  const int64_t total = (int64_t)Bn * m2 * Cout * K1;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int j = (int)(idx % K1);
-    int64_t t = idx / K1;
-    int oc = (int)(t % Cout);
-    int64_t nk = t / Cout;  // n * m2 + k
-    int k = (int)(nk % m2);
-    const float2* xv = X + nk * Cin * K1 + j;
-    const float2* wv = Wt + ((int64_t)k * K1 + j) * Ci * Co;
+  // per-mode channel mix
+  const float2* wk = Wt + (int64_t)k * K1 * Ci * Co;
+  for (int o = t; o < Cout * K1; o += blockDim.x) {
+    const int oc = o % Cout, j = o / Cout;
+    const float2* wj = wk + (int64_t)j * Ci * Co;
     float re = 0.f, im = 0.f;
     for (int q = 0; q < Cin; ++q) {
-      float2 a = xv[(int64_t)q * K1];
+      const float2 a = sX[q * K1 + j];
       if (DIR == 0) {
-        float2 w = wv[(int64_t)q * Co + oc];
+        const float2 w = wj[q * Co + oc];
         re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
         im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
       } else {
-        float2 w = wv[(int64_t)oc * Co + q];
-        // conj(w) * a
+        const float2 w = wj[oc * Co + q];              // conj(w) * a
         re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
         im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
       }
     }
-    Y[idx] = make_float2(re, im);
+    sY[oc * K1 + j] = make_float2(re, im);
+  }
+  __syncthreads();
+
+  // column inverse at the kept rows -> Z[n][h][k][c]
+  const float s = DIR == 0 ? ck : 1.0f;
+  const int split = (K1 == P1) ? K1 : m1;         // rows j < split have r_j = j
+  for (int o = t; o < P1 * Cout; o += blockDim.x) {
+    const int c = o % Cout, h = o / Cout;
+    const float2* y = sY + c * K1;
+    float re = 0.f, im = 0.f;
+    int ph = 0;
+    for (int j = 0; j < split; ++j) {
+      const float2 a = y[j];
+      const float2 e = stw[ph];
+      re = fmaf(a.x, e.x, fmaf(-a.y, e.y, re));
+      im = fmaf(a.x, e.y, fmaf(a.y, e.x, im));
+      ph += h;
+      if (ph >= P1) ph -= P1;
+    }
+    if (split < K1) {
+      ph = (int)(((int64_t)(P1 - m1) * h) % P1);
+      for (int j = split; j < K1; ++j) {
+        const float2 a = y[j];
+        const float2 e = stw[ph];
+        re = fmaf(a.x, e.x, fmaf(-a.y, e.y, re));
+        im = fmaf(a.x, e.y, fmaf(a.y, e.x, im));
+        ph += h;
+        if (ph >= P1) ph -= P1;
+      }
+    }
+    Z[(((int64_t)n * P1 + h) * m2 + k) * Cout + c] = make_float2(re * s, im * s);
   }
 }
 
+// dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]
 __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restrict__ X,
                                                            const float2* __restrict__ G,
                                                            float2* __restrict__ dWt, int Bn,
@@ -172,17 +213,16 @@ __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restr
   const int64_t total = (int64_t)m2 * K1 * Ci * Co;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int o = (int)(idx % Co);
+    const int o = (int)(idx % Co);
     int64_t t = idx / Co;
-    int i = (int)(t % Ci);
+    const int i = (int)(t % Ci);
     t /= Ci;
-    int j = (int)(t % K1);
-    int k = (int)(t / K1);
+    const int j = (int)(t % K1);
+    const int k = (int)(t / K1);
     float re = 0.f, im = 0.f;
     for (int n = 0; n < Bn; ++n) {
-      float2 a = X[(((int64_t)n * m2 + k) * Ci + i) * K1 + j];
-      float2 g = G[(((int64_t)n * m2 + k) * Co + o) * K1 + j];
-      // conj(a) * g
+      const float2 a = X[(((int64_t)n * m2 + k) * Ci + i) * K1 + j];
+      const float2 g = G[(((int64_t)n * m2 + k) * Co + o) * K1 + j];
       re = fmaf(a.x, g.x, fmaf(a.y, g.y, re));
       im = fmaf(a.x, g.y, fmaf(-a.y, g.x, im));
     }
@@ -190,61 +230,55 @@ __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restr
   }
 }
 
-// ---------------------------------------------------------------- 1D mode mix
+// ------------------------------------------------------------------------------ 1D mode mix
+// At[n][k][c] (P1 = 1).  Forward: Xs = h_k At (DC halved) ; Z[n][k][o] = c_k/P2 sum_i Xs W.
+// Backward: Xs = c_k/P2 At (= spectrum gradient) ; Z[n][k][i] = h_k sum_o conj(W) Xs.
 template <int DIR>
 __global__ __launch_bounds__(kBlock) void mix1d_kernel(const float2* __restrict__ At,
                                                        const float2* __restrict__ Wt,
                                                        float2* __restrict__ Xs,
                                                        float2* __restrict__ Z, int Bn, int Ci,
                                                        int Co, int m, int P2) {
-  // At[n][k][c] (P1 = 1).  Forward: Xs = At * h_k ; Z[n][o][k] = c_k/P2 sum_i Xs W
-  // Backward: Xs = c_k/P2 At ; Z[n][i][k] = h_k sum_o conj(W) Xs
   const int Cout = DIR == 0 ? Co : Ci;
   const int Cin = DIR == 0 ? Ci : Co;
-  const int64_t total = (int64_t)Bn * Cout * m;
   const float invP = 1.0f / (float)P2;
+  const int64_t total = (int64_t)Bn * m * Cout;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int k = (int)(idx % m);
-    int64_t t = idx / m;
-    int oc = (int)(t % Cout);
-    int n = (int)(t / Cout);
+    const int oc = (int)(idx % Cout);
+    const int64_t nk = idx / Cout;
+    const int k = (int)(nk % m);
     const float hk = k == 0 ? 0.5f : 1.0f;
     const float ck = c2r_weight(k, P2) * invP;
-    const float2* av = At + ((int64_t)n * m + k) * Cin;
+    const float2* av = At + nk * Cin;
     const float2* wv = Wt + (int64_t)k * Ci * Co;
     float re = 0.f, im = 0.f;
     for (int q = 0; q < Cin; ++q) {
       float2 a = av[q];
       if (DIR == 0) {
-        a.x *= hk;
-        a.y *= hk;
-        float2 w = wv[(int64_t)q * Co + oc];
+        const float2 w = wv[q * Co + oc];
         re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
         im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
       } else {
-        a.x *= ck;
-        a.y *= ck;
-        float2 w = wv[(int64_t)oc * Co + q];
+        const float2 w = wv[oc * Co + q];
         re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
         im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
       }
     }
-    float s = DIR == 0 ? ck : hk;
-    Z[((int64_t)n * Cout + oc) * m + k] = make_float2(re * s, im * s);
+    const float sc = DIR == 0 ? hk * ck : ck * hk;
+    Z[idx] = make_float2(re * sc, im * sc);
   }
-  // saved spectrum, layout Xs[n][k][c] (= colspec with K1 = 1)
   const int64_t tot2 = (int64_t)Bn * m * Cin;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot2;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int k = (int)((idx / Cin) % m);
-    float2 a = At[idx];
-    float s = DIR == 0 ? (k == 0 ? 0.5f : 1.0f) : c2r_weight(k, P2) * invP;
-    Xs[idx] = make_float2(a.x * s, a.y * s);
+    const int k = (int)((idx / Cin) % m);
+    const float2 a = At[idx];
+    const float sc = DIR == 0 ? (k == 0 ? 0.5f : 1.0f) : c2r_weight(k, P2) * invP;
+    Xs[idx] = make_float2(a.x * sc, a.y * sc);
   }
 }
 
-// ---------------------------------------------------------------- weight packing
+// ------------------------------------------------------------------------------ weight packing
 __global__ void pack_w2d_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
                                 float2* __restrict__ Wt, int Ci, int Co, int m1, int m2,
                                 int P1) {
@@ -252,22 +286,16 @@ __global__ void pack_w2d_kernel(const float* __restrict__ w1, const float* __res
   const int64_t total = (int64_t)m2 * K1 * Ci * Co;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int o = (int)(idx % Co);
+    const int o = (int)(idx % Co);
     int64_t t = idx / Co;
-    int i = (int)(t % Ci);
+    const int i = (int)(t % Ci);
     t /= Ci;
-    int j = (int)(t % K1);
-    int k = (int)(t / K1);
-    int r = kept_row(j, K1, m1, P1);
-    const float* src;
-    int jj;
-    if (r >= P1 - m1) {
-      src = w2;
-      jj = r - (P1 - m1);
-    } else {
-      src = w1;
-      jj = r;
-    }
+    const int j = (int)(t % K1);
+    const int k = (int)(t / K1);
+    const int r = kept_row(j, K1, m1, P1);
+    const bool second = r >= P1 - m1;
+    const float* src = second ? w2 : w1;
+    const int jj = second ? r - (P1 - m1) : r;
     const float* p = src + ((((int64_t)i * Co + o) * m1 + jj) * m2 + k) * 2;
     Wt[idx] = make_float2(p[0], p[1]);
   }
@@ -280,23 +308,22 @@ __global__ void unpack_w2d_kernel(const float2* __restrict__ dWt, float* __restr
   const int64_t per = (int64_t)Ci * Co * m1 * m2;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < 2 * per;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int which = idx >= per;
-    int64_t e = which ? idx - per : idx;
-    int k = (int)(e % m2);
+    const int which = idx >= per;
+    const int64_t e = which ? idx - per : idx;
+    const int k = (int)(e % m2);
     int64_t t = e / m2;
-    int jj = (int)(t % m1);
+    const int jj = (int)(t % m1);
     t /= m1;
-    int o = (int)(t % Co);
-    int i = (int)(t / Co);
-    float2 v = make_float2(0.f, 0.f);
-    int r, j = -1;
+    const int o = (int)(t % Co);
+    const int i = (int)(t / Co);
+    int j = -1;
     if (which) {
-      r = P1 - m1 + jj;
+      const int r = P1 - m1 + jj;
       j = (K1 == P1) ? r : m1 + jj;
-    } else {
-      r = jj;
-      if (r < P1 - m1) j = r;  // otherwise shadowed by weights2
+    } else if (jj < P1 - m1) {
+      j = jj;                     // otherwise shadowed by weights2 (overlapping rows)
     }
+    float2 v = make_float2(0.f, 0.f);
     if (j >= 0) v = dWt[(((int64_t)k * K1 + j) * Ci + i) * Co + o];
     float* dst = (which ? dw2 : dw1) + e * 2;
     dst[0] = v.x;
@@ -304,77 +331,89 @@ __global__ void unpack_w2d_kernel(const float2* __restrict__ dWt, float* __restr
   }
 }
 
-__global__ void pack_w1d_kernel(const float2* __restrict__ w, float2* __restrict__ Wt, int Ci,
+__global__ void pack_w1d_kernel(const float2* __restrict__ src, float2* __restrict__ dst, int Ci,
                                 int Co, int m, int dir) {
   const int64_t total = (int64_t)Ci * Co * m;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    int k = (int)(idx % m);
-    int64_t t = idx / m;
-    int o = (int)(t % Co);
-    int i = (int)(t / Co);
-    int64_t pidx = ((int64_t)k * Ci + i) * Co + o;
+    const int k = (int)(idx % m);
+    const int64_t t = idx / m;
+    const int o = (int)(t % Co);
+    const int i = (int)(t / Co);
+    const int64_t pidx = ((int64_t)k * Ci + i) * Co + o;
     if (dir == 0)
-      Wt[pidx] = w[idx];
+      dst[pidx] = src[idx];          // (Ci,Co,m) -> (m,Ci,Co)
     else
-      ((float2*)Wt)[idx] = w[pidx];  // unpack: w is dWt, Wt is dW
+      dst[idx] = src[pidx];          // (m,Ci,Co) -> (Ci,Co,m)
   }
 }
 
 }  // namespace
 
-BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* tw2, int Bn, int C,
+BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int Bn, int C,
                                int P1, int P2, int m2, int act, void* stream) {
-  if (Bn <= 0 || C <= 0 || P1 <= 0 || P2 <= 0 || m2 <= 0 || m2 > P2 / 2 + 1 || P2 > 8192)
+  if (Bn <= 0 || C <= 0 || P1 <= 0 || P2 <= 0 || m2 <= 0 || m2 > P2 / 2 + 1)
     return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)Bn * m2 * C * P1;
-  dim3 g(grid_for(total, kBlock, 65536)), b(kBlock);
-  size_t sh = sizeof(float2) * P2;
-  if (act)
-    rowdft_kernel<1><<<g, b, sh, (hipStream_t)stream>>>(x, (float2*)At, (const float2*)tw2,
-                                                         Bn, C, P1, P2, m2);
-  else
-    rowdft_kernel<0><<<g, b, sh, (hipStream_t)stream>>>(x, (float2*)At, (const float2*)tw2,
-                                                         Bn, C, P1, P2, m2);
+  const int64_t nrows64 = (int64_t)Bn * C * P1;
+  if (nrows64 > INT32_MAX) return (int)hipErrorInvalidValue;
+  const int nrows = (int)nrows64;
+  const int KB = (P2 + 15) / 16;
+  const int Npad = ((2 * m2 + 15) / 16) * 16;
+  const int ntiles = Npad / 16;
+  const size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+  // tiles per wave: all of them when there are many row tiles, else split for parallelism
+  const int nrt = (nrows + 15) / 16;
+  int nt = ntiles;
+  if (nt > 4) nt = 4;
+  while (nt > 1 && (int64_t)nrt * ((ntiles + nt - 1) / nt) < 4096) nt >>= 1;
+  while (ntiles % nt) --nt;
+  const int groups = ntiles / nt;
+  const int64_t nwork = (int64_t)nrt * groups;
+  const int blocks = (int)((nwork + 3) / 4 < 4096 ? (nwork + 3) / 4 : 4096);
+  const bool aligned = (P2 % 4) == 0 && (((uintptr_t)x) & 15) == 0;
+  hipStream_t st = (hipStream_t)stream;
+#define RD(NT_, AL_)                                                                       \
+  rowdft_mfma_kernel<NT_, AL_><<<blocks, 256, sh, st>>>(x, At, Tp, nrows, C, P1, P2, m2, KB, \
+                                                        Npad, groups, act)
+#define RD_AL(NT_) \
+  if (aligned) RD(NT_, 1); else RD(NT_, 0);
+  switch (nt) {
+    case 1: RD_AL(1) break;
+    case 2: RD_AL(2) break;
+    case 3: RD_AL(3) break;
+    default: RD_AL(4) break;
+  }
+#undef RD_AL
+#undef RD
   return (int)hipGetLastError();
 }
 
-BLINDNO_API int blindno_coldft(const float* At, float* X, const float* tw1, int Bn, int C,
-                               int P1, int m1, int m2, int P2, int scale_mode, void* stream) {
-  if (m1 <= 0 || m1 > P1 || P1 > 8192) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)Bn * m2 * C * kept_rows_count(m1, P1);
-  coldft_kernel<<<grid_for(total, kBlock, 65536), kBlock, sizeof(float2) * P1,
-                  (hipStream_t)stream>>>((const float2*)At, (float2*)X, (const float2*)tw1, Bn,
-                                         C, P1, m1, m2, P2, scale_mode);
-  return (int)hipGetLastError();
-}
-
-BLINDNO_API int blindno_colidft(const float* Y, float* Z, const float* tw1, int Bn, int C,
-                                int P1, int m1, int m2, int P2, int scale_mode, void* stream) {
-  if (m1 <= 0 || m1 > P1 || P1 > 8192) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)Bn * C * P1 * m2;
-  colidft_kernel<<<grid_for(total, kBlock, 65536), kBlock, sizeof(float2) * P1,
-                   (hipStream_t)stream>>>((const float2*)Y, (float2*)Z, (const float2*)tw1, Bn,
-                                          C, P1, m1, m2, P2, scale_mode);
-  return (int)hipGetLastError();
-}
-
-BLINDNO_API int blindno_mix(const float* X, const float* Wt, float* Y, int Bn, int Ci, int Co,
-                            int K1, int m2, int dir, void* stream) {
-  int64_t total = (int64_t)Bn * m2 * (dir == 0 ? Co : Ci) * K1;
-  dim3 g(grid_for(total, kBlock, 65536));
+BLINDNO_API int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Z,
+                                const float* tw1, int Bn, int Ci, int Co, int P1, int m1, int m2,
+                                int P2, int dir, void* stream) {
+  if (m1 <= 0 || m1 > P1 || m2 > P2 / 2 + 1) return (int)hipErrorInvalidValue;
+  const int K1 = kept_rows_count(m1, P1);
+  const int cin = dir == 0 ? Ci : Co, cout = dir == 0 ? Co : Ci;
+  const size_t sh = sizeof(float2) * ((size_t)P1 + (size_t)cin * P1 + (size_t)cin * K1 +
+                                      (size_t)cout * K1);
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+  dim3 g(Bn * m2);
+  hipStream_t st = (hipStream_t)stream;
   if (dir == 0)
-    mix_kernel<0><<<g, kBlock, 0, (hipStream_t)stream>>>((const float2*)X, (const float2*)Wt,
-                                                         (float2*)Y, Bn, Ci, Co, K1, m2);
+    colpass_kernel<0><<<g, kBlock, sh, st>>>((const float2*)At, (const float2*)Wt, (float2*)Xs,
+                                             (float2*)Z, (const float2*)tw1, Ci, Co, P1, m1, m2,
+                                             P2);
   else
-    mix_kernel<1><<<g, kBlock, 0, (hipStream_t)stream>>>((const float2*)X, (const float2*)Wt,
-                                                         (float2*)Y, Bn, Ci, Co, K1, m2);
+    colpass_kernel<1><<<g, kBlock, sh, st>>>((const float2*)At, (const float2*)Wt, (float2*)Xs,
+                                             (float2*)Z, (const float2*)tw1, Ci, Co, P1, m1, m2,
+                                             P2);
   return (int)hipGetLastError();
 }
 
 BLINDNO_API int blindno_mix_wgrad(const float* X, const float* G, float* dWt, int Bn, int Ci,
                                   int Co, int K1, int m2, void* stream) {
-  int64_t total = (int64_t)m2 * K1 * Ci * Co;
+  const int64_t total = (int64_t)m2 * K1 * Ci * Co;
   mix_wgrad_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, (hipStream_t)stream>>>(
       (const float2*)X, (const float2*)G, (float2*)dWt, Bn, Ci, Co, K1, m2);
   return (int)hipGetLastError();
@@ -383,22 +422,23 @@ BLINDNO_API int blindno_mix_wgrad(const float* X, const float* G, float* dWt, in
 BLINDNO_API int blindno_mix1d(const float* At, const float* Wt, float* Xs, float* Z, int Bn,
                               int Ci, int Co, int m, int P2, int dir, void* stream) {
   if (m > P2 / 2 + 1) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)Bn * (dir == 0 ? Co : Ci) * m;
-  int64_t t2 = (int64_t)Bn * m * (dir == 0 ? Ci : Co);
-  dim3 g(grid_for(total > t2 ? total : t2, kBlock, 65536));
+  const int64_t t1 = (int64_t)Bn * m * (dir == 0 ? Co : Ci);
+  const int64_t t2 = (int64_t)Bn * m * (dir == 0 ? Ci : Co);
+  dim3 g(grid_for(t1 > t2 ? t1 : t2, kBlock, 65536));
+  hipStream_t st = (hipStream_t)stream;
   if (dir == 0)
-    mix1d_kernel<0><<<g, kBlock, 0, (hipStream_t)stream>>>(
-        (const float2*)At, (const float2*)Wt, (float2*)Xs, (float2*)Z, Bn, Ci, Co, m, P2);
+    mix1d_kernel<0><<<g, kBlock, 0, st>>>((const float2*)At, (const float2*)Wt, (float2*)Xs,
+                                          (float2*)Z, Bn, Ci, Co, m, P2);
   else
-    mix1d_kernel<1><<<g, kBlock, 0, (hipStream_t)stream>>>(
-        (const float2*)At, (const float2*)Wt, (float2*)Xs, (float2*)Z, Bn, Ci, Co, m, P2);
+    mix1d_kernel<1><<<g, kBlock, 0, st>>>((const float2*)At, (const float2*)Wt, (float2*)Xs,
+                                          (float2*)Z, Bn, Ci, Co, m, P2);
   return (int)hipGetLastError();
 }
 
 BLINDNO_API int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, int Ci, int Co,
                                  int m1, int m2, int P1, void* stream) {
   if (m1 > P1) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)m2 * kept_rows_count(m1, P1) * Ci * Co;
+  const int64_t total = (int64_t)m2 * kept_rows_count(m1, P1) * Ci * Co;
   pack_w2d_kernel<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(w1, w2, (float2*)Wt, Ci,
                                                                        Co, m1, m2, P1);
   return (int)hipGetLastError();
@@ -407,7 +447,7 @@ BLINDNO_API int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, in
 BLINDNO_API int blindno_unpack_w2d(const float* dWt, float* dw1, float* dw2, int Ci, int Co,
                                    int m1, int m2, int P1, void* stream) {
   if (m1 > P1) return (int)hipErrorInvalidValue;
-  int64_t total = 2 * (int64_t)Ci * Co * m1 * m2;
+  const int64_t total = 2 * (int64_t)Ci * Co * m1 * m2;
   unpack_w2d_kernel<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(
       (const float2*)dWt, dw1, dw2, Ci, Co, m1, m2, P1);
   return (int)hipGetLastError();
@@ -415,7 +455,7 @@ BLINDNO_API int blindno_unpack_w2d(const float* dWt, float* dw1, float* dw2, int
 
 BLINDNO_API int blindno_pack_w1d(const float* w, float* Wt, int Ci, int Co, int m, int dir,
                                  void* stream) {
-  int64_t total = (int64_t)Ci * Co * m;
+  const int64_t total = (int64_t)Ci * Co * m;
   pack_w1d_kernel<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(
       (const float2*)w, (float2*)Wt, Ci, Co, m, dir);
   return (int)hipGetLastError();
