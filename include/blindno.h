@@ -88,21 +88,28 @@ int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo);
 int blindno_rowdft(const float* x, float* At, const float* Tp, int Bn, int C, int P1,
                    int P2, int m2, int act, blindno_stream_t stream);
 
-/* Column pass of SpectralConv2d, one workgroup per (sample, column mode): column DFT at
- * the K1 kept rows, per-mode complex channel mix (compl_mul2d, 2d_FPE/FNOModules.py:141-154,
- * 170-173), column inverse.  tw1: P1-entry table (cos, sin)(2 pi j / P1).
+/* Column pass of SpectralConv2d: column DFT at the K1 kept rows, per-mode complex channel
+ * mix (compl_mul2d, 2d_FPE/FNOModules.py:141-154, 170-173), column inverse -- two complex
+ * GEMMs against F[h][j] = e^{-2 pi i r_j h / P1} on the matrix cores.
+ * FB: (ceil(K1/16), ceil(P1/16), 64, 4) complex image, FB[jt][hb][l][s] =
+ *     F[16 hb + 4 (l>>4) + s][16 jt + (l&15)];  GB: (ceil(P1/16), ceil(K1/16), 64, 4) complex,
+ *     GB[ht][jb][l][s] = conj F[16 ht + (l&15)][16 jb + 4 (l>>4) + s]  (zero outside).
+ * Y: scratch (Bn, m2, C_out, K1p = 16 ceil(K1/16)) complex.
  * dir 0 (forward): Xs = colDFT(At) (Bn,m2,Ci,K1) saved for the weight gradient;
  *                  Z[n][h][k][o] = c_k/(P1 P2) colIDFT(sum_i Xs W)   (rowcoef, Co channels).
  * dir 1 (adjoint): At holds the row DFT of the output gradient (Co channels);
  *                  Xs = c_k/(P1 P2) colDFT(At) = spectrum gradient G (Bn,m2,Co,K1);
  *                  Z[n][h][k][i] = colIDFT(sum_o conj(W) G)             (Ci channels). */
-int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Z, const float* tw1,
-                    int Bn, int Ci, int Co, int P1, int m1, int m2, int P2, int dir,
-                    blindno_stream_t stream);
+int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
+                    const float* FB, const float* GB, int Bn, int Ci, int Co, int P1, int m1,
+                    int m2, int P2, int dir, blindno_stream_t stream);
 
-/* dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]  (weight gradient of the mix). */
-int blindno_mix_wgrad(const float* X, const float* G, float* dWt, int Bn, int Ci, int Co,
-                      int K1, int m2, blindno_stream_t stream);
+/* dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]  (weight gradient of the mix).  The
+ * samples are split into nsplit slices (blindno_mix_wgrad_nsplit); with nsplit > 1 the
+ * slice sums go to partial (nsplit x 2 m2 K1 Ci Co floats) and are reduced in fixed order. */
+int blindno_mix_wgrad_nsplit(int Bn, int Ci, int Co, int K1, int m2);
+int blindno_mix_wgrad(const float* X, const float* G, float* dWt, float* partial, int nsplit,
+                      int Bn, int Ci, int Co, int K1, int m2, blindno_stream_t stream);
 
 /* 1D mode mix (compl_mul1d + DC halving, 1d_FPE/FNOModules.py:43-58).  At (Bn,m,C,1).
  * dir 0 (forward):  Xs = At with X[.,0] *= 0.5 (saved); Z[n][0][k][o] = c_k/P2 sum_i Xs W.

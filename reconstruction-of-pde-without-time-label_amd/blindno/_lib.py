@@ -24,8 +24,8 @@ SIGNATURES = {
     "blindno_project_fwd": "ppppppiiiiiiiiiis",
     "blindno_project_bwd": "pppppppiiiiiiiiiiiis",
     "blindno_rowdft": "pppiiiiiis",
-    "blindno_colpass": "pppppiiiiiiiis",
-    "blindno_mix_wgrad": "pppiiiiis",
+    "blindno_colpass": "pppppppiiiiiiiis",
+    "blindno_mix_wgrad": "ppppiiiiiis",
     "blindno_mix1d": "ppppiiiiiis",
     "blindno_rowidft_epi": "ppppppiiiiiis",
     "blindno_rowidft_bwd": "pppppppiiiiiis",
@@ -44,6 +44,7 @@ SIGNATURES = {
     "blindno_conv_wgrad_nchunk": "iii",
     "blindno_rowidft_bwd_nchunk": "iii",
     "blindno_project_bwd_nchunk": "iii",
+    "blindno_mix_wgrad_nsplit": "iiiii",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,

@@ -92,6 +92,44 @@ def twiddle_mfma(P2: int, m2: int, device) -> torch.Tensor:
     return t
 
 
+_TWC = {}
+
+
+def kept_rows(m1: int, P1: int):
+    """Frequency rows r_j kept by SpectralConv2d: [0, m1) from weights1 and [P1-m1, P1) from
+    weights2 (all rows when 2 m1 >= P1; 2d_FPE/FNOModules.py:170-173)."""
+    K1 = kept_rows_count(m1, P1)
+    return [j if (K1 == P1 or j < m1) else P1 - 2 * m1 + j for j in range(K1)]
+
+
+def twiddle_cols(P1: int, m1: int, device):
+    """MFMA B-operand images of F[h][j] = e^{-2 pi i r_j h / P1} for the column pass:
+    FB[jt][hb][l][s] = F[16 hb + 4 (l>>4) + s][16 jt + (l&15)] and
+    GB[ht][jb][l][s] = conj F[16 ht + (l&15)][16 jb + 4 (l>>4) + s], zero outside, complex
+    interleaved (include/blindno.h blindno_colpass)."""
+    dev = torch.device(device)
+    key = (P1, m1, dev.index)
+    t = _TWC.get(key)
+    if t is None:
+        K1 = kept_rows_count(m1, P1)
+        Jt, Ht = (K1 + 15) // 16, (P1 + 15) // 16
+        r = torch.zeros(Jt * 16, dtype=torch.int64)
+        r[:K1] = torch.tensor(kept_rows(m1, P1), dtype=torch.int64)
+        h = torch.arange(Ht * 16, dtype=torch.int64)
+        ph = ((h[:, None] * r[None, :]) % P1).to(torch.float64) * (2.0 * torch.pi / P1)
+        F = torch.complex(torch.cos(ph), -torch.sin(ph))            # (Ht*16, Jt*16)
+        F[P1:, :] = 0
+        F[:, K1:] = 0
+        # FB: [jt][hb][kq][c][s] = F[16hb + 4kq + s][16jt + c]
+        FB = F.view(Ht, 4, 4, Jt, 16).permute(3, 0, 1, 4, 2)
+        # GB: [ht][jb][kq][c][s] = conj F[16ht + c][16jb + 4kq + s]
+        GB = F.conj().view(Ht, 16, Jt, 4, 4).permute(0, 2, 3, 1, 4)
+        cv = lambda z: torch.view_as_real(z.contiguous()).to(F32).to(dev).contiguous()
+        t = (cv(FB), cv(GB))
+        _TWC[key] = t
+    return t
+
+
 def require_device(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -128,20 +166,26 @@ def k_rowdft(x, Bn, C, P1, P2, m2, act):
 
 
 def k_colpass(At, Wt, Bn, Ci, Co, P1, m1, m2, P2, direction):
-    """Column DFT at the kept rows + per-mode mix + column inverse (one launch).
+    """Column DFT at the kept rows + per-mode mix + column inverse (matrix-core GEMMs).
     Returns (saved spectrum (Bn, m2, Cin, K1), row coefficients Z (Bn, P1, m2, Cout))."""
     K1 = kept_rows_count(m1, P1)
+    K1p = 16 * ((K1 + 15) // 16)
     cin, cout = (Ci, Co) if direction == 0 else (Co, Ci)
     Xs = _empty(Bn, m2, cin, K1, 2, like=At)
+    Y = _empty(Bn, m2, cout, K1p, 2, like=At)
     Z = _empty(Bn, P1, m2, cout, 2, like=At)
-    call("blindno_colpass", ptr(At), ptr(Wt), ptr(Xs), ptr(Z), ptr(twiddle(P1, At.device)), Bn,
+    FB, GB = twiddle_cols(P1, m1, At.device)
+    call("blindno_colpass", ptr(At), ptr(Wt), ptr(Xs), ptr(Y), ptr(Z), ptr(FB), ptr(GB), Bn,
          Ci, Co, P1, m1, m2, P2, direction, stream_ptr())
     return Xs, Z
 
 
 def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2):
     dWt = _empty(m2, K1, Ci, Co, 2, like=X)
-    call("blindno_mix_wgrad", ptr(X), ptr(G), ptr(dWt), Bn, Ci, Co, K1, m2, stream_ptr())
+    ns = query("blindno_mix_wgrad_nsplit", Bn, Ci, Co, K1, m2)
+    part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X) if ns > 1 else None
+    call("blindno_mix_wgrad", ptr(X), ptr(G), ptr(dWt), ptr(part) if part is not None else None, ns,
+         Bn, Ci, Co, K1, m2, stream_ptr())
     return dWt
 
 

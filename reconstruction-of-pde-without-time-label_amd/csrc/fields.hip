@@ -12,6 +12,7 @@
 // 1x1 conv and GELU happen once per point; per-row spectral coefficients are wave-uniform
 // and come through scalar loads.
 #include "common.h"
+#include "blindno.h"
 
 using namespace blindno;
 
@@ -385,13 +386,11 @@ __global__ __launch_bounds__(kBlock) void project_fwd_kernel(
   }
   __syncthreads();
   const int64_t HW = (int64_t)P1 * P2;
-  const int64_t total = (int64_t)Bn * Ho * Wo;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int w = (int)(idx % Wo);
-    const int64_t t = idx / Wo;
-    const int h = (int)(t % Ho);
-    const int n = (int)(t / Ho);
+  const unsigned total = (unsigned)((int64_t)Bn * Ho * Wo);
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const unsigned w = idx % (unsigned)Wo, t = idx / (unsigned)Wo;
+    const unsigned h = t % (unsigned)Ho, n = t / (unsigned)Ho;
     float zi[CM];
     const float* zp = z + (int64_t)n * C * HW + (int64_t)h * P2 + w;
 #pragma unroll
@@ -414,31 +413,34 @@ __global__ __launch_bounds__(kBlock) void project_fwd_kernel(
   }
 }
 
-// Backward for narrow fields (C <= 4): lanes = crop points (64-point tiles, coalesced), the
-// 16 waves of a 1024-thread workgroup split the hidden units (JW = Hd/16 each), so every lane
-// keeps its wave's weight gradients in registers for the whole kernel; dz of a tile is summed
-// over the waves through LDS.  The next tile's z / dout are prefetched into registers while
-// the current tile computes (double-buffered LDS).  One workgroup partial per parameter.
-template <int CM, int JW, int COM>
-__global__ __launch_bounds__(1024) void project_bwd_split_kernel(
+// Backward for narrow fields (C <= 16): lanes = crop points (64-point tiles, coalesced), the
+// 16 waves of a 1024-thread workgroup split the hidden units (JW each; gridDim.y workgroups
+// share a tile when 16 JW < Hd), so every lane keeps its wave's weight gradients in registers
+// for the whole kernel; dz of a tile is summed over the waves through LDS (and over the <= 2
+// hidden groups by an atomic add onto zeroed dz: two addends commute exactly, so the result
+// stays deterministic).  The next tile's z / dout are prefetched into registers while the
+// current tile computes (double-buffered LDS).  One workgroup partial per parameter.
+template <int CM, int JW, int COM, int NWV>
+__global__ __launch_bounds__(NWV * 64) void project_bwd_split_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
     float* __restrict__ partial, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd,
     int Cout, int ostride, int ooff, int dout_div) {
-  constexpr int NWV = 16;
   __shared__ float sz[2][CM][64], sg[2][COM][64], red[NWV][CM][64];
   __shared__ float sw1[NWV * JW][CM], sb1[NWV * JW], sw2[NWV * JW][COM];
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
-  const int j0 = wave * JW;
-  for (int e = threadIdx.x; e < Hd * CM; e += blockDim.x) {
+  constexpr int HB = NWV * JW;              // hidden units of this workgroup
+  const int jb = blockIdx.y * HB;
+  const int j0 = wave * JW;                  // local to the workgroup's hidden group
+  for (int e = threadIdx.x; e < HB * CM; e += blockDim.x) {
     const int j = e / CM, i = e % CM;
-    sw1[j][i] = i < C ? w1[j * C + i] : 0.f;
+    sw1[j][i] = i < C ? w1[(jb + j) * C + i] : 0.f;
   }
-  for (int e = threadIdx.x; e < Hd; e += blockDim.x) sb1[e] = b1[e];
-  for (int e = threadIdx.x; e < Hd * COM; e += blockDim.x) {
+  for (int e = threadIdx.x; e < HB; e += blockDim.x) sb1[e] = b1[jb + e];
+  for (int e = threadIdx.x; e < HB * COM; e += blockDim.x) {
     const int j = e / COM, c = e % COM;
-    sw2[j][c] = c < Cout ? w2[c * Hd + j] : 0.f;
+    sw2[j][c] = c < Cout ? w2[c * Hd + jb + j] : 0.f;
   }
   float gW1[JW][CM], gb1[JW], gW2[JW][COM], gb2[COM];
 #pragma unroll
@@ -456,27 +458,38 @@ __global__ __launch_bounds__(1024) void project_bwd_split_kernel(
   const int64_t ntiles = (npts + 63) / 64;
 
   // loader role: waves [0, CM) fetch one z channel, waves [CM, CM+COM) one dout channel
-  auto fetch = [&](int64_t tile) -> float {
-    const int64_t p = tile * 64 + lane;
-    if (tile >= ntiles || p >= npts || wave >= CM + COM) return 0.f;
-    const int w = (int)(p % Wo);
-    const int64_t r = p / Wo;
-    const int h = (int)(r % Ho);
-    const int n = (int)(r / Ho);
-    if (wave < CM) return wave < C ? z[(int64_t)n * C * HW + wave * HW + (int64_t)h * P2 + w] : 0.f;
-    const int c = wave - CM;
-    return c < Cout ? dout[((((int64_t)(n / dout_div)) * Ho + h) * Wo + w) * ostride + ooff + c] : 0.f;
+  // 32-bit point decomposition (npts < 2^31 is checked by the launcher)
+  auto zoff = [&](unsigned p, unsigned& n_out) -> int64_t {
+    const unsigned w = p % (unsigned)Wo, r = p / (unsigned)Wo;
+    const unsigned h = r % (unsigned)Ho, n = r / (unsigned)Ho;
+    n_out = n;
+    return (int64_t)n * C * HW + (int64_t)h * P2 + w;
   };
-  auto stash = [&](int buf, float v) {
-    if (wave < CM) sz[buf][wave][lane] = v;
-    else if (wave < CM + COM) sg[buf][wave - CM][lane] = v;
+  // loader rows r = wave, wave + 16, ...: rows [0, CM) are z channels, [CM, CM+COM) dout
+  constexpr int NR = (CM + COM + NWV - 1) / NWV;
+  auto fetch = [&](int64_t tile, int r) -> float {
+    const int64_t p = tile * 64 + lane;
+    if (tile >= ntiles || p >= npts || r >= CM + COM) return 0.f;
+    unsigned n;
+    const int64_t zo = zoff((unsigned)p, n);
+    if (r < CM) return r < C ? z[zo + r * HW] : 0.f;
+    const int c = r - CM;
+    const unsigned q = (unsigned)p % (unsigned)(Ho * Wo);
+    return c < Cout ? dout[((int64_t)(n / (unsigned)dout_div) * (Ho * Wo) + q) * ostride + ooff + c] : 0.f;
+  };
+  auto stash = [&](int buf, int r, float v) {
+    if (r < CM) sz[buf][r][lane] = v;
+    else if (r < CM + COM) sg[buf][r - CM][lane] = v;
   };
   int64_t tile = blockIdx.x;
-  stash(0, fetch(tile));
+#pragma unroll
+  for (int q = 0; q < NR; ++q) stash(0, wave + q * NWV, fetch(tile, wave + q * NWV));
   int buf = 0;
   for (; tile < ntiles; tile += gridDim.x, buf ^= 1) {
     __syncthreads();
-    const float pre = fetch(tile + gridDim.x);
+    float pre[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) pre[q] = fetch(tile + gridDim.x, wave + q * NWV);
     float zi[CM], gv[COM], dzp[CM];
 #pragma unroll
     for (int i = 0; i < CM; ++i) {
@@ -512,19 +525,19 @@ __global__ __launch_bounds__(1024) void project_bwd_split_kernel(
     }
 #pragma unroll
     for (int i = 0; i < CM; ++i) red[wave][i][lane] = dzp[i];
-    stash(buf ^ 1, pre);
+#pragma unroll
+    for (int q = 0; q < NR; ++q) stash(buf ^ 1, wave + q * NWV, pre[q]);
     __syncthreads();
-    if (wave < C) {
+    for (int i = wave; i < C; i += NWV) {
       const int64_t p = tile * 64 + lane;
       if (p < npts) {
         float s2 = 0.f;
 #pragma unroll
-        for (int wv = 0; wv < NWV; ++wv) s2 += red[wv][wave][lane];
-        const int w = (int)(p % Wo);
-        const int64_t r = p / Wo;
-        const int h = (int)(r % Ho);
-        const int n = (int)(r / Ho);
-        dz[(int64_t)n * C * HW + wave * HW + (int64_t)h * P2 + w] = s2;
+        for (int wv = 0; wv < NWV; ++wv) s2 += red[wv][i][lane];
+        unsigned n;
+        float* dst = dz + zoff((unsigned)p, n) + i * HW;
+        if (gridDim.y == 1) *dst = s2;
+        else atomicAdd(dst, s2);
       }
     }
   }
@@ -533,7 +546,7 @@ __global__ __launch_bounds__(1024) void project_bwd_split_kernel(
   float* pp = partial + (int64_t)blockIdx.x * np;
 #pragma unroll
   for (int q = 0; q < JW; ++q) {
-    const int j = j0 + q;
+    const int j = jb + j0 + q;
 #pragma unroll
     for (int i = 0; i < CM; ++i) {
       if (i >= C) continue;
@@ -551,7 +564,7 @@ __global__ __launch_bounds__(1024) void project_bwd_split_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  if (wave == 0) {
+  if (wave == 0 && blockIdx.y == 0) {
 #pragma unroll
     for (int c = 0; c < COM; ++c) {
       if (c >= Cout) continue;
@@ -561,150 +574,135 @@ __global__ __launch_bounds__(1024) void project_bwd_split_kernel(
   }
 }
 
-// Backward: lanes = hidden units (j = lane + 64 q), one batch of PB consecutive crop points
-// (wave-uniform, their z / dout in scalar registers) at a time.  Weight gradients accumulate
-// in each lane's registers for the whole kernel; dz of the batch is a sum over hidden units
-// = over lanes, done by a transpose through the wave's LDS slice.
-template <int CM, int JPL, int PB, int COM>
-__global__ __launch_bounds__(kBlock) void project_bwd_kernel(
+// Backward for wider fields (C > 4): lanes = crop points (64-point tiles), the 16 waves of a
+// 1024-thread workgroup split the hidden units (JW each); weight-gradient contributions of a
+// tile are summed over lanes (wave reduction) and accumulated in the wave's own LDS slots;
+// dz is summed over waves through LDS.  One workgroup partial per parameter at the end.
+template <int CM, int JW, int COM>
+__global__ __launch_bounds__(1024) void project_bwd_wsum_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
-    float* __restrict__ partial, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout,
-    int ostride, int ooff, int dout_div) {
-  extern __shared__ float sm[];
-  constexpr int NCOL = PB * CM;
-  constexpr int LD = NCOL + 1;
+    float* __restrict__ partial, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd,
+    int Cout, int ostride, int ooff, int dout_div) {
+  constexpr int NWV = 16;
+  constexpr int PJ = CM + 1 + COM;
+  extern __shared__ float smw[];
+  float* sz = smw;                          // [CM][64]
+  float* sg = sz + CM * 64;                 // [COM][64]
+  float* red = sg + COM * 64;               // [NWV][CM][64]
+  float* sw1 = red + NWV * CM * 64;         // [Hd][CM]
+  float* sb1 = sw1 + Hd * CM;               // [Hd]
+  float* sw2 = sb1 + Hd;                    // [Hd][COM]
+  float* acc = sw2 + Hd * COM;              // [Hd][PJ] then [COM]
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
-  float* red = sm + wave * 64 * LD;
+  const int j0 = wave * JW;
+  for (int e = threadIdx.x; e < Hd * CM; e += blockDim.x) {
+    const int j = e / CM, i = e % CM;
+    sw1[e] = i < C ? w1[j * C + i] : 0.f;
+  }
+  for (int e = threadIdx.x; e < Hd; e += blockDim.x) sb1[e] = b1[e];
+  for (int e = threadIdx.x; e < Hd * COM; e += blockDim.x) {
+    const int j = e / COM, c = e % COM;
+    sw2[e] = c < Cout ? w2[c * Hd + j] : 0.f;
+  }
+  for (int e = threadIdx.x; e < Hd * PJ + COM; e += blockDim.x) acc[e] = 0.f;
   const int64_t HW = (int64_t)P1 * P2;
-
-  float w1r[JPL][CM], b1r[JPL], w2r[JPL][COM];
-  float gW1[JPL][CM], gb1[JPL], gW2[JPL][COM], gb2[COM];
-#pragma unroll
-  for (int q = 0; q < JPL; ++q) {
-    const int j = lane + 64 * q;
-    b1r[q] = b1[j];
-    gb1[q] = 0.f;
+  const int64_t npts = (int64_t)Bn * Ho * Wo;
+  const int64_t ntiles = (npts + 63) / 64;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t p = tile * 64 + lane;
+    const bool ok = p < npts;
+    const unsigned pu = ok ? (unsigned)p : 0u;
+    const unsigned w = pu % (unsigned)Wo, r = pu / (unsigned)Wo;
+    const unsigned h = r % (unsigned)Ho, n = r / (unsigned)Ho;
+    const int64_t zo = (int64_t)n * C * HW + (int64_t)h * P2 + w;
+    __syncthreads();
+    for (int r = wave; r < CM + COM; r += NWV) {   // CM + COM rows over the 16 waves
+      if (r < CM) {
+        sz[r * 64 + lane] = (ok && r < C) ? z[zo + r * HW] : 0.f;
+      } else {
+        const int c = r - CM;
+        const unsigned q = pu % (unsigned)(Ho * Wo);
+        sg[c * 64 + lane] = (ok && c < Cout)
+            ? dout[((int64_t)(n / (unsigned)dout_div) * (Ho * Wo) + q) * ostride + ooff + c] : 0.f;
+      }
+    }
+    __syncthreads();
+    float zi[CM], gv[COM], dzp[CM];
 #pragma unroll
     for (int i = 0; i < CM; ++i) {
-      w1r[q][i] = i < C ? w1[j * C + i] : 0.f;
-      gW1[q][i] = 0.f;
+      zi[i] = sz[i * 64 + lane];
+      dzp[i] = 0.f;
     }
 #pragma unroll
-    for (int c = 0; c < COM; ++c) {
-      w2r[q][c] = c < Cout ? w2[c * Hd + j] : 0.f;
-      gW2[q][c] = 0.f;
-    }
-  }
+    for (int c = 0; c < COM; ++c) gv[c] = sg[c * 64 + lane];
+    for (int q = 0; q < JW; ++q) {
+      const int j = j0 + q;
+      const float* wj = sw1 + j * CM;
+      float hv = sb1[j];
 #pragma unroll
-  for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
-
-  const int nbr = (Wo + PB - 1) / PB;
-  const int64_t NB = (int64_t)Bn * Ho * nbr;
-  for (int64_t b = (int64_t)blockIdx.x * kWaves + wave; b < NB; b += (int64_t)gridDim.x * kWaves) {
-    const int n = (int)(b / ((int64_t)Ho * nbr));
-    const int rem = (int)(b % ((int64_t)Ho * nbr));
-    const int h = rem / nbr;
-    const int w0 = (rem % nbr) * PB;
-    float zv[PB][CM], gv[PB][COM];
-    const float* zp = z + (int64_t)n * C * HW + (int64_t)h * P2 + w0;
-    const float* dp = dout + ((((int64_t)(n / dout_div)) * Ho + h) * Wo + w0) * ostride + ooff;
+      for (int i = 0; i < CM; ++i) hv = fmaf(wj[i], zi[i], hv);
+      float a, dg;
+      gelu_both(hv, a, dg);
+      float da = 0.f;
 #pragma unroll
-    for (int p = 0; p < PB; ++p) {
-      const bool ok = w0 + p < Wo;
+      for (int c = 0; c < COM; ++c) da = fmaf(sw2[j * COM + c], gv[c], da);
+      const float dh = da * dg;
+      float* aj = acc + j * PJ;
 #pragma unroll
-      for (int i = 0; i < CM; ++i) zv[p][i] = (ok && i < C) ? zp[i * HW + p] : 0.f;
-#pragma unroll
-      for (int c = 0; c < COM; ++c) gv[p][c] = (ok && c < Cout) ? dp[p * ostride + c] : 0.f;
-    }
-    float dzp[PB][CM];
-#pragma unroll
-    for (int p = 0; p < PB; ++p)
-#pragma unroll
-      for (int i = 0; i < CM; ++i) dzp[p][i] = 0.f;
-#pragma unroll
-    for (int q = 0; q < JPL; ++q) {
-#pragma unroll
-      for (int p = 0; p < PB; ++p) {
-        float hv = b1r[q];
-#pragma unroll
-        for (int i = 0; i < CM; ++i) hv = fmaf(w1r[q][i], zv[p][i], hv);
-        float a, dg;
-        gelu_both(hv, a, dg);
-        float da = 0.f;
-#pragma unroll
-        for (int c = 0; c < COM; ++c) da = fmaf(w2r[q][c], gv[p][c], da);
-        const float dh = da * dg;
-#pragma unroll
-        for (int i = 0; i < CM; ++i) {
-          dzp[p][i] = fmaf(w1r[q][i], dh, dzp[p][i]);
-          gW1[q][i] = fmaf(dh, zv[p][i], gW1[q][i]);
+      for (int i = 0; i < CM; ++i) {
+        dzp[i] = fmaf(wj[i], dh, dzp[i]);
+        if (i < C) {
+          const float sv = wave_sum(dh * zi[i]);
+          if (lane == 0) aj[i] += sv;
         }
-        gb1[q] += dh;
+      }
+      const float sb = wave_sum(dh);
+      if (lane == 0) aj[CM] += sb;
 #pragma unroll
-        for (int c = 0; c < COM; ++c) gW2[q][c] = fmaf(gv[p][c], a, gW2[q][c]);
+      for (int c = 0; c < COM; ++c) {
+        if (c >= Cout) continue;
+        const float sv = wave_sum(gv[c] * a);
+        if (lane == 0) aj[CM + 1 + c] += sv;
+      }
+    }
+    if (wave == 0) {
+#pragma unroll
+      for (int c = 0; c < COM; ++c) {
+        if (c >= Cout) continue;
+        const float sv = wave_sum(gv[c]);
+        if (lane == 0) acc[Hd * PJ + c] += sv;
       }
     }
 #pragma unroll
-    for (int p = 0; p < PB; ++p)
+    for (int i = 0; i < CM; ++i) red[(wave * CM + i) * 64 + lane] = dzp[i];
+    __syncthreads();
+    for (int i = wave; i < C; i += NWV) {
+      if (ok) {
+        float s2 = 0.f;
 #pragma unroll
-      for (int c = 0; c < COM; ++c) gb2[c] += gv[p][c];
-    // dz for the batch: column sums of the 64 x NCOL lane partials
-#pragma unroll
-    for (int p = 0; p < PB; ++p)
-#pragma unroll
-      for (int i = 0; i < CM; ++i) red[lane * LD + p * CM + i] = dzp[p][i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (NCOL <= 32) {
-      const int col = lane & 31, half = lane >> 5;
-      float s = 0.f;
-      if (col < NCOL)
-        for (int r = half * 32; r < half * 32 + 32; ++r) s += red[r * LD + col];
-      s += __shfl_xor(s, 32, 64);
-      if (half == 0 && col < NCOL) {
-        const int p = col / CM, i = col % CM;
-        if (i < C && w0 + p < Wo) dz[(int64_t)n * C * HW + i * HW + (int64_t)h * P2 + w0 + p] = s;
-      }
-    } else {
-      for (int col = lane; col < NCOL; col += 64) {
-        float s = 0.f;
-        for (int r = 0; r < 64; ++r) s += red[r * LD + col];
-        const int p = col / CM, i = col % CM;
-        if (i < C && w0 + p < Wo) dz[(int64_t)n * C * HW + i * HW + (int64_t)h * P2 + w0 + p] = s;
+        for (int wv = 0; wv < NWV; ++wv) s2 += red[(wv * CM + i) * 64 + lane];
+        dz[zo + i * HW] = s2;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // block reduction of the per-lane weight-gradient registers
   __syncthreads();
   const int np = Hd * C + Hd + Cout * Hd + Cout;
-  float* slot = sm + wave * np;
-#pragma unroll
-  for (int q = 0; q < JPL; ++q) {
-    const int j = lane + 64 * q;
-#pragma unroll
-    for (int i = 0; i < CM; ++i)
-      if (i < C) slot[j * C + i] = gW1[q][i];
-    slot[Hd * C + j] = gb1[q];
-#pragma unroll
-    for (int c = 0; c < COM; ++c)
-      if (c < Cout) slot[Hd * C + Hd + c * Hd + j] = gW2[q][c];
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < COM; ++c)
-      if (c < Cout) slot[Hd * C + Hd + Cout * Hd + c] = gb2[c];
-  }
-  __syncthreads();
-  for (int p = threadIdx.x; p < np; p += blockDim.x) {
-    float s = 0.f;
-    for (int w = 0; w < kWaves; ++w) s += sm[w * np + p];
-    partial[(int64_t)blockIdx.x * np + p] = s;
+  float* pp = partial + (int64_t)blockIdx.x * np;
+  for (int e = threadIdx.x; e < np; e += blockDim.x) {
+    float v;
+    if (e < Hd * C) {
+      v = acc[(e / C) * PJ + e % C];
+    } else if (e < Hd * C + Hd) {
+      v = acc[(e - Hd * C) * PJ + CM];
+    } else if (e < Hd * C + Hd + Cout * Hd) {
+      const int q = e - Hd * C - Hd;
+      v = acc[(q % Hd) * PJ + CM + 1 + q / Hd];
+    } else {
+      v = acc[Hd * PJ + (e - Hd * C - Hd - Cout * Hd)];
+    }
+    pp[e] = v;
   }
 }
 
@@ -981,7 +979,8 @@ BLINDNO_API int blindno_project_fwd(const float* z, const float* w1, const float
                                     const float* w2, const float* b2, float* out, int Bn, int C,
                                     int P1, int P2, int Ho, int Wo, int Hd, int Cout,
                                     int ostride, int ooff, void* stream) {
-  if (Ho > P1 || Wo > P2 || C > 32 || Cout > 4) return (int)hipErrorInvalidValue;
+  if (Ho > P1 || Wo > P2 || C > 32 || Cout > 4 || (int64_t)Bn * Ho * Wo >= INT32_MAX)
+    return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)Bn * Ho * Wo;
   const dim3 g(grid_for(total, kBlock, 2048));
   hipStream_t st = (hipStream_t)stream;
@@ -1012,53 +1011,51 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
                                     float* partial, int nchunk, int Bn, int C, int P1, int P2,
                                     int Ho, int Wo, int Hd, int Cout, int ostride, int ooff,
                                     int dout_div, void* stream) {
-  if (Ho > P1 || Wo > P2 || dout_div < 1 || Hd % 64 != 0 || C > 32 || Cout > 4 || !dz ||
-      !partial || nchunk < 1)
+  if (Ho > P1 || Wo > P2 || dout_div < 1 || C > 32 || Cout > 4 || !dz || !partial ||
+      nchunk < 1 || (int64_t)Bn * Ho * Wo >= INT32_MAX)
     return (int)hipErrorInvalidValue;
-  const int jpl = Hd / 64;
-  if (jpl != 1 && jpl != 2 && jpl != 4) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const int np = Hd * C + Hd + Cout * Hd + Cout;
   const dim3 g(nchunk);
-  if (C <= 4 && Hd == 128) {
-    if (Cout == 1)
-      project_bwd_split_kernel<4, 8, 1><<<g, 1024, 0, st>>>(z, w1, b1, w2, dout, dz, partial, Bn, C,
-                                                            P1, P2, Ho, Wo, Hd, Cout, ostride,
-                                                            ooff, dout_div);
-    else
-      project_bwd_split_kernel<4, 8, 4><<<g, 1024, 0, st>>>(z, w1, b1, w2, dout, dz, partial, Bn, C,
-                                                            P1, P2, Ho, Wo, Hd, Cout, ostride,
-                                                            ooff, dout_div);
+  // register-resident weight gradients: C <= 4 -> 8 hidden units per wave (one group);
+  // C <= 16 -> 4 per wave, two hidden groups (dz summed by a two-addend atomic, exact)
+  if (Hd == 128 && Cout == 1 && C <= 12) {
+    if (C <= 4) {
+      project_bwd_split_kernel<4, 8, 1, 16><<<g, 1024, 0, st>>>(z, w1, b1, w2, dout, dz, partial,
+                                                                Bn, C, P1, P2, Ho, Wo, Hd, Cout,
+                                                                ostride, ooff, dout_div);
+    } else {
+      // 8 waves x 8 hidden units = 64 per workgroup, two hidden groups
+      const dim3 g2(nchunk, 2);
+#define PS(CM_)                                                                               \
+  project_bwd_split_kernel<CM_, 8, 1, 8><<<g2, 512, 0, st>>>(z, w1, b1, w2, dout, dz, partial, \
+                                                             Bn, C, P1, P2, Ho, Wo, Hd, Cout,  \
+                                                             ostride, ooff, dout_div)
+      if (C <= 8) PS(8);
+      else PS(12);
+#undef PS
+    }
     return (int)hipGetLastError();
   }
-#define PB_LAUNCH(CM_, JPL_, PB_, CO_)                                                        \
-  {                                                                                           \
-    size_t sh = sizeof(float) * (size_t)kWaves * 64 * (PB_ * CM_ + 1);                        \
-    const size_t need = sizeof(float) * (size_t)kWaves * np;                                  \
-    if (need > sh) sh = need;                                                                 \
-    project_bwd_kernel<CM_, JPL_, PB_, CO_><<<g, kBlock, sh, st>>>(                           \
-        z, w1, b1, w2, dout, dz, partial, Bn, C, P1, P2, Ho, Wo, Hd, Cout, ostride, ooff,     \
-        dout_div);                                                                            \
-  }
-#define PB_CO(CM_, JPL_, PB_)                    \
-  if (Cout == 1) PB_LAUNCH(CM_, JPL_, PB_, 1)    \
-  else PB_LAUNCH(CM_, JPL_, PB_, 4)
-#define PB_JPL(CM_, PB_)                      \
-  if (jpl == 2) { PB_CO(CM_, 2, PB_) }        \
-  else if (jpl == 1) { PB_CO(CM_, 1, PB_) }   \
-  else { PB_CO(CM_, 4, PB_) }
-  if (C <= 4) {
-    PB_JPL(4, 8)
-  } else if (C <= 8) {
-    PB_JPL(8, 4)
-  } else if (C <= 16) {
-    PB_JPL(16, 4)
+  if (Hd != 128) return (int)hipErrorInvalidValue;   // fc1 = Linear(width, 128) everywhere
+  const int cm = C <= 8 ? 8 : (C <= 16 ? 16 : 32);
+  const int com = Cout == 1 ? 1 : 4;
+  const size_t sh = sizeof(float) * ((size_t)cm * 64 + com * 64 + 16 * (size_t)cm * 64 +
+                                     (size_t)Hd * cm + Hd + (size_t)Hd * com +
+                                     (size_t)Hd * (cm + 1 + com) + com);
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+#define PW(CM_, CO_)                                                                        \
+  project_bwd_wsum_kernel<CM_, 8, CO_><<<g, 1024, sh, st>>>(z, w1, b1, w2, dout, dz, partial, \
+                                                           Bn, C, P1, P2, Ho, Wo, Hd, Cout,   \
+                                                           ostride, ooff, dout_div)
+  if (cm == 8) {
+    if (com == 1) PW(8, 1); else PW(8, 4);
+  } else if (cm == 16) {
+    if (com == 1) PW(16, 1); else PW(16, 4);
   } else {
-    PB_JPL(32, 2)
+    if (com == 1) PW(32, 1); else PW(32, 4);
   }
-#undef PB_JPL
-#undef PB_CO
-#undef PB_LAUNCH
+#undef PW
   return (int)hipGetLastError();
 }
 

@@ -9,6 +9,7 @@
 // fields.hip: inverse row DFT + epilogue); the column transforms and the mix work on the
 // m2/P2-sized row spectra and run one workgroup per (sample, column mode).
 #include "common.h"
+#include "blindno.h"
 
 using namespace blindno;
 
@@ -96,137 +97,204 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
 }
 
 // ------------------------------------------------------------------------------ column pass
-// One workgroup per (n, k).  DIR 0 (forward):  X = coldft(At) (saved), Y = mix(X, W),
-//   Z[n][h][k][c] = c_k/(P1 P2) * colidft(Y).
-// DIR 1 (adjoint):  G = c_k/(P1 P2) * coldft(At) (saved, the gradient of the spectrum),
-//   GX = mix^H(G, W), Z = colidft(GX).
-// colidft/coldft run over the K1 kept frequency rows r_j (kept_row); the phase r h mod P1
-// is advanced incrementally, twiddles come from an LDS copy of tw1[P1].
+// The column transforms are two complex GEMMs against the shared twiddle matrix
+// F[h][j] = e^{-2 pi i r_j h / P1} (r_j the K1 kept frequency rows), on the f32 matrix cores
+// (v_mfma_f32_16x16x4f32, four real MFMAs per complex step), with the per-mode channel mix
+// fused behind the first one:
+//   coldft_mix:  X[q][c][j] = sum_h At[q][c][h] F[h][j]          (q = n m2 + k, the pair)
+//                DIR 0: Xs = X (saved),        Y[q][o][j] = c_k/(P1 P2) sum_c X W[k][j][c][o]
+//                DIR 1: Xs = c_k/(P1 P2) X = G, Y[q][i][j] = sum_o conj(W[k][j][i][o]) G
+//   colidft:     Z[n][h][k][o] = sum_j Y[q][o][j] conj(F[h][j])
+// Y is a K1p = 16 ceil(K1/16) padded scratch spectrum.  Both GEMMs take their B operand from
+// host-built twiddle images in MFMA lane order (one 32-byte load per lane and k-block) and
+// permute the k order inside each 16-block exactly like the row DFT (k = 16 kb + 4 kq + s),
+// so every lane streams 4 consecutive complex A values.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void cmfma4(const float (&ar)[4], const float (&ai)[4],
+                                       const f32x4& b0, const f32x4& b1, f32x4& dr, f32x4& di) {
+  const float br[4] = {b0.x, b0.z, b1.x, b1.z};
+  const float bi[4] = {b0.y, b0.w, b1.y, b1.w};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    dr = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[s], br[s], dr, 0, 0, 0);
+    dr = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai[s], bi[s], dr, 0, 0, 0);
+    di = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[s], bi[s], di, 0, 0, 0);
+    di = __builtin_amdgcn_mfma_f32_16x16x4f32(ai[s], br[s], di, 0, 0, 0);
+  }
+}
+
+// 4 consecutive complex values src[0..3] (zero past len) split into re / im
+__device__ __forceinline__ void load4c(const float2* src, int len, bool vec, float (&re)[4],
+                                       float (&im)[4]) {
+  if (vec && len >= 4) {
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(src + 2);
+    re[0] = v0.x; im[0] = v0.y; re[1] = v0.z; im[1] = v0.w;
+    re[2] = v1.x; im[2] = v1.y; re[3] = v1.z; im[3] = v1.w;
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float2 v = s < len ? src[s] : make_float2(0.f, 0.f);
+      re[s] = v.x;
+      im[s] = v.y;
+    }
+  }
+}
+
 template <int DIR>
-__global__ __launch_bounds__(kBlock) void colpass_kernel(const float2* __restrict__ At,
+__global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restrict__ At,
                                                          const float2* __restrict__ Wt,
+                                                         const f32x4* __restrict__ FB,
                                                          float2* __restrict__ Xs,
-                                                         float2* __restrict__ Z,
-                                                         const float2* __restrict__ tw1, int Ci,
-                                                         int Co, int P1, int m1, int m2, int P2) {
-  extern __shared__ float2 sm[];
+                                                         float2* __restrict__ Y, int npairs,
+                                                         int Ci, int Co, int P1, int m1, int m2,
+                                                         int P2, int G, int vec) {
+  extern __shared__ float2 sX[];                  // [G Cin][K1p + 1]
   const int K1 = kept_rows_count(m1, P1);
+  const int Jt = (K1 + 15) >> 4, K1p = Jt * 16, LDX = K1p + 1;
   const int Cin = DIR == 0 ? Ci : Co;
   const int Cout = DIR == 0 ? Co : Ci;
-  float2* stw = sm;
-  float2* sA = stw + P1;
-  float2* sX = sA + Cin * P1;
-  float2* sY = sX + Cin * K1;
-  const int n = blockIdx.x / m2, k = blockIdx.x % m2;
-  const int t = threadIdx.x;
-  const float ck = c2r_weight(k, P2) / ((float)P1 * (float)P2);
+  const int HB = (P1 + 15) >> 4;
+  const int q0 = blockIdx.x * G;
+  const int np = min(G, npairs - q0);
+  const int rows = np * Cin;
+  const int Mt = (rows + 15) >> 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int r16 = lane & 15, kq = lane >> 4;
+  const float inv = 1.0f / ((float)P1 * (float)P2);
 
-  for (int i = t; i < P1; i += blockDim.x) stw[i] = tw1[i];
-  const float2* src = At + ((int64_t)n * m2 + k) * Cin * P1;
-  for (int i = t; i < Cin * P1; i += blockDim.x) sA[i] = src[i];
-  __syncthreads();
-
-  // column DFT at the kept rows
-  float2* xs = Xs + ((int64_t)n * m2 + k) * Cin * K1;
-  for (int o = t; o < Cin * K1; o += blockDim.x) {
-    const int c = o / K1, j = o % K1;
-    const int r = kept_row(j, K1, m1, P1);
-    const float2* a = sA + c * P1;
-    float re = 0.f, im = 0.f;
-    int ph = 0;
-    for (int h = 0; h < P1; ++h) {
-      const float2 v = a[h];
-      const float2 e = stw[ph];
-      re = fmaf(v.x, e.x, fmaf(v.y, e.y, re));    // v * conj(e)
-      im = fmaf(v.y, e.x, fmaf(-v.x, e.y, im));
-      ph += r;
-      if (ph >= P1) ph -= P1;
+  for (int item = wave; item < Mt * Jt; item += 4) {
+    const int mt = item / Jt, jt = item % Jt;
+    const int row = mt * 16 + r16;
+    const bool rok = row < rows;
+    const float2* ar = At + ((int64_t)q0 * Cin + (rok ? row : 0)) * P1;
+    const f32x4* fb = FB + ((int64_t)jt * HB * 64 + lane) * 2;
+    f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
+    for (int hb = 0; hb < HB; ++hb) {
+      const int h0 = hb * 16 + kq * 4;
+      float re[4], im[4];
+      load4c(ar + h0, rok ? P1 - h0 : 0, vec, re, im);
+      cmfma4(re, im, fb[hb * 128], fb[hb * 128 + 1], dr, di);
     }
-    if (DIR == 1) {
-      re *= ck;
-      im *= ck;
+    const int j = jt * 16 + r16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int orow = mt * 16 + kq * 4 + r;
+      if (orow >= rows) continue;
+      float sc = 1.0f;
+      if (DIR == 1) sc = c2r_weight((q0 + orow / Cin) % m2, P2) * inv;
+      const float2 v = make_float2(dr[r] * sc, di[r] * sc);
+      sX[orow * LDX + j] = v;
+      if (j < K1) Xs[((int64_t)q0 * Cin + orow) * K1 + j] = v;
     }
-    const float2 v = make_float2(re, im);
-    sX[o] = v;
-    xs[o] = v;
   }
   __syncthreads();
 
-  // per-mode channel mix
-  const float2* wk = Wt + (int64_t)k * K1 * Ci * Co;
-  for (int o = t; o < Cout * K1; o += blockDim.x) {
-    const int oc = o % Cout, j = o / Cout;
-    const float2* wj = wk + (int64_t)j * Ci * Co;
+  const int nout = np * Cout * K1p;
+  for (int e = threadIdx.x; e < nout; e += blockDim.x) {
+    const int j = e % K1p;
+    const int t = e / K1p;
+    const int o = t % Cout, p = t / Cout;
+    const int k = (q0 + p) % m2;
     float re = 0.f, im = 0.f;
-    for (int q = 0; q < Cin; ++q) {
-      const float2 a = sX[q * K1 + j];
+    if (j < K1) {
+      const float2* wj = Wt + ((int64_t)k * K1 + j) * Ci * Co;
+      const float2* xp = sX + p * Cin * LDX + j;
+      for (int c = 0; c < Cin; ++c) {
+        const float2 a = xp[c * LDX];
+        if (DIR == 0) {
+          const float2 w = wj[c * Co + o];
+          re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
+          im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
+        } else {
+          const float2 w = wj[o * Co + c];            // conj(w) * a
+          re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
+          im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+        }
+      }
       if (DIR == 0) {
-        const float2 w = wj[q * Co + oc];
-        re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
-        im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
-      } else {
-        const float2 w = wj[oc * Co + q];              // conj(w) * a
-        re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
-        im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+        const float sc = c2r_weight(k, P2) * inv;
+        re *= sc;
+        im *= sc;
       }
     }
-    sY[oc * K1 + j] = make_float2(re, im);
+    Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
+  }
+}
+
+// Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
+// tile, 64 spectrum rows (k, o)); one 16-row MFMA tile per wave; the result is transposed
+// through LDS so that each h row of Z is written as one contiguous run.
+__global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__ Y,
+                                                      const f32x4* __restrict__ GB,
+                                                      float2* __restrict__ Z, int Cout, int P1,
+                                                      int m1, int m2) {
+  __shared__ float2 sZ[16][65];
+  const int K1 = kept_rows_count(m1, P1);
+  const int Jt = (K1 + 15) >> 4, K1p = Jt * 16;
+  const int Ht = (P1 + 15) >> 4;
+  const int R = m2 * Cout;
+  const int Mt = (R + 15) >> 4;
+  const int n = blockIdx.x / Ht, ht = blockIdx.x % Ht;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int mt = blockIdx.y * 4 + wave;
+  if (mt < Mt) {
+    const int row = mt * 16 + r16;
+    const bool rok = row < R;
+    const float2* yr = Y + ((int64_t)n * R + (rok ? row : 0)) * K1p;
+    const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
+    f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
+    for (int jb = 0; jb < Jt; ++jb) {
+      float re[4], im[4];
+      load4c(yr + jb * 16 + kq * 4, rok ? 4 : 0, true, re, im);
+      cmfma4(re, im, gb[jb * 128], gb[jb * 128 + 1], dr, di);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sZ[r16][wave * 16 + kq * 4 + r] = make_float2(dr[r], di[r]);
   }
   __syncthreads();
-
-  // column inverse at the kept rows -> Z[n][h][k][c]
-  const float s = DIR == 0 ? ck : 1.0f;
-  const int split = (K1 == P1) ? K1 : m1;         // rows j < split have r_j = j
-  for (int o = t; o < P1 * Cout; o += blockDim.x) {
-    const int c = o % Cout, h = o / Cout;
-    const float2* y = sY + c * K1;
-    float re = 0.f, im = 0.f;
-    int ph = 0;
-    for (int j = 0; j < split; ++j) {
-      const float2 a = y[j];
-      const float2 e = stw[ph];
-      re = fmaf(a.x, e.x, fmaf(-a.y, e.y, re));
-      im = fmaf(a.x, e.y, fmaf(a.y, e.x, im));
-      ph += h;
-      if (ph >= P1) ph -= P1;
-    }
-    if (split < K1) {
-      ph = (int)(((int64_t)(P1 - m1) * h) % P1);
-      for (int j = split; j < K1; ++j) {
-        const float2 a = y[j];
-        const float2 e = stw[ph];
-        re = fmaf(a.x, e.x, fmaf(-a.y, e.y, re));
-        im = fmaf(a.x, e.y, fmaf(a.y, e.x, im));
-        ph += h;
-        if (ph >= P1) ph -= P1;
-      }
-    }
-    Z[(((int64_t)n * P1 + h) * m2 + k) * Cout + c] = make_float2(re * s, im * s);
+  const int row0 = blockIdx.y * 64;
+  for (int e = threadIdx.x; e < 16 * 64; e += blockDim.x) {
+    const int hl = e >> 6, rl = e & 63;
+    const int h = ht * 16 + hl, row = row0 + rl;
+    if (h < P1 && row < R) Z[((int64_t)n * P1 + h) * R + row] = sZ[hl][rl];
   }
 }
 
 // dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]
 __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restrict__ X,
                                                            const float2* __restrict__ G,
-                                                           float2* __restrict__ dWt, int Bn,
+                                                           float2* __restrict__ out, int Bn,
                                                            int Ci, int Co, int K1, int m2) {
-  const int64_t total = (int64_t)m2 * K1 * Ci * Co;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int o = (int)(idx % Co);
-    int64_t t = idx / Co;
-    const int i = (int)(t % Ci);
+  // blockIdx.y = sample slice: out[y][idx] = sum over this slice's samples (partials when
+  // gridDim.y > 1, reduced in fixed order afterwards)
+  const int total = m2 * K1 * Ci * Co;
+  const int ns = (Bn + gridDim.y - 1) / gridDim.y;
+  const int n0 = blockIdx.y * ns, n1 = min(Bn, n0 + ns);
+  const int sX = m2 * Ci * K1, sG = m2 * Co * K1;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int o = idx % Co;
+    int t = idx / Co;
+    const int i = t % Ci;
     t /= Ci;
-    const int j = (int)(t % K1);
-    const int k = (int)(t / K1);
+    const int j = t % K1;
+    const int k = t / K1;
+    const float2* xp = X + ((int64_t)n0 * m2 + k) * Ci * K1 + i * K1 + j;
+    const float2* gp = G + ((int64_t)n0 * m2 + k) * Co * K1 + o * K1 + j;
     float re = 0.f, im = 0.f;
-    for (int n = 0; n < Bn; ++n) {
-      const float2 a = X[(((int64_t)n * m2 + k) * Ci + i) * K1 + j];
-      const float2 g = G[(((int64_t)n * m2 + k) * Co + o) * K1 + j];
+#pragma unroll 4
+    for (int n = n0; n < n1; ++n, xp += sX, gp += sG) {
+      const float2 a = *xp;
+      const float2 g = *gp;
       re = fmaf(a.x, g.x, fmaf(a.y, g.y, re));
       im = fmaf(a.x, g.y, fmaf(-a.y, g.x, im));
     }
-    dWt[idx] = make_float2(re, im);
+    out[(int64_t)blockIdx.y * total + idx] = make_float2(re, im);
   }
 }
 
@@ -389,33 +457,71 @@ BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int B
   return (int)hipGetLastError();
 }
 
-BLINDNO_API int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Z,
-                                const float* tw1, int Bn, int Ci, int Co, int P1, int m1, int m2,
-                                int P2, int dir, void* stream) {
-  if (m1 <= 0 || m1 > P1 || m2 > P2 / 2 + 1) return (int)hipErrorInvalidValue;
+BLINDNO_API int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
+                                const float* FB, const float* GB, int Bn, int Ci, int Co, int P1,
+                                int m1, int m2, int P2, int dir, void* stream) {
+  if (Bn <= 0 || m1 <= 0 || m1 > P1 || m2 <= 0 || m2 > P2 / 2 + 1 || (dir != 0 && dir != 1))
+    return (int)hipErrorInvalidValue;
   const int K1 = kept_rows_count(m1, P1);
+  const int Jt = (K1 + 15) / 16, K1p = Jt * 16;
   const int cin = dir == 0 ? Ci : Co, cout = dir == 0 ? Co : Ci;
-  const size_t sh = sizeof(float2) * ((size_t)P1 + (size_t)cin * P1 + (size_t)cin * K1 +
-                                      (size_t)cout * K1);
+  const int64_t npairs = (int64_t)Bn * m2;
+  if (npairs * (cin > cout ? cin : cout) * (P1 > K1p ? P1 : K1p) >= INT32_MAX)
+    return (int)hipErrorInvalidValue;
+  // pairs per workgroup: enough 16-row tiles for the four waves, tiles filled
+  int G = 1;
+  while (((G * cin + 15) / 16) * Jt < 4 && G * cin < 64) ++G;
+  G = ((G * cin + 15) / 16) * 16 / cin;
+  if (G < 1) G = 1;
+  const size_t sh = sizeof(float2) * (size_t)G * cin * (K1p + 1);
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
-  dim3 g(Bn * m2);
+  const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
   hipStream_t st = (hipStream_t)stream;
+  const dim3 g1((unsigned)cdiv(npairs, G));
   if (dir == 0)
-    colpass_kernel<0><<<g, kBlock, sh, st>>>((const float2*)At, (const float2*)Wt, (float2*)Xs,
-                                             (float2*)Z, (const float2*)tw1, Ci, Co, P1, m1, m2,
-                                             P2);
+    coldft_mix_kernel<0><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,
+                                              (const f32x4*)FB, (float2*)Xs, (float2*)Y,
+                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec);
   else
-    colpass_kernel<1><<<g, kBlock, sh, st>>>((const float2*)At, (const float2*)Wt, (float2*)Xs,
-                                             (float2*)Z, (const float2*)tw1, Ci, Co, P1, m1, m2,
-                                             P2);
+    coldft_mix_kernel<1><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,
+                                              (const f32x4*)FB, (float2*)Xs, (float2*)Y,
+                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec);
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  const int Ht = (P1 + 15) / 16;
+  const int Mt = (m2 * cout + 15) / 16;
+  const dim3 g2((unsigned)(Bn * Ht), (unsigned)((Mt + 3) / 4));
+  colidft_kernel<<<g2, 256, 0, st>>>((const float2*)Y, (const f32x4*)GB, (float2*)Z, cout, P1, m1,
+                                     m2);
   return (int)hipGetLastError();
 }
 
-BLINDNO_API int blindno_mix_wgrad(const float* X, const float* G, float* dWt, int Bn, int Ci,
-                                  int Co, int K1, int m2, void* stream) {
+BLINDNO_API int blindno_mix_wgrad_nsplit(int Bn, int Ci, int Co, int K1, int m2) {
   const int64_t total = (int64_t)m2 * K1 * Ci * Co;
-  mix_wgrad_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, (hipStream_t)stream>>>(
-      (const float2*)X, (const float2*)G, (float2*)dWt, Bn, Ci, Co, K1, m2);
+  const int64_t bx = cdiv(total, kBlock);
+  int64_t ns = cdiv(2048, bx);                 // aim at >= 2048 workgroups
+  const int64_t per = cdiv(Bn, 8);             // but >= 8 samples per slice
+  if (ns > per) ns = per;
+  if (ns < 1) ns = 1;
+  return (int)(ns > 1024 ? 1024 : ns);
+}
+
+BLINDNO_API int blindno_mix_wgrad(const float* X, const float* G, float* dWt, float* partial,
+                                  int nsplit, int Bn, int Ci, int Co, int K1, int m2,
+                                  void* stream) {
+  const int64_t total = (int64_t)m2 * K1 * Ci * Co;
+  if (total >= INT32_MAX / 2 || nsplit < 1 || (nsplit > 1 && !partial))
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((unsigned)cdiv(total, kBlock), nsplit);
+  mix_wgrad_kernel<<<g, kBlock, 0, st>>>((const float2*)X, (const float2*)G,
+                                         (float2*)(nsplit > 1 ? partial : dWt), Bn, Ci, Co, K1,
+                                         m2);
+  if (nsplit > 1) {
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+    return blindno_reduce_partials(partial, dWt, nsplit, (int)(2 * total), stream);
+  }
   return (int)hipGetLastError();
 }
 
