@@ -194,6 +194,25 @@ int blindno_adam(float* p, const float* g, float* m, float* v, int64_t n, float 
                  float beta2, float eps, float step_size, float bc2s, float gscale,
                  blindno_stream_t stream);
 
+/* --- density evaluators (fp64) ----------------------------------------------------------- */
+
+/* Batched 1D GPE split-step pseudo-spectral solver, one workgroup per trajectory
+ * (solve_GPE_custom, 1d_GPE/datagen_GPE.py:86-115; steps :29-81).  psi0 (Nx complex, or
+ * B x Nx when psi0_batched), V (B, Nx), g/kappa (B); order 2 = Strang, 4 = Yoshida;
+ * k = 2 pi fftfreq(Nx, dx).  Records psi at steps n = 0, rec_every, 2 rec_every, ... (n <=
+ * nsteps): rec_abs (B, nrec, Nx) |psi| and/or rec_psi (B, nrec, Nx) complex, nrec =
+ * nsteps/rec_every + 1 (either may be NULL); psi_out (B, Nx) complex final state (may be
+ * NULL).  Nx must be a power of two <= 2048. */
+int blindno_gpe_solve(const double* psi0, const double* V, const double* g, const double* kappa,
+                      double dx, double dt, int nsteps, int order, int rec_every, double* rec_abs,
+                      double* rec_psi, double* psi_out, int B, int Nx, int psi0_batched,
+                      blindno_stream_t stream);
+
+/* Trapezoid-rule spatial integrals of time_averaged_L2_error (1d_FPE/compute_time_error.py:
+ * 268-275): out[2r] = trapz((a_r - b_r)^2, x), out[2r+1] = trapz(b_r^2, x), rows of n. */
+int blindno_trapz_rows(const double* a, const double* b, const double* x, double* out, int rows,
+                       int n, blindno_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

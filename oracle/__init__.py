@@ -19,3 +19,4 @@ importing the reference itself in the build container
 ``tests/test_oracle_golden.py``.
 """
 from .fno_ref import *  # noqa: F401,F403
+from . import gpe_ref  # noqa: F401,E402

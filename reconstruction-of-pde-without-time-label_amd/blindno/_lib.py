@@ -16,7 +16,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BLINDNO_LIB", os.path.join(_HERE, "libblindno.so"))
 
-# argument codes: p pointer, i int32, l int64, f float, s stream
+# argument codes: p pointer, i int32, l int64, f float, d double, s stream
 SIGNATURES = {
     "blindno_abi_version": "",
     "blindno_lift_fwd": "ppppiiiiiiis",
@@ -39,6 +39,8 @@ SIGNATURES = {
     "blindno_mse": "pppplips",
     "blindno_rowsq": "pppiiiiiis",
     "blindno_adam": "pppplffffffs",
+    "blindno_gpe_solve": "ppppddiiipppiiis",
+    "blindno_trapz_rows": "ppppiis",
     # size queries (return a count, not an error code)
     "blindno_lift_bwd_nchunk": "iii",
     "blindno_conv_wgrad_nchunk": "iii",
@@ -48,7 +50,7 @@ SIGNATURES = {
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,
-       "s": ctypes.c_void_p}
+       "d": ctypes.c_double, "s": ctypes.c_void_p}
 
 _lock = threading.Lock()
 _lib = None

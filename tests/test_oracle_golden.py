@@ -159,3 +159,31 @@ def test_metrics():
     g = load_golden("metric_time_avg_L2_1d")
     v = oracle.time_averaged_L2_error(g["t"], g["rho_ref"], g["t"], g["rho_pred"], g["x"])
     assert abs(v - float(g["val"])) <= 1e-12
+
+
+def test_gpe_solver_oracle():
+    """oracle.gpe_ref (explicit DFT) vs the reference's numpy-FFT solver (a14)."""
+    from oracle import gpe_ref
+    for order in (2, 4):
+        g = load_golden(f"gpe_solve_o{order}")
+        x = g["x"]
+        t, rec = gpe_ref.solve(gpe_ref.initial_condition(2, x), x, float(g["dt"]), float(g["t_final"]), order,
+                               float(g["g"]), float(g["kappa"]), g["V"])
+        assert np.allclose(t, g["t"])
+        assert rel_l2(rec, g["psi"]) <= 1e-11, (order, rel_l2(rec, g["psi"]))
+    g = load_golden("gpe_solve_ic")
+    x = np.linspace(-10, 10, 32)
+    for ic in (1, 3):
+        _, rec = gpe_ref.solve(gpe_ref.initial_condition(ic, x), x, 0.01, 0.2, 2, 1.0, 0.5, g[f"V_ic{ic}"])
+        assert rel_l2(rec, g[f"psi_ic{ic}"]) <= 1e-11
+
+
+def test_gpe_datagen_oracle():
+    from oracle import gpe_ref
+    g = load_golden("gpe_datagen")
+    x = np.linspace(-10, 10, 128)
+    rng = np.random.RandomState(int(g["seed"]))
+    V = gpe_ref.training_potentials(3, x, 1001, rng=rng)
+    assert np.array_equal(V, g["V"])
+    _, rec = gpe_ref.solve(gpe_ref.initial_condition(2, x), x, 0.005, 5.0, 2, 2.0, 2.0, V[0])
+    assert rel_l2(np.abs(rec)[::10], g["y"][0]) <= 1e-10
