@@ -27,6 +27,12 @@ CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUD
             "-fvisibility=hidden", "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
 
 
+# per-file extra flags.  project.hip: its packed fp32 math is written explicitly (the SLP
+# vectoriser's own packing is off), and MFMA results go straight to VGPRs (no
+# v_accvgpr_read between the fc1 MFMA and the GELU that consumes it)
+FILE_FLAGS = {"project.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _hipcc():
     h = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(h):
@@ -56,7 +62,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
 
     def compile_one(so):
         s, o = so
-        cmd = [hipcc, *CXXFLAGS, "-c", s, "-o", o]
+        cmd = [hipcc, *CXXFLAGS, *FILE_FLAGS.get(os.path.basename(s), []), "-c", s, "-o", o]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {s}:\n{r.stderr}")

@@ -13,6 +13,7 @@
 // and come through scalar loads.
 #include "common.h"
 #include "blindno.h"
+#include "kernels.h"
 
 using namespace blindno;
 
@@ -192,36 +193,52 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restr
   }
 }
 
-// out[p] = sum_c partial[c][p]: 64 consecutive parameters per wave (coalesced), the 16
-// waves of a workgroup split the chunks, combined in fixed order (deterministic).
-constexpr int kRedWaves = 16;
+// out[p] = sum_c partial[c][p], deterministic.  A workgroup owns PB <= 64 consecutive
+// parameters and splits the chunks into S = 1024 / PB slices (thread t: parameter t % PB,
+// slice t / PB); every slice sums its chunks with four independent accumulators in a fixed
+// order, then the slices are added in slice order.  Small parameter counts (the lift's 16,
+// a conv's 20) therefore still use all 1024 threads instead of 16 lanes.
 __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __restrict__ partial,
                                                                float* __restrict__ out,
-                                                               int nchunk, int np) {
-  __shared__ float red[kRedWaves][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int p = blockIdx.x * 64 + lane;
-  float acc = 0.f;
-  if (p < np)
-    for (int c = wv; c < nchunk; c += kRedWaves) acc += partial[(int64_t)c * np + p];
-  red[wv][lane] = acc;
+                                                               int nchunk, int np, int PB) {
+  __shared__ float red[1024];
+  const int S = 1024 / PB;
+  const int t = threadIdx.x;
+  const int pl = t % PB, sl = t / PB;
+  const int p = blockIdx.x * PB + pl;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (sl < S && p < np) {
+    int c = sl;
+    for (; c + 3 * S < nchunk; c += 4 * S) {
+      a0 += partial[(int64_t)c * np + p];
+      a1 += partial[(int64_t)(c + S) * np + p];
+      a2 += partial[(int64_t)(c + 2 * S) * np + p];
+      a3 += partial[(int64_t)(c + 3 * S) * np + p];
+    }
+    for (; c < nchunk; c += S) a0 += partial[(int64_t)c * np + p];
+  }
+  red[t] = (a0 + a1) + (a2 + a3);
   __syncthreads();
-  if (wv == 0 && p < np) {
-    float s = red[0][lane];
-    for (int w = 1; w < kRedWaves; ++w) s += red[w][lane];
-    out[p] = s;
+  if (sl == 0 && p < np) {
+    float v = red[pl];
+    for (int k = 1; k < S; ++k) v += red[k * PB + pl];
+    out[p] = v;
   }
 }
 
 // ---------------------------------------------------------------- inverse row transform
-// One wave per grid row (n, h); lane owns w = lane + 64 q (q < NQ) and all channels.
-//   acc[q][c] = sum_k Re(Z[n][h][k][c] e^{+2 pi i k w / P2})
+// One wave per (grid row (n, h), channel group); lane owns w = lane + 64 q (q < NQ).
+//   acc[q][c] = sum_k Re(Z[n][h][k][c] e^{+2 pi i k w / P2})      for the CG channels of group g
 // The workgroup keeps the (m2 x P2) twiddle table T[k][w] in LDS (lane-contiguous reads) and
-// each wave stages its row's m2*C coefficients in LDS (broadcast reads).
+// each wave stages its row's m2 x CG coefficients in LDS (broadcast reads).  The field values
+// the epilogue needs (x for the conv, dz for the adjoint) are loaded BEFORE the k loop so
+// their latency hides behind the transform.  Wide fields (the C = 12 heads) are split into
+// NG = C / CG channel groups so a 4-sample head layer still spreads over ~2000 waves.
 // MODE 0 (forward epilogue): z = acc + bc + Wc f(x)            (f = GELU if ACT)
 // MODE 1 (adjoint):          dx = (acc + Wc^T dz) * (ACT ? GELU'(xsrc) : 1)
-//                            and, with WG, per-lane sums of dz (x) f(xsrc) for dWc / dbc.
-template <int CM, int NQ, int MODE, int ACT, int WG>
+//                            and, with WG (one group only), per-lane sums of dz (x) f(xsrc)
+//                            for dWc / dbc.
+template <int CM, int CG, int NQ, int MODE, int ACT, int WG>
 __global__ __launch_bounds__(kBlock) void rowinv_kernel(
     const float2* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
@@ -232,42 +249,64 @@ __global__ __launch_bounds__(kBlock) void rowinv_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
   const int mc = m2 * C;
-  float2* zrow = T + m2 * P2 + wave * mc;           // [m2][C] of the wave's current row
+  float2* zrow = T + m2 * P2 + wave * m2 * CG;      // [m2][CG] of the wave's current row
   for (int e = threadIdx.x; e < m2 * P2; e += blockDim.x) {
     const int k = e / P2, w = e % P2;
     T[e] = twk[(int64_t)w * m2 + k];
   }
   __syncthreads();
   constexpr int NW = WG ? CM * CM + CM : 1;
-  const int nrows = Bn * P1;
+  const int NG = (C + CG - 1) / CG;
+  const int nitems = Bn * P1 * NG;
   const int64_t HW = (int64_t)P1 * P2;
   float wacc[NW];
 #pragma unroll
   for (int e = 0; e < NW; ++e) wacc[e] = 0.f;
   const bool has_wc = wc != nullptr;
-  for (int row = blockIdx.x * kWaves + wave; row < nrows; row += gridDim.x * kWaves) {
+  for (int item = blockIdx.x * kWaves + wave; item < nitems; item += gridDim.x * kWaves) {
+    const int row = item / NG, g = item - (item / NG) * NG;
+    const int c0 = g * CG;
     const int n = row / P1, h = row % P1;
-    const float2* zr = Z + (int64_t)row * mc;
-    for (int e = lane; e < mc; e += 64) zrow[e] = zr[e];
+    const int64_t rbase = (int64_t)n * C * HW + (int64_t)h * P2;
+    // ---- epilogue operands first (in flight during the transform)
+    constexpr int NF = (MODE == 0 || !WG) ? CM : CM;   // all C channels of the other side
+    float fv[NQ][NF];          // MODE 0: x (all inputs); MODE 1: dz (all outputs)
+    float sv[NQ][CG];          // MODE 1: xsrc of this group's channels (ACT / WG)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int w = lane + 64 * q;
+      const bool ok = w < P2 && has_wc;
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+        fv[q][i] = (ok && i < C) ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
+#pragma unroll
+      for (int cl = 0; cl < CG; ++cl)
+        sv[q][cl] = (MODE == 1 && (ACT || WG) && w < P2 && c0 + cl < C) ? xs[rbase + (c0 + cl) * HW + w] : 0.f;
+    }
+    const float2* zr = Z + (int64_t)row * mc + c0;
+    for (int e = lane; e < m2 * CG; e += 64) {
+      const int k = e / CG, cl = e - (e / CG) * CG;
+      zrow[e] = c0 + cl < C ? zr[k * C + cl] : make_float2(0.f, 0.f);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float acc[NQ][CM];
+    float acc[NQ][CG];
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
-      for (int c = 0; c < CM; ++c) acc[q][c] = 0.f;
+      for (int c = 0; c < CG; ++c) acc[q][c] = 0.f;
     for (int k = 0; k < m2; ++k) {
-      float2 zc[CM];
+      float2 zc[CG];
 #pragma unroll
-      for (int c = 0; c < CM; ++c) zc[c] = c < C ? zrow[k * C + c] : make_float2(0.f, 0.f);
+      for (int c = 0; c < CG; ++c) zc[c] = zrow[k * CG + c];
       const float2* Tk = T + k * P2;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const int w = lane + 64 * q;
         const float2 e = Tk[w < P2 ? w : 0];
 #pragma unroll
-        for (int c = 0; c < CM; ++c)
+        for (int c = 0; c < CG; ++c)
           acc[q][c] = fmaf(zc[c].x, e.x, fmaf(-zc[c].y, e.y, acc[q][c]));
       }
     }
@@ -278,20 +317,17 @@ __global__ __launch_bounds__(kBlock) void rowinv_kernel(
     for (int q = 0; q < NQ; ++q) {
       const int w = lane + 64 * q;
       if (w >= P2) continue;
-      const int64_t base = (int64_t)n * C * HW + (int64_t)h * P2 + w;
+      const int64_t base = rbase + w;
       if (MODE == 0) {
         if (has_wc) {
           float xv[CM];
 #pragma unroll
-          for (int i = 0; i < CM; ++i) {
-            float v = i < C ? xs[base + i * HW] : 0.f;
-            if (ACT) v = gelu_f(v);
-            xv[i] = v;
-          }
+          for (int i = 0; i < CM; ++i) xv[i] = ACT ? gelu_f(fv[q][i]) : fv[q][i];
 #pragma unroll
-          for (int o = 0; o < CM; ++o) {
+          for (int cl = 0; cl < CG; ++cl) {
+            const int o = c0 + cl;
             if (o >= C) continue;
-            float v = acc[q][o] + bc[o];
+            float v = acc[q][cl] + bc[o];
 #pragma unroll
             for (int i = 0; i < CM; ++i)
               if (i < C) v = fmaf(wc[o * C + i], xv[i], v);
@@ -299,48 +335,46 @@ __global__ __launch_bounds__(kBlock) void rowinv_kernel(
           }
         } else {
 #pragma unroll
-          for (int o = 0; o < CM; ++o)
-            if (o < C) out[base + o * HW] = acc[q][o];
+          for (int cl = 0; cl < CG; ++cl)
+            if (c0 + cl < C) out[base + (c0 + cl) * HW] = acc[q][cl];
         }
       } else {
         if (has_wc) {
-          float dv[CM], xv[CM], g[CM];
+          float xa[CG];
 #pragma unroll
-          for (int o = 0; o < CM; ++o) dv[o] = o < C ? dz[base + o * HW] : 0.f;
+          for (int cl = 0; cl < CG; ++cl) {
+            const int i = c0 + cl;
+            float gi = acc[q][cl];
 #pragma unroll
-          for (int i = 0; i < CM; ++i) {
-            g[i] = acc[q][i];
-#pragma unroll
-            for (int o = 0; o < CM; ++o) g[i] = fmaf(o < C ? wc[o * C + i] : 0.f, dv[o], g[i]);
-            xv[i] = ((WG || ACT) && i < C) ? xs[base + i * HW] : 0.f;
+            for (int o = 0; o < CM; ++o) gi = fmaf((o < C && i < C) ? wc[o * C + i] : 0.f, fv[q][o], gi);
+            xa[cl] = sv[q][cl];
             if (ACT) {
               float a, dg;
-              gelu_both(xv[i], a, dg);
-              g[i] *= dg;
-              xv[i] = a;
+              gelu_both(sv[q][cl], a, dg);
+              gi *= dg;
+              xa[cl] = a;
             }
+            if (i < C) out[base + i * HW] = gi;
           }
-#pragma unroll
-          for (int i = 0; i < CM; ++i)
-            if (i < C) out[base + i * HW] = g[i];
           if constexpr (WG != 0) {
 #pragma unroll
             for (int o = 0; o < CM; ++o) {
 #pragma unroll
-              for (int i = 0; i < CM; ++i) wacc[o * CM + i] = fmaf(dv[o], xv[i], wacc[o * CM + i]);
-              wacc[CM * CM + o] += dv[o];
+              for (int cl = 0; cl < CG; ++cl) wacc[o * CM + cl] = fmaf(fv[q][o], xa[cl], wacc[o * CM + cl]);
+              wacc[CM * CM + o] += fv[q][o];
             }
           }
         } else {
 #pragma unroll
-          for (int i = 0; i < CM; ++i)
-            if (i < C) out[base + i * HW] = acc[q][i];
+          for (int cl = 0; cl < CG; ++cl)
+            if (c0 + cl < C) out[base + (c0 + cl) * HW] = acc[q][cl];
         }
       }
     }
   }
   if (WG) {
     // block reduction of the per-lane conv-weight partials -> partial[blockIdx.x][C*C + C]
+    // (WG runs with a single channel group: CG == CM, c0 == 0)
     __syncthreads();
     float* red = reinterpret_cast<float*>(sm2);   // reuse LDS (sized by the launcher)
     const int np = C * C + C;
@@ -413,168 +447,8 @@ __global__ __launch_bounds__(kBlock) void project_fwd_kernel(
   }
 }
 
-// Backward for narrow fields (C <= 16): lanes = crop points (64-point tiles, coalesced), the
-// 16 waves of a 1024-thread workgroup split the hidden units (JW each; gridDim.y workgroups
-// share a tile when 16 JW < Hd), so every lane keeps its wave's weight gradients in registers
-// for the whole kernel; dz of a tile is summed over the waves through LDS (and over the <= 2
-// hidden groups by an atomic add onto zeroed dz: two addends commute exactly, so the result
-// stays deterministic).  The next tile's z / dout are prefetched into registers while the
-// current tile computes (double-buffered LDS).  One workgroup partial per parameter.
-template <int CM, int JW, int COM, int NWV>
-__global__ __launch_bounds__(NWV * 64) void project_bwd_split_kernel(
-    const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
-    const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
-    float* __restrict__ partial, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd,
-    int Cout, int ostride, int ooff, int dout_div) {
-  __shared__ float sz[2][CM][64], sg[2][COM][64], red[NWV][CM][64];
-  __shared__ float sw1[NWV * JW][CM], sb1[NWV * JW], sw2[NWV * JW][COM];
-  const int lane = threadIdx.x & 63;
-  const int wave = uniform_int(threadIdx.x >> 6);
-  constexpr int HB = NWV * JW;              // hidden units of this workgroup
-  const int jb = blockIdx.y * HB;
-  const int j0 = wave * JW;                  // local to the workgroup's hidden group
-  for (int e = threadIdx.x; e < HB * CM; e += blockDim.x) {
-    const int j = e / CM, i = e % CM;
-    sw1[j][i] = i < C ? w1[(jb + j) * C + i] : 0.f;
-  }
-  for (int e = threadIdx.x; e < HB; e += blockDim.x) sb1[e] = b1[jb + e];
-  for (int e = threadIdx.x; e < HB * COM; e += blockDim.x) {
-    const int j = e / COM, c = e % COM;
-    sw2[j][c] = c < Cout ? w2[c * Hd + jb + j] : 0.f;
-  }
-  float gW1[JW][CM], gb1[JW], gW2[JW][COM], gb2[COM];
-#pragma unroll
-  for (int q = 0; q < JW; ++q) {
-    gb1[q] = 0.f;
-#pragma unroll
-    for (int i = 0; i < CM; ++i) gW1[q][i] = 0.f;
-#pragma unroll
-    for (int c = 0; c < COM; ++c) gW2[q][c] = 0.f;
-  }
-#pragma unroll
-  for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
-  const int64_t HW = (int64_t)P1 * P2;
-  const int64_t npts = (int64_t)Bn * Ho * Wo;
-  const int64_t ntiles = (npts + 63) / 64;
-
-  // loader role: waves [0, CM) fetch one z channel, waves [CM, CM+COM) one dout channel
-  // 32-bit point decomposition (npts < 2^31 is checked by the launcher)
-  auto zoff = [&](unsigned p, unsigned& n_out) -> int64_t {
-    const unsigned w = p % (unsigned)Wo, r = p / (unsigned)Wo;
-    const unsigned h = r % (unsigned)Ho, n = r / (unsigned)Ho;
-    n_out = n;
-    return (int64_t)n * C * HW + (int64_t)h * P2 + w;
-  };
-  // loader rows r = wave, wave + 16, ...: rows [0, CM) are z channels, [CM, CM+COM) dout
-  constexpr int NR = (CM + COM + NWV - 1) / NWV;
-  auto fetch = [&](int64_t tile, int r) -> float {
-    const int64_t p = tile * 64 + lane;
-    if (tile >= ntiles || p >= npts || r >= CM + COM) return 0.f;
-    unsigned n;
-    const int64_t zo = zoff((unsigned)p, n);
-    if (r < CM) return r < C ? z[zo + r * HW] : 0.f;
-    const int c = r - CM;
-    const unsigned q = (unsigned)p % (unsigned)(Ho * Wo);
-    return c < Cout ? dout[((int64_t)(n / (unsigned)dout_div) * (Ho * Wo) + q) * ostride + ooff + c] : 0.f;
-  };
-  auto stash = [&](int buf, int r, float v) {
-    if (r < CM) sz[buf][r][lane] = v;
-    else if (r < CM + COM) sg[buf][r - CM][lane] = v;
-  };
-  int64_t tile = blockIdx.x;
-#pragma unroll
-  for (int q = 0; q < NR; ++q) stash(0, wave + q * NWV, fetch(tile, wave + q * NWV));
-  int buf = 0;
-  for (; tile < ntiles; tile += gridDim.x, buf ^= 1) {
-    __syncthreads();
-    float pre[NR];
-#pragma unroll
-    for (int q = 0; q < NR; ++q) pre[q] = fetch(tile + gridDim.x, wave + q * NWV);
-    float zi[CM], gv[COM], dzp[CM];
-#pragma unroll
-    for (int i = 0; i < CM; ++i) {
-      zi[i] = sz[buf][i][lane];
-      dzp[i] = 0.f;
-    }
-#pragma unroll
-    for (int c = 0; c < COM; ++c) gv[c] = sg[buf][c][lane];
-#pragma unroll
-    for (int q = 0; q < JW; ++q) {
-      const int j = j0 + q;
-      float hv = sb1[j];
-#pragma unroll
-      for (int i = 0; i < CM; ++i) hv = fmaf(sw1[j][i], zi[i], hv);
-      float a, dg;
-      gelu_both(hv, a, dg);
-      float da = 0.f;
-#pragma unroll
-      for (int c = 0; c < COM; ++c) da = fmaf(sw2[j][c], gv[c], da);
-      const float dh = da * dg;
-#pragma unroll
-      for (int i = 0; i < CM; ++i) {
-        dzp[i] = fmaf(sw1[j][i], dh, dzp[i]);
-        gW1[q][i] = fmaf(dh, zi[i], gW1[q][i]);
-      }
-      gb1[q] += dh;
-#pragma unroll
-      for (int c = 0; c < COM; ++c) gW2[q][c] = fmaf(gv[c], a, gW2[q][c]);
-    }
-    if (wave == 0) {
-#pragma unroll
-      for (int c = 0; c < COM; ++c) gb2[c] += gv[c];
-    }
-#pragma unroll
-    for (int i = 0; i < CM; ++i) red[wave][i][lane] = dzp[i];
-#pragma unroll
-    for (int q = 0; q < NR; ++q) stash(buf ^ 1, wave + q * NWV, pre[q]);
-    __syncthreads();
-    for (int i = wave; i < C; i += NWV) {
-      const int64_t p = tile * 64 + lane;
-      if (p < npts) {
-        float s2 = 0.f;
-#pragma unroll
-        for (int wv = 0; wv < NWV; ++wv) s2 += red[wv][i][lane];
-        unsigned n;
-        float* dst = dz + zoff((unsigned)p, n) + i * HW;
-        if (gridDim.y == 1) *dst = s2;
-        else atomicAdd(dst, s2);
-      }
-    }
-  }
-  // per-wave lane sums -> this workgroup's partial (each wave owns its hidden units)
-  const int np = Hd * C + Hd + Cout * Hd + Cout;
-  float* pp = partial + (int64_t)blockIdx.x * np;
-#pragma unroll
-  for (int q = 0; q < JW; ++q) {
-    const int j = jb + j0 + q;
-#pragma unroll
-    for (int i = 0; i < CM; ++i) {
-      if (i >= C) continue;
-      const float s2 = wave_sum(gW1[q][i]);
-      if (lane == 0) pp[j * C + i] = s2;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const float sb = wave_sum(gb1[q]);
-    if (lane == 0) pp[Hd * C + j] = sb;
-#pragma unroll
-    for (int c = 0; c < COM; ++c) {
-      if (c >= Cout) continue;
-      const float s2 = wave_sum(gW2[q][c]);
-      if (lane == 0) pp[Hd * C + Hd + c * Hd + j] = s2;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (wave == 0 && blockIdx.y == 0) {
-#pragma unroll
-    for (int c = 0; c < COM; ++c) {
-      if (c >= Cout) continue;
-      const float s2 = wave_sum(gb2[c]);
-      if (lane == 0) pp[Hd * C + Hd + Cout * Hd + c] = s2;
-    }
-  }
-}
-
-// Backward for wider fields (C > 4): lanes = crop points (64-point tiles), the 16 waves of a
+// Backward for wide fields (C > 15, the 1D heads; narrower ones run on the matrix cores,
+// project.hip): lanes = crop points (64-point tiles), the 16 waves of a
 // 1024-thread workgroup split the hidden units (JW each); weight-gradient contributions of a
 // tile are summed over lanes (wave reduction) and accumulated in the wave's own LDS slots;
 // dz is summed over waves through LDS.  One workgroup partial per parameter at the end.
@@ -826,9 +700,14 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ p,
   }
 }
 
-int rowinv_blocks(int Bn, int P1) {
-  const int64_t rows = (int64_t)Bn * P1;
-  const int64_t b = (rows + kWaves - 1) / kWaves;
+// channels per wave: all of them up to 8 (one group, the conv-weight gradient can fuse),
+// groups of 4 above (the C = 12 heads: 3 groups)
+int rowinv_cg(int C) { return C <= 8 ? (C <= 4 ? 4 : 8) : 4; }
+
+int rowinv_blocks(int Bn, int P1, int C) {
+  const int ng = (C + rowinv_cg(C) - 1) / rowinv_cg(C);
+  const int64_t items = (int64_t)Bn * P1 * ng;
+  const int64_t b = (items + kWaves - 1) / kWaves;
   return (int)(b < 2048 ? b : 2048);
 }
 
@@ -838,9 +717,10 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
                   int Bn, int C, int P1, int P2, int m2, hipStream_t st) {
   const int nq = (P2 + 63) / 64;
   const int cm = C <= 4 ? 4 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
+  const int cg = rowinv_cg(C);
   if (C > 32 || nq > 5) return (int)hipErrorInvalidValue;
   if (WG && cm > 8) return (int)hipErrorInvalidValue;
-  size_t sh = sizeof(float2) * ((size_t)m2 * P2 + (size_t)kWaves * m2 * C);
+  size_t sh = sizeof(float2) * ((size_t)m2 * P2 + (size_t)kWaves * m2 * cg);
   if (WG) {
     const size_t need = sizeof(float) * (size_t)kWaves * (C * C + C);
     if (need > sh) sh = need;
@@ -849,26 +729,26 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   const dim3 g(nblocks), b(kBlock);
   const float2* z2 = (const float2*)Z;
   const float2* t2 = (const float2*)tw;
-#define RI(CM_, NQ_)                                                                        \
-  rowinv_kernel<CM_, NQ_, MODE, ACT, WG><<<g, b, sh, st>>>(z2, xs, dz, wc, bc, out, t2,      \
-                                                           partial, Bn, C, P1, P2, m2)
-#define RI_NQ(CM_)             \
-  switch (nq) {                \
-    case 1: RI(CM_, 1); break; \
-    case 2: RI(CM_, 2); break; \
-    case 3: RI(CM_, 3); break; \
-    case 4: RI(CM_, 4); break; \
-    default: RI(CM_, 5); break; \
+#define RI(CM_, CG_, NQ_)                                                                      \
+  rowinv_kernel<CM_, CG_, NQ_, MODE, ACT, WG><<<g, b, sh, st>>>(z2, xs, dz, wc, bc, out, t2,     \
+                                                                partial, Bn, C, P1, P2, m2)
+#define RI_NQ(CM_, CG_)             \
+  switch (nq) {                     \
+    case 1: RI(CM_, CG_, 1); break; \
+    case 2: RI(CM_, CG_, 2); break; \
+    case 3: RI(CM_, CG_, 3); break; \
+    case 4: RI(CM_, CG_, 4); break; \
+    default: RI(CM_, CG_, 5); break; \
   }
   if (cm == 4) {
-    RI_NQ(4)
+    RI_NQ(4, 4)
   } else if (cm == 8) {
-    RI_NQ(8)
+    RI_NQ(8, 8)
   } else if constexpr (!WG) {
     if (cm == 16) {
-      RI_NQ(16)
+      RI_NQ(16, 4)
     } else {
-      RI_NQ(32)
+      RI_NQ(32, 4)
     }
   }
 #undef RI_NQ
@@ -940,14 +820,17 @@ BLINDNO_API int blindno_conv_wgrad(const float* dz, const float* x, float* parti
 
 BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np,
                                         void* stream) {
-  reduce_partials_kernel<<<cdiv(np, 64), 1024, 0, (hipStream_t)stream>>>(partial, out, nchunk, np);
+  if (nchunk < 1 || np < 1) return (int)hipErrorInvalidValue;
+  const int PB = np < 64 ? np : 64;
+  reduce_partials_kernel<<<cdiv(np, PB), 1024, 0, (hipStream_t)stream>>>(partial, out, nchunk, np,
+                                                                           PB);
   return (int)hipGetLastError();
 }
 
 BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float* wc,
                                     const float* bc, float* z, const float* tw2, int Bn, int C,
                                     int P1, int P2, int m2, int act, void* stream) {
-  const int nb = rowinv_blocks(Bn, P1);
+  const int nb = rowinv_blocks(Bn, P1, C);
   hipStream_t st = (hipStream_t)stream;
   if (act)
     return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
@@ -955,14 +838,14 @@ BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float*
 }
 
 BLINDNO_API int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1) {
-  return C <= 8 ? rowinv_blocks(Bn, P1) : 0;
+  return C <= 8 ? rowinv_blocks(Bn, P1, C) : 0;
 }
 
 BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc,
                                     const float* xsrc, float* dx, const float* tw2,
                                     float* partial, int Bn, int C, int P1, int P2, int m2,
                                     int act, void* stream) {
-  const int nb = rowinv_blocks(Bn, P1);
+  const int nb = rowinv_blocks(Bn, P1, C);
   hipStream_t st = (hipStream_t)stream;
   if (partial) {
     if (C > 8 || !wc) return (int)hipErrorInvalidValue;
@@ -981,6 +864,9 @@ BLINDNO_API int blindno_project_fwd(const float* z, const float* w1, const float
                                     int ostride, int ooff, void* stream) {
   if (Ho > P1 || Wo > P2 || C > 32 || Cout > 4 || (int64_t)Bn * Ho * Wo >= INT32_MAX)
     return (int)hipErrorInvalidValue;
+  if (project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
+    return project_fwd_mfma(z, w1, b1, w2, b2, out, Bn, C, P1, P2, Ho, Wo, Cout, ostride, ooff,
+                            (hipStream_t)stream);
   const int64_t total = (int64_t)Bn * Ho * Wo;
   const dim3 g(grid_for(total, kBlock, 2048));
   hipStream_t st = (hipStream_t)stream;
@@ -1001,9 +887,7 @@ BLINDNO_API int blindno_project_fwd(const float* z, const float* w1, const float
 }
 
 BLINDNO_API int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo) {
-  const int64_t pts = (int64_t)Bn * Ho * Wo;
-  const int64_t b = (pts / 8 + 4 * 16 - 1) / (4 * 16);     // >= ~16 point batches per wave
-  return (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
+  return project_bwd_mfma_nchunk((int64_t)Bn * Ho * Wo);
 }
 
 BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float* b1,
@@ -1017,26 +901,9 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
   hipStream_t st = (hipStream_t)stream;
   const int np = Hd * C + Hd + Cout * Hd + Cout;
   const dim3 g(nchunk);
-  // register-resident weight gradients: C <= 4 -> 8 hidden units per wave (one group);
-  // C <= 16 -> 4 per wave, two hidden groups (dz summed by a two-addend atomic, exact)
-  if (Hd == 128 && Cout == 1 && C <= 12) {
-    if (C <= 4) {
-      project_bwd_split_kernel<4, 8, 1, 16><<<g, 1024, 0, st>>>(z, w1, b1, w2, dout, dz, partial,
-                                                                Bn, C, P1, P2, Ho, Wo, Hd, Cout,
-                                                                ostride, ooff, dout_div);
-    } else {
-      // 8 waves x 8 hidden units = 64 per workgroup, two hidden groups
-      const dim3 g2(nchunk, 2);
-#define PS(CM_)                                                                               \
-  project_bwd_split_kernel<CM_, 8, 1, 8><<<g2, 512, 0, st>>>(z, w1, b1, w2, dout, dz, partial, \
-                                                             Bn, C, P1, P2, Ho, Wo, Hd, Cout,  \
-                                                             ostride, ooff, dout_div)
-      if (C <= 8) PS(8);
-      else PS(12);
-#undef PS
-    }
-    return (int)hipGetLastError();
-  }
+  if (project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
+    return project_bwd_mfma(z, w1, b1, w2, dout, dz, partial, nchunk, Bn, C, P1, P2, Ho, Wo, Cout,
+                            ostride, ooff, dout_div, st);
   if (Hd != 128) return (int)hipErrorInvalidValue;   // fc1 = Linear(width, 128) everywhere
   const int cm = C <= 8 ? 8 : (C <= 16 ? 16 : 32);
   const int com = Cout == 1 ? 1 : 4;

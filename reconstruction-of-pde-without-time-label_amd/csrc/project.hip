@@ -1,0 +1,492 @@
+// Projection MLP of FNO1d/FNO2d on the matrix cores: crop -> fc1 (C -> 128) -> GELU ->
+// fc2 (128 -> Cout), forward and backward, with the 128-wide hidden layer never leaving
+// registers (2d_FPE/FNOModules.py:234-239, 1d_FPE/FNOModules.py:116-121).
+//
+// Orientation "points x hidden": a wave takes 16 crop points at a time and sweeps the 8
+// hidden tiles of 16 units.  For each tile one v_mfma_f32_16x16x4f32 chain forms
+//     H^T (16 pts x 16 hid) = Z^T (16 pts x C) . W1^T (C x 16 hid)          (K = C)
+// so lane l holds h for points 4 (l>>4) + r (r < 4) of the tile and hidden unit l & 15.
+// The GELU (and in the backward its derivative) is VALU work on those 4 values.  The
+// backward keeps the fc1 weight gradient on the matrix cores too, in the same layout:
+//     dW1^T-tile (16 hid x 16 cols) += dH (16 hid x 4 pts) . [Z^T | 1] (4 pts x 16 cols)
+// where column C of the B operand is 1.0, which accumulates db1 for free; the D-layout rows of
+// the forward MFMA are exactly the K index of this one, so no transposition is needed.
+// fc2, its gradients and dz = W1^T dH stay on the VALU (they would waste 15/16 or 3/4 of an
+// MFMA); dz is summed over the 16 hidden lanes by a reduce-scatter of 4 shuffles.
+#include "common.h"
+#include "blindno.h"
+#include "kernels.h"
+
+using namespace blindno;
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kHd = 128;          // fc1 = Linear(width, 128) in every reference FNO
+constexpr int kNT = kHd / 16;     // hidden tiles
+constexpr int kWaves = 4;
+
+struct PointMap {
+  unsigned HoWo, Wo;
+  int64_t HW;
+  int P2, C;
+  __device__ __forceinline__ int64_t zoff(unsigned p, unsigned& n, unsigned& q) const {
+    n = p / HoWo;
+    q = p - n * HoWo;
+    const unsigned h = q / Wo, w = q - (q / Wo) * Wo;
+    return (int64_t)n * C * HW + (int64_t)h * P2 + w;
+  }
+};
+
+// sum v over the 16 lanes sharing (lane >> 4): butterfly, result in every lane
+__device__ __forceinline__ float sum16(float v) {
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// GELU on k-scaled pre-activations.  W1 and b1 are staged multiplied by k = sqrt(log2(e)/2),
+// so the MFMA yields hk = k h and e^{-h^2/2} = 2^{-(hk)^2} costs one multiply and one v_exp;
+// with half = erfc(|h|/sqrt2)/2 (A&S 7.1.26, common.h) GELU(h) = (max(hk, 0) - |hk| half)/k,
+// and the 1/k is folded into W2 (forward) or applied once to the accumulated sums (backward).
+constexpr float kK = 0.84932180028801904f;        // sqrt(log2(e) / 2)
+constexpr float kInvK = 1.1774100225154747f;
+constexpr float kT = 0.27273748087922245f;        // A&S p / (sqrt2 k)
+constexpr float kPdfK = 0.46971863934982566f;     // 1 / (sqrt(2 pi) k)
+
+struct GeluK {
+  float g;      // k GELU(h)
+  float e;      // e^{-h^2/2}
+  float half;   // erfc(|h|/sqrt2) / 2
+};
+
+__device__ __forceinline__ GeluK gelu_k(float hk) {
+  GeluK o;
+  const float t = __builtin_amdgcn_rcpf(fmaf(fabsf(hk), kT, 1.0f));
+  o.e = __builtin_amdgcn_exp2f(-(hk * hk));
+  float q = fmaf(t, 0.5307027145f, -0.7265760135f);
+  q = fmaf(t, q, 0.7107068705f);
+  q = fmaf(t, q, -0.142248368f);
+  q = fmaf(t, q, 0.127414796f);
+  o.half = q * t * o.e;
+  o.g = fmaf(-fabsf(hk), o.half, fmaxf(hk, 0.0f));
+  return o;
+}
+
+// GELU'(h) = Phi(h) + h phi(h), Phi(h) = h >= 0 ? 1 - half : half
+__device__ __forceinline__ float gelu_k_grad(float hk, const GeluK& o) {
+  const float cdf = hk >= 0.f ? 1.0f - o.half : o.half;
+  return fmaf(hk * kPdfK, o.e, cdf);
+}
+
+// Two GELUs per lane-instruction: the polynomial / product steps as packed fp32 (v_pk_fma_f32,
+// v_pk_mul_f32 on <2 x float>), the transcendentals and max stay scalar.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+struct GeluK2 {
+  f32x2 g, e, half;
+};
+
+__device__ __forceinline__ GeluK2 gelu_k2(f32x2 hk) {
+  GeluK2 o;
+  const f32x2 ahk = {fabsf(hk.x), fabsf(hk.y)};
+  const f32x2 one = {1.0f, 1.0f};
+  const f32x2 ta = __builtin_elementwise_fma(ahk, (f32x2){kT, kT}, one);
+  const f32x2 t = {__builtin_amdgcn_rcpf(ta.x), __builtin_amdgcn_rcpf(ta.y)};
+  const f32x2 sq = hk * hk;
+  o.e = (f32x2){__builtin_amdgcn_exp2f(-sq.x), __builtin_amdgcn_exp2f(-sq.y)};
+  f32x2 q = __builtin_elementwise_fma(t, (f32x2){0.5307027145f, 0.5307027145f}, (f32x2){-0.7265760135f, -0.7265760135f});
+  q = __builtin_elementwise_fma(t, q, (f32x2){0.7107068705f, 0.7107068705f});
+  q = __builtin_elementwise_fma(t, q, (f32x2){-0.142248368f, -0.142248368f});
+  q = __builtin_elementwise_fma(t, q, (f32x2){0.127414796f, 0.127414796f});
+  o.half = q * t * o.e;
+  const f32x2 mx = {fmaxf(hk.x, 0.0f), fmaxf(hk.y, 0.0f)};
+  o.g = __builtin_elementwise_fma(-ahk, o.half, mx);
+  return o;
+}
+
+// Weights staged once per workgroup: W1 rows zero-padded to CK, b1, W2 (COM rows).
+template <int CK, int COM>
+struct ProjWeights {
+  float w1[kHd][CK];
+  float b1[kHd];
+  float w2[COM][kHd];
+};
+
+template <int CK, int COM>
+__device__ __forceinline__ void stage_weights(ProjWeights<CK, COM>& sw, const float* w1,
+                                              const float* b1, const float* w2, int C, int Cout,
+                                              float w2scale) {
+  for (int e = threadIdx.x; e < kHd * CK; e += blockDim.x) {
+    const int j = e / CK, i = e % CK;
+    sw.w1[j][i] = i < C ? kK * w1[j * C + i] : 0.f;
+  }
+  for (int e = threadIdx.x; e < kHd; e += blockDim.x) sw.b1[e] = kK * b1[e];
+  for (int e = threadIdx.x; e < COM * kHd; e += blockDim.x) {
+    const int c = e / kHd, j = e % kHd;
+    sw.w2[c][j] = c < Cout ? w2scale * w2[c * kHd + j] : 0.f;
+  }
+}
+
+// A operand of fc1 for NP point tiles: lane supplies z[ch 4 kk + g4][pt 16 tile + c16]
+template <int KS>
+__device__ __forceinline__ void load_az(const float* __restrict__ z, const PointMap& pm,
+                                        unsigned p, unsigned npts, int g4, float (&az)[KS]) {
+  unsigned n, q;
+  const int64_t zo = pm.zoff(p < npts ? p : 0, n, q);
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int ch = 4 * kk + g4;
+    az[kk] = (p < npts && ch < pm.C) ? z[zo + (int64_t)ch * pm.HW] : 0.f;
+  }
+}
+
+// Forward: each wave owns NP point tiles (16 points each) per step and sweeps the 8 hidden
+// tiles in a rolled loop (weights from LDS), so NP independent MFMA -> GELU chains overlap.
+template <int CK, int COM, int NP>
+__global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
+    const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ out, int C,
+    int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff, unsigned npts) {
+  constexpr int KS = CK / 4;
+  __shared__ ProjWeights<CK, COM> sw;
+  stage_weights<CK, COM>(sw, w1, b1, w2, C, Cout, kInvK);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  float b2v[COM];
+#pragma unroll
+  for (int c = 0; c < COM; ++c) b2v[c] = c < Cout ? b2[c] : 0.f;
+  const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C};
+  const unsigned ngroups = (npts + 16 * NP - 1) / (16 * NP);
+  for (unsigned grp = blockIdx.x * kWaves + wave; grp < ngroups; grp += gridDim.x * kWaves) {
+    float az[NP][KS];
+#pragma unroll
+    for (int np = 0; np < NP; ++np) load_az<KS>(z, pm, (grp * NP + np) * 16 + c16, npts, g4, az[np]);
+    f32x2 acc[NP][COM][2];                        // (r0, r1), (r2, r3)
+#pragma unroll
+    for (int np = 0; np < NP; ++np)
+#pragma unroll
+      for (int c = 0; c < COM; ++c) acc[np][c][0] = acc[np][c][1] = (f32x2){0.f, 0.f};
+#pragma unroll 1
+    for (int t = 0; t < kNT; ++t) {
+      const int j = 16 * t + c16;
+      float bw[KS];
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) bw[kk] = sw.w1[j][4 * kk + g4];
+      const float bb = sw.b1[j];
+      float w2v[COM];
+#pragma unroll
+      for (int c = 0; c < COM; ++c) w2v[c] = sw.w2[c][j];
+#pragma unroll
+      for (int np = 0; np < NP; ++np) {
+        f32x4 d = {bb, bb, bb, bb};
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x4f32(az[np][kk], bw[kk], d, 0, 0, 0);
+        const GeluK2 g01 = gelu_k2((f32x2){d[0], d[1]});
+        const GeluK2 g23 = gelu_k2((f32x2){d[2], d[3]});
+#pragma unroll
+        for (int c = 0; c < COM; ++c) {
+          const f32x2 wv = {w2v[c], w2v[c]};
+          acc[np][c][0] = __builtin_elementwise_fma(wv, g01.g, acc[np][c][0]);
+          acc[np][c][1] = __builtin_elementwise_fma(wv, g23.g, acc[np][c][1]);
+        }
+      }
+    }
+    // fc2: sum over the 16 hidden lanes; lane with c16 == r (< 4) writes point 4 g4 + r
+#pragma unroll
+    for (int np = 0; np < NP; ++np) {
+      float accs[COM][4];
+#pragma unroll
+      for (int c = 0; c < COM; ++c) {
+        accs[c][0] = sum16(acc[np][c][0].x);
+        accs[c][1] = sum16(acc[np][c][0].y);
+        accs[c][2] = sum16(acc[np][c][1].x);
+        accs[c][3] = sum16(acc[np][c][1].y);
+      }
+      if (c16 < 4) {
+        const unsigned p = (grp * NP + np) * 16 + 4 * g4 + c16;
+        if (p < npts) {
+          float* op = out + (int64_t)p * ostride + ooff;
+#pragma unroll
+          for (int c = 0; c < COM; ++c) {
+            float v = accs[c][0];
+            if (c16 == 1) v = accs[c][1];
+            if (c16 == 2) v = accs[c][2];
+            if (c16 == 3) v = accs[c][3];
+            if (c < Cout) op[c] = v + b2v[c];
+          }
+        }
+      }
+    }
+  }
+}
+
+// Backward.  Per wave and NP point tiles: recompute H^T (MFMA), GELU and GELU' (VALU),
+// dH = (W2^T g) * GELU', accumulate dW2 (VALU) and dW1 / db1 (MFMA) -- both kept per lane in
+// LDS between steps because the hidden-tile loop is rolled -- and dz = W1^T dH (VALU,
+// summed over the 16 hidden lanes by a reduce-scatter of four shuffles per value block).
+// The four waves of a workgroup fold their accumulators into one partial per workgroup
+// (fixed order; reduced afterwards by blindno_reduce_partials).
+template <int CK, int COM, int NP>
+__global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
+    const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
+    float* __restrict__ partial, int C, int P1, int P2, int Ho, int Wo, int Cout, int ostride,
+    int ooff, int dout_div, unsigned npts) {
+  constexpr int KS = CK / 4;
+  constexpr int NV = 4 * CK;                       // dz values per lane per tile: (ch, r)
+  __shared__ ProjWeights<CK, COM> sw;
+  // dW1 (/ db1) accumulators in MFMA D layout.  CK == 4: v_mfma_f32_4x4x1f32, 16 blocks of
+  // (4 hidden x 4 channels), block b = 4 g4 + (c16 >> 2) <-> hidden 4 (c16 >> 2) + reg, channel
+  // c16 & 3, K = one point of group g4 per instruction; db1 then sums on the VALU (sgb1).
+  // CK > 4: v_mfma_f32_16x16x4f32 against [Z^T | 1] (column C = db1).
+  constexpr bool kGW44 = CK == 4;
+  __shared__ f32x4 sgw1[kWaves][kNT][64];
+  __shared__ float sgb1[kWaves][kNT][64];
+  __shared__ float sgw2[kWaves][kNT][COM][64];     // dW2 accumulators (lane = hidden c16)
+  stage_weights<CK, COM>(sw, w1, b1, w2, C, Cout, 1.0f);
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  for (int t = 0; t < kNT; ++t) {
+    sgw1[wave][t][lane] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    sgb1[wave][t][lane] = 0.f;
+#pragma unroll
+    for (int c = 0; c < COM; ++c) sgw2[wave][t][c][lane] = 0.f;
+  }
+  __syncthreads();
+  float gb2[COM];
+#pragma unroll
+  for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
+  const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C};
+  const unsigned ngroups = (npts + 16 * NP - 1) / (16 * NP);
+  for (unsigned grp = blockIdx.x * kWaves + wave; grp < ngroups; grp += gridDim.x * kWaves) {
+    float az[NP][KS], zb[NP][4], gv[NP][4][COM];
+    int zo4[NP][4];                                 // element offsets (< 2^31, checked)
+#pragma unroll
+    for (int np = 0; np < NP; ++np) {
+      const unsigned tile = grp * NP + np;
+      load_az<KS>(z, pm, tile * 16 + c16, npts, g4, az[np]);
+      // this lane's 4 points (D layout rows): z column c16 (1.0 at c16 == C: db1), dout
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const unsigned p = tile * 16 + 4 * g4 + r;
+        const bool ok = p < npts;
+        unsigned n, q;
+        zo4[np][r] = (int)pm.zoff(ok ? p : 0, n, q);
+        const int zc = kGW44 ? (c16 & 3) : c16;
+        zb[np][r] = !ok ? 0.f : (zc < C ? z[zo4[np][r] + (int64_t)zc * pm.HW] : (zc == C ? 1.f : 0.f));
+        const float* gp = dout + ((int64_t)(n / (unsigned)dout_div) * pm.HoWo + q) * ostride + ooff;
+#pragma unroll
+        for (int c = 0; c < COM; ++c) gv[np][r][c] = (ok && c < Cout) ? gp[c] : 0.f;
+      }
+      if (c16 == 0) {
+#pragma unroll
+        for (int c = 0; c < COM; ++c) gb2[c] += (gv[np][0][c] + gv[np][1][c]) + (gv[np][2][c] + gv[np][3][c]);
+      }
+    }
+    float dzp[NP][NV];
+#pragma unroll
+    for (int np = 0; np < NP; ++np)
+#pragma unroll
+      for (int e = 0; e < NV; ++e) dzp[np][e] = 0.f;
+#pragma unroll 1
+    for (int t = 0; t < kNT; ++t) {
+      const int j = 16 * t + c16;
+      float bw[KS], wr[CK];
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) bw[kk] = sw.w1[j][4 * kk + g4];
+#pragma unroll
+      for (int i = 0; i < CK; i += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(&sw.w1[j][i]);
+        wr[i] = v.x; wr[i + 1] = v.y; wr[i + 2] = v.z; wr[i + 3] = v.w;
+      }
+      const float bb = sw.b1[j];
+      float w2v[COM], gw2[COM];
+#pragma unroll
+      for (int c = 0; c < COM; ++c) {
+        w2v[c] = sw.w2[c][j];
+        gw2[c] = sgw2[wave][t][c][lane];
+      }
+      f32x4 gw1 = sgw1[wave][t][lane];
+      float gb1 = kGW44 ? sgb1[wave][t][lane] : 0.f;
+#pragma unroll
+      for (int np = 0; np < NP; ++np) {
+        f32x4 d = {bb, bb, bb, bb};
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x4f32(az[np][kk], bw[kk], d, 0, 0, 0);
+        const GeluK2 g01 = gelu_k2((f32x2){d[0], d[1]});
+        const GeluK2 g23 = gelu_k2((f32x2){d[2], d[3]});
+        f32x2 da01 = {0.f, 0.f}, da23 = {0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < COM; ++c) {
+          const f32x2 wv = {w2v[c], w2v[c]};
+          const f32x2 g01v = {gv[np][0][c], gv[np][1][c]}, g23v = {gv[np][2][c], gv[np][3][c]};
+          da01 = __builtin_elementwise_fma(wv, g01v, da01);
+          da23 = __builtin_elementwise_fma(wv, g23v, da23);
+          // k dW2 (scaled at the fold): pairs summed into one lane register
+          const f32x2 p = __builtin_elementwise_fma(g01v, g01.g, g23v * g23.g);
+          gw2[c] += p.x + p.y;
+        }
+        // GELU' = Phi + h phi; Phi = h >= 0 ? 1 - half : half
+        const f32x2 cdf01 = {d[0] >= 0.f ? 1.0f - g01.half.x : g01.half.x, d[1] >= 0.f ? 1.0f - g01.half.y : g01.half.y};
+        const f32x2 cdf23 = {d[2] >= 0.f ? 1.0f - g23.half.x : g23.half.x, d[3] >= 0.f ? 1.0f - g23.half.y : g23.half.y};
+        const f32x2 kp = {kPdfK, kPdfK};
+        const f32x2 dh01 = da01 * __builtin_elementwise_fma((f32x2){d[0], d[1]} * kp, g01.e, cdf01);
+        const f32x2 dh23 = da23 * __builtin_elementwise_fma((f32x2){d[2], d[3]} * kp, g23.e, cdf23);
+        const float dh[4] = {dh01.x, dh01.y, dh23.x, dh23.y};
+#pragma unroll
+        for (int i = 0; i < CK; ++i) {                                 // k dz (scaled at the store)
+          const f32x2 wi = {wr[i], wr[i]};
+          f32x2 p01 = {dzp[np][i * 4 + 0], dzp[np][i * 4 + 1]};
+          f32x2 p23 = {dzp[np][i * 4 + 2], dzp[np][i * 4 + 3]};
+          p01 = __builtin_elementwise_fma(dh01, wi, p01);
+          p23 = __builtin_elementwise_fma(dh23, wi, p23);
+          dzp[np][i * 4 + 0] = p01.x; dzp[np][i * 4 + 1] = p01.y;
+          dzp[np][i * 4 + 2] = p23.x; dzp[np][i * 4 + 3] = p23.y;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if constexpr (kGW44) gw1 = __builtin_amdgcn_mfma_f32_4x4x1f32(dh[r], zb[np][r], gw1, 0, 0, 0);
+          else gw1 = __builtin_amdgcn_mfma_f32_16x16x4f32(dh[r], zb[np][r], gw1, 0, 0, 0);
+        }
+        if constexpr (kGW44) gb1 += (dh[0] + dh[1]) + (dh[2] + dh[3]);
+      }
+      sgw1[wave][t][lane] = gw1;
+      if constexpr (kGW44) sgb1[wave][t][lane] = gb1;
+#pragma unroll
+      for (int c = 0; c < COM; ++c) sgw2[wave][t][c][lane] = gw2[c];
+    }
+    // reduce-scatter dzp over the 16 hidden lanes: lane keeps value index e = 16 m + c16,
+    // i.e. channel 4 m + (c16 >> 2), point 4 g4 + (c16 & 3)
+#pragma unroll
+    for (int np = 0; np < NP; ++np) {
+#pragma unroll
+      for (int s = 8; s >= 1; s >>= 1) {
+        const bool up = (c16 & s) != 0;
+#pragma unroll
+        for (int e = 0; e < NV; ++e) {
+          if ((e & 15) >= s) continue;          // live pairs: (e, e + s) in each 16-block
+          const float keep = up ? dzp[np][e + s] : dzp[np][e];
+          const float send = up ? dzp[np][e] : dzp[np][e + s];
+          dzp[np][e] = keep + __shfl_xor(send, s, 64);
+        }
+      }
+      const int r = c16 & 3;
+      const unsigned p = (grp * NP + np) * 16 + 4 * g4 + r;
+      if (p < npts) {
+#pragma unroll
+        for (int m = 0; m < NV / 16; ++m) {
+          const int ch = 4 * m + (c16 >> 2);
+          if (ch < C) dz[zo4[np][r] + (int64_t)ch * pm.HW] = kInvK * dzp[np][16 * m];
+        }
+      }
+    }
+  }
+  // ---- fold the accumulators of the four waves into this workgroup's partial
+  // layout: [dW1 (Hd*C) | db1 (Hd) | dW2 (Cout*Hd) | db2 (Cout)]
+  __shared__ float sgb2[kWaves][COM];
+#pragma unroll
+  for (int c = 0; c < COM; ++c) {
+    const float v = wave_sum(gb2[c]);
+    if (lane == 0) sgb2[wave][c] = v;
+  }
+  __syncthreads();
+  const int np_ = kHd * C + kHd + Cout * kHd + Cout;
+  float* pp = partial + (int64_t)blockIdx.x * np_;
+  for (int e = threadIdx.x; e < np_; e += blockDim.x) {
+    float v = 0.f;
+    if (e < kHd * C + kHd) {
+      const int j = e < kHd * C ? e / C : e - kHd * C;
+      const int col = e < kHd * C ? e % C : C;
+      const int t = j >> 4, row = j & 15;
+      if (kGW44) {
+        // hidden row = 4 hg + r'; dW1: lanes 16 g4 + 4 hg + col, reg r' (all four point groups);
+        // db1: lanes 16 g4 + row
+        const int hg = row >> 2, rr = row & 3;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            v += col < C ? sgw1[w][t][16 * g + 4 * hg + col][rr] : sgb1[w][t][16 * g + row];
+      } else {
+        // 16x16 D layout: t = j/16, row = j%16 = 4 g4 + r, lane = 16 g4 + col
+        const int ln = 16 * (row >> 2) + col, r = row & 3;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v += sgw1[w][t][ln][r];
+      }
+    } else if (e < kHd * C + kHd + Cout * kHd) {
+      const int q = e - kHd * C - kHd, c = q / kHd, j = q % kHd;
+      const int t = j >> 4, cl = j & 15;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v += sgw2[w][t][c][16 * g + cl];
+      v *= kInvK;
+    } else {
+      const int c = e - kHd * C - kHd - Cout * kHd;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) v += sgb2[w][c];
+    }
+    pp[e] = v;
+  }
+}
+
+}  // namespace
+
+namespace blindno {
+
+bool project_mfma_ok(int C, int Hd, int Cout, int64_t field_elems) {
+  return Hd == kHd && C >= 1 && C <= 15 && Cout >= 1 && Cout <= 2 && field_elems < INT32_MAX;
+}
+
+int project_fwd_mfma(const float* z, const float* w1, const float* b1, const float* w2,
+                     const float* b2, float* out, int Bn, int C, int P1, int P2, int Ho, int Wo,
+                     int Cout, int ostride, int ooff, hipStream_t st) {
+  const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
+  const unsigned ntiles = (npts + 15) / 16;
+  unsigned blocks = (ntiles + kWaves * 16 - 1) / (kWaves * 16);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+#define PF(CK_, CO_)                                                                           \
+  project_fwd_mfma_kernel<CK_, CO_, (CK_ <= 8 ? 4 : 2)><<<blocks, 256, 0, st>>>(z, w1, b1, w2, b2, out, C, P1, P2, \
+                                                            Ho, Wo, Cout, ostride, ooff, npts)
+  const int ck = (C + 3) / 4 * 4;
+  if (Cout == 1) {
+    if (ck == 4) PF(4, 1); else if (ck == 8) PF(8, 1); else if (ck == 12) PF(12, 1); else PF(16, 1);
+  } else {
+    if (ck == 4) PF(4, 2); else if (ck == 8) PF(8, 2); else if (ck == 12) PF(12, 2); else PF(16, 2);
+  }
+#undef PF
+  return (int)hipGetLastError();
+}
+
+int project_bwd_mfma_nchunk(int64_t npts) {
+  const int64_t tiles = (npts + 15) / 16;
+  int64_t b = (tiles + kWaves * 16 - 1) / (kWaves * 16);     // >= 16 tiles per wave
+  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
+int project_bwd_mfma(const float* z, const float* w1, const float* b1, const float* w2,
+                     const float* dout, float* dz, float* partial, int nchunk, int Bn, int C,
+                     int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff,
+                     int dout_div, hipStream_t st) {
+  const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
+#define PB(CK_, CO_)                                                                          \
+  project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? 2 : 1)><<<nchunk, 256, 0, st>>>(z, w1, b1, w2, dout, dz, partial, \
+                                                            C, P1, P2, Ho, Wo, Cout, ostride,  \
+                                                            ooff, dout_div, npts)
+  const int ck = (C + 3) / 4 * 4;
+  if (Cout == 1) {
+    if (ck == 4) PB(4, 1); else if (ck == 8) PB(8, 1); else if (ck == 12) PB(12, 1); else PB(16, 1);
+  } else {
+    if (ck == 4) PB(4, 2); else if (ck == 8) PB(8, 2); else if (ck == 12) PB(12, 2); else PB(16, 2);
+  }
+#undef PB
+  return (int)hipGetLastError();
+}
+
+}  // namespace blindno

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks at config-C shapes (HIP events on the launch stream).
+
+    python tools/kbench.py [filter-regex]
+
+Times the C-ABI entry points of the FNO_input body (Bn = 4 * 75 snapshots, width 4,
+P = 160, m = 12) and of one head layer (Bn = 4, width 12, m = 32) in isolation, so kernel
+variants can be compared without a full training step.  Prints one line per case:
+name, us per call, algorithmic GB/s.
+"""
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "reconstruction-of-pde-without-time-label_amd"))
+
+import torch  # noqa: E402
+
+import blindno  # noqa: E402
+from blindno import ops  # noqa: E402
+from blindno._lib import call, ptr, query, stream_ptr  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e3 / iters
+
+
+def main():
+    pat = sys.argv[1] if len(sys.argv) > 1 else ""
+    blindno.load_library()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    res = []
+
+    def case(name, fn, nbytes):
+        if pat and not re.search(pat, name):
+            return
+        us = timeit(fn)
+        res.append((name, us, nbytes / (us * 1e-6) / 1e9))
+        print(f"{name:40s} {us:9.1f} us  {nbytes / (us * 1e-6) / 1e9:8.0f} GB/s", flush=True)
+
+    for tag, Bn, C, m, Cout in (("input", 300, 4, 12, 1), ("head", 4, 12, 32, 1)):
+        P, N = 160, 128
+        z = torch.randn(Bn, C, P, P, device=dev)
+        w1 = torch.randn(128, C, device=dev) * 0.3
+        b1 = torch.randn(128, device=dev) * 0.1
+        w2 = torch.randn(Cout, 128, device=dev) * 0.1
+        b2 = torch.randn(Cout, device=dev)
+        out = torch.empty(Bn, N, N, Cout, device=dev)
+        dout = torch.randn(Bn, N, N, Cout, device=dev)
+        dz = torch.zeros_like(z)
+        nch = query("blindno_project_bwd_nchunk", Bn, N, N)
+        npar = 128 * C + 128 + Cout * 128 + Cout
+        part = torch.empty(nch, npar, device=dev)
+        pts = Bn * N * N
+        case(f"project_fwd[{tag}]", lambda: call("blindno_project_fwd", ptr(z), ptr(w1), ptr(b1), ptr(w2), ptr(b2),
+                                                  ptr(out), Bn, C, P, P, N, N, 128, Cout, Cout, 0, stream_ptr()),
+             4 * pts * (C + Cout))
+        case(f"project_bwd[{tag}]", lambda: call("blindno_project_bwd", ptr(z), ptr(w1), ptr(b1), ptr(w2), ptr(dout),
+                                                  ptr(dz), ptr(part), nch, Bn, C, P, P, N, N, 128, Cout, Cout, 0, 1,
+                                                  stream_ptr()),
+             4 * pts * (2 * C + Cout))
+        # spectral pieces of one layer
+        sh = ops.SpecShape(Bn, C, C, P, P, m, m, 2)
+        w = torch.rand(C, C, m, m, 2, device=dev) / (C * C)
+        Wt = ops.k_pack_w2d(w, w.clone(), P)
+        fld = 4 * Bn * C * P * P
+        case(f"rowdft[{tag}]", lambda: ops.k_rowdft(z, Bn, C, P, P, m, 1), fld)
+        At = ops.k_rowdft(z, Bn, C, P, P, m, 1)
+        case(f"colpass[{tag}]", lambda: ops.k_colpass(At, Wt, Bn, C, C, P, m, m, P, 0), 8 * Bn * m * C * P * 3)
+        X, Z = ops.k_colpass(At, Wt, Bn, C, C, P, m, m, P, 0)
+        cw = torch.randn(C, C, 1, 1, device=dev) * 0.3
+        cb = torch.randn(C, device=dev) * 0.1
+        case(f"rowidft_epi[{tag}]", lambda: ops.k_rowidft_epi(Z, z, cw, cb, Bn, C, P, P, m, 1), 2 * fld)
+        case(f"rowidft_bwd[{tag}]", lambda: ops.k_rowidft_bwd(Z, z, cw, z, Bn, C, P, P, m, 1, C <= 4), 3 * fld)
+        if C > 4:
+            case(f"conv_wgrad[{tag}]", lambda: ops.k_conv_wgrad(z, z, Bn, C, P, P, 1), 2 * fld)
+        inp = torch.randn(Bn, N, N, 3 if tag == "input" else C, device=dev)
+        fc0w = torch.randn(C, inp.shape[-1], device=dev)
+        fc0b = torch.randn(C, device=dev)
+        x0 = torch.empty(Bn, C, P, P, device=dev)
+        case(f"lift_fwd[{tag}]", lambda: call("blindno_lift_fwd", ptr(inp), ptr(fc0w), ptr(fc0b), ptr(x0), Bn, N, N,
+                                               inp.shape[-1], C, P, P, stream_ptr()), fld + inp.numel() * 4)
+        nl = query("blindno_lift_bwd_nchunk", Bn, N, N)
+        pl = torch.empty(nl, C * inp.shape[-1] + C, device=dev)
+        case(f"lift_bwd[{tag}]", lambda: call("blindno_lift_bwd", ptr(x0), ptr(inp), ptr(fc0w), None, ptr(pl), nl, Bn,
+                                               N, N, inp.shape[-1], C, P, P, stream_ptr()), fld + inp.numel() * 4)
+    return res
+
+
+if __name__ == "__main__":
+    main()
