@@ -119,26 +119,28 @@ int blindno_mix1d(const float* At, const float* Wt, float* Xs, float* Z, int Bn,
                   int Co, int m, int P2, int dir, blindno_stream_t stream);
 
 /* Inverse row transform + 1x1 conv + bias epilogue (irfft2 second stage, nn.Conv2d(k=1),
- * x1 + x2; 2d_FPE/FNOModules.py:177,226-230):
+ * x1 + x2; 2d_FPE/FNOModules.py:177,226-230), on the f32 matrix cores:
  *   z[n,o,h,w] = sum_k Re(Z[n,h,k,o] e^{+2pi i k w/P2}) + sum_i Wc[o,i] f(x[n,i,h,w]) + bc[o]
  * f = identity (act 0) or GELU (act 1: x holds pre-activations).  wc == NULL drops the
- * conv/bias term (bare SpectralConv2d/1d; x, bc unused).  twk: (P2*m2 + 16) complex table
- * twk[w*m2 + k] = e^{+2 pi i k w/P2} (16 zero pads).  C <= 32, P2 <= 320, (m2*P2 + 4*m2*C) complex must fit in 160 KiB LDS. */
+ * conv/bias term (bare SpectralConv2d/1d; x, bc unused).  tb: B-operand image of the row
+ * inverse, (ceil(m2/2), ceil(P2/16), 64) floats, tb[s][t][l] = cos (kk even) or -sin (kk odd)
+ * of 2 pi k w / P2 with kk = 4 s + (l >> 4), k = kk / 2, w = 16 t + (l & 15), zero for k >= m2
+ * or w >= P2.  C <= 32, m2 <= 48. */
 int blindno_rowidft_epi(const float* Z, const float* x, const float* wc, const float* bc,
-                        float* z, const float* tw2, int Bn, int C, int P1, int P2, int m2,
+                        float* z, const float* tb, int Bn, int C, int P1, int P2, int m2,
                         int act, blindno_stream_t stream);
 
 /* Adjoint of rowidft_epi w.r.t. its input field:
  *   dx[n,i,h,w] = sum_k Re(G[n,h,k,i] e^{+2pi i k w/P2}) + sum_o Wc[o,i] dz[n,o,h,w]
  * then, if act == 1, dx *= GELU'(xsrc[n,i,h,w]) (xsrc = the layer input's pre-activation).
- * wc == NULL drops the conv term.  twk as in blindno_rowidft_epi.
- * If partial != NULL (requires C <= 8 and wc), the 1x1-conv
- * gradients are reduced in the same pass into partial[blindno_rowidft_bwd_nchunk()][C*C + C]
+ * wc == NULL drops the conv term.  tb as in blindno_rowidft_epi.
+ * If partial != NULL (requires C <= 4 and wc), the 1x1-conv gradients are reduced in the same
+ * pass into partial[blindno_rowidft_bwd_nchunk(...)][C*C + C]
  * = [dWc[o][i] = sum dz_o f(xsrc_i) | dbc[o] = sum dz_o]. */
 int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc, const float* xsrc,
-                        float* dx, const float* tw2, float* partial, int Bn, int C, int P1,
+                        float* dx, const float* tb, float* partial, int Bn, int C, int P1,
                         int P2, int m2, int act, blindno_stream_t stream);
-int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1);
+int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2);
 
 /* 1x1-conv weight/bias gradient partials (for C > 8): partial[nchunk][C*C + C] with
  * dWc[o,i] = sum dz[n,o,.] f(x[n,i,.]),  dbc[o] = sum dz[n,o,.];

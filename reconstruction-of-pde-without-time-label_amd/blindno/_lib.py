@@ -44,7 +44,7 @@ SIGNATURES = {
     # size queries (return a count, not an error code)
     "blindno_lift_bwd_nchunk": "iii",
     "blindno_conv_wgrad_nchunk": "iii",
-    "blindno_rowidft_bwd_nchunk": "iii",
+    "blindno_rowidft_bwd_nchunk": "iiiii",
     "blindno_project_bwd_nchunk": "iii",
     "blindno_mix_wgrad_nsplit": "iiiii",
 }

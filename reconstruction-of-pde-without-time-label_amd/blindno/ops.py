@@ -49,19 +49,25 @@ def twiddle(P: int, device) -> torch.Tensor:
 _TWR = {}
 
 
-def twiddle_rows(P2: int, m2: int, device) -> torch.Tensor:
-    """Device table twk[w][k] = (cos 2 pi k w/P2, sin 2 pi k w/P2), padded by 16 entries
-    (the row-DFT kernel reads whole mode chunks)."""
+def twiddle_rowinv(P2: int, m2: int, device) -> torch.Tensor:
+    """B-operand image of the inverse row transform (include/blindno.h blindno_rowidft_epi):
+    tb[s][t][l] = cos / -sin (kk = 4 s + (l >> 4) even / odd) of 2 pi k w / P2, k = kk // 2,
+    w = 16 t + (l & 15); zero for k >= m2 or w >= P2.  Built in double."""
     dev = torch.device(device)
     key = (P2, m2, dev.index)
     t = _TWR.get(key)
     if t is None:
-        w = torch.arange(P2, dtype=torch.int64)[:, None]
-        k = torch.arange(m2, dtype=torch.int64)[None, :]
-        ph = ((w * k) % P2).to(torch.float64) * (2.0 * torch.pi / P2)
-        tab = torch.stack([torch.cos(ph), torch.sin(ph)], -1).reshape(-1, 2)
-        tab = torch.cat([tab, torch.zeros(16, 2, dtype=torch.float64)], 0)
-        t = tab.to(F32).to(dev).contiguous()
+        KS, NT = (m2 + 1) // 2, (P2 + 15) // 16
+        s = torch.arange(KS)[:, None, None]
+        tt = torch.arange(NT)[None, :, None]
+        ln = torch.arange(64)[None, None, :]
+        kk = 4 * s + (ln >> 4)
+        k = kk // 2
+        w = 16 * tt + (ln & 15)
+        ph = ((k * w) % P2).to(torch.float64) * (2.0 * torch.pi / P2)
+        v = torch.where(kk % 2 == 0, torch.cos(ph), -torch.sin(ph))
+        v = torch.where((k < m2) & (w < P2), v, torch.zeros_like(v))
+        t = v.to(F32).to(dev).reshape(-1).contiguous()
         _TWR[key] = t
     return t
 
@@ -232,20 +238,20 @@ def k_mix1d(At, Wt, Bn, Ci, Co, m, P2, direction):
 def k_rowidft_epi(Z, x, wc, bc, Bn, C, P1, P2, m2, act):
     z = _empty(Bn, C, P1, P2, like=Z)
     call("blindno_rowidft_epi", ptr(Z), ptr(x), ptr(wc), ptr(bc), ptr(z),
-         ptr(twiddle_rows(P2, m2, Z.device)), Bn, C, P1, P2, m2, act, stream_ptr())
+         ptr(twiddle_rowinv(P2, m2, Z.device)), Bn, C, P1, P2, m2, act, stream_ptr())
     return z
 
 
 def k_rowidft_bwd(G, dz, wc, xsrc, Bn, C, P1, P2, m2, act, want_wgrad=False):
     """dx = irow^H(G) + Wc^T dz, times GELU'(xsrc) if act.  With want_wgrad (C <= 8) the
-    1x1-conv weight/bias gradients are reduced in the same pass: returns (dx, gw, gb)."""
+    1x1-conv weight/bias gradients are reduced in the same pass (C <= 4): returns (dx, gw, gb)."""
     dx = _empty(Bn, C, P1, P2, like=G)
     partial, nchunk = None, 0
     if want_wgrad:
-        nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1)
+        nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, m2)
         partial = _empty(nchunk, C * C + C, like=G)
     call("blindno_rowidft_bwd", ptr(G), ptr(dz), ptr(wc), ptr(xsrc), ptr(dx),
-         ptr(twiddle_rows(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, stream_ptr())
+         ptr(twiddle_rowinv(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, stream_ptr())
     if not want_wgrad:
         return dx, None, None
     g = reduce_partials(partial, nchunk, C * C + C)

@@ -1,7 +1,7 @@
-// Field kernels of the FNO body: lift (fc0 + pad), inverse row transform with the fused
-// 1x1-conv / bias / GELU epilogue and its adjoint (with the fused 1x1-conv weight-gradient
-// reduction), weight-gradient partial reductions, the projection MLP (fc1 -> GELU -> fc2)
-// forward and backward, the snapshot-bag mean, loss, metrics and Adam.
+// Field kernels of the FNO body: lift (fc0 + pad), 1x1-conv weight-gradient partial reductions,
+// the projection MLP fallback for wide fields (fc1 -> GELU -> fc2, forward and backward; the
+// narrow ones run on the matrix cores in project.hip), the snapshot-bag mean, loss, metrics and
+// Adam.  The inverse row transform with its fused epilogue lives in rowinv.hip.
 //
 // Reference: FNO2d.forward 2d_FPE/FNOModules.py:218-240, FNO1d.forward
 // 1d_FPE/FNOModules.py:99-122, NIOFP2D_FNO bag mean 2d_FPE/NIOModules.py:565-575,
@@ -18,8 +18,6 @@
 using namespace blindno;
 
 namespace {
-
-constexpr int kWaves = kBlock / 64;
 
 // ---------------------------------------------------------------- lift
 __global__ __launch_bounds__(kBlock) void lift_fwd_kernel(const float* __restrict__ in,
@@ -223,177 +221,6 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __re
     float v = red[pl];
     for (int k = 1; k < S; ++k) v += red[k * PB + pl];
     out[p] = v;
-  }
-}
-
-// ---------------------------------------------------------------- inverse row transform
-// One wave per (grid row (n, h), channel group); lane owns w = lane + 64 q (q < NQ).
-//   acc[q][c] = sum_k Re(Z[n][h][k][c] e^{+2 pi i k w / P2})      for the CG channels of group g
-// The workgroup keeps the (m2 x P2) twiddle table T[k][w] in LDS (lane-contiguous reads) and
-// each wave stages its row's m2 x CG coefficients in LDS (broadcast reads).  The field values
-// the epilogue needs (x for the conv, dz for the adjoint) are loaded BEFORE the k loop so
-// their latency hides behind the transform.  Wide fields (the C = 12 heads) are split into
-// NG = C / CG channel groups so a 4-sample head layer still spreads over ~2000 waves.
-// MODE 0 (forward epilogue): z = acc + bc + Wc f(x)            (f = GELU if ACT)
-// MODE 1 (adjoint):          dx = (acc + Wc^T dz) * (ACT ? GELU'(xsrc) : 1)
-//                            and, with WG (one group only), per-lane sums of dz (x) f(xsrc)
-//                            for dWc / dbc.
-template <int CM, int CG, int NQ, int MODE, int ACT, int WG>
-__global__ __launch_bounds__(kBlock) void rowinv_kernel(
-    const float2* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
-    const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
-    const float2* __restrict__ twk, float* __restrict__ partial, int Bn, int C, int P1, int P2,
-    int m2) {
-  extern __shared__ float2 sm2[];
-  float2* T = sm2;                                  // [m2][P2]
-  const int lane = threadIdx.x & 63;
-  const int wave = uniform_int(threadIdx.x >> 6);
-  const int mc = m2 * C;
-  float2* zrow = T + m2 * P2 + wave * m2 * CG;      // [m2][CG] of the wave's current row
-  for (int e = threadIdx.x; e < m2 * P2; e += blockDim.x) {
-    const int k = e / P2, w = e % P2;
-    T[e] = twk[(int64_t)w * m2 + k];
-  }
-  __syncthreads();
-  constexpr int NW = WG ? CM * CM + CM : 1;
-  const int NG = (C + CG - 1) / CG;
-  const int nitems = Bn * P1 * NG;
-  const int64_t HW = (int64_t)P1 * P2;
-  float wacc[NW];
-#pragma unroll
-  for (int e = 0; e < NW; ++e) wacc[e] = 0.f;
-  const bool has_wc = wc != nullptr;
-  for (int item = blockIdx.x * kWaves + wave; item < nitems; item += gridDim.x * kWaves) {
-    const int row = item / NG, g = item - (item / NG) * NG;
-    const int c0 = g * CG;
-    const int n = row / P1, h = row % P1;
-    const int64_t rbase = (int64_t)n * C * HW + (int64_t)h * P2;
-    // ---- epilogue operands first (in flight during the transform)
-    constexpr int NF = (MODE == 0 || !WG) ? CM : CM;   // all C channels of the other side
-    float fv[NQ][NF];          // MODE 0: x (all inputs); MODE 1: dz (all outputs)
-    float sv[NQ][CG];          // MODE 1: xsrc of this group's channels (ACT / WG)
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int w = lane + 64 * q;
-      const bool ok = w < P2 && has_wc;
-#pragma unroll
-      for (int i = 0; i < NF; ++i)
-        fv[q][i] = (ok && i < C) ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
-#pragma unroll
-      for (int cl = 0; cl < CG; ++cl)
-        sv[q][cl] = (MODE == 1 && (ACT || WG) && w < P2 && c0 + cl < C) ? xs[rbase + (c0 + cl) * HW + w] : 0.f;
-    }
-    const float2* zr = Z + (int64_t)row * mc + c0;
-    for (int e = lane; e < m2 * CG; e += 64) {
-      const int k = e / CG, cl = e - (e / CG) * CG;
-      zrow[e] = c0 + cl < C ? zr[k * C + cl] : make_float2(0.f, 0.f);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float acc[NQ][CG];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int c = 0; c < CG; ++c) acc[q][c] = 0.f;
-    for (int k = 0; k < m2; ++k) {
-      float2 zc[CG];
-#pragma unroll
-      for (int c = 0; c < CG; ++c) zc[c] = zrow[k * CG + c];
-      const float2* Tk = T + k * P2;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int w = lane + 64 * q;
-        const float2 e = Tk[w < P2 ? w : 0];
-#pragma unroll
-        for (int c = 0; c < CG; ++c)
-          acc[q][c] = fmaf(zc[c].x, e.x, fmaf(-zc[c].y, e.y, acc[q][c]));
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int w = lane + 64 * q;
-      if (w >= P2) continue;
-      const int64_t base = rbase + w;
-      if (MODE == 0) {
-        if (has_wc) {
-          float xv[CM];
-#pragma unroll
-          for (int i = 0; i < CM; ++i) xv[i] = ACT ? gelu_f(fv[q][i]) : fv[q][i];
-#pragma unroll
-          for (int cl = 0; cl < CG; ++cl) {
-            const int o = c0 + cl;
-            if (o >= C) continue;
-            float v = acc[q][cl] + bc[o];
-#pragma unroll
-            for (int i = 0; i < CM; ++i)
-              if (i < C) v = fmaf(wc[o * C + i], xv[i], v);
-            out[base + o * HW] = v;
-          }
-        } else {
-#pragma unroll
-          for (int cl = 0; cl < CG; ++cl)
-            if (c0 + cl < C) out[base + (c0 + cl) * HW] = acc[q][cl];
-        }
-      } else {
-        if (has_wc) {
-          float xa[CG];
-#pragma unroll
-          for (int cl = 0; cl < CG; ++cl) {
-            const int i = c0 + cl;
-            float gi = acc[q][cl];
-#pragma unroll
-            for (int o = 0; o < CM; ++o) gi = fmaf((o < C && i < C) ? wc[o * C + i] : 0.f, fv[q][o], gi);
-            xa[cl] = sv[q][cl];
-            if (ACT) {
-              float a, dg;
-              gelu_both(sv[q][cl], a, dg);
-              gi *= dg;
-              xa[cl] = a;
-            }
-            if (i < C) out[base + i * HW] = gi;
-          }
-          if constexpr (WG != 0) {
-#pragma unroll
-            for (int o = 0; o < CM; ++o) {
-#pragma unroll
-              for (int cl = 0; cl < CG; ++cl) wacc[o * CM + cl] = fmaf(fv[q][o], xa[cl], wacc[o * CM + cl]);
-              wacc[CM * CM + o] += fv[q][o];
-            }
-          }
-        } else {
-#pragma unroll
-          for (int cl = 0; cl < CG; ++cl)
-            if (c0 + cl < C) out[base + (c0 + cl) * HW] = acc[q][cl];
-        }
-      }
-    }
-  }
-  if (WG) {
-    // block reduction of the per-lane conv-weight partials -> partial[blockIdx.x][C*C + C]
-    // (WG runs with a single channel group: CG == CM, c0 == 0)
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(sm2);   // reuse LDS (sized by the launcher)
-    const int np = C * C + C;
-#pragma unroll
-    for (int e = 0; e < NW; ++e) {
-      const int o = e < CM * CM ? e / CM : e - CM * CM;
-      const int i = e < CM * CM ? e % CM : -1;
-      if (o >= C || i >= C) continue;
-      const float s = wave_sum(wacc[e]);
-      const int pidx = i >= 0 ? o * C + i : C * C + o;
-      if (lane == 0) red[wave * np + pidx] = s;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-    for (int p = threadIdx.x; p < np; p += blockDim.x) {
-      float s = 0.f;
-      for (int w = 0; w < kWaves; ++w) s += red[w * np + p];
-      partial[(int64_t)blockIdx.x * np + p] = s;
-    }
   }
 }
 
@@ -700,62 +527,6 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float* __restrict__ p,
   }
 }
 
-// channels per wave: all of them up to 8 (one group, the conv-weight gradient can fuse),
-// groups of 4 above (the C = 12 heads: 3 groups)
-int rowinv_cg(int C) { return C <= 8 ? (C <= 4 ? 4 : 8) : 4; }
-
-int rowinv_blocks(int Bn, int P1, int C) {
-  const int ng = (C + rowinv_cg(C) - 1) / rowinv_cg(C);
-  const int64_t items = (int64_t)Bn * P1 * ng;
-  const int64_t b = (items + kWaves - 1) / kWaves;
-  return (int)(b < 2048 ? b : 2048);
-}
-
-template <int MODE, int ACT, int WG>
-int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
-                  const float* bc, float* out, const float* tw, float* partial, int nblocks,
-                  int Bn, int C, int P1, int P2, int m2, hipStream_t st) {
-  const int nq = (P2 + 63) / 64;
-  const int cm = C <= 4 ? 4 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
-  const int cg = rowinv_cg(C);
-  if (C > 32 || nq > 5) return (int)hipErrorInvalidValue;
-  if (WG && cm > 8) return (int)hipErrorInvalidValue;
-  size_t sh = sizeof(float2) * ((size_t)m2 * P2 + (size_t)kWaves * m2 * cg);
-  if (WG) {
-    const size_t need = sizeof(float) * (size_t)kWaves * (C * C + C);
-    if (need > sh) sh = need;
-  }
-  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
-  const dim3 g(nblocks), b(kBlock);
-  const float2* z2 = (const float2*)Z;
-  const float2* t2 = (const float2*)tw;
-#define RI(CM_, CG_, NQ_)                                                                      \
-  rowinv_kernel<CM_, CG_, NQ_, MODE, ACT, WG><<<g, b, sh, st>>>(z2, xs, dz, wc, bc, out, t2,     \
-                                                                partial, Bn, C, P1, P2, m2)
-#define RI_NQ(CM_, CG_)             \
-  switch (nq) {                     \
-    case 1: RI(CM_, CG_, 1); break; \
-    case 2: RI(CM_, CG_, 2); break; \
-    case 3: RI(CM_, CG_, 3); break; \
-    case 4: RI(CM_, CG_, 4); break; \
-    default: RI(CM_, CG_, 5); break; \
-  }
-  if (cm == 4) {
-    RI_NQ(4, 4)
-  } else if (cm == 8) {
-    RI_NQ(8, 8)
-  } else if constexpr (!WG) {
-    if (cm == 16) {
-      RI_NQ(16, 4)
-    } else {
-      RI_NQ(32, 4)
-    }
-  }
-#undef RI_NQ
-#undef RI
-  return (int)hipGetLastError();
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------------------ C ABI
@@ -827,37 +598,6 @@ BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nc
   return (int)hipGetLastError();
 }
 
-BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float* wc,
-                                    const float* bc, float* z, const float* tw2, int Bn, int C,
-                                    int P1, int P2, int m2, int act, void* stream) {
-  const int nb = rowinv_blocks(Bn, P1, C);
-  hipStream_t st = (hipStream_t)stream;
-  if (act)
-    return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
-  return rowinv_launch<0, 0, 0>(Z, x, nullptr, wc, bc, z, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
-}
-
-BLINDNO_API int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1) {
-  return C <= 8 ? rowinv_blocks(Bn, P1, C) : 0;
-}
-
-BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc,
-                                    const float* xsrc, float* dx, const float* tw2,
-                                    float* partial, int Bn, int C, int P1, int P2, int m2,
-                                    int act, void* stream) {
-  const int nb = rowinv_blocks(Bn, P1, C);
-  hipStream_t st = (hipStream_t)stream;
-  if (partial) {
-    if (C > 8 || !wc) return (int)hipErrorInvalidValue;
-    if (act)
-      return rowinv_launch<1, 1, 1>(G, xsrc, dz, wc, nullptr, dx, tw2, partial, nb, Bn, C, P1, P2, m2, st);
-    return rowinv_launch<1, 0, 1>(G, xsrc, dz, wc, nullptr, dx, tw2, partial, nb, Bn, C, P1, P2, m2, st);
-  }
-  if (act)
-    return rowinv_launch<1, 1, 0>(G, xsrc, dz, wc, nullptr, dx, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
-  return rowinv_launch<1, 0, 0>(G, xsrc, dz, wc, nullptr, dx, tw2, nullptr, nb, Bn, C, P1, P2, m2, st);
-}
-
 BLINDNO_API int blindno_project_fwd(const float* z, const float* w1, const float* b1,
                                     const float* w2, const float* b2, float* out, int Bn, int C,
                                     int P1, int P2, int Ho, int Wo, int Hd, int Cout,
@@ -899,7 +639,6 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
       nchunk < 1 || (int64_t)Bn * Ho * Wo >= INT32_MAX)
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const int np = Hd * C + Hd + Cout * Hd + Cout;
   const dim3 g(nchunk);
   if (project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
     return project_bwd_mfma(z, w1, b1, w2, dout, dz, partial, nchunk, Bn, C, P1, P2, Ho, Wo, Cout,

@@ -1,0 +1,280 @@
+// Inverse row transform of the spectral layers on the matrix cores, with the FNO layer
+// epilogue fused (irfft2 second stage + nn.Conv2d(k=1) + bias + residual add, and the GELU of
+// the layer input; 2d_FPE/FNOModules.py:177,226-232; 1d_FPE/FNOModules.py:58,108-114) and its
+// adjoint (with the GELU' of the layer input and, for narrow fields, the 1x1-conv weight
+// gradient reduced in the same pass).
+//
+// GEMM view: for a group of 4 grid rows (n, h) and 4 channels,
+//     out[(row, c)][w] = sum_k Re(Z[row][k][c] e^{+2 pi i k w / P2})
+//                      = sum_kk A[(row, c)][kk] B[kk][w],   kk = 2 k + part,
+//     A = (Re Z, Im Z) interleaved,  B = (cos, -sin)(2 pi k w / P2)
+// one v_mfma_f32_16x16x4f32 chain of ceil(m2 / 2) steps per 16-column tile: M = 16 = (4 rows x
+// 4 channels), N = 16 columns, K = 2 m2.  The D layout puts rows 4 (l>>4) + r of column l & 15 in
+// lane l; with M index 4 row + channel, lane l therefore holds ALL FOUR channels of one point
+// (row l>>4, column l&15), so the 1x1 conv / bias / GELU epilogue stays in registers.  Wider
+// fields (the C = 12 heads) run as channel groups of 4.  The B operand comes from a host-built
+// image in MFMA lane order (twiddle_rowinv, staged once per workgroup in LDS).
+#include "common.h"
+#include "blindno.h"
+#include "kernels.h"
+
+using namespace blindno;
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kW = 4;      // waves per workgroup
+
+// MODE 0 (forward epilogue): z = acc + bc + Wc f(x)                (f = GELU if ACT)
+// MODE 1 (adjoint):          dx = (acc + Wc^T dz) * (ACT ? GELU'(xsrc) : 1)
+//                            + with WG (C <= 4, one group): per-lane dWc / dbc sums
+// CM: channel bound of the conv (C rounded up to 4, 8, 16, 32).
+template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB>
+__global__ __launch_bounds__(256) void rowinv_mfma_kernel(
+    const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
+    const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
+    const float* __restrict__ TB, float* __restrict__ partial, int Bn, int C, int P1, int P2,
+    int m2, int TPW) {
+  extern __shared__ float sTB[];                    // [KS][NT][64] when LDSB
+  const int KS = (m2 + 1) >> 1;
+  const int NT = (P2 + 15) >> 4;
+  if (LDSB) {
+    const int ntb = KS * NT * 64;
+    for (int e = threadIdx.x; e < ntb; e += blockDim.x) sTB[e] = TB[e];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const int NG = (C + 3) >> 2;                      // channel groups of 4
+  const int nrows = Bn * P1;
+  const int nquads = (nrows + 3) >> 2;
+  const int NC = (NT + TPW - 1) / TPW;              // column chunks per (quad, group)
+  const int nitems = nquads * NG * NC;
+  const int64_t HW = (int64_t)P1 * P2;
+  const bool has_wc = wc != nullptr;
+  constexpr int NW = WG ? CM * CM + CM : 1;
+  float wacc[NW];
+#pragma unroll
+  for (int e = 0; e < NW; ++e) wacc[e] = 0.f;
+  for (int item = blockIdx.x * kW + wave; item < nitems; item += gridDim.x * kW) {
+    const int chunk = item % NC;
+    const int qg = item / NC;
+    const int g = qg % NG, quad = qg / NG;
+    const int c0 = 4 * g;
+    // A operand row of this lane: grid row R0 + (c16 >> 2), channel c0 + (c16 & 3)
+    const int ra = 4 * quad + (c16 >> 2), ca = c0 + (c16 & 3);
+    const bool aok = ra < nrows && ca < C;
+    const float* zrow = Z + ((int64_t)(aok ? ra : 0) * m2) * C * 2;
+    float av[KSM];                                  // A operand, reused by every column tile
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) {
+      const int kk = 4 * s + g4;                    // K index supplied by this lane
+      const int k = kk >> 1;
+      av[s] = (aok && s < KS && k < m2) ? zrow[(k * C + ca) * 2 + (kk & 1)] : 0.f;
+    }
+    // this lane's output point: row R0 + g4, column 16 tile + c16, channels c0 + r
+    const int ro = 4 * quad + g4;
+    const bool rok = ro < nrows;
+    const int n = rok ? ro / P1 : 0, h = rok ? ro - (ro / P1) * P1 : 0;
+    const int64_t rbase = (int64_t)n * C * HW + (int64_t)h * P2;
+    const int t0 = chunk * TPW, t1 = min(NT, t0 + TPW);
+    for (int tile = t0; tile < t1; ++tile) {
+      const int w = 16 * tile + c16;
+      const bool pok = rok && w < P2;
+      // epilogue operands first: their loads fly while the MFMA chain runs
+      float fv[CM];        // MODE 0: x of every input channel; MODE 1: dz of every output channel
+      float sv[4];         // MODE 1: xsrc of this group's channels
+#pragma unroll
+      for (int i = 0; i < CM; ++i)
+        fv[i] = (pok && has_wc && i < C) ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sv[r] = (MODE == 1 && (ACT || WG) && pok && c0 + r < C) ? xs[rbase + (c0 + r) * HW + w] : 0.f;
+      f32x4 d = {0.f, 0.f, 0.f, 0.f};
+      const float* tb = (LDSB ? (const float*)sTB : TB) + tile * 64 + lane;
+#pragma unroll
+      for (int s = 0; s < KSM; ++s)
+        if (s < KS) d = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], tb[s * NT * 64], d, 0, 0, 0);
+      if (!pok) continue;
+      if (MODE == 0) {
+        if (has_wc) {
+          float xv[CM];
+#pragma unroll
+          for (int i = 0; i < CM; ++i) xv[i] = ACT ? gelu_f(fv[i]) : fv[i];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int o = c0 + r;
+            if (o >= C) continue;
+            float v = d[r] + bc[o];
+#pragma unroll
+            for (int i = 0; i < CM; ++i)
+              if (i < C) v = fmaf(wc[o * C + i], xv[i], v);
+            out[rbase + o * HW + w] = v;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c0 + r < C) out[rbase + (c0 + r) * HW + w] = d[r];
+        }
+      } else {
+        if (has_wc) {
+          float xa[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = c0 + r;
+            float gi = d[r];
+#pragma unroll
+            for (int o = 0; o < CM; ++o) gi = fmaf((o < C && i < C) ? wc[o * C + i] : 0.f, fv[o], gi);
+            xa[r] = sv[r];
+            if (ACT) {
+              float a, dg;
+              gelu_both(sv[r], a, dg);
+              gi *= dg;
+              xa[r] = a;
+            }
+            if (i < C) out[rbase + i * HW + w] = gi;
+          }
+          if constexpr (WG != 0) {
+#pragma unroll
+            for (int o = 0; o < CM; ++o) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (r < CM) wacc[o * CM + r] = fmaf(fv[o], xa[r], wacc[o * CM + r]);
+              wacc[CM * CM + o] += fv[o];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c0 + r < C) out[rbase + (c0 + r) * HW + w] = d[r];
+        }
+      }
+    }
+  }
+  if (WG) {
+    // block reduction of the per-lane conv-weight partials -> partial[blockIdx.x][C*C + C]
+    __syncthreads();
+    float* red = sTB;                               // reuse LDS (sized by the launcher)
+    const int np = C * C + C;
+#pragma unroll
+    for (int e = 0; e < NW; ++e) {
+      const int o = e < CM * CM ? e / CM : e - CM * CM;
+      const int i = e < CM * CM ? e % CM : -1;
+      if (o >= C || i >= C) continue;
+      const float s = wave_sum(wacc[e]);
+      const int pidx = i >= 0 ? o * C + i : C * C + o;
+      if (lane == 0) red[wave * np + pidx] = s;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+      float s = 0.f;
+      for (int w = 0; w < kW; ++w) s += red[w * np + p];
+      partial[(int64_t)blockIdx.x * np + p] = s;
+    }
+  }
+}
+
+struct RowinvGeom {
+  int nitems, TPW, blocks;
+  bool ldsb;
+  size_t lds;
+};
+
+RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
+  RowinvGeom g;
+  const int KS = (m2 + 1) / 2, NT = (P2 + 15) / 16;
+  const int NG = (C + 3) / 4;
+  const int64_t base = (int64_t)((Bn * P1 + 3) / 4) * NG;
+  // columns per work item: all of a row group when there is plenty of row parallelism,
+  // split down to one tile for the small head layers
+  int tpw = NT;
+  while (tpw > 1 && base * ((NT + tpw - 1) / tpw) < 8192) tpw = (tpw + 1) / 2;
+  g.TPW = tpw;
+  g.nitems = (int)(base * ((NT + tpw - 1) / tpw));
+  // persistent workgroups; the twiddle image is staged in LDS only when each workgroup
+  // reuses it over several items (otherwise every MFMA step reads it from L1/L2)
+  const int b = (g.nitems + kW - 1) / kW;
+  const size_t tbytes = sizeof(float) * (size_t)KS * NT * 64;
+  g.ldsb = tbytes <= 48 * 1024 && g.nitems >= 8192;
+  const int cap = g.ldsb ? 1024 : 2048;
+  g.blocks = b < cap ? b : cap;
+  g.lds = g.ldsb ? tbytes : 0;
+  return g;
+}
+
+template <int MODE, int ACT, int WG>
+int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
+                  const float* bc, float* out, const float* TB, float* partial, int nblocks,
+                  int Bn, int C, int P1, int P2, int m2, hipStream_t st) {
+  if (Bn <= 0 || C <= 0 || C > 32 || m2 <= 0 || P2 <= 0) return (int)hipErrorInvalidValue;
+  if (WG && C > 4) return (int)hipErrorInvalidValue;
+  const int64_t zel = (int64_t)Bn * P1 * m2 * C * 2, fel = (int64_t)Bn * C * P1 * P2;
+  if (zel >= INT32_MAX || fel >= ((int64_t)1 << 40)) return (int)hipErrorInvalidValue;
+  RowinvGeom g = rowinv_geom(Bn, C, P1, P2, m2);
+  size_t sh = g.lds;
+  if (WG) {
+    const size_t need = sizeof(float) * (size_t)kW * (C * C + C);
+    if (need > sh) sh = need;
+  }
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+  const int cm = C <= 4 ? 4 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
+  const int ks = (m2 + 1) / 2;
+  if (ks > 24) return (int)hipErrorInvalidValue;               // m2 <= 48
+#define RI(CM_, KS_)                                                                         \
+  do {                                                                                       \
+    if (g.ldsb)                                                                              \
+      rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 1><<<nblocks, 256, sh, st>>>(              \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW);                    \
+    else                                                                                     \
+      rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 0><<<nblocks, 256, sh, st>>>(              \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW);                    \
+  } while (0)
+#define RI_K(CM_) \
+  if (ks <= 8) RI(CM_, 8); else if (ks <= 16) RI(CM_, 16); else RI(CM_, 24);
+  if (cm == 4) {
+    RI_K(4)
+  } else if constexpr (!WG) {
+    if (cm == 8) { RI_K(8) }
+    else if (cm == 16) { RI_K(16) }
+    else { RI_K(32) }
+  }
+#undef RI_K
+#undef RI
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float* wc,
+                                    const float* bc, float* z, const float* tb, int Bn, int C,
+                                    int P1, int P2, int m2, int act, void* stream) {
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  hipStream_t st = (hipStream_t)stream;
+  if (act)
+    return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
+  return rowinv_launch<0, 0, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
+}
+
+BLINDNO_API int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2) {
+  return C <= 4 ? rowinv_geom(Bn, C, P1, P2, m2).blocks : 0;
+}
+
+BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc,
+                                    const float* xsrc, float* dx, const float* tb,
+                                    float* partial, int Bn, int C, int P1, int P2, int m2,
+                                    int act, void* stream) {
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  hipStream_t st = (hipStream_t)stream;
+  if (partial) {
+    if (C > 4 || !wc) return (int)hipErrorInvalidValue;
+    if (act)
+      return rowinv_launch<1, 1, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st);
+    return rowinv_launch<1, 0, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st);
+  }
+  if (act)
+    return rowinv_launch<1, 1, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
+  return rowinv_launch<1, 0, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
+}
