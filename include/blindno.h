@@ -142,6 +142,34 @@ int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc, const 
                         int P2, int m2, int act, blindno_stream_t stream);
 int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2);
 
+/* --- snapshot-encoder first layer with the lift folded in (NIOFP2D_FNO.FNO_input) ----------
+ * The encoder input is cat(u_l, gx, gy) for snapshots u_l = X[b][idx[l]] of the bag tensor X
+ * (B, T, N1, N2) (2d_FPE/NIOModules.py:548-560), lifted by fc0 (C x 3) and zero-padded to
+ * P1 x P2 (2d_FPE/FNOModules.py:219-224).  These entry points read u straight from X through
+ * the device index list idx (L int32) and never materialise the gathered bag, the input or x0. */
+
+/* Row DFT of x0: At[n][k][c][h] = w0[c*3] U[n][k][h] + Gt[k][c][h] (n = b L + l), U the row
+ * DFT of the zero-padded snapshot, Gt (m2, C, P1) complex the row DFT of the grid/bias part of x0
+ * (x0 of an all-zero snapshot).  At as blindno_rowdft; Tp its B-operand image. */
+int blindno_rowdft_bag_lift(const float* X, const int* idx, const float* w0, const float* Gt,
+                            float* At, const float* Tp, int B, int T, int L, int N1, int N2,
+                            int C, int P1, int P2, int m2, blindno_stream_t stream);
+
+/* blindno_rowidft_epi (act 0) with x = x0 recomputed from (X, idx, grid, w0, b0); C <= 4. */
+int blindno_rowidft_epi_lift(const float* Z, const float* X, const int* idx, const float* grid,
+                             const float* w0, const float* b0, const float* wc, const float* bc,
+                             float* z, const float* tb, int B, int T, int L, int N1, int N2,
+                             int C, int P1, int P2, int m2, blindno_stream_t stream);
+
+/* Adjoint of blindno_rowidft_epi_lift: dx0 = irow^H(G) + Wc^T dz is NOT written; the pass
+ * reduces partial[blindno_rowidft_bwd_nchunk(B L, C, P1, P2, m2)][C*C + C + 4 C] =
+ * [dWc | dbc | dW0 (C x 3) | db0 (C)] with dWc[o][i] = sum dz_o x0_i, dW0[c][j] = sum over the
+ * N1 x N2 crop of dx0_c [u, gx, gy]_j, db0[c] = sum dx0_c.  C <= 4. */
+int blindno_rowidft_bwd_lift(const float* G, const float* dz, const float* X, const int* idx,
+                             const float* grid, const float* w0, const float* b0, const float* wc,
+                             const float* tb, float* partial, int B, int T, int L, int N1, int N2,
+                             int C, int P1, int P2, int m2, blindno_stream_t stream);
+
 /* 1x1-conv weight/bias gradient partials (for C > 8): partial[nchunk][C*C + C] with
  * dWc[o,i] = sum dz[n,o,.] f(x[n,i,.]),  dbc[o] = sum dz[n,o,.];
  * nchunk must equal blindno_conv_wgrad_nchunk(Bn, P1, P2). */

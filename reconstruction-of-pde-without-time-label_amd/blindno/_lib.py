@@ -24,6 +24,9 @@ SIGNATURES = {
     "blindno_project_fwd": "ppppppiiiiiiiiiis",
     "blindno_project_bwd": "pppppppiiiiiiiiiiiis",
     "blindno_rowdft": "pppiiiiiis",
+    "blindno_rowdft_bag_lift": "ppppppiiiiiiiiis",
+    "blindno_rowidft_epi_lift": "ppppppppppiiiiiiiiis",
+    "blindno_rowidft_bwd_lift": "ppppppppppiiiiiiiiis",
     "blindno_colpass": "pppppppiiiiiiiis",
     "blindno_mix_wgrad": "ppppiiiiiis",
     "blindno_mix1d": "ppppiiiiiis",

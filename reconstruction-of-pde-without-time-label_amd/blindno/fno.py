@@ -75,7 +75,7 @@ class SpectralConv2d(nn.Module):
         return ops.SpectralConvFn.apply(x, w1, w2)
 
 
-def _fno_params(m, dim):
+def fno_params(m, dim):
     ps = [m.fc0.weight, m.fc0.bias]
     for s, c in zip(m.spectral_list, m.conv_list):
         if dim == 2:
@@ -110,7 +110,7 @@ class FNO1d(nn.Module):
                            self.fc2.out_features, cin)
 
     def forward(self, x):
-        return ops.FNOFn.apply(self.meta(x.shape[-1]), x, *_fno_params(self, 1))
+        return ops.FNOFn.apply(self.meta(x.shape[-1]), x, *fno_params(self, 1))
 
 
 class FNO2d(nn.Module):
@@ -142,7 +142,7 @@ class FNO2d(nn.Module):
                            self.fc1.out_features, self.fc2.out_features, cin)
 
     def forward(self, x):
-        return ops.FNOFn.apply(self.meta(x.shape[-1]), x, *_fno_params(self, 2))
+        return ops.FNOFn.apply(self.meta(x.shape[-1]), x, *fno_params(self, 2))
 
 
 class SpectralConv3d(nn.Module):

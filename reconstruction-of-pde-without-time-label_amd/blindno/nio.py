@@ -20,7 +20,7 @@ import torch.nn as nn
 from . import ops
 from .deeponet import FFN, DeepOnetNoBiasOrg
 from .encoders import Encoder, Encoder2D
-from .fno import FNO1d, FNO2d
+from .fno import FNO1d, FNO2d, fno_params
 
 
 def draw_bag(T: int):
@@ -73,8 +73,30 @@ class NIOFP2D_FNO(nn.Module):
             setattr(self, name, FNO2d(modes=modes, width=width, n_layers=self.fno_layers,
                                       input_dim=width, output_dim=1))
 
+    def _fused_ok(self, x, grid):
+        return (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and
+                grid.dtype == torch.float32 and tuple(grid.shape) == (x.shape[2], x.shape[3], 2) and
+                self.FNO_input.width <= 4 and
+                not (torch.is_grad_enabled() and (x.requires_grad or grid.requires_grad)))
+
     def forward(self, x, grid, bag_idx=None):
-        """x (B, T, Nx, Ny) standardised snapshots, grid (Nx, Ny, 2) -> (B, Nx, Ny, 2)."""
+        """x (B, T, Nx, Ny) standardised snapshots, grid (Nx, Ny, 2) -> (B, Nx, Ny, 2).
+
+        Without input gradients the snapshot encoder + bag mean run as the fused HIP path
+        (ops.BagEncoderFn: snapshots read from x through the bag's indices); otherwise as the
+        generic composition below (same numerics, gradients for x and grid)."""
+        if self._fused_ok(x, grid):
+            if bag_idx is not None:
+                idx = np.asarray(bag_idx)
+            elif self.training:
+                _, idx = draw_bag(x.shape[1])
+            else:
+                idx = np.arange(x.shape[1])
+            idx_t = torch.as_tensor(np.asarray(idx, dtype=np.int32), device=x.device)
+            fno = self.FNO_input
+            h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, grid, self.fc0.weight.data,
+                                       self.fc0.bias.data, *fno_params(fno, 2))
+            return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
         x, L = _select(self, x, bag_idx)
         B, _, nx, ny = x.shape
         x_in = x.reshape(B * L, 1, nx, ny)

@@ -497,6 +497,136 @@ class FNOFn(torch.autograd.Function):
         return (None, d_inp, *grads)
 
 
+# ---------------------------------------------------------------------------- fused snapshot encoder
+
+
+def k_rowdft_bag_lift(X, idx_t, w0, Gt, B, T, L, N1, N2, C, P1, P2, m2):
+    At = _empty(B * L, m2, C, P1, 2, like=X)
+    call("blindno_rowdft_bag_lift", ptr(X), ptr(idx_t), ptr(w0), ptr(Gt), ptr(At),
+         ptr(twiddle_mfma(P2, m2, X.device)), B, T, L, N1, N2, C, P1, P2, m2, stream_ptr())
+    return At
+
+
+class BagEncoderFn(torch.autograd.Function):
+    """The snapshot-bag encoder of NIOFP2D_FNO as ONE autograd node (2d_FPE/NIOModules.py:
+    548-575): FNO_input (an FNO2d of input [u, gx, gy]) on every snapshot of the bag, then the
+    fixed-weight bag mean.  Snapshots are read straight from the bag tensor X (B, T, N1, N2)
+    through the device index list idx_t (the bag draw); the gathered bag, the concatenated
+    input and the lifted field x0 are never materialised (the lift is folded into the first
+    row DFT and recomputed in the first layer's epilogue / adjoint, which also reduces fc0's
+    gradient).  The bag mean's gradient reaches the projection as a per-bag field (dout_div =
+    L) instead of an L-fold broadcast copy.  No gradient flows to X or grid (the caller uses
+    the generic path when they require one)."""
+
+    @staticmethod
+    def forward(ctx, meta, X, idx_t, grid, bw, bb, *prm):
+        require_device(X, grid, *prm)
+        X, grid = _c(X), _c(grid)
+        prm = [_c(p) for p in prm]
+        bw, bb = _c(bw.detach()), _c(bb.detach())
+        B, T, N1, N2 = X.shape
+        L = idx_t.numel()
+        Bn = B * L
+        fake = torch.empty((Bn, N1, N2, 3), device="meta")
+        _, _, _, _, P1, P2, Ho, Wo = _fno_geometry(fake, meta)
+        C, n = meta.width, meta.n_layers
+        if C > 4 or meta.dim != 2 or n < 1:
+            raise BlindnoError("BagEncoderFn: needs a 2D FNO of width <= 4")
+        fc0w, fc0b = prm[0], prm[1]
+        # grid / bias part of x0 (x0 of an all-zero snapshot) and its row DFT
+        inp0 = torch.cat([torch.zeros(1, N1, N2, 1, device=X.device), grid.view(1, N1, N2, 2)], -1)
+        g0 = _empty(1, C, P1, P2, like=X)
+        call("blindno_lift_fwd", ptr(inp0), ptr(fc0w), ptr(fc0b), ptr(g0), 1, N1, N2, 3, C, P1, P2,
+             stream_ptr())
+        Gt = k_rowdft(g0, 1, C, P1, P2, meta.m2, 0)
+        sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
+        Xs, Wts, zs = [], [], []
+        for k in range(n):
+            off = 2 + k * 4
+            w1, w2, cw, cb = prm[off:off + 4]
+            Wt = pack_weights((w1, w2), P1, 2)
+            if k == 0:
+                At = k_rowdft_bag_lift(X, idx_t, fc0w, Gt, B, T, L, N1, N2, C, P1, P2, meta.m2)
+                Xk, Z = k_colpass(At, Wt, Bn, C, C, P1, meta.m1, meta.m2, P2, 0)
+                z = _empty(Bn, C, P1, P2, like=X)
+                call("blindno_rowidft_epi_lift", ptr(Z), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),
+                     ptr(fc0b), ptr(cw), ptr(cb), ptr(z), ptr(twiddle_rowinv(P2, meta.m2, X.device)),
+                     B, T, L, N1, N2, C, P1, P2, meta.m2, stream_ptr())
+            else:
+                Xk, Z = spec_forward(zs[-1], 1, Wt, sh)
+                z = k_rowidft_epi(Z, zs[-1], cw, cb, Bn, C, P1, P2, meta.m2, 1)
+            Xs.append(Xk)
+            Wts.append(Wt)
+            zs.append(z)
+        fc1w, fc1b, fc2w, fc2b = prm[2 + 4 * n:6 + 4 * n]
+        Hd, Cout = fc1w.shape[0], fc2w.shape[0]
+        u = _empty(Bn, Ho, Wo, Cout, like=X)
+        call("blindno_project_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b), ptr(u),
+             Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, stream_ptr())
+        S = Ho * Wo
+        width = bw.shape[0]
+        h = _empty(B, S, width, like=X)
+        call("blindno_bagmean_fwd", ptr(u), ptr(grid), ptr(bw), ptr(bb), ptr(h), B, L, S, 2, width,
+             stream_ptr())
+        ctx.meta, ctx.n, ctx.dims = meta, n, (B, T, L, N1, N2, C, P1, P2, Ho, Wo, Hd, Cout, width)
+        ctx.save_for_backward(X, idx_t, grid, bw, *Xs, *Wts, *zs, *prm)
+        return h.view(B, N1, N2, width)
+
+    @staticmethod
+    def backward(ctx, gh):
+        meta, n = ctx.meta, ctx.n
+        B, T, L, N1, N2, C, P1, P2, Ho, Wo, Hd, Cout, width = ctx.dims
+        t = ctx.saved_tensors
+        X, idx_t, grid, bw = t[:4]
+        Xs, Wts, zs = list(t[4:4 + n]), list(t[4 + n:4 + 2 * n]), list(t[4 + 2 * n:4 + 3 * n])
+        prm = list(t[4 + 3 * n:])
+        Bn, S = B * L, Ho * Wo
+        gh = _c(gh)
+        grads = [None] * len(prm)
+        # bag mean: every snapshot of bag b receives the same gradient s[b]
+        sgr = _empty(B, S, like=gh)
+        call("blindno_bagmean_bwd", ptr(gh), ptr(bw), ptr(sgr), B, S, 2, width, L, stream_ptr())
+        # projection (dout read per bag: dout_div = L)
+        off_fc1 = 2 + 4 * n
+        fc1w, fc1b, fc2w = prm[off_fc1:off_fc1 + 3]
+        dz = torch.zeros(Bn, C, P1, P2, dtype=F32, device=gh.device)
+        np_p = Hd * C + Hd + Cout * Hd + Cout
+        nchunk = query("blindno_project_bwd_nchunk", Bn, Ho, Wo)
+        partial = _empty(nchunk, np_p, like=gh)
+        call("blindno_project_bwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(sgr), ptr(dz),
+             ptr(partial), nchunk, Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, L, stream_ptr())
+        gp = reduce_partials(partial, nchunk, np_p)
+        o = 0
+        grads[off_fc1] = gp[o:o + Hd * C].view(Hd, C); o += Hd * C
+        grads[off_fc1 + 1] = gp[o:o + Hd]; o += Hd
+        grads[off_fc1 + 2] = gp[o:o + Cout * Hd].view(Cout, Hd); o += Cout * Hd
+        grads[off_fc1 + 3] = gp[o:o + Cout]
+        sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
+        fc0w, fc0b = prm[0], prm[1]
+        for k in reversed(range(n)):
+            off = 2 + 4 * k
+            w1, w2, cw, cb = prm[off:off + 4]
+            dWt, GZ = spec_backward(dz, Xs[k], Wts[k], sh)
+            grads[off], grads[off + 1] = unpack_weights(dWt, (w1, w2), P1, 2)
+            if k > 0:
+                dz, gw, gb = k_rowidft_bwd(GZ, dz, cw, zs[k - 1], Bn, C, P1, P2, meta.m2, 1, True)
+                grads[off + 2], grads[off + 3] = gw.view_as(cw), gb
+            else:
+                nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, meta.m2)
+                npl = C * C + C + 4 * C
+                part = _empty(nchunk, npl, like=gh)
+                call("blindno_rowidft_bwd_lift", ptr(GZ), ptr(dz), ptr(X), ptr(idx_t), ptr(grid),
+                     ptr(fc0w), ptr(fc0b), ptr(cw), ptr(twiddle_rowinv(P2, meta.m2, X.device)),
+                     ptr(part), B, T, L, N1, N2, C, P1, P2, meta.m2, stream_ptr())
+                g = reduce_partials(part, nchunk, npl)
+                grads[off + 2] = g[:C * C].view_as(cw)
+                grads[off + 3] = g[C * C:C * C + C]
+                grads[0] = g[C * C + C:C * C + 4 * C].view(C, 3)
+                grads[1] = g[C * C + 4 * C:]
+        grads = [gr if ctx.needs_input_grad[6 + i] else None for i, gr in enumerate(grads)]
+        return (None, None, None, None, None, None, *grads)
+
+
 # ---------------------------------------------------------------------------- bag mean
 
 

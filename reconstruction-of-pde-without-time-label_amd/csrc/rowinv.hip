@@ -26,16 +26,31 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW = 4;      // waves per workgroup
 
+// Snapshot-encoder lift source (LIFT kernels): the layer input is x0 = fc0([u, gx, gy]),
+// zero outside the N1 x N2 crop, recomputed from the bag tensor instead of being stored.
+struct BagLift {
+  const float* X;      // bags (B, T, N1, N2); snapshot n = b L + l -> X[b][idx[l]]
+  const int* idx;      // (L,) device indices of the bag draw
+  const float* grid;   // (N1, N2, 2)
+  const float* w0;     // fc0.weight (C, 3)
+  const float* b0;     // fc0.bias (C)
+  int T, L, N1, N2;
+};
+
 // MODE 0 (forward epilogue): z = acc + bc + Wc f(x)                (f = GELU if ACT)
 // MODE 1 (adjoint):          dx = (acc + Wc^T dz) * (ACT ? GELU'(xsrc) : 1)
 //                            + with WG (C <= 4, one group): per-lane dWc / dbc sums
 // CM: channel bound of the conv (C rounded up to 4, 8, 16, 32).
-template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB>
+// LIFT: the layer input is the snapshot encoder's lifted field (BagLift); MODE 0 recomputes
+// x0 for the conv term, MODE 1 (with WG, ACT 0, C <= 4) recomputes it for dWc and, instead of
+// writing dx0, reduces fc0's gradient dW0[c][j] = sum dx0[c] [u, gx, gy]_j, db0[c] = sum dx0[c]
+// over the crop into partial[..][C*C + C + 4 C] (after the conv terms).
+template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB, int LIFT>
 __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int C, int P1, int P2,
-    int m2, int TPW) {
+    int m2, int TPW, BagLift bl) {
   extern __shared__ float sTB[];                    // [KS][NT][64] when LDSB
   const int KS = (m2 + 1) >> 1;
   const int NT = (P2 + 15) >> 4;
@@ -54,7 +69,9 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
   const int nitems = nquads * NG * NC;
   const int64_t HW = (int64_t)P1 * P2;
   const bool has_wc = wc != nullptr;
-  constexpr int NW = WG ? CM * CM + CM : 1;
+  constexpr int NWC = WG ? CM * CM + CM : 0;      // conv weight / bias sums
+  constexpr int NWL = LIFT && MODE == 1 ? 4 * CM : 0;   // fc0 weight / bias sums
+  constexpr int NW = NWC + NWL > 0 ? NWC + NWL : 1;
   float wacc[NW];
 #pragma unroll
   for (int e = 0; e < NW; ++e) wacc[e] = 0.f;
@@ -79,6 +96,13 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     const bool rok = ro < nrows;
     const int n = rok ? ro / P1 : 0, h = rok ? ro - (ro / P1) * P1 : 0;
     const int64_t rbase = (int64_t)n * C * HW + (int64_t)h * P2;
+    const float* urow = nullptr;                    // LIFT: snapshot row / grid row
+    const float* grow = nullptr;
+    if (LIFT && rok && h < bl.N1) {
+      const int b = n / bl.L, l = n - (n / bl.L) * bl.L;
+      urow = bl.X + (((int64_t)b * bl.T + bl.idx[l]) * bl.N1 + h) * bl.N2;
+      grow = bl.grid + (int64_t)h * bl.N2 * 2;
+    }
     const int t0 = chunk * TPW, t1 = min(NT, t0 + TPW);
     for (int tile = t0; tile < t1; ++tile) {
       const int w = 16 * tile + c16;
@@ -86,12 +110,30 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
       // epilogue operands first: their loads fly while the MFMA chain runs
       float fv[CM];        // MODE 0: x of every input channel; MODE 1: dz of every output channel
       float sv[4];         // MODE 1: xsrc of this group's channels
+      float lin[3] = {0.f, 0.f, 0.f};               // LIFT: [u, gx, gy] at this point
+      bool lok = false;
+      if (LIFT) {
+        lok = pok && urow != nullptr && w < bl.N2;
+        if (lok) {
+          lin[0] = urow[w];
+          lin[1] = grow[2 * w];
+          lin[2] = grow[2 * w + 1];
+        }
+      }
+      auto x0 = [&](int c) -> float {               // the lifted field (0 outside the crop)
+        return lok ? fmaf(bl.w0[c * 3], lin[0], fmaf(bl.w0[c * 3 + 1], lin[1],
+                                                     fmaf(bl.w0[c * 3 + 2], lin[2], bl.b0[c]))) : 0.f;
+      };
 #pragma unroll
-      for (int i = 0; i < CM; ++i)
-        fv[i] = (pok && has_wc && i < C) ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
+      for (int i = 0; i < CM; ++i) {
+        if (LIFT && MODE == 0) fv[i] = (has_wc && i < C) ? x0(i) : 0.f;
+        else fv[i] = (pok && has_wc && i < C) ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
+      }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        sv[r] = (MODE == 1 && (ACT || WG) && pok && c0 + r < C) ? xs[rbase + (c0 + r) * HW + w] : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        if (LIFT && MODE == 1) sv[r] = c0 + r < C ? x0(c0 + r) : 0.f;
+        else sv[r] = (MODE == 1 && (ACT || WG) && pok && c0 + r < C) ? xs[rbase + (c0 + r) * HW + w] : 0.f;
+      }
       f32x4 d = {0.f, 0.f, 0.f, 0.f};
       const float* tb = (LDSB ? (const float*)sTB : TB) + tile * 64 + lane;
 #pragma unroll
@@ -134,7 +176,15 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
               gi *= dg;
               xa[r] = a;
             }
-            if (i < C) out[rbase + i * HW + w] = gi;
+            if (LIFT) {
+              if (i < C && lok) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) wacc[NWC + 4 * r + j] = fmaf(gi, lin[j], wacc[NWC + 4 * r + j]);
+                wacc[NWC + 4 * r + 3] += gi;
+              }
+            } else if (i < C) {
+              out[rbase + i * HW + w] = gi;
+            }
           }
           if constexpr (WG != 0) {
 #pragma unroll
@@ -154,17 +204,28 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     }
   }
   if (WG) {
-    // block reduction of the per-lane conv-weight partials -> partial[blockIdx.x][C*C + C]
+    // block reduction of the per-lane partials -> partial[blockIdx.x][np],
+    // np = C*C + C (+ 4 C for LIFT: dW0 (C x 3) then db0 (C))
     __syncthreads();
     float* red = sTB;                               // reuse LDS (sized by the launcher)
-    const int np = C * C + C;
+    const int np = C * C + C + (NWL ? 4 * C : 0);
 #pragma unroll
     for (int e = 0; e < NW; ++e) {
-      const int o = e < CM * CM ? e / CM : e - CM * CM;
-      const int i = e < CM * CM ? e % CM : -1;
-      if (o >= C || i >= C) continue;
+      int pidx;
+      if (e < CM * CM) {
+        const int o = e / CM, i = e % CM;
+        if (o >= C || i >= C) continue;
+        pidx = o * C + i;
+      } else if (e < NWC) {
+        const int o = e - CM * CM;
+        if (o >= C) continue;
+        pidx = C * C + o;
+      } else {
+        const int c = (e - NWC) >> 2, j = (e - NWC) & 3;
+        if (c >= C) continue;
+        pidx = C * C + C + (j < 3 ? c * 3 + j : 3 * C + c);
+      }
       const float s = wave_sum(wacc[e]);
-      const int pidx = i >= 0 ? o * C + i : C * C + o;
       if (lane == 0) red[wave * np + pidx] = s;
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -205,10 +266,10 @@ RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   return g;
 }
 
-template <int MODE, int ACT, int WG>
+template <int MODE, int ACT, int WG, int LIFT = 0>
 int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
                   const float* bc, float* out, const float* TB, float* partial, int nblocks,
-                  int Bn, int C, int P1, int P2, int m2, hipStream_t st) {
+                  int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{}) {
   if (Bn <= 0 || C <= 0 || C > 32 || m2 <= 0 || P2 <= 0) return (int)hipErrorInvalidValue;
   if (WG && C > 4) return (int)hipErrorInvalidValue;
   const int64_t zel = (int64_t)Bn * P1 * m2 * C * 2, fel = (int64_t)Bn * C * P1 * P2;
@@ -216,7 +277,7 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   RowinvGeom g = rowinv_geom(Bn, C, P1, P2, m2);
   size_t sh = g.lds;
   if (WG) {
-    const size_t need = sizeof(float) * (size_t)kW * (C * C + C);
+    const size_t need = sizeof(float) * (size_t)kW * (C * C + C + (LIFT ? 4 * C : 0));
     if (need > sh) sh = need;
   }
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
@@ -226,17 +287,17 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
 #define RI(CM_, KS_)                                                                         \
   do {                                                                                       \
     if (g.ldsb)                                                                              \
-      rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 1><<<nblocks, 256, sh, st>>>(              \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW);                    \
+      rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 1, LIFT><<<nblocks, 256, sh, st>>>(        \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl);                \
     else                                                                                     \
-      rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 0><<<nblocks, 256, sh, st>>>(              \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW);                    \
+      rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 0, LIFT><<<nblocks, 256, sh, st>>>(        \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl);                \
   } while (0)
 #define RI_K(CM_) \
   if (ks <= 8) RI(CM_, 8); else if (ks <= 16) RI(CM_, 16); else RI(CM_, 24);
   if (cm == 4) {
     RI_K(4)
-  } else if constexpr (!WG) {
+  } else if constexpr (!WG && !LIFT) {
     if (cm == 8) { RI_K(8) }
     else if (cm == 16) { RI_K(16) }
     else { RI_K(32) }
@@ -277,4 +338,32 @@ BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float
   if (act)
     return rowinv_launch<1, 1, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
   return rowinv_launch<1, 0, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
+}
+
+// Snapshot-encoder first layer (LIFT): the layer input is fc0([u, gx, gy]) recomputed from
+// the bag tensor (see BagLift); forward epilogue / adjoint with fc0's gradient reduced in pass.
+BLINDNO_API int blindno_rowidft_epi_lift(const float* Z, const float* X, const int* idx,
+                                         const float* grid, const float* w0, const float* b0,
+                                         const float* wc, const float* bc, float* z,
+                                         const float* tb, int B, int T, int L, int N1, int N2,
+                                         int C, int P1, int P2, int m2, void* stream) {
+  if (!wc || !bc || C > 4 || N1 > P1 || N2 > P2) return (int)hipErrorInvalidValue;
+  const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
+  const int Bn = B * L;
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  return rowinv_launch<0, 0, 0, 1>(Z, nullptr, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2,
+                                   m2, (hipStream_t)stream, bl);
+}
+
+BLINDNO_API int blindno_rowidft_bwd_lift(const float* G, const float* dz, const float* X,
+                                         const int* idx, const float* grid, const float* w0,
+                                         const float* b0, const float* wc, const float* tb,
+                                         float* partial, int B, int T, int L, int N1, int N2,
+                                         int C, int P1, int P2, int m2, void* stream) {
+  if (!wc || !partial || C > 4 || N1 > P1 || N2 > P2) return (int)hipErrorInvalidValue;
+  const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
+  const int Bn = B * L;
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  return rowinv_launch<1, 0, 1, 1>(G, nullptr, dz, wc, nullptr, nullptr, tb, partial,
+                                   nb, Bn, C, P1, P2, m2, (hipStream_t)stream, bl);
 }

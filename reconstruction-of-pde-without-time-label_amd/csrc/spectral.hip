@@ -96,6 +96,81 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
   }
 }
 
+// Row DFT of the first FNO layer of the snapshot encoder with the lift folded in.  The lifted
+// field x0[n][c][h][w] = W0[c,0] u[n][h][w] + W0[c,1] gx[h][w] + W0[c,2] gy[h][w] + b0[c]
+// (zero-padded to P1 x P2; 2d_FPE/FNOModules.py:219-224) is affine in the snapshot u, and the
+// DFT is linear, so
+//     At[n][k][c][h] = W0[c,0] U[n][k][h] + Gt[k][c][h],   U = rowDFT(u),
+// with Gt = rowDFT of the grid/bias part (one sample, computed once per forward).  Only the
+// 1-channel snapshot is transformed, and it is read straight out of the bag tensor
+// X (B, T, N1, N2) through the bag's index list (snapshot n = b L + l -> X[b][idx[l]]), so
+// neither the gathered bag, the concatenated input nor x0 is ever materialised.
+template <int NT, int ALIGNED>
+__global__ __launch_bounds__(256) void rowdft_bag_lift_kernel(
+    const float* __restrict__ X, const int* __restrict__ idx, const float* __restrict__ w0,
+    const float* __restrict__ Gt, float* __restrict__ At, const float* __restrict__ Tp, int nrows,
+    int T, int L, int N1, int N2, int C, int P1, int m2, int KB, int Npad, int ntile_groups) {
+  extern __shared__ float smT[];                 // [KB][4][Npad][4]
+  const int nT = KB * 16 * Npad;
+  for (int e = threadIdx.x; e < nT; e += blockDim.x) smT[e] = Tp[e];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int nrt = (nrows + 15) >> 4;
+  const int64_t nwork = (int64_t)nrt * ntile_groups;
+  for (int64_t wk = (int64_t)blockIdx.x * 4 + wave; wk < nwork; wk += (int64_t)gridDim.x * 4) {
+    const int rt = (int)(wk / ntile_groups);
+    const int tg = (int)(wk % ntile_groups);
+    const int t0 = tg * NT;
+    const int row = rt * 16 + r16;
+    const int n = row / P1, h = row - (row / P1) * P1;
+    const bool rok = row < nrows && h < N1;
+    const float* xr = X;
+    if (rok) {
+      const int b = n / L, l = n - (n / L) * L;
+      xr = X + (((int64_t)b * T + idx[l]) * N1 + h) * N2;
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < KB; ++kb) {
+      const int w0c = kb * 16 + kq * 4;
+      float a[4];
+      if (ALIGNED && w0c + 3 < N2) {
+        const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[s] = (rok && w0c + s < N2) ? xr[w0c + s] : 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(smT + (((kb * 4 + kq) * Npad) + (t0 + t) * 16 + r16) * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bt[s], acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = (t0 + t) * 16 + r16;
+      const int k = col >> 1, part = col & 1;
+      if (k >= m2) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int orow = rt * 16 + kq * 4 + r;
+        if (orow >= nrows) continue;
+        const int on = orow / P1, oh = orow - (orow / P1) * P1;
+        const float u = acc[t][r];
+        for (int c = 0; c < C; ++c) {
+          const int64_t gi = (((int64_t)k * C + c) * P1 + oh) * 2 + part;
+          At[((((int64_t)on * m2 + k) * C + c) * P1 + oh) * 2 + part] = fmaf(w0[c * 3], u, Gt[gi]);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ column pass
 // The column transforms are two complex GEMMs against the shared twiddle matrix
 // F[h][j] = e^{-2 pi i r_j h / P1} (r_j the K1 kept frequency rows), on the f32 matrix cores
@@ -454,6 +529,47 @@ BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int B
   }
 #undef RD_AL
 #undef RD
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const float* w0,
+                                        const float* Gt, float* At, const float* Tp, int B, int T,
+                                        int L, int N1, int N2, int C, int P1, int P2, int m2,
+                                        void* stream) {
+  if (B <= 0 || L <= 0 || T <= 0 || C <= 0 || N1 > P1 || N2 > P2 || m2 <= 0 || m2 > P2 / 2 + 1)
+    return (int)hipErrorInvalidValue;
+  const int64_t nrows64 = (int64_t)B * L * P1;
+  if (nrows64 > INT32_MAX || (int64_t)B * T * N1 * N2 >= ((int64_t)1 << 40))
+    return (int)hipErrorInvalidValue;
+  const int nrows = (int)nrows64;
+  const int KB = (P2 + 15) / 16;
+  const int Npad = ((2 * m2 + 15) / 16) * 16;
+  const int ntiles = Npad / 16;
+  const size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+  const int nrt = (nrows + 15) / 16;
+  int nt = ntiles;
+  if (nt > 4) nt = 4;
+  while (nt > 1 && (int64_t)nrt * ((ntiles + nt - 1) / nt) < 4096) nt >>= 1;
+  while (ntiles % nt) --nt;
+  const int groups = ntiles / nt;
+  const int64_t nwork = (int64_t)nrt * groups;
+  const int blocks = (int)((nwork + 3) / 4 < 4096 ? (nwork + 3) / 4 : 4096);
+  const bool aligned = (N2 % 4) == 0 && (((uintptr_t)X) & 15) == 0;
+  hipStream_t st = (hipStream_t)stream;
+#define RB(NT_, AL_)                                                                          \
+  rowdft_bag_lift_kernel<NT_, AL_><<<blocks, 256, sh, st>>>(X, idx, w0, Gt, At, Tp, nrows, T, L, \
+                                                            N1, N2, C, P1, m2, KB, Npad, groups)
+#define RB_AL(NT_) \
+  if (aligned) RB(NT_, 1); else RB(NT_, 0);
+  switch (nt) {
+    case 1: RB_AL(1) break;
+    case 2: RB_AL(2) break;
+    case 3: RB_AL(3) break;
+    default: RB_AL(4) break;
+  }
+#undef RB_AL
+#undef RB
   return (int)hipGetLastError();
 }
 

@@ -167,7 +167,7 @@ def test_mse_and_metrics():
     loss = ops.mse_loss(p, t)
     loss.backward()
     ref = torch.nn.functional.mse_loss(p.detach().double(), t.double())
-    assert abs(float(loss) - float(ref)) <= 1e-6 * float(ref)
+    assert abs(float(loss.detach()) - float(ref)) <= 1e-6 * float(ref)
     assert rel_l2(p.grad.cpu().numpy(), (2 * (p.detach() - t) / p.numel()).cpu().numpy()) <= 1e-6
     g = load_golden("metric_train_rel_l2")
     e0, e1 = ops.train_rel_l2_2ch(torch.from_numpy(g["pred"]).cuda(), torch.from_numpy(g["out"]).cuda())
@@ -175,3 +175,37 @@ def test_mse_and_metrics():
     g = load_golden("metric_time_avg_rel_l2_2d")
     v = ops.time_averaged_relative_l2(torch.from_numpy(g["pt_pred"]).cuda(), torch.from_numpy(g["pt_ref"]).cuda())
     assert abs(v - float(g["val"])) <= 1e-5 * float(g["val"])  # inputs rounded to fp32
+
+
+@pytest.mark.parametrize("case,heads,train", [("nio2d_fno_train", ("fno_drift", "fno_diffusion"), True),
+                                              ("nio2d_fno_eval", ("fno_drift", "fno_diffusion"), False),
+                                              ("nc_nio2d_fno_eval", ("fno_Fx", "fno_Fy"), False)])
+def test_niofp2d_fno_fused_encoder(case, heads, train):
+    """Same goldens through the fused snapshot-encoder path (ops.BagEncoderFn: bags read through
+    the index list, lift folded into the first row DFT, fc0 gradient reduced in the adjoint),
+    which NIOFP2D_FNO takes whenever x and grid need no gradient."""
+    from blindno import NIOFP2D_FNO, ops
+    g = load_golden(case)
+    m = _load(NIOFP2D_FNO(2, 3, 100, 25, 2, 6, 5, 2, heads=heads), g, strict=False).cuda()
+    m.train(train)
+    x = torch.from_numpy(g["in.x"]).cuda()
+    grid = torch.from_numpy(g["in.grid"]).cuda()
+    assert m._fused_ok(x, grid)
+    calls = []
+    orig = ops.BagEncoderFn.forward
+    ops.BagEncoderFn.forward = staticmethod(lambda *a: calls.append(1) or orig(*a))
+    try:
+        out = m(x, grid, bag_idx=g["idx"] if train else None)
+    finally:
+        ops.BagEncoderFn.forward = staticmethod(orig)
+    assert calls, "fused encoder path not taken"
+    assert rel_l2(out.detach().cpu().numpy(), g["out"]) <= FWD_TOL
+    (out * torch.from_numpy(g["cot"]).cuda()).sum().backward()
+    named = dict(m.named_parameters())
+    n = 0
+    for k, v in g.items():
+        if k.startswith("g."):
+            e = float(rel_l2(named[k[2:]].grad.detach().cpu().numpy(), v))
+            assert e <= GRAD_TOL, (k, e)
+            n += 1
+    assert n > 20

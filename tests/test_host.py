@@ -139,3 +139,14 @@ def test_pad_and_crop_geometry():
     meta = ops.FNOMeta(2, 3, 12, 32, 32, 128, 1, 12)
     g = ops._fno_geometry(torch.empty(4, 128, 128, 12), meta)
     assert g[4:] == (160, 160, 128, 128)
+
+
+def test_ctypes_signatures_match_header_arity():
+    """Every ctypes signature in blindno/_lib.py has as many arguments as the declaration."""
+    from blindno import _lib
+    txt = open(HEADER).read()
+    for name, sig in _lib.SIGNATURES.items():
+        m = re.search(r"^(?:int|const char\*)\s+" + name + r"\(([^)]*)\)", txt, re.M | re.S)
+        assert m, name
+        args = [a for a in m.group(1).split(",") if a.strip() and a.strip() != "void"]
+        assert len(args) == len(sig), (name, len(args), len(sig))
