@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="cpu baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
+    ap.add_argument("--timer-steps", type=int, default=4,
+                    help="eager steps after the timed region that time the dominant kernel (graph mode)")
     return ap.parse_args()
 
 
@@ -55,7 +58,8 @@ def main():
     a = parse()
     import blindno
     from blindno import timing
-    from blindno.train import DataParallel, FlatAdam, grid2d, synthetic_bags, trained_parameters
+    from blindno.train import (DataParallel, FlatAdam, GraphedBagStep, grid2d, synthetic_bags,
+                               trained_parameters)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -83,13 +87,29 @@ def main():
     order = torch.randperm(n_local, device=dev, generator=torch.Generator(device=dev).manual_seed(seed + rank))
     loss_acc = torch.zeros((), device=dev)
 
-    def step(i):
+    xb = torch.empty((B,) + tuple(X.shape[1:]), device=dev)
+    yb = torch.empty((B,) + tuple(Y.shape[1:]), device=dev)
+    graphed = None
+    if not a.no_graph:
+        # one HIP graph per bag size L = randint(50, T) (captured here, before the warm-up; the
+        # numpy draw below stays the reference's: L and idx are drawn on the host every step)
+        graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc)
+        torch.index_select(X, 0, order[:B], out=xb)
+        torch.index_select(Y, 0, order[:B], out=yb)
+        for L in range(50, T):
+            graphed.capture(L)
+        torch.cuda.synchronize()
+
+    def step(i, eager=False):
         j = (i * B) % (n_local - B + 1)
         ids = order[j:j + B]
-        x = X.index_select(0, ids)
-        y = Y.index_select(0, ids)
-        out = model(x, grid)
-        loss = blindno.mse_loss(out, y)
+        torch.index_select(X, 0, ids, out=xb)
+        torch.index_select(Y, 0, ids, out=yb)
+        if graphed is not None and not eager:
+            graphed.step(blindno.draw_bag(T)[1])
+            return
+        out = model(xb, grid)
+        loss = blindno.mse_loss(out, yb)
         loss.backward()
         dp.step()
         opt.zero_grad()
@@ -104,14 +124,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if timer:
+    if timer and graphed is None:
         timer.start()
     for i in range(a.steps):
         step(a.warmup + i)
+    t_enq = time.perf_counter() - t0          # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if timer and graphed is not None:
+        # graph replays cannot be hooked: time the dominant kernel (the identical launches) with
+        # HIP events on its stream over a few eager steps right after the timed region
+        timer.start()
+        for i in range(a.timer_steps):
+            step(a.warmup + a.steps + i, eager=True)
     if timer:
         timer.stop()
     dtt = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -137,16 +164,59 @@ def main():
             "config": {"workload": f"2d_FPE train_fno.py NIOFP2D_FNO(2,3,100,25,3,12,32,2) {N}x{N}",
                        "per_gpu_batch": B, "global_batch": B * world, "T": T,
                        "bag_size": "L=randint(50,T) with replacement", "dataset_bags": a.bags,
-                       "parallelism": f"dp{world}", "optimizer": "Adam lr 5e-4 (fused flat)"},
+                       "parallelism": f"dp{world}", "optimizer": "Adam lr 5e-4 (fused flat)",
+                       "launch": "eager" if a.no_graph else "hip-graph per bag size L (all kernels replayed each step)"},
         }
         if timer:
-            res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS)
+            res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS,
+                                             traffic_per_point=timing.pmc_traffic(ROOT, timing.DOMINANT))
+            res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a, budget=a.cpu_seconds)
         res["loss_mean"] = float(loss_acc) / (a.warmup + a.steps)
+        res["host_enqueue_ms_per_step"] = round(1000.0 * t_enq / a.steps, 4)
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
+
+
+def spectral_roofline(model, grid, B, T, N, dev):
+    """HBM roofline of one FNO_input spectral layer (the north star's 'spectral-conv kernel'):
+    row DFT + column pass + inverse row transform with its epilogue, at the mean bag size
+    (L = 75), timed with HIP events on the launch stream; algorithmic bytes per SURVEY.md 8d:
+    4 Bn Ci P^2 (read x) + 4 Bn Co P^2 (write y) + 16 Ci Co m1 m2 (weights)."""
+    from blindno import ops
+    fno = model.FNO_input
+    C, m = fno.width, fno.modes1
+    P = N + ops.pad_amount(N)
+    Bn = B * 75
+    x = torch.randn(Bn, C, P, P, device=dev)
+    s0 = fno.spectral_list[1]
+    w1, w2 = s0._real_view()
+    cw, cb = fno.conv_list[1].weight.detach(), fno.conv_list[1].bias.detach()
+    sh = ops.SpecShape(Bn, C, C, P, P, m, m, 2)
+    Wt = ops.pack_weights((w1.detach(), w2.detach()), P, 2)
+
+    def layer():
+        _, Z = ops.spec_forward(x, 1, Wt, sh)
+        return ops.k_rowidft_epi(Z, x, cw, cb, Bn, C, P, P, m, 1)
+
+    for _ in range(3):
+        layer()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    ev0.record()
+    for _ in range(reps):
+        layer()
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / reps
+    nbytes = 4 * Bn * C * P * P * 2 + 16 * C * C * m * m
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"kernels": "blindno_rowdft + blindno_colpass + blindno_rowidft_epi (one FNO_input layer)",
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_per_layer": round(ms, 4),
+            "algorithmic_bytes": int(nbytes), "snapshots": Bn}
 
 
 def cpu_baseline(a, budget):

@@ -86,6 +86,13 @@ class NIOFP2D_FNO(nn.Module):
         (ops.BagEncoderFn: snapshots read from x through the bag's indices); otherwise as the
         generic composition below (same numerics, gradients for x and grid)."""
         if self._fused_ok(x, grid):
+            if torch.is_tensor(bag_idx) and bag_idx.is_cuda and bag_idx.dtype == torch.int32:
+                # device-resident bag indices (graph-captured training steps, train.GraphedBagStep)
+                idx_t = bag_idx
+                fno = self.FNO_input
+                h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, grid, self.fc0.weight.data,
+                                           self.fc0.bias.data, *fno_params(fno, 2))
+                return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
             if bag_idx is not None:
                 idx = np.asarray(bag_idx)
             elif self.training:

@@ -140,11 +140,84 @@ class DataParallel:
             dist.broadcast(self.opt.flat, src, group=self.group)
 
     def step(self):
-        g = self.opt.gather_grads()
+        self.opt.gather_grads()
+        self.reduce_and_step()
+
+    def reduce_and_step(self):
+        """All-reduce the already-gathered flat gradient and apply the fused Adam update."""
+        g = self.opt.grad
         if self.world > 1:
             for off in range(0, g.numel(), self.bucket):
                 dist.all_reduce(g[off:off + self.bucket], group=self.group)
         self.opt.step(grad_scale=1.0 / self.world, gather=False)
+
+
+class GraphedBagStep:
+    """One training step of a snapshot-bag model (forward, loss, backward, gradient gather)
+    replayed from a HIP graph.
+
+    The bag size L = randint(50, T) changes every step (2d_FPE/NIOModules.py:548-553), so one
+    graph is captured per L, all sharing one memory pool (graphs replay one at a time and keep
+    nothing alive between replays).  The bag indices reach the graph through a static device
+    buffer per L, filled from a small ring of pinned host buffers; the inputs x / y are static
+    buffers the caller fills (e.g. index_select(..., out=)).  After the replay the gradient
+    all-reduce (RCCL, N > 1) and the fused Adam update run eagerly.  Every kernel of the step
+    still runs on every replay: the graph removes the host launch overhead, not work."""
+
+    def __init__(self, model, loss_fn, opt: "FlatAdam", dp: "DataParallel", x, y, grid,
+                 loss_acc: Optional[torch.Tensor] = None):
+        self.model, self.loss_fn, self.opt, self.dp = model, loss_fn, opt, dp
+        self.x, self.y, self.grid = x, y, grid
+        self.loss_acc = loss_acc
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs = {}
+        self.idx = {}
+        self.T = x.shape[1]
+        self._ring = [torch.empty(self.T, dtype=torch.int32).pin_memory() for _ in range(4)]
+        self._ev = [None] * len(self._ring)
+        self._k = 0
+
+    def _body(self, L):
+        out = self.model(self.x, self.grid, bag_idx=self.idx[L])
+        loss = self.loss_fn(out, self.y)
+        loss.backward()
+        self.opt.gather_grads()
+        if self.loss_acc is not None:
+            self.loss_acc.add_(loss.detach())
+
+    def capture(self, L: int):
+        if L in self.graphs:
+            return
+        self.idx[L] = torch.zeros(L, dtype=torch.int32, device=self.x.device)
+        side = torch.cuda.Stream(self.x.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):                 # eager warm-up: caches, lazy init
+            self._body(L)
+            self.opt.zero_grad()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.pool):
+            self._body(L)
+        self.opt.zero_grad()
+        self.graphs[L] = g
+
+    def step(self, idx) -> None:
+        idx = np.asarray(idx, dtype=np.int32)
+        L = len(idx)
+        if L not in self.graphs:
+            self.capture(L)
+        k = self._k
+        self._k = (k + 1) % len(self._ring)
+        if self._ev[k] is not None:
+            self._ev[k].synchronize()                 # ring slot's previous copy has landed
+        buf = self._ring[k]
+        buf[:L].numpy()[:] = idx
+        self.idx[L].copy_(buf[:L], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ev[k] = ev
+        self.graphs[L].replay()
+        self.dp.reduce_and_step()
 
 
 def synthetic_bags(n_bags: int, T: int, grid_shape, out_ch: int, seed: int, device,

@@ -57,7 +57,8 @@ def main():
         w2 = torch.randn(Cout, 128, device=dev) * 0.1
         b2 = torch.randn(Cout, device=dev)
         out = torch.empty(Bn, N, N, Cout, device=dev)
-        dout = torch.randn(Bn, N, N, Cout, device=dev)
+        div = 75 if tag == "input" else 1          # the encoder's bag-mean gradient: one field per bag
+        dout = torch.randn(Bn // div, N, N, Cout, device=dev)
         dz = torch.zeros_like(z)
         nch = query("blindno_project_bwd_nchunk", Bn, N, N)
         npar = 128 * C + 128 + Cout * 128 + Cout
@@ -67,9 +68,9 @@ def main():
                                                   ptr(out), Bn, C, P, P, N, N, 128, Cout, Cout, 0, stream_ptr()),
              4 * pts * (C + Cout))
         case(f"project_bwd[{tag}]", lambda: call("blindno_project_bwd", ptr(z), ptr(w1), ptr(b1), ptr(w2), ptr(dout),
-                                                  ptr(dz), ptr(part), nch, Bn, C, P, P, N, N, 128, Cout, Cout, 0, 1,
+                                                  ptr(dz), ptr(part), nch, Bn, C, P, P, N, N, 128, Cout, Cout, 0, div,
                                                   stream_ptr()),
-             4 * pts * (2 * C + Cout))
+             8 * pts * C + 4 * (pts // div) * Cout)
         # spectral pieces of one layer
         sh = ops.SpecShape(Bn, C, C, P, P, m, m, 2)
         w = torch.rand(C, C, m, m, 2, device=dev) / (C * C)
