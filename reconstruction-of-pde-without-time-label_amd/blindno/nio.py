@@ -40,6 +40,32 @@ def _select(module, x, bag_idx):
     return x, x.shape[1]
 
 
+_SIDE = {}
+
+
+def _run_heads(module, h):
+    """The FNO heads on h, concatenated (2d_FPE/NIOModules.py:577-581).  On the GPU two heads run
+    concurrently: the second on a side stream forked from and joined back into the current
+    one (inside a graph capture this becomes two parallel branches).  Each head is one autograd
+    node, so its backward runs on the stream of its forward; the heads are small (B samples),
+    latency-bound launches, which is why overlapping them pays."""
+    heads = [getattr(module, n) for n in module._heads]
+    if len(heads) != 2 or not h.is_cuda:
+        return torch.cat([f(h) for f in heads], dim=-1)
+    main = torch.cuda.current_stream(h.device)
+    side = _SIDE.get(h.device)
+    if side is None:
+        side = _SIDE[h.device] = torch.cuda.Stream(h.device)
+    side.wait_stream(main)
+    o0 = heads[0](h)
+    with torch.cuda.stream(side):
+        o1 = heads[1](h)
+    main.wait_stream(side)
+    h.record_stream(side)
+    o1.record_stream(main)
+    return torch.cat([o0, o1], dim=-1)
+
+
 def _bag_mean_2d(module, u, grid, B, L, nx, ny):
     g = grid.reshape(nx * ny, 2)
     h = ops.BagMeanFn.apply(u.reshape(B, L, nx * ny), g, module.fc0.weight.data,
@@ -92,7 +118,7 @@ class NIOFP2D_FNO(nn.Module):
                 fno = self.FNO_input
                 h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, grid, self.fc0.weight.data,
                                            self.fc0.bias.data, *fno_params(fno, 2))
-                return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
+                return _run_heads(self, h)
             if bag_idx is not None:
                 idx = np.asarray(bag_idx)
             elif self.training:
@@ -103,7 +129,7 @@ class NIOFP2D_FNO(nn.Module):
             fno = self.FNO_input
             h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, grid, self.fc0.weight.data,
                                        self.fc0.bias.data, *fno_params(fno, 2))
-            return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
+            return _run_heads(self, h)
         x, L = _select(self, x, bag_idx)
         B, _, nx, ny = x.shape
         x_in = x.reshape(B * L, 1, nx, ny)
