@@ -36,14 +36,49 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip tab
 FP32_PEAK_TFLOPS = 157.3       # fp32 vector = fp32 MFMA dense peak (same table)
 
 
+# BASELINE.json configs (SURVEY.md section 8 "Configs restated")
+CONFIGS = {
+    "A": dict(desc="1d_FPE train_fno.py NIOFP_FNO(3,30,15,2) on a 64-point grid", dim=1, N=64, T=256, B=32,
+              lr=1e-3),
+    "B": dict(desc="1d_GPE train_fno_GPE.py NIOFP_FNO(3,20,40,1) head fno_V on a 256-point grid", dim=1,
+              N=256, T=101, B=32, lr=1e-3),
+    "C": dict(desc="2d_FPE train_fno.py NIOFP2D_FNO(2,3,100,25,3,12,32,2)", dim=2, N=128, T=100, B=4,
+              lr=5e-4),
+    "D": dict(desc="2d_Non_conservative_FPE train_nio.py NIOFP2D(2,3,100,25,3,12,32,2) heads Fx,Fy", dim=2,
+              N=128, T=100, B=4, lr=5e-4),
+    "E": dict(desc="2D FNO-NIO NIOFP2D_FNO(2,3,100,25,3,12,32,2) on a 256x256 grid (no 2d_GPE in the "
+                   "reference; real-valued synthetic bags)", dim=2, N=256, T=100, B=4, lr=5e-4),
+}
+
+
+def build_model(cfg_name, N, dev):
+    import blindno
+    from blindno.train import trained_parameters
+    if cfg_name == "A":
+        m = blindno.NIOFP_FNO(3, 30, 15, 2, dev)
+        return m.to(dev), trained_parameters(m), 2
+    if cfg_name == "B":
+        m = blindno.NIOFP_FNO(3, 20, 40, 1, dev, heads=("fno_V",))
+        return m.to(dev), trained_parameters(m), 1
+    if cfg_name == "D":
+        m = blindno.NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, heads=("fno_Fx", "fno_Fy"),
+                            branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N))
+        return m.to(dev), trained_parameters(m, exclude_prefixes=("fc0.",)), 2
+    m = blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2,
+                            branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N))
+    return m.to(dev), trained_parameters(m), 2
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=4)
-    ap.add_argument("--grid", type=int, default=128)
-    ap.add_argument("--T", type=int, default=100)
+    ap.add_argument("--config", default="C", choices=sorted(CONFIGS),
+                    help="BASELINE.json config (C = the headline metric)")
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--bags", type=int, default=4096, help="dataset size (all ranks)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="cpu baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -58,8 +93,8 @@ def main():
     a = parse()
     import blindno
     from blindno import timing
-    from blindno.train import (DataParallel, FlatAdam, GraphedBagStep, grid2d, synthetic_bags,
-                               trained_parameters)
+    from blindno.train import (DataParallel, FlatAdam, GraphedBagStep, grid1d, grid2d,
+                               synthetic_bags)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,24 +108,28 @@ def main():
     seed = 1234
     np.random.seed(seed + rank)
     torch.manual_seed(seed + rank)
-    N, T, B = a.grid, a.T, a.batch
-    model = blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2,
-                                branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N)).to(dev)
+    cfg = CONFIGS[a.config]
+    N = a.grid or cfg["N"]
+    T = a.T or cfg["T"]
+    B = a.batch or cfg["B"]
+    model, params, out_ch = build_model(a.config, N, dev)
     model.train()
-    opt = FlatAdam(trained_parameters(model), lr=5e-4)
+    opt = FlatAdam(params, lr=cfg["lr"])
     dp = DataParallel(opt)
     dp.broadcast_parameters(0)
 
     n_local = max(B, a.bags // world)
-    X, Y = synthetic_bags(n_local, T, (N, N), 2, seed=seed + 7919 * rank, device=dev)
-    grid = grid2d(N, N, dev)
+    gshape = (N, N) if cfg["dim"] == 2 else (N,)
+    X, Y = synthetic_bags(n_local, T, gshape, out_ch, seed=seed + 7919 * rank, device=dev)
+    grid = grid2d(N, N, dev) if cfg["dim"] == 2 else grid1d(N, dev)
     order = torch.randperm(n_local, device=dev, generator=torch.Generator(device=dev).manual_seed(seed + rank))
     loss_acc = torch.zeros((), device=dev)
 
     xb = torch.empty((B,) + tuple(X.shape[1:]), device=dev)
     yb = torch.empty((B,) + tuple(Y.shape[1:]), device=dev)
     graphed = None
-    if not a.no_graph:
+    # graphs need the fused snapshot encoder (device-resident bag indices): the 2D FNO-NIO models
+    if not a.no_graph and a.config in ("C", "E"):
         # one HIP graph per bag size L = randint(50, T) (captured here, before the warm-up; the
         # numpy draw below stays the reference's: L and idx are drawn on the host every step)
         graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc)
@@ -116,7 +155,11 @@ def main():
         loss_acc.add_(loss.detach())
 
     for i in range(a.warmup):
+        tw = time.perf_counter()
         step(i)
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup step {i}: {time.perf_counter() - tw:.3f}s", file=sys.stderr, flush=True)
     timer = None
     if not a.no_kernel_timer:
         timer = timing.KernelTimer(timing.DOMINANT)
@@ -149,7 +192,8 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": "snapshot-bags/sec (train step), 2D FPE 128^2 FNO-NIO",
+            "metric": ("snapshot-bags/sec (train step), 2D FPE 128^2 FNO-NIO" if a.config == "C" else
+                       f"snapshot-bags/sec (train step), config {a.config}"),
             "value": round(value, 3),
             "unit": "snapshot-bags/s",
             "n_gpus": world,
@@ -161,18 +205,20 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (standardised N(0,1) bags resident in HBM; reference datasets not shipped)",
-            "config": {"workload": f"2d_FPE train_fno.py NIOFP2D_FNO(2,3,100,25,3,12,32,2) {N}x{N}",
+            "config": {"workload": f"{cfg['desc']} ({a.config}), grid {'x'.join([str(N)] * cfg['dim'])}",
                        "per_gpu_batch": B, "global_batch": B * world, "T": T,
                        "bag_size": "L=randint(50,T) with replacement", "dataset_bags": a.bags,
-                       "parallelism": f"dp{world}", "optimizer": "Adam lr 5e-4 (fused flat)",
-                       "launch": "eager" if a.no_graph else "hip-graph per bag size L (all kernels replayed each step)"},
+                       "parallelism": f"dp{world}", "optimizer": f"Adam lr {cfg['lr']} (fused flat)",
+                       "launch": "hip-graph per bag size L (all kernels replayed each step)" if graphed else "eager"},
         }
         if timer:
             res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS,
-                                             traffic_per_point=timing.pmc_traffic(ROOT, timing.DOMINANT))
-            res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
-        if world == 1 and not a.no_cpu:
-            res["cpu_baseline"] = cpu_baseline(a, budget=a.cpu_seconds)
+                                             traffic_per_point=timing.pmc_traffic(ROOT, timing.DOMINANT)
+                                             if a.config == "C" else None)
+            if a.config in ("C", "E"):
+                res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
+        if world == 1 and not a.no_cpu and a.config == "C":
+            res["cpu_baseline"] = cpu_baseline(N, T, budget=a.cpu_seconds)
         res["loss_mean"] = float(loss_acc) / (a.warmup + a.steps)
         res["host_enqueue_ms_per_step"] = round(1000.0 * t_enq / a.steps, 4)
         print(json.dumps(res))
@@ -219,7 +265,7 @@ def spectral_roofline(model, grid, B, T, N, dev):
             "algorithmic_bytes": int(nbytes), "snapshots": Bn}
 
 
-def cpu_baseline(a, budget):
+def cpu_baseline(N, T, budget):
     """float32 CPU oracle (oracle/ restates the reference's algorithm) timed on this host:
     forward + backward of one bag per step (L = 75, the mean bag size), until ~budget s."""
     import oracle
@@ -228,7 +274,6 @@ def cpu_baseline(a, budget):
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    N, T = a.grid, a.T
     m = blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2,
                             branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N))
     p = {k: v.detach().float().requires_grad_(True) for k, v in m.state_dict().items()

@@ -243,6 +243,24 @@ int blindno_gpe_solve(const double* psi0, const double* V, const double* g, cons
 int blindno_trapz_rows(const double* a, const double* b, const double* x, double* out, int rows,
                        int n, blindno_stream_t stream);
 
+/* ---- NIO encoder ConvBlock normalisation: BatchNorm2d fused with LeakyReLU
+ * (2d_FPE/Baselines.py:40-52 ConvBlock = Conv -> BatchNorm2d -> LeakyReLU(slope); replaces the
+ * nn.BatchNorm2d + nn.LeakyReLU(inplace) pair of each block).  z (Npad, C, HW) NCHW, batch =
+ * rows [0, N); rows [N, Npad) of y / dz are written 0.  training != 0: batch statistics
+ * (biased variance), running_mean/var updated with momentum (unbiased variance) when non-NULL;
+ * training == 0: running statistics.  save (C, 4) = mean, invstd, gamma invstd,
+ * beta - mean gamma invstd (written by the forward, read by the backward).  partial: scratch of
+ * C * blindno_bn_act_nslices(N, C, HW) * 2 floats; coef (C, 3) scratch of the backward.
+ * gamma/beta may be NULL (affine=False); dgamma/dbeta may be NULL. */
+int blindno_bn_act_nslices(int N, int C, int HW);
+int blindno_bn_act_fwd(const float* z, const float* gamma, const float* beta, float* run_mean,
+                       float* run_var, float* y, float* save, float* partial, int N, int Npad,
+                       int C, int HW, float eps, float momentum, float slope, int training,
+                       blindno_stream_t stream);
+int blindno_bn_act_bwd(const float* dy, const float* z, const float* gamma, const float* save,
+                       float* dz, float* dgamma, float* dbeta, float* partial, float* coef, int N,
+                       int Npad, int C, int HW, float slope, int training, blindno_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,9 @@ SIGNATURES = {
     "blindno_rowidft_bwd_nchunk": "iiiii",
     "blindno_project_bwd_nchunk": "iii",
     "blindno_mix_wgrad_nsplit": "iiiii",
+    "blindno_bn_act_nslices": "iii",
+    "blindno_bn_act_fwd": "ppppppppiiiifffis",
+    "blindno_bn_act_bwd": "pppppppppiiiifis",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,

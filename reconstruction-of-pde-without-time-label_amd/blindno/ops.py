@@ -727,3 +727,51 @@ def time_averaged_relative_l2(pt_pred, pt_ref, eps=1e-12):
     n = pt_pred[0].numel()
     s = rowsq(pt_pred.float(), pt_ref.float(), nt, n, 1, 0, 0, 0)
     return float((s[:, 0].sqrt() / (s[:, 1].sqrt() + eps)).mean())
+
+
+# ---------------------------------------------------------------------------- NIO encoder blocks
+
+class BNActFn(torch.autograd.Function):
+    """BatchNorm2d + LeakyReLU of a ConvBlock (2d_FPE/Baselines.py:40-52) on rows [0, n) of z
+    (rows [n, Npad) are the convolution chunks' padding and come out 0).  Running statistics
+    are updated like torch.nn.BatchNorm2d (momentum, or the cumulative average when momentum
+    is None)."""
+
+    @staticmethod
+    def forward(ctx, z, gamma, beta, bn, n, slope):
+        require_device(z)
+        z = _c(z)
+        Npad, C = z.shape[0], z.shape[1]
+        HW = z[0, 0].numel()
+        use_batch = bn.training or bn.running_mean is None
+        track = bn.training and bn.track_running_stats and bn.running_mean is not None
+        mom = 0.0
+        if track:
+            bn.num_batches_tracked.add_(1)
+            mom = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+        S = query("blindno_bn_act_nslices", n, C, HW)
+        partial = torch.empty(C * S * 2, device=z.device, dtype=F32)
+        save = torch.empty(C, 4, device=z.device, dtype=F32)
+        y = torch.empty_like(z)
+        rm = bn.running_mean if (track or not use_batch) else None
+        rv = bn.running_var if (track or not use_batch) else None
+        call("blindno_bn_act_fwd", ptr(z), ptr(gamma), ptr(beta), ptr(rm), ptr(rv), ptr(y), ptr(save),
+             ptr(partial), n, Npad, C, HW, float(bn.eps), float(mom), float(slope), int(use_batch),
+             stream_ptr())
+        ctx.save_for_backward(z, gamma, save)
+        ctx.meta = (n, Npad, C, HW, float(slope), int(use_batch), S)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        z, gamma, save = ctx.saved_tensors
+        n, Npad, C, HW, slope, use_batch, S = ctx.meta
+        dy = _c(dy)
+        dz = torch.empty_like(z)
+        dgamma = torch.empty(C, device=z.device, dtype=F32) if gamma is not None and ctx.needs_input_grad[1] else None
+        dbeta = torch.empty(C, device=z.device, dtype=F32) if ctx.needs_input_grad[2] else None
+        partial = torch.empty(C * S * 2, device=z.device, dtype=F32)
+        coef = torch.empty(C, 3, device=z.device, dtype=F32)
+        call("blindno_bn_act_bwd", ptr(dy), ptr(z), ptr(gamma), ptr(save), ptr(dz), ptr(dgamma), ptr(dbeta),
+             ptr(partial), ptr(coef), n, Npad, C, HW, slope, use_batch, stream_ptr())
+        return dz, dgamma, dbeta, None, None, None

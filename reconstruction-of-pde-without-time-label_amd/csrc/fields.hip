@@ -287,11 +287,12 @@ __global__ __launch_bounds__(1024) void project_bwd_wsum_kernel(
     int Cout, int ostride, int ooff, int dout_div) {
   constexpr int NWV = 16;
   constexpr int PJ = CM + 1 + COM;
+  constexpr int RC = CM < 16 ? CM : 16;
   extern __shared__ float smw[];
   float* sz = smw;                          // [CM][64]
   float* sg = sz + CM * 64;                 // [COM][64]
-  float* red = sg + COM * 64;               // [NWV][CM][64]
-  float* sw1 = red + NWV * CM * 64;         // [Hd][CM]
+  float* red = sg + COM * 64;               // [NWV][RC][64]
+  float* sw1 = red + NWV * RC * 64;         // [Hd][CM]
   float* sb1 = sw1 + Hd * CM;               // [Hd]
   float* sw2 = sb1 + Hd;                    // [Hd][COM]
   float* acc = sw2 + Hd * COM;              // [Hd][PJ] then [COM]
@@ -376,15 +377,21 @@ __global__ __launch_bounds__(1024) void project_bwd_wsum_kernel(
         if (lane == 0) acc[Hd * PJ + c] += sv;
       }
     }
+    // dz summed over the waves through LDS, RC channels at a time (keeps red within LDS at CM 32)
 #pragma unroll
-    for (int i = 0; i < CM; ++i) red[(wave * CM + i) * 64 + lane] = dzp[i];
-    __syncthreads();
-    for (int i = wave; i < C; i += NWV) {
-      if (ok) {
-        float s2 = 0.f;
+    for (int i0 = 0; i0 < CM; i0 += RC) {
+      if (i0 >= C) break;                     // uniform
+      if (i0 > 0) __syncthreads();            // previous chunk's reads done
 #pragma unroll
-        for (int wv = 0; wv < NWV; ++wv) s2 += red[(wv * CM + i) * 64 + lane];
-        dz[zo + i * HW] = s2;
+      for (int i = 0; i < RC; ++i) red[(wave * RC + i) * 64 + lane] = dzp[i0 + i];
+      __syncthreads();
+      for (int i = wave; i < RC && i0 + i < C; i += NWV) {
+        if (ok) {
+          float s2 = 0.f;
+#pragma unroll
+          for (int wv = 0; wv < NWV; ++wv) s2 += red[(wv * RC + i) * 64 + lane];
+          dz[zo + (i0 + i) * HW] = s2;
+        }
       }
     }
   }
@@ -646,7 +653,7 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
   if (Hd != 128) return (int)hipErrorInvalidValue;   // fc1 = Linear(width, 128) everywhere
   const int cm = C <= 8 ? 8 : (C <= 16 ? 16 : 32);
   const int com = Cout == 1 ? 1 : 4;
-  const size_t sh = sizeof(float) * ((size_t)cm * 64 + com * 64 + 16 * (size_t)cm * 64 +
+  const size_t sh = sizeof(float) * ((size_t)cm * 64 + com * 64 + 16 * (size_t)(cm < 16 ? cm : 16) * 64 +
                                      (size_t)Hd * cm + Hd + (size_t)Hd * com +
                                      (size_t)Hd * (cm + 1 + com) + com);
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;

@@ -1,0 +1,123 @@
+"""NIO snapshot-encoder ConvBlocks on the HIP path vs plain PyTorch fp32 (needs a GPU).
+
+ops.BNActFn (csrc/batchnorm.hip) replaces BatchNorm2d + LeakyReLU(0.2) of ConvBlock
+(2d_FPE/Baselines.py:40-52); the convolution runs on MIOpen over fixed-size chunks of
+encoders.CONV_CHUNK snapshots.  Reference: torch.nn.BatchNorm2d / F.leaky_relu in fp64 on the
+same inputs.  Tolerances: outputs and gradients rel-L2 <= 1e-5 (one normalisation of fp32
+data), running statistics 1e-6.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import blindno
+    blindno.load_library()
+
+
+def _ref_bn_act(z, bn, slope, training):
+    return F.leaky_relu(F.batch_norm(z, bn.running_mean, bn.running_var, bn.weight, bn.bias, training,
+                                     bn.momentum, bn.eps), slope)
+
+
+@pytest.mark.parametrize("shape,n", [((64, 5, 6, 8), 37), ((32, 7, 3, 7), 32), ((96, 3, 1, 1), 70)])
+def test_bn_act_matches_torch(shape, n):
+    from blindno import ops
+    torch.manual_seed(0)
+    Npad, C = shape[0], shape[1]
+    z = (torch.randn(shape, dtype=torch.float64) * 2.0 + 3.0).cuda()   # |mean| > std
+    z[n:] = float("nan")                                                 # padding rows never read
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref = torch.nn.BatchNorm2d(C).double().cuda()
+    ref.load_state_dict(bn.state_dict())
+    for it in range(2):                                   # twice: running statistics compound
+        zf = z.float().requires_grad_(True)
+        y = ops.BNActFn.apply(zf, bn.weight, bn.bias, bn, n, 0.2)
+        zr = z[:n].clone().requires_grad_(True)
+        yr = _ref_bn_act(zr, ref, 0.2, True)
+        assert n == Npad or float(y[n:].detach().abs().max()) == 0.0
+        assert rel_l2(y[:n].detach().cpu().numpy(), yr.detach().cpu().numpy()) <= 1e-5
+        cot = torch.randn_like(yr)
+        bn.weight.grad = bn.bias.grad = None
+        (y[:n] * cot.float()).sum().backward()
+        (yr * cot).sum().backward()
+        assert n == Npad or float(zf.grad[n:].abs().max()) == 0.0
+        assert rel_l2(zf.grad[:n].cpu().numpy(), zr.grad.cpu().numpy()) <= 1e-5
+        assert rel_l2(bn.weight.grad.cpu().numpy(), ref.weight.grad.cpu().numpy()) <= 1e-5
+        assert rel_l2(bn.bias.grad.cpu().numpy(), ref.bias.grad.cpu().numpy()) <= 1e-5
+        ref.weight.grad = ref.bias.grad = None
+        assert rel_l2(bn.running_mean.cpu().numpy(), ref.running_mean.cpu().numpy()) <= 1e-6
+        assert rel_l2(bn.running_var.cpu().numpy(), ref.running_var.cpu().numpy()) <= 1e-6
+        assert int(bn.num_batches_tracked) == it + 1
+    # eval mode: running statistics, no update
+    bn.eval()
+    ref.eval()
+    rm = bn.running_mean.clone()
+    zf = z.float().requires_grad_(True)
+    y = ops.BNActFn.apply(zf, bn.weight, bn.bias, bn, n, 0.2)
+    zr = z[:n].clone().requires_grad_(True)
+    yr = _ref_bn_act(zr, ref, 0.2, False)
+    assert rel_l2(y[:n].detach().cpu().numpy(), yr.detach().cpu().numpy()) <= 1e-5
+    cot = torch.randn_like(yr)
+    (y[:n] * cot.float()).sum().backward()
+    (yr * cot).sum().backward()
+    assert rel_l2(zf.grad[:n].cpu().numpy(), zr.grad.cpu().numpy()) <= 1e-5
+    assert torch.equal(rm, bn.running_mean)
+
+
+def test_encoder2d_chunked_matches_torch_modules():
+    """Encoder2D (64x64 snapshots, 2 bags of 37: 74 rows -> 3 chunks of 32) through the
+    chunked HIP path vs the same modules run as plain torch (nn.Sequential).  Both fp32 paths
+    are measured against the torch modules in fp64; the HIP path's error must stay within 2x of
+    plain fp32 torch's own (ten train-mode BatchNorm'd conv layers amplify fp32 rounding: the
+    first layer's weight gradient differs by ~1e-3 between any two fp32 convolution algorithms)."""
+    import blindno
+    torch.manual_seed(1)
+    enc = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().train()
+    ref32 = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().train()
+    ref64 = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().double().train()
+    ref32.load_state_dict(enc.state_dict())
+    ref64.load_state_dict(enc.state_dict())
+    x = torch.randn(2, 37, 1, 64, 64, device="cuda")
+
+    def ref_fwd(m, x):
+        b, L = x.shape[:2]
+        h = x.reshape(b * L, 1, 64, 64)
+        for blk in (m.convblock1, m.convblock2_1, m.convblock2_2, m.convblock3_1, m.convblock3_2,
+                    m.convblock4_1, m.convblock4_2, m.convblock7_1, m.convblock7_2, m.convblock7_3):
+            h = blk.layers(h)
+        return m.linear(h.flatten(1).view(b, L, -1))
+
+    out = enc(x)
+    out32 = ref_fwd(ref32, x)
+    out64 = ref_fwd(ref64, x.double())
+    e_out = rel_l2(out.detach().cpu().numpy(), out64.detach().cpu().numpy())
+    e_out32 = rel_l2(out32.detach().cpu().numpy(), out64.detach().cpu().numpy())
+    assert e_out <= max(2 * e_out32, 1e-5), (e_out, e_out32)
+    cot = torch.randn_like(out64)
+    (out * cot.float()).sum().backward()
+    (out32 * cot.float()).sum().backward()
+    (out64 * cot).sum().backward()
+    p32, p64 = dict(ref32.named_parameters()), dict(ref64.named_parameters())
+    for k, p in enc.named_parameters():
+        if k.endswith("layers.0.bias"):
+            continue    # conv bias ahead of a batch-statistics BatchNorm: true gradient is exactly 0
+        g64 = p64[k].grad.cpu().numpy()
+        e = rel_l2(p.grad.cpu().numpy(), g64)
+        e32 = rel_l2(p32[k].grad.cpu().numpy(), g64)
+        assert e <= max(2 * e32, 1e-5), (k, e, e32)
+    b64 = dict(ref64.named_buffers())
+    for k, b in enc.named_buffers():
+        if b.dtype.is_floating_point:
+            assert rel_l2(b.cpu().numpy(), b64[k].cpu().numpy()) <= 1e-5, k

@@ -158,6 +158,37 @@ def test_niofp2d_fno_vs_oracle_64():
             assert e <= GRAD_TOL, (k, e)
 
 
+@pytest.mark.parametrize("args,heads,N", [((3, 30, 15, 2), ("fno_drift", "fno_diffusion"), 64),
+                                          ((3, 20, 40, 1), ("fno_V",), 256)])
+def test_niofp_fno_1d_full_width_vs_oracle(args, heads, N):
+    """The 1D models at the reference's own widths (configs A: width 30, B: width 20) vs the
+    fp64 oracle: the head projections take the wide (C > 15) VALU kernels, which the
+    width-5/6 fixtures never reach."""
+    import oracle
+    from blindno import NIOFP_FNO
+    torch.manual_seed(11)
+    m = NIOFP_FNO(*args, "cuda", heads=heads).cuda().train()
+    B, T = 3, 40
+    x = torch.randn(B, T, N).cuda()
+    grid = torch.linspace(0, 1, N).unsqueeze(-1).cuda()
+    idx = np.random.RandomState(4).choice(T, 33)
+    out = m(x, grid, bag_idx=idx)
+    cot = torch.randn_like(out)
+    (out * cot).sum().backward()
+    p = {k: (v.detach().cpu().to(torch.complex128) if v.is_complex() else v.detach().cpu().double())
+         .requires_grad_(True) for k, v in m.state_dict().items()}
+    ref = oracle.niofp_fno(p, x.cpu(), grid.cpu(), idx=idx.tolist(), heads=heads)
+    assert rel_l2(out.detach().cpu().numpy(), ref.detach().numpy()) <= FWD_TOL
+    (ref * cot.cpu().double()).sum().backward()
+    n = 0
+    for k, prm in m.named_parameters():
+        if k in p and p[k].grad is not None and prm.grad is not None:
+            e = rel_l2(prm.grad.cpu().numpy(), p[k].grad.numpy())
+            assert e <= GRAD_TOL, (k, e)
+            n += 1
+    assert n > 10
+
+
 def test_mse_and_metrics():
     from blindno import ops
     import oracle
