@@ -26,6 +26,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kHd = 128;          // fc1 = Linear(width, 128) in every reference FNO
 constexpr int kNT = kHd / 16;     // hidden tiles
 constexpr int kWaves = 4;
+// point tiles per wave step for the width-4 (FNO_input) projections
+#ifndef PROJ_FWD_NP4
+#define PROJ_FWD_NP4 4
+#endif
+#ifndef PROJ_BWD_NP4
+#define PROJ_BWD_NP4 2
+#endif
+constexpr int kFwdNP4 = PROJ_FWD_NP4;
+constexpr int kBwdNP4 = PROJ_BWD_NP4;
 
 struct PointMap {
   unsigned HoWo, Wo;
@@ -55,55 +64,32 @@ constexpr float kInvK = 1.1774100225154747f;
 constexpr float kT = 0.27273748087922245f;        // A&S p / (sqrt2 k)
 constexpr float kPdfK = 0.46971863934982566f;     // 1 / (sqrt(2 pi) k)
 
-struct GeluK {
-  float g;      // k GELU(h)
-  float e;      // e^{-h^2/2}
-  float half;   // erfc(|h|/sqrt2) / 2
-};
-
-__device__ __forceinline__ GeluK gelu_k(float hk) {
-  GeluK o;
-  const float t = __builtin_amdgcn_rcpf(fmaf(fabsf(hk), kT, 1.0f));
-  o.e = __builtin_amdgcn_exp2f(-(hk * hk));
-  float q = fmaf(t, 0.5307027145f, -0.7265760135f);
-  q = fmaf(t, q, 0.7107068705f);
-  q = fmaf(t, q, -0.142248368f);
-  q = fmaf(t, q, 0.127414796f);
-  o.half = q * t * o.e;
-  o.g = fmaf(-fabsf(hk), o.half, fmaxf(hk, 0.0f));
-  return o;
-}
-
-// GELU'(h) = Phi(h) + h phi(h), Phi(h) = h >= 0 ? 1 - half : half
-__device__ __forceinline__ float gelu_k_grad(float hk, const GeluK& o) {
-  const float cdf = hk >= 0.f ? 1.0f - o.half : o.half;
-  return fmaf(hk * kPdfK, o.e, cdf);
-}
-
 // Two GELUs per lane-instruction: the polynomial / product steps as packed fp32 (v_pk_fma_f32,
-// v_pk_mul_f32 on <2 x float>), the transcendentals and max stay scalar.
+// v_pk_mul_f32 on <2 x float>); the transcendentals, |hk| (a free VOP3 source modifier on the
+// scalar fma) and the sign transfer (v_bfi_b32) stay scalar.  With half = erfc(|h|/sqrt2)/2,
+//     s = copysign(1/2 - half, h),   Phi(h) = 1/2 + s,
+// so no compare/select and no max is needed: k GELU(h) = hk Phi(h), GELU'(h) = Phi + h phi(h).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-struct GeluK2 {
-  f32x2 g, e, half;
-};
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
 
-__device__ __forceinline__ GeluK2 gelu_k2(f32x2 hk) {
-  GeluK2 o;
-  const f32x2 ahk = {fabsf(hk.x), fabsf(hk.y)};
-  const f32x2 one = {1.0f, 1.0f};
-  const f32x2 ta = __builtin_elementwise_fma(ahk, (f32x2){kT, kT}, one);
-  const f32x2 t = {__builtin_amdgcn_rcpf(ta.x), __builtin_amdgcn_rcpf(ta.y)};
+__device__ __forceinline__ f32x2 splat2(float v) { return (f32x2){v, v}; }
+
+// Phi(h) (as cdf) and e = e^{-h^2/2} for a pair of k-scaled pre-activations
+__device__ __forceinline__ f32x2 norm_cdf_pair(f32x2 hk, f32x2& e) {
+  const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(hk.x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk.y), kT, 1.0f))};
   const f32x2 sq = hk * hk;
-  o.e = (f32x2){__builtin_amdgcn_exp2f(-sq.x), __builtin_amdgcn_exp2f(-sq.y)};
-  f32x2 q = __builtin_elementwise_fma(t, (f32x2){0.5307027145f, 0.5307027145f}, (f32x2){-0.7265760135f, -0.7265760135f});
-  q = __builtin_elementwise_fma(t, q, (f32x2){0.7107068705f, 0.7107068705f});
-  q = __builtin_elementwise_fma(t, q, (f32x2){-0.142248368f, -0.142248368f});
-  q = __builtin_elementwise_fma(t, q, (f32x2){0.127414796f, 0.127414796f});
-  o.half = q * t * o.e;
-  const f32x2 mx = {fmaxf(hk.x, 0.0f), fmaxf(hk.y, 0.0f)};
-  o.g = __builtin_elementwise_fma(-ahk, o.half, mx);
-  return o;
+  e = (f32x2){__builtin_amdgcn_exp2f(-sq.x), __builtin_amdgcn_exp2f(-sq.y)};
+  f32x2 q = pk_fma(t, splat2(0.5307027145f), splat2(-0.7265760135f));
+  q = pk_fma(t, q, splat2(0.7107068705f));
+  q = pk_fma(t, q, splat2(-0.142248368f));
+  q = pk_fma(t, q, splat2(0.127414796f));
+  const f32x2 m = pk_fma(-(q * t), e, splat2(0.5f));          // 1/2 - half
+  const f32x2 sgn = {copysignf(m.x, hk.x), copysignf(m.y, hk.y)};
+  return sgn + splat2(0.5f);
 }
 
 // Weights staged once per workgroup: W1 rows zero-padded to CK, b1, W2 (COM rows).
@@ -185,13 +171,15 @@ __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
         f32x4 d = {bb, bb, bb, bb};
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x4f32(az[np][kk], bw[kk], d, 0, 0, 0);
-        const GeluK2 g01 = gelu_k2((f32x2){d[0], d[1]});
-        const GeluK2 g23 = gelu_k2((f32x2){d[2], d[3]});
+        const f32x2 h01 = {d[0], d[1]}, h23 = {d[2], d[3]};
+        f32x2 e01, e23;
+        const f32x2 g01 = h01 * norm_cdf_pair(h01, e01);          // k GELU
+        const f32x2 g23 = h23 * norm_cdf_pair(h23, e23);
 #pragma unroll
         for (int c = 0; c < COM; ++c) {
-          const f32x2 wv = {w2v[c], w2v[c]};
-          acc[np][c][0] = __builtin_elementwise_fma(wv, g01.g, acc[np][c][0]);
-          acc[np][c][1] = __builtin_elementwise_fma(wv, g23.g, acc[np][c][1]);
+          const f32x2 wv = splat2(w2v[c]);
+          acc[np][c][0] = pk_fma(wv, g01, acc[np][c][0]);
+          acc[np][c][1] = pk_fma(wv, g23, acc[np][c][1]);
         }
       }
     }
@@ -305,11 +293,12 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
         wr[i] = v.x; wr[i + 1] = v.y; wr[i + 2] = v.z; wr[i + 3] = v.w;
       }
       const float bb = sw.b1[j];
-      float w2v[COM], gw2[COM];
+      float w2v[COM];
+      f32x2 gw2[COM];
 #pragma unroll
       for (int c = 0; c < COM; ++c) {
         w2v[c] = sw.w2[c][j];
-        gw2[c] = sgw2[wave][t][c][lane];
+        gw2[c] = (f32x2){sgw2[wave][t][c][lane], 0.f};
       }
       f32x4 gw1 = sgw1[wave][t][lane];
       float gb1 = kGW44 ? sgb1[wave][t][lane] : 0.f;
@@ -318,25 +307,24 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
         f32x4 d = {bb, bb, bb, bb};
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x4f32(az[np][kk], bw[kk], d, 0, 0, 0);
-        const GeluK2 g01 = gelu_k2((f32x2){d[0], d[1]});
-        const GeluK2 g23 = gelu_k2((f32x2){d[2], d[3]});
+        const f32x2 h01 = {d[0], d[1]}, h23 = {d[2], d[3]};
+        f32x2 e01, e23;
+        const f32x2 cdf01 = norm_cdf_pair(h01, e01), cdf23 = norm_cdf_pair(h23, e23);
         f32x2 da01 = {0.f, 0.f}, da23 = {0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < COM; ++c) {
-          const f32x2 wv = {w2v[c], w2v[c]};
+          const f32x2 wv = splat2(w2v[c]);
           const f32x2 g01v = {gv[np][0][c], gv[np][1][c]}, g23v = {gv[np][2][c], gv[np][3][c]};
-          da01 = __builtin_elementwise_fma(wv, g01v, da01);
-          da23 = __builtin_elementwise_fma(wv, g23v, da23);
-          // k dW2 (scaled at the fold): pairs summed into one lane register
-          const f32x2 p = __builtin_elementwise_fma(g01v, g01.g, g23v * g23.g);
-          gw2[c] += p.x + p.y;
+          da01 = pk_fma(wv, g01v, da01);
+          da23 = pk_fma(wv, g23v, da23);
+          // k dW2 (scaled at the fold), pair accumulators
+          gw2[c] = pk_fma(g01v, h01 * cdf01, gw2[c]);
+          gw2[c] = pk_fma(g23v, h23 * cdf23, gw2[c]);
         }
-        // GELU' = Phi + h phi; Phi = h >= 0 ? 1 - half : half
-        const f32x2 cdf01 = {d[0] >= 0.f ? 1.0f - g01.half.x : g01.half.x, d[1] >= 0.f ? 1.0f - g01.half.y : g01.half.y};
-        const f32x2 cdf23 = {d[2] >= 0.f ? 1.0f - g23.half.x : g23.half.x, d[3] >= 0.f ? 1.0f - g23.half.y : g23.half.y};
-        const f32x2 kp = {kPdfK, kPdfK};
-        const f32x2 dh01 = da01 * __builtin_elementwise_fma((f32x2){d[0], d[1]} * kp, g01.e, cdf01);
-        const f32x2 dh23 = da23 * __builtin_elementwise_fma((f32x2){d[2], d[3]} * kp, g23.e, cdf23);
+        // GELU' = Phi + h phi
+        const f32x2 kp = splat2(kPdfK);
+        const f32x2 dh01 = da01 * pk_fma(h01 * kp, e01, cdf01);
+        const f32x2 dh23 = da23 * pk_fma(h23 * kp, e23, cdf23);
         const float dh[4] = {dh01.x, dh01.y, dh23.x, dh23.y};
 #pragma unroll
         for (int i = 0; i < CK; ++i) {                                 // k dz (scaled at the store)
@@ -358,7 +346,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
       sgw1[wave][t][lane] = gw1;
       if constexpr (kGW44) sgb1[wave][t][lane] = gb1;
 #pragma unroll
-      for (int c = 0; c < COM; ++c) sgw2[wave][t][c][lane] = gw2[c];
+      for (int c = 0; c < COM; ++c) sgw2[wave][t][c][lane] = gw2[c].x + gw2[c].y;
     }
     // reduce-scatter dzp over the 16 hidden lanes: lane keeps value index e = 16 m + c16,
     // i.e. channel 4 m + (c16 >> 2), point 4 g4 + (c16 & 3)
@@ -452,7 +440,7 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
 #define PF(CK_, CO_)                                                                           \
-  project_fwd_mfma_kernel<CK_, CO_, (CK_ <= 8 ? 4 : 2)><<<blocks, 256, 0, st>>>(z, w1, b1, w2, b2, out, C, P1, P2, \
+  project_fwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kFwdNP4 : (CK_ <= 8 ? 4 : 2))><<<blocks, 256, 0, st>>>(z, w1, b1, w2, b2, out, C, P1, P2, \
                                                             Ho, Wo, Cout, ostride, ooff, npts)
   const int ck = (C + 3) / 4 * 4;
   if (Cout == 1) {
@@ -476,7 +464,7 @@ int project_bwd_mfma(const float* z, const float* w1, const float* b1, const flo
                      int dout_div, hipStream_t st) {
   const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
 #define PB(CK_, CO_)                                                                          \
-  project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? 2 : 1)><<<nchunk, 256, 0, st>>>(z, w1, b1, w2, dout, dz, partial, \
+  project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kBwdNP4 : 1)><<<nchunk, 256, 0, st>>>(z, w1, b1, w2, dout, dz, partial, \
                                                             C, P1, P2, Ho, Wo, Cout, ostride,  \
                                                             ooff, dout_div, npts)
   const int ck = (C + 3) / 4 * 4;
