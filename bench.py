@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--serial-heads", action="store_true", help="run the two heads on one stream")
     ap.add_argument("--config", default="C", choices=sorted(CONFIGS),
                     help="BASELINE.json config (C = the headline metric)")
     ap.add_argument("--batch", type=int, default=None)
@@ -109,6 +110,9 @@ def main():
     np.random.seed(seed + rank)
     torch.manual_seed(seed + rank)
     cfg = CONFIGS[a.config]
+    if a.serial_heads:
+        import blindno.nio
+        blindno.nio.HEAD_STREAMS = False
     N = a.grid or cfg["N"]
     T = a.T or cfg["T"]
     B = a.batch or cfg["B"]

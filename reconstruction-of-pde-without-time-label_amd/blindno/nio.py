@@ -43,27 +43,24 @@ def _select(module, x, bag_idx):
 _SIDE = {}
 
 
+HEAD_STREAMS = True     # fork the two heads over two streams (ops.HeadPairFn)
+
+
 def _run_heads(module, h):
     """The FNO heads on h, concatenated (2d_FPE/NIOModules.py:577-581).  On the GPU two heads run
-    concurrently: the second on a side stream forked from and joined back into the current
-    one (inside a graph capture this becomes two parallel branches).  Each head is one autograd
-    node, so its backward runs on the stream of its forward; the heads are small (B samples),
-    latency-bound launches, which is why overlapping them pays."""
+    concurrently, forward and backward (ops.HeadPairFn: the second on a side stream forked from
+    and joined back into the current one; inside a graph capture, two parallel branches).  The
+    heads are small (B samples), latency-bound launches, which is why overlapping them pays."""
     heads = [getattr(module, n) for n in module._heads]
-    if len(heads) != 2 or not h.is_cuda:
+    if len(heads) != 2 or not h.is_cuda or not HEAD_STREAMS:
         return torch.cat([f(h) for f in heads], dim=-1)
-    main = torch.cuda.current_stream(h.device)
     side = _SIDE.get(h.device)
     if side is None:
         side = _SIDE[h.device] = torch.cuda.Stream(h.device)
-    side.wait_stream(main)
-    o0 = heads[0](h)
-    with torch.cuda.stream(side):
-        o1 = heads[1](h)
-    main.wait_stream(side)
-    h.record_stream(side)
-    o1.record_stream(main)
-    return torch.cat([o0, o1], dim=-1)
+    dim = 2 if isinstance(heads[0], FNO2d) else 1
+    p0, p1 = fno_params(heads[0], dim), fno_params(heads[1], dim)
+    return ops.HeadPairFn.apply(heads[0].meta(h.shape[-1]), heads[1].meta(h.shape[-1]), len(p0), side,
+                                h, *p0, *p1)
 
 
 def _bag_mean_2d(module, u, grid, B, L, nx, ny):

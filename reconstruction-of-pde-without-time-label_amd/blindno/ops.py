@@ -497,6 +497,61 @@ class FNOFn(torch.autograd.Function):
         return (None, d_inp, *grads)
 
 
+class HeadPairFn(torch.autograd.Function):
+    """Two FNO heads on the same input h (2d_FPE/NIOModules.py:577-581: cat of fno_drift and
+    fno_diffusion), forward AND backward forked over two HIP streams: head 0 on the current
+    stream, head 1 on ``side`` (waiting on the current stream first, joined back after).  The
+    heads are small (B samples), latency-bound chains of launches, so the two chains overlap;
+    doing the backward fork here rather than relying on autograd's per-node streams keeps the
+    two backward chains concurrent (inside a graph capture: two parallel branches)."""
+
+    @staticmethod
+    def forward(ctx, meta0, meta1, n0, side, h, *prm):
+        require_device(h, *prm)
+        h = _c(h)
+        prm = [_c(p) for p in prm]
+        p0, p1 = prm[:n0], prm[n0:]
+        main = torch.cuda.current_stream(h.device)
+        side.wait_stream(main)
+        o0, s0 = fno_forward(meta0, h, p0, save=True)
+        with torch.cuda.stream(side):
+            o1, s1 = fno_forward(meta1, h, p1, save=True)
+        main.wait_stream(side)
+        h.record_stream(side)
+        o1.record_stream(main)
+        out = torch.cat([o0, o1], dim=-1)
+        ctx.save_for_backward(h, *prm)
+        ctx.meta = (meta0, meta1, n0, side, o0.shape[-1])
+        ctx.s0, ctx.s1 = s0, s1
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        meta0, meta1, n0, side, c0 = ctx.meta
+        t = ctx.saved_tensors
+        h, prm = t[0], list(t[1:])
+        p0, p1 = prm[:n0], prm[n0:]
+        need = ctx.needs_input_grad[4]
+        gout = _c(gout)
+        g0 = gout[..., :c0].contiguous()
+        g1 = gout[..., c0:].contiguous()
+        main = torch.cuda.current_stream(h.device)
+        side.wait_stream(main)
+        # side branch captured first: a graph replay submits nodes in capture order, and the
+        # side chain must not queue behind the whole main chain
+        with torch.cuda.stream(side):
+            d1, gr1 = fno_backward(meta1, h, p1, ctx.s1, g1, need)
+        d0, gr0 = fno_backward(meta0, h, p0, ctx.s0, g0, need)
+        main.wait_stream(side)
+        g1.record_stream(side)
+        for g in ([d1] if d1 is not None else []) + [g for g in gr1 if g is not None]:
+            g.record_stream(main)
+        ctx.s0 = ctx.s1 = None
+        dh = d0 + d1 if need else None
+        grads = [g if ctx.needs_input_grad[5 + i] else None for i, g in enumerate(gr0 + gr1)]
+        return (None, None, None, None, dh, *grads)
+
+
 # ---------------------------------------------------------------------------- fused snapshot encoder
 
 
