@@ -72,6 +72,25 @@ __host__ __device__ __forceinline__ int kept_rows_count(int m1, int P1) {
   return 2 * m1 < P1 ? 2 * m1 : P1;
 }
 
+// Block-wide copy of n floats global -> LDS (16-B aligned src/dst): float4 loads, four in flight
+// per thread, so a workgroup's table staging costs one memory latency rather than n/blockDim.
+__device__ __forceinline__ void stage_to_lds(float* __restrict__ dst, const float* __restrict__ src,
+                                             int n) {
+  const int n4 = n >> 2, st = blockDim.x;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  int e = threadIdx.x;
+  for (; e + 3 * st < n4; e += 4 * st) {
+    const float4 a = s4[e], b = s4[e + st], c = s4[e + 2 * st], d = s4[e + 3 * st];
+    d4[e] = a;
+    d4[e + st] = b;
+    d4[e + 2 * st] = c;
+    d4[e + 3 * st] = d;
+  }
+  for (; e < n4; e += st) d4[e] = s4[e];
+  for (int t = (n4 << 2) + (int)threadIdx.x; t < n; t += st) dst[t] = src[t];
+}
+
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 inline int grid_for(int64_t n, int block = kBlock, int cap = 1 << 20) {

@@ -34,6 +34,13 @@ constexpr int kWaves = 4;
 #define PROJ_BWD_NP4 2
 #endif
 constexpr int kFwdNP4 = PROJ_FWD_NP4;
+// point tiles per wave when sizing the grids (small fields: more workgroups)
+#ifndef PF_TPW
+#define PF_TPW 2
+#endif
+#ifndef PB_TPW
+#define PB_TPW 2
+#endif
 constexpr int kBwdNP4 = PROJ_BWD_NP4;
 
 struct PointMap {
@@ -436,7 +443,7 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
                      int Cout, int ostride, int ooff, hipStream_t st) {
   const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
   const unsigned ntiles = (npts + 15) / 16;
-  unsigned blocks = (ntiles + kWaves * 16 - 1) / (kWaves * 16);
+  unsigned blocks = (ntiles + kWaves * PF_TPW - 1) / (kWaves * PF_TPW);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
 #define PF(CK_, CO_)                                                                           \
@@ -454,7 +461,7 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
 
 int project_bwd_mfma_nchunk(int64_t npts) {
   const int64_t tiles = (npts + 15) / 16;
-  int64_t b = (tiles + kWaves * 16 - 1) / (kWaves * 16);     // >= 16 tiles per wave
+  int64_t b = (tiles + kWaves * PB_TPW - 1) / (kWaves * PB_TPW);
   return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
 }
 

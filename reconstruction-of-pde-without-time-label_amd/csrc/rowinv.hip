@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
   const int NT = (P2 + 15) >> 4;
   if (LDSB) {
     const int ntb = KS * NT * 64;
-    for (int e = threadIdx.x; e < ntb; e += blockDim.x) sTB[e] = TB[e];
+    stage_to_lds(sTB, TB, ntb);
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;

@@ -13,6 +13,7 @@
 
 using namespace blindno;
 
+
 namespace {
 
 // ------------------------------------------------------------------------------ row DFT
@@ -36,7 +37,7 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
                                                           int act) {
   extern __shared__ float smT[];                 // [KB][4][Npad][4]
   const int nT = KB * 16 * Npad;
-  for (int e = threadIdx.x; e < nT; e += blockDim.x) smT[e] = Tp[e];
+  stage_to_lds(smT, Tp, nT);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
@@ -53,9 +54,9 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int kb = 0; kb < KB; ++kb) {
+    // x loads run two K blocks ahead of the MFMAs (small fields are latency-bound)
+    auto load_a = [&](int kb, float (&a)[4]) {
       const int w0 = kb * 16 + kq * 4;
-      float a[4];
       if (ALIGNED && w0 + 3 < P2) {
         const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
         a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
@@ -63,6 +64,15 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < P2) ? xr[w0 + s] : 0.f;
       }
+    };
+    float a1[4], a2[4] = {0.f, 0.f, 0.f, 0.f};
+    load_a(0, a1);
+    if (KB > 1) load_a(1, a2);
+    for (int kb = 0; kb < KB; ++kb) {
+      float a[4] = {a1[0], a1[1], a1[2], a1[3]};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a1[s] = a2[s];
+      if (kb + 2 < KB) load_a(kb + 2, a2);
       if (act) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = gelu_f(a[s]);
@@ -112,7 +122,7 @@ __global__ __launch_bounds__(256) void rowdft_bag_lift_kernel(
     int T, int L, int N1, int N2, int C, int P1, int m2, int KB, int Npad, int ntile_groups) {
   extern __shared__ float smT[];                 // [KB][4][Npad][4]
   const int nT = KB * 16 * Npad;
-  for (int e = threadIdx.x; e < nT; e += blockDim.x) smT[e] = Tp[e];
+  stage_to_lds(smT, Tp, nT);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
@@ -247,11 +257,22 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
     const float2* ar = At + ((int64_t)q0 * Cin + (rok ? row : 0)) * P1;
     const f32x4* fb = FB + ((int64_t)jt * HB * 64 + lane) * 2;
     f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
+    // operands of the next 16-row block are loaded before this block's MFMAs
+    float nre[4], nim[4];
+    load4c(ar + kq * 4, rok ? P1 - kq * 4 : 0, vec, nre, nim);
+    f32x4 nf0 = fb[0], nf1 = fb[1];
     for (int hb = 0; hb < HB; ++hb) {
-      const int h0 = hb * 16 + kq * 4;
       float re[4], im[4];
-      load4c(ar + h0, rok ? P1 - h0 : 0, vec, re, im);
-      cmfma4(re, im, fb[hb * 128], fb[hb * 128 + 1], dr, di);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { re[s] = nre[s]; im[s] = nim[s]; }
+      const f32x4 f0 = nf0, f1 = nf1;
+      if (hb + 1 < HB) {
+        const int h1 = (hb + 1) * 16 + kq * 4;
+        load4c(ar + h1, rok ? P1 - h1 : 0, vec, nre, nim);
+        nf0 = fb[(hb + 1) * 128];
+        nf1 = fb[(hb + 1) * 128 + 1];
+      }
+      cmfma4(re, im, f0, f1, dr, di);
     }
     const int j = jt * 16 + r16;
 #pragma unroll
@@ -277,6 +298,7 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
     if (j < K1) {
       const float2* wj = Wt + ((int64_t)k * K1 + j) * Ci * Co;
       const float2* xp = sX + p * Cin * LDX + j;
+#pragma unroll 4
       for (int c = 0; c < Cin; ++c) {
         const float2 a = xp[c * LDX];
         if (DIR == 0) {

