@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--serial-heads", action="store_true", help="run the two heads on one stream")
+    ap.add_argument("--forked-heads", action="store_true",
+                    help="two heads as two forked launch chains instead of one grouped chain")
     ap.add_argument("--config", default="C", choices=sorted(CONFIGS),
                     help="BASELINE.json config (C = the headline metric)")
     ap.add_argument("--batch", type=int, default=None)
@@ -113,6 +115,9 @@ def main():
     if a.serial_heads:
         import blindno.nio
         blindno.nio.HEAD_STREAMS = False
+    if a.forked_heads or a.serial_heads:
+        from blindno import ops as _ops
+        _ops.GROUPED_HEADS = False
     N = a.grid or cfg["N"]
     T = a.T or cfg["T"]
     B = a.batch or cfg["B"]

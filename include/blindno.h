@@ -243,6 +243,50 @@ int blindno_gpe_solve(const double* psi0, const double* V, const double* g, cons
 int blindno_trapz_rows(const double* a, const double* b, const double* x, double* out, int rows,
                        int n, blindno_stream_t stream);
 
+/* ---- grouped launches: two FNO heads over one field in one chain (ops.HeadPairFn) ----------
+ * G weight groups over consecutive blocks of Bg = Bn/G samples.  Group g's small weights (fc0,
+ * 1x1 convs, fc1/fc2 -- packed per head in one buffer) are read at + g*wgs floats from the
+ * given pointers, its packed spectral weights at Wt + g*wtgs floats.  Semantics otherwise as
+ * the ungrouped entry points above (which are these with G = 1), plus:
+ *  lift_fwd_g:    the input holds Bg samples shared by every group (x0 sample g Bg + n reads
+ *                 in[n]);
+ *  lift_bwd_g:    d_in (Bg samples) sums all groups' contributions; partial[nchunk][G][np],
+ *                 nchunk = blindno_lift_bwd_nchunk(Bg, N1, N2);
+ *  project_fwd_g: sample g Bg + n writes output sample n at channel offset ooff + g*Cout
+ *                 (matrix-core path only: Hd 128, C <= 15, Cout <= 2);
+ *  project_bwd_g: dout addressed like project_fwd_g's output; partial[nchunk][G][np] with
+ *                 nchunk = blindno_project_bwd_nchunk(Bg, Ho, Wo);
+ *  conv_wgrad_g:  partial[nchunk][G][np], nchunk = blindno_conv_wgrad_nchunk(Bg, P1, P2);
+ *  mix_wgrad_g:   dWt (G, m2, K1, Ci, Co) complex, nsplit = blindno_mix_wgrad_nsplit(Bg, ...),
+ *                 partial nsplit x G x 2 m2 K1 Ci Co floats. */
+int blindno_lift_fwd_g(const float* in, const float* w0, const float* b0, float* x0, int G,
+                       int64_t wgs, int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
+                       blindno_stream_t stream);
+int blindno_lift_bwd_g(const float* dx0, const float* in, const float* w0, float* d_in,
+                       float* partial, int nchunk, int G, int64_t wgs, int Bn, int N1, int N2,
+                       int Cin, int C, int P1, int P2, blindno_stream_t stream);
+int blindno_project_fwd_g(const float* z, const float* w1, const float* b1, const float* w2,
+                          const float* b2, float* out, int G, int64_t wgs, int Bn, int C, int P1,
+                          int P2, int Ho, int Wo, int Hd, int Cout, int ostride, int ooff,
+                          blindno_stream_t stream);
+int blindno_project_bwd_g(const float* z, const float* w1, const float* b1, const float* w2,
+                          const float* dout, float* dz, float* partial, int nchunk, int G,
+                          int64_t wgs, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd,
+                          int Cout, int ostride, int ooff, blindno_stream_t stream);
+int blindno_colpass_g(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
+                      const float* FB, const float* GB, int G, int64_t wtgs, int Bn, int Ci,
+                      int Co, int P1, int m1, int m2, int P2, int dir, blindno_stream_t stream);
+int blindno_mix_wgrad_g(const float* X, const float* Gs, float* dWt, float* partial, int nsplit,
+                        int G, int Bn, int Ci, int Co, int K1, int m2, blindno_stream_t stream);
+int blindno_rowidft_epi_g(const float* Z, const float* x, const float* wc, const float* bc,
+                          float* z, const float* tb, int G, int64_t wgs, int Bn, int C, int P1,
+                          int P2, int m2, int act, blindno_stream_t stream);
+int blindno_rowidft_bwd_g(const float* Gs, const float* dz, const float* wc, const float* xsrc,
+                          float* dx, const float* tb, int G, int64_t wgs, int Bn, int C, int P1,
+                          int P2, int m2, int act, blindno_stream_t stream);
+int blindno_conv_wgrad_g(const float* dz, const float* x, float* partial, int nchunk, int G,
+                         int Bn, int C, int P1, int P2, int act, blindno_stream_t stream);
+
 /* ---- NIO encoder ConvBlock normalisation: BatchNorm2d fused with LeakyReLU
  * (2d_FPE/Baselines.py:40-52 ConvBlock = Conv -> BatchNorm2d -> LeakyReLU(slope); replaces the
  * nn.BatchNorm2d + nn.LeakyReLU(inplace) pair of each block).  z (Npad, C, HW) NCHW, batch =

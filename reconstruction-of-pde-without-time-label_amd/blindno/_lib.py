@@ -50,6 +50,15 @@ SIGNATURES = {
     "blindno_rowidft_bwd_nchunk": "iiiii",
     "blindno_project_bwd_nchunk": "iii",
     "blindno_mix_wgrad_nsplit": "iiiii",
+    "blindno_lift_fwd_g": "ppppiliiiiiiis",
+    "blindno_lift_bwd_g": "pppppiiliiiiiiis",
+    "blindno_project_fwd_g": "ppppppiliiiiiiiiiis",
+    "blindno_project_bwd_g": "pppppppiiliiiiiiiiiis",
+    "blindno_colpass_g": "pppppppiliiiiiiiis",
+    "blindno_mix_wgrad_g": "ppppiiiiiiis",
+    "blindno_rowidft_epi_g": "ppppppiliiiiiis",
+    "blindno_rowidft_bwd_g": "ppppppiliiiiiis",
+    "blindno_conv_wgrad_g": "pppiiiiiiis",
     "blindno_bn_act_nslices": "iii",
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",

@@ -497,6 +497,174 @@ class FNOFn(torch.autograd.Function):
         return (None, d_inp, *grads)
 
 
+# ---------------------------------------------------------------------------- grouped heads
+# Two FNO2d heads on the same input run as ONE chain of launches over 2 B samples: every
+# kernel selects the weights of the sample's head (blindno_*_g entry points).  The heads'
+# small weights (fc0, 1x1 convs, fc1/fc2) are packed into one buffer per step (one copy
+# kernel), the spectral weights into one packed Wt per layer.
+
+
+def _small_params(prm, n, nw):
+    """[fc0w, fc0b, (cw, cb) * n, fc1w, fc1b, fc2w, fc2b] out of an FNO parameter list."""
+    out = [prm[0], prm[1]]
+    for k in range(n):
+        off = 2 + k * (nw + 2)
+        out += [prm[off + nw], prm[off + nw + 1]]
+    off = 2 + n * (nw + 2)
+    return out + list(prm[off:off + 4])
+
+
+def _offsets(tensors):
+    offs, o = [], 0
+    for t in tensors:
+        offs.append(o)
+        o += t.numel()
+    return offs, o
+
+
+def grouped_ok(meta: FNOMeta, inp, prms) -> bool:
+    if meta.dim != 2 or len(prms) != 2:
+        return False
+    n = meta.n_layers
+    fc1w, fc2w = prms[0][2 + 4 * n], prms[0][4 + 4 * n]
+    Hd, Cout = fc1w.shape[0], fc2w.shape[0]
+    if Hd != 128 or meta.width > 15 or Cout > 2:
+        return False
+    if any(a.shape != b.shape for a, b in zip(prms[0], prms[1])):
+        return False
+    Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
+    return (Bg * Ho * Wo) % 64 == 0
+
+
+def _sub(buf, off):
+    return buf[off:] if off else buf
+
+
+def fno_forward_grouped(meta: FNOMeta, inp, prms):
+    """Both heads' FNO2d forward in one chain; returns (out (Bg, Ho, Wo, G*Cout), saved)."""
+    G = len(prms)
+    Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
+    Bn = G * Bg
+    C, n = meta.width, meta.n_layers
+    smalls = [_small_params(p, n, 2) for p in prms]
+    offs, S = _offsets(smalls[0])
+    small = torch.cat([t.reshape(-1) for sm in smalls for t in sm])
+    x0 = _empty(Bn, C, P1, P2, like=inp)
+    call("blindno_lift_fwd_g", ptr(inp), ptr(_sub(small, offs[0])), ptr(_sub(small, offs[1])), ptr(x0),
+         G, S, Bn, N1, N2, Cin, C, P1, P2, stream_ptr())
+    K1 = kept_rows_count(meta.m1, P1)
+    K1p = 16 * ((K1 + 15) // 16)
+    FB, GB = twiddle_cols(P1, meta.m1, inp.device)
+    src, act = x0, 0
+    Xs, Wts, zs = [], [], []
+    for k in range(n):
+        off = 2 + 4 * k
+        Wt = _empty(G, meta.m2, K1, C, C, 2, like=inp)
+        for g in range(G):
+            call("blindno_pack_w2d", ptr(_c(prms[g][off])), ptr(_c(prms[g][off + 1])), ptr(Wt[g]), C, C,
+                 meta.m1, meta.m2, P1, stream_ptr())
+        At = k_rowdft(src, Bn, C, P1, P2, meta.m2, act)
+        X = _empty(Bn, meta.m2, C, K1, 2, like=inp)
+        Y = _empty(Bn, meta.m2, C, K1p, 2, like=inp)
+        Z = _empty(Bn, P1, meta.m2, C, 2, like=inp)
+        call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(X), ptr(Y), ptr(Z), ptr(FB), ptr(GB), G,
+             Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, 0, stream_ptr())
+        z = _empty(Bn, C, P1, P2, like=inp)
+        call("blindno_rowidft_epi_g", ptr(Z), ptr(src), ptr(_sub(small, offs[2 + 2 * k])),
+             ptr(_sub(small, offs[3 + 2 * k])), ptr(z), ptr(twiddle_rowinv(P2, meta.m2, inp.device)),
+             G, S, Bn, C, P1, P2, meta.m2, act, stream_ptr())
+        Xs.append(X)
+        Wts.append(Wt)
+        zs.append(z)
+        src, act = z, 1
+    o1 = 2 + 2 * n
+    Hd, Cout = smalls[0][o1].shape[0], smalls[0][o1 + 2].shape[0]
+    out = _empty(Bg, Ho, Wo, G * Cout, like=inp)
+    call("blindno_project_fwd_g", ptr(zs[-1]), ptr(_sub(small, offs[o1])), ptr(_sub(small, offs[o1 + 1])),
+         ptr(_sub(small, offs[o1 + 2])), ptr(_sub(small, offs[o1 + 3])), ptr(out), G, S, Bn, C, P1, P2,
+         Ho, Wo, Hd, Cout, G * Cout, 0, stream_ptr())
+    return out, (small, x0, Xs, Wts, zs)
+
+
+def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
+    """Adjoint of fno_forward_grouped: (d_inp summed over the heads, [grads of head g])."""
+    G = len(prms)
+    Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
+    Bn = G * Bg
+    C, n = meta.width, meta.n_layers
+    small, x0, Xs, Wts, zs = saved
+    smalls = [_small_params(p, n, 2) for p in prms]
+    offs, S = _offsets(smalls[0])
+    o1 = 2 + 2 * n
+    Hd, Cout = smalls[0][o1].shape[0], smalls[0][o1 + 2].shape[0]
+    gout = _c(gout)
+    grads = [[None] * len(p) for p in prms]
+    off_fc1 = 2 + 4 * n
+    # projection
+    dz = torch.zeros(Bn, C, P1, P2, dtype=F32, device=inp.device)
+    np_p = Hd * C + Hd + Cout * Hd + Cout
+    nchunk = query("blindno_project_bwd_nchunk", Bg, Ho, Wo)
+    partial = _empty(nchunk, G, np_p, like=inp)
+    call("blindno_project_bwd_g", ptr(zs[-1]), ptr(_sub(small, offs[o1])), ptr(_sub(small, offs[o1 + 1])),
+         ptr(_sub(small, offs[o1 + 2])), ptr(gout), ptr(dz), ptr(partial), nchunk, G, S, Bn, C, P1, P2,
+         Ho, Wo, Hd, Cout, G * Cout, 0, stream_ptr())
+    gp = reduce_partials(partial, nchunk, G * np_p).view(G, np_p)
+    for g in range(G):
+        o = 0
+        grads[g][off_fc1] = gp[g, o:o + Hd * C].view(Hd, C); o += Hd * C
+        grads[g][off_fc1 + 1] = gp[g, o:o + Hd]; o += Hd
+        grads[g][off_fc1 + 2] = gp[g, o:o + Cout * Hd].view(Cout, Hd); o += Cout * Hd
+        grads[g][off_fc1 + 3] = gp[g, o:o + Cout]
+    K1 = kept_rows_count(meta.m1, P1)
+    K1p = 16 * ((K1 + 15) // 16)
+    FB, GB = twiddle_cols(P1, meta.m1, inp.device)
+    tb = twiddle_rowinv(P2, meta.m2, inp.device)
+    np_c = C * C + C
+    for k in reversed(range(n)):
+        off = 2 + 4 * k
+        src, act = (x0, 0) if k == 0 else (zs[k - 1], 1)
+        Wt = Wts[k]
+        At = k_rowdft(dz, Bn, C, P1, P2, meta.m2, 0)
+        Gs = _empty(Bn, meta.m2, C, K1, 2, like=inp)
+        Y = _empty(Bn, meta.m2, C, K1p, 2, like=inp)
+        GZ = _empty(Bn, P1, meta.m2, C, 2, like=inp)
+        call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(Gs), ptr(Y), ptr(GZ), ptr(FB), ptr(GB), G,
+             Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, 1, stream_ptr())
+        dWt = _empty(G, meta.m2, K1, C, C, 2, like=inp)
+        ns = query("blindno_mix_wgrad_nsplit", Bg, C, C, K1, meta.m2)
+        part = _empty(ns, G, meta.m2 * K1 * C * C * 2, like=inp) if ns > 1 else None
+        call("blindno_mix_wgrad_g", ptr(Xs[k]), ptr(Gs), ptr(dWt), ptr(part) if part is not None else None,
+             ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
+        for g in range(G):
+            dw1, dw2 = k_unpack_w2d(dWt[g], prms[g][off], P1)
+            grads[g][off], grads[g][off + 1] = dw1, dw2
+        nch = query("blindno_conv_wgrad_nchunk", Bg, P1, P2)
+        pc = _empty(nch, G, np_c, like=inp)
+        call("blindno_conv_wgrad_g", ptr(dz), ptr(src), ptr(pc), nch, G, Bn, C, P1, P2, act, stream_ptr())
+        gc = reduce_partials(pc, nch, G * np_c).view(G, np_c)
+        for g in range(G):
+            grads[g][off + 2] = gc[g, :C * C].view_as(prms[g][off + 2])
+            grads[g][off + 3] = gc[g, C * C:]
+        dz_new = _empty(Bn, C, P1, P2, like=inp)
+        call("blindno_rowidft_bwd_g", ptr(GZ), ptr(dz), ptr(_sub(small, offs[2 + 2 * k])), ptr(src),
+             ptr(dz_new), ptr(tb), G, S, Bn, C, P1, P2, meta.m2, act, stream_ptr())
+        dz = dz_new
+    np_l = C * Cin + C
+    nchunk = query("blindno_lift_bwd_nchunk", Bg, N1, N2)
+    partial = _empty(nchunk, G, np_l, like=inp)
+    d_inp = torch.empty_like(inp) if need_inp_grad else None
+    call("blindno_lift_bwd_g", ptr(dz), ptr(inp), ptr(small), ptr(d_inp), ptr(partial), nchunk, G, S,
+         Bn, N1, N2, Cin, C, P1, P2, stream_ptr())
+    gl = reduce_partials(partial, nchunk, G * np_l).view(G, np_l)
+    for g in range(G):
+        grads[g][0] = gl[g, :C * Cin].view(C, Cin)
+        grads[g][1] = gl[g, C * Cin:]
+    return d_inp, grads
+
+
+GROUPED_HEADS = True    # batch the two heads into one chain of grouped launches when possible
+
+
 class HeadPairFn(torch.autograd.Function):
     """Two FNO heads on the same input h (2d_FPE/NIOModules.py:577-581: cat of fno_drift and
     fno_diffusion), forward AND backward forked over two HIP streams: head 0 on the current
@@ -511,6 +679,13 @@ class HeadPairFn(torch.autograd.Function):
         h = _c(h)
         prm = [_c(p) for p in prm]
         p0, p1 = prm[:n0], prm[n0:]
+        ctx.grouped = GROUPED_HEADS and meta0.__dict__ == meta1.__dict__ and grouped_ok(meta0, h, [p0, p1])
+        if ctx.grouped:
+            out, saved = fno_forward_grouped(meta0, h, [p0, p1])
+            ctx.save_for_backward(h, *prm)
+            ctx.meta = (meta0, meta1, n0, side, None)
+            ctx.s0, ctx.s1 = saved, None
+            return out
         main = torch.cuda.current_stream(h.device)
         side.wait_stream(main)
         o0, s0 = fno_forward(meta0, h, p0, save=True)
@@ -533,6 +708,11 @@ class HeadPairFn(torch.autograd.Function):
         p0, p1 = prm[:n0], prm[n0:]
         need = ctx.needs_input_grad[4]
         gout = _c(gout)
+        if ctx.grouped:
+            dh, gr = fno_backward_grouped(meta0, h, [p0, p1], ctx.s0, gout, need)
+            ctx.s0 = None
+            grads = [g if ctx.needs_input_grad[5 + i] else None for i, g in enumerate(gr[0] + gr[1])]
+            return (None, None, None, None, dh, *grads)
         g0 = gout[..., :c0].contiguous()
         g1 = gout[..., c0:].contiguous()
         main = torch.cuda.current_stream(h.device)

@@ -20,12 +20,56 @@ using namespace blindno;
 namespace {
 
 // ---------------------------------------------------------------- lift
+// Grouped launches (G > 1): samples n = g Bg + n' of group g use that group's weights at
+// w + g wgs and read the shared input sample n' (two FNO heads on one field).
+// One thread per point computing every output channel (the input vector is read once):
+// Bn x P1 x P2 threads; channels-last input, NCHW output (coalesced across w).
+template <int CM>
+__global__ __launch_bounds__(kBlock) void lift_fwd_pt_kernel(const float* __restrict__ in,
+                                                             const float* __restrict__ w0,
+                                                             const float* __restrict__ b0,
+                                                             float* __restrict__ x0, int Bn,
+                                                             int N1, int N2, int Cin, int C,
+                                                             int P1, int P2, int Bg,
+                                                             int64_t wgs) {
+  const int64_t HW = (int64_t)P1 * P2;
+  const int64_t total = (int64_t)Bn * HW;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = idx / HW;
+    const int64_t s = idx - n * HW;
+    const int h = (int)(s / P2), w = (int)(s - (s / P2) * P2);
+    float* xp = x0 + n * C * HW + s;
+    if (h >= N1 || w >= N2) {
+      for (int c = 0; c < C; ++c) xp[c * HW] = 0.f;
+      continue;
+    }
+    const int g = (int)(n / Bg);
+    const int64_t ni = n - (int64_t)g * Bg;
+    const float* wg = w0 + g * wgs;
+    const float* bg = b0 + g * wgs;
+    const float* ip = in + ((ni * N1 + h) * N2 + w) * Cin;
+    float acc[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) acc[c] = c < C ? bg[c] : 0.f;
+    for (int j = 0; j < Cin; ++j) {
+      const float v = ip[j];
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C) acc[c] = fmaf(wg[c * Cin + j], v, acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) xp[c * HW] = acc[c];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void lift_fwd_kernel(const float* __restrict__ in,
                                                           const float* __restrict__ w0,
                                                           const float* __restrict__ b0,
                                                           float* __restrict__ x0, int Bn, int N1,
                                                           int N2, int Cin, int C, int P1,
-                                                          int P2) {
+                                                          int P2, int Bg, int64_t wgs) {
   const int64_t total = (int64_t)Bn * C * P1 * P2;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -37,9 +81,11 @@ __global__ __launch_bounds__(kBlock) void lift_fwd_kernel(const float* __restric
     const int n = (int)(t / C);
     float v = 0.f;
     if (h < N1 && w < N2) {
-      const float* ip = in + (((int64_t)n * N1 + h) * N2 + w) * Cin;
-      v = b0[c];
-      for (int j = 0; j < Cin; ++j) v = fmaf(w0[c * Cin + j], ip[j], v);
+      const int g = n / Bg, ni = n - g * Bg;
+      const float* wg = w0 + g * wgs;
+      const float* ip = in + (((int64_t)ni * N1 + h) * N2 + w) * Cin;
+      v = b0[g * wgs + c];
+      for (int j = 0; j < Cin; ++j) v = fmaf(wg[c * Cin + j], ip[j], v);
     }
     x0[idx] = v;
   }
@@ -49,7 +95,8 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_kernel(const float* __rest
                                                              const float* __restrict__ w0,
                                                              float* __restrict__ d_in, int Bn,
                                                              int N1, int N2, int Cin, int C,
-                                                             int P1, int P2) {
+                                                             int P1, int P2, int G, int64_t wgs) {
+  // d_in has Bn samples; with G groups the gradient sums over the groups' samples g Bn + n
   const int64_t total = (int64_t)Bn * N1 * N2 * Cin;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -60,8 +107,9 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_kernel(const float* __rest
     const int h = (int)(t % N1);
     const int n = (int)(t / N1);
     float v = 0.f;
-    for (int c = 0; c < C; ++c)
-      v = fmaf(w0[c * Cin + j], dx0[(((int64_t)n * C + c) * P1 + h) * P2 + w], v);
+    for (int g = 0; g < G; ++g)
+      for (int c = 0; c < C; ++c)
+        v = fmaf(w0[g * wgs + c * Cin + j], dx0[((((int64_t)g * Bn + n) * C + c) * P1 + h) * P2 + w], v);
     d_in[idx] = v;
   }
 }
@@ -81,7 +129,11 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_w_kernel(const float* __restr
                                                             float* __restrict__ partial, int Bn,
                                                             int N1, int N2, int Cin, int C,
                                                             int P1, int P2) {
+  // blockIdx.y = group g: dx0 samples g Bn + n against the shared input sample n;
+  // partial[blockIdx.x][g][np]
   extern __shared__ float sm[];
+  const int grp = blockIdx.y;
+  dx0 += (int64_t)grp * Bn * C * P1 * P2;
   float* sa = sm;                       // [C][TP+1]
   float* sb = sa + C * (TP + 1);        // [Cin][TP+1]
   const int64_t npts = (int64_t)Bn * N1 * N2;
@@ -132,11 +184,13 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_w_kernel(const float* __restr
 #pragma unroll
   for (int e = 0; e < PPT; ++e) {
     const int pr = t + e * kBlock;
-    if (pr < np) partial[(int64_t)blockIdx.x * np + pr] = acc[e];
+    if (pr < np) partial[((int64_t)blockIdx.x * gridDim.y + grp) * np + pr] = acc[e];
   }
 }
 
-// conv: A = dz, B = f(x) (NCHW, HW points per sample); tiles never straddle samples
+// conv: A = dz, B = f(x) (NCHW, HW points per sample); tiles never straddle samples.
+// blockIdx.y = group: samples [g Bn', (g+1) Bn') with Bn' = ntiles / tiles_per_n;
+// partial[blockIdx.x][g][np]
 template <int ACT>
 __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restrict__ dz,
                                                             const float* __restrict__ x,
@@ -148,6 +202,10 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restr
   float* sb = sa + C * (TP + 1);
   const int t = threadIdx.x;
   const int np = C * C + C;
+  const int grp = blockIdx.y;
+  const int64_t gofs = (int64_t)grp * (ntiles / tiles_per_n) * C * HW;
+  dz += gofs;
+  x += gofs;
   float acc[PPT];
 #pragma unroll
   for (int e = 0; e < PPT; ++e) acc[e] = 0.f;
@@ -187,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restr
 #pragma unroll
   for (int e = 0; e < PPT; ++e) {
     const int pr = t + e * kBlock;
-    if (pr < np) partial[(int64_t)blockIdx.x * np + pr] = acc[e];
+    if (pr < np) partial[((int64_t)blockIdx.x * gridDim.y + grp) * np + pr] = acc[e];
   }
 }
 
@@ -543,14 +601,29 @@ BLINDNO_API const char* blindno_error_string(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
+BLINDNO_API int blindno_lift_fwd_g(const float* in, const float* w0, const float* b0, float* x0,
+                                   int G, int64_t wgs, int Bn, int N1, int N2, int Cin, int C,
+                                   int P1, int P2, void* stream) {
+  if (N1 > P1 || N2 > P2 || G < 1 || Bn % G) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int Bg = G > 1 ? Bn / G : Bn;
+  if (G == 1) wgs = 0;
+  if (C > 4 && C <= 16) {         // wide lifts (the heads): one thread per point, all channels
+    const int64_t pts = (int64_t)Bn * P1 * P2;
+    lift_fwd_pt_kernel<16><<<grid_for(pts, kBlock, 65536), kBlock, 0, st>>>(
+        in, w0, b0, x0, Bn, N1, N2, Cin, C, P1, P2, Bg, wgs);
+    return (int)hipGetLastError();
+  }
+  const int64_t total = (int64_t)Bn * C * P1 * P2;
+  lift_fwd_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(
+      in, w0, b0, x0, Bn, N1, N2, Cin, C, P1, P2, Bg, wgs);
+  return (int)hipGetLastError();
+}
+
 BLINDNO_API int blindno_lift_fwd(const float* in, const float* w0, const float* b0, float* x0,
                                  int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
                                  void* stream) {
-  if (N1 > P1 || N2 > P2) return (int)hipErrorInvalidValue;
-  const int64_t total = (int64_t)Bn * C * P1 * P2;
-  lift_fwd_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, (hipStream_t)stream>>>(
-      in, w0, b0, x0, Bn, N1, N2, Cin, C, P1, P2);
-  return (int)hipGetLastError();
+  return blindno_lift_fwd_g(in, w0, b0, x0, 1, 0, Bn, N1, N2, Cin, C, P1, P2, stream);
 }
 
 BLINDNO_API int blindno_lift_bwd_nchunk(int Bn, int N1, int N2) {
@@ -558,22 +631,33 @@ BLINDNO_API int blindno_lift_bwd_nchunk(int Bn, int N1, int N2) {
   return nt < 1024 ? nt : 1024;
 }
 
+BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const float* w0,
+                                   float* d_in, float* partial, int nchunk, int G, int64_t wgs,
+                                   int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
+                                   void* stream) {
+  if (G < 1 || Bn % G) return (int)hipErrorInvalidValue;
+  const int Bg = Bn / G;
+  hipStream_t st = (hipStream_t)stream;
+  if (d_in) {
+    const int64_t total = (int64_t)Bg * N1 * N2 * Cin;
+    lift_bwd_in_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(
+        dx0, w0, d_in, Bg, N1, N2, Cin, C, P1, P2, G, G > 1 ? wgs : 0);
+  }
+  if (partial) {
+    if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)
+      return (int)hipErrorInvalidValue;
+    const size_t sh = sizeof(float) * (size_t)(C + Cin) * (TP + 1);
+    lift_bwd_w_kernel<<<dim3(nchunk, G), kBlock, sh, st>>>(dx0, in, partial, Bg, N1, N2, Cin, C,
+                                                          P1, P2);
+  }
+  return (int)hipGetLastError();
+}
+
 BLINDNO_API int blindno_lift_bwd(const float* dx0, const float* in, const float* w0,
                                  float* d_in, float* partial, int nchunk, int Bn, int N1,
                                  int N2, int Cin, int C, int P1, int P2, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  if (d_in) {
-    const int64_t total = (int64_t)Bn * N1 * N2 * Cin;
-    lift_bwd_in_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(dx0, w0, d_in, Bn, N1,
-                                                                          N2, Cin, C, P1, P2);
-  }
-  if (partial) {
-    if (nchunk != blindno_lift_bwd_nchunk(Bn, N1, N2) || C * Cin + C > PPT * kBlock)
-      return (int)hipErrorInvalidValue;
-    const size_t sh = sizeof(float) * (size_t)(C + Cin) * (TP + 1);
-    lift_bwd_w_kernel<<<nchunk, kBlock, sh, st>>>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2);
-  }
-  return (int)hipGetLastError();
+  return blindno_lift_bwd_g(dx0, in, w0, d_in, partial, nchunk, 1, 0, Bn, N1, N2, Cin, C, P1, P2,
+                            stream);
 }
 
 BLINDNO_API int blindno_conv_wgrad_nchunk(int Bn, int P1, int P2) {
@@ -581,19 +665,27 @@ BLINDNO_API int blindno_conv_wgrad_nchunk(int Bn, int P1, int P2) {
   return (int)(nt < 1024 ? nt : 1024);
 }
 
-BLINDNO_API int blindno_conv_wgrad(const float* dz, const float* x, float* partial, int nchunk,
-                                   int Bn, int C, int P1, int P2, int act, void* stream) {
-  if (nchunk != blindno_conv_wgrad_nchunk(Bn, P1, P2) || C * C + C > PPT * kBlock)
+BLINDNO_API int blindno_conv_wgrad_g(const float* dz, const float* x, float* partial, int nchunk,
+                                     int G, int Bn, int C, int P1, int P2, int act, void* stream) {
+  if (G < 1 || Bn % G) return (int)hipErrorInvalidValue;
+  const int Bg = Bn / G;
+  if (nchunk != blindno_conv_wgrad_nchunk(Bg, P1, P2) || C * C + C > PPT * kBlock)
     return (int)hipErrorInvalidValue;
   const int64_t HW = (int64_t)P1 * P2;
   const int tpn = cdiv(HW, TP);
-  const int64_t ntiles = (int64_t)Bn * tpn;
+  const int64_t ntiles = (int64_t)Bg * tpn;
   const size_t sh = sizeof(float) * 2 * (size_t)C * (TP + 1);
+  const dim3 grid(nchunk, G);
   if (act)
-    conv_wgrad_kernel<1><<<nchunk, kBlock, sh, (hipStream_t)stream>>>(dz, x, partial, C, HW, tpn, ntiles);
+    conv_wgrad_kernel<1><<<grid, kBlock, sh, (hipStream_t)stream>>>(dz, x, partial, C, HW, tpn, ntiles);
   else
-    conv_wgrad_kernel<0><<<nchunk, kBlock, sh, (hipStream_t)stream>>>(dz, x, partial, C, HW, tpn, ntiles);
+    conv_wgrad_kernel<0><<<grid, kBlock, sh, (hipStream_t)stream>>>(dz, x, partial, C, HW, tpn, ntiles);
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_conv_wgrad(const float* dz, const float* x, float* partial, int nchunk,
+                                   int Bn, int C, int P1, int P2, int act, void* stream) {
+  return blindno_conv_wgrad_g(dz, x, partial, nchunk, 1, Bn, C, P1, P2, act, stream);
 }
 
 BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np,
@@ -605,6 +697,17 @@ BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nc
   return (int)hipGetLastError();
 }
 
+BLINDNO_API int blindno_project_fwd_g(const float* z, const float* w1, const float* b1,
+                                      const float* w2, const float* b2, float* out, int G,
+                                      int64_t wgs, int Bn, int C, int P1, int P2, int Ho, int Wo,
+                                      int Hd, int Cout, int ostride, int ooff, void* stream) {
+  if (Ho > P1 || Wo > P2 || C > 32 || Cout > 4 || (int64_t)Bn * Ho * Wo >= INT32_MAX ||
+      !project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
+    return (int)hipErrorInvalidValue;
+  return project_fwd_mfma(z, w1, b1, w2, b2, out, Bn, C, P1, P2, Ho, Wo, Cout, ostride, ooff, G,
+                          wgs, (hipStream_t)stream);
+}
+
 BLINDNO_API int blindno_project_fwd(const float* z, const float* w1, const float* b1,
                                     const float* w2, const float* b2, float* out, int Bn, int C,
                                     int P1, int P2, int Ho, int Wo, int Hd, int Cout,
@@ -612,8 +715,8 @@ BLINDNO_API int blindno_project_fwd(const float* z, const float* w1, const float
   if (Ho > P1 || Wo > P2 || C > 32 || Cout > 4 || (int64_t)Bn * Ho * Wo >= INT32_MAX)
     return (int)hipErrorInvalidValue;
   if (project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
-    return project_fwd_mfma(z, w1, b1, w2, b2, out, Bn, C, P1, P2, Ho, Wo, Cout, ostride, ooff,
-                            (hipStream_t)stream);
+    return project_fwd_mfma(z, w1, b1, w2, b2, out, Bn, C, P1, P2, Ho, Wo, Cout, ostride, ooff, 1,
+                            0, (hipStream_t)stream);
   const int64_t total = (int64_t)Bn * Ho * Wo;
   const dim3 g(grid_for(total, kBlock, 2048));
   hipStream_t st = (hipStream_t)stream;
@@ -637,6 +740,18 @@ BLINDNO_API int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo) {
   return project_bwd_mfma_nchunk((int64_t)Bn * Ho * Wo);
 }
 
+BLINDNO_API int blindno_project_bwd_g(const float* z, const float* w1, const float* b1,
+                                      const float* w2, const float* dout, float* dz,
+                                      float* partial, int nchunk, int G, int64_t wgs, int Bn,
+                                      int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout,
+                                      int ostride, int ooff, void* stream) {
+  if (Ho > P1 || Wo > P2 || C > 32 || Cout > 4 || !dz || !partial || nchunk < 1 ||
+      (int64_t)Bn * Ho * Wo >= INT32_MAX || !project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
+    return (int)hipErrorInvalidValue;
+  return project_bwd_mfma(z, w1, b1, w2, dout, dz, partial, nchunk, Bn, C, P1, P2, Ho, Wo, Cout,
+                          ostride, ooff, 1, G, wgs, (hipStream_t)stream);
+}
+
 BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float* b1,
                                     const float* w2, const float* dout, float* dz,
                                     float* partial, int nchunk, int Bn, int C, int P1, int P2,
@@ -649,7 +764,7 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
   const dim3 g(nchunk);
   if (project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
     return project_bwd_mfma(z, w1, b1, w2, dout, dz, partial, nchunk, Bn, C, P1, P2, Ho, Wo, Cout,
-                            ostride, ooff, dout_div, st);
+                            ostride, ooff, dout_div, 1, 0, st);
   if (Hd != 128) return (int)hipErrorInvalidValue;   // fc1 = Linear(width, 128) everywhere
   const int cm = C <= 8 ? 8 : (C <= 16 ? 16 : 32);
   const int com = Cout == 1 ? 1 : 4;

@@ -43,6 +43,17 @@ constexpr int kFwdNP4 = PROJ_FWD_NP4;
 #endif
 constexpr int kBwdNP4 = PROJ_BWD_NP4;
 
+// Grouped launches: G weight groups (two FNO heads over one field), each owning gpts
+// consecutive points (Bg samples); group g's weights sit at + g wgs and its outputs at channel
+// offset ooff + g goff of the shared output sample.
+constexpr int kMaxGroups = 2;
+struct Groups {
+  int G;
+  unsigned gpts;
+  int64_t wgs;
+  int goff;
+};
+
 struct PointMap {
   unsigned HoWo, Wo;
   int64_t HW;
@@ -141,20 +152,24 @@ template <int CK, int COM, int NP>
 __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ out, int C,
-    int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff, unsigned npts) {
+    int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff, unsigned npts, Groups gr) {
   constexpr int KS = CK / 4;
-  __shared__ ProjWeights<CK, COM> sw;
-  stage_weights<CK, COM>(sw, w1, b1, w2, C, Cout, kInvK);
+  __shared__ ProjWeights<CK, COM> sws[kMaxGroups];
+  for (int g = 0; g < gr.G; ++g)
+    stage_weights<CK, COM>(sws[g], w1 + g * gr.wgs, b1 + g * gr.wgs, w2 + g * gr.wgs, C, Cout, kInvK);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
-  float b2v[COM];
-#pragma unroll
-  for (int c = 0; c < COM; ++c) b2v[c] = c < Cout ? b2[c] : 0.f;
   const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C};
   const unsigned ngroups = (npts + 16 * NP - 1) / (16 * NP);
   for (unsigned grp = blockIdx.x * kWaves + wave; grp < ngroups; grp += gridDim.x * kWaves) {
+    // weight group of this step's points (uniform: the launcher checks group alignment)
+    const int g = gr.G > 1 ? uniform_int((int)((grp * NP * 16) / gr.gpts)) : 0;
+    const ProjWeights<CK, COM>& sw = sws[g];
+    float b2v[COM];
+#pragma unroll
+    for (int c = 0; c < COM; ++c) b2v[c] = c < Cout ? b2[g * gr.wgs + c] : 0.f;
     float az[NP][KS];
 #pragma unroll
     for (int np = 0; np < NP; ++np) load_az<KS>(z, pm, (grp * NP + np) * 16 + c16, npts, g4, az[np]);
@@ -204,7 +219,7 @@ __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
       if (c16 < 4) {
         const unsigned p = (grp * NP + np) * 16 + 4 * g4 + c16;
         if (p < npts) {
-          float* op = out + (int64_t)p * ostride + ooff;
+          float* op = out + (int64_t)(p - g * gr.gpts) * ostride + ooff + g * gr.goff;
 #pragma unroll
           for (int c = 0; c < COM; ++c) {
             float v = accs[c][0];
@@ -230,8 +245,16 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
     float* __restrict__ partial, int C, int P1, int P2, int Ho, int Wo, int Cout, int ostride,
-    int ooff, int dout_div, unsigned npts) {
+    int ooff, int dout_div, unsigned gpts, Groups gr) {
+  // blockIdx.y = weight group g: points [g gpts, (g+1) gpts), weights at + g wgs, dout sample
+  // n - g Bg at channel offset ooff + g goff, partial[blockIdx.x][g]
   constexpr int KS = CK / 4;
+  const int g = blockIdx.y;
+  w1 += g * gr.wgs;
+  b1 += g * gr.wgs;
+  w2 += g * gr.wgs;
+  const unsigned pbase = g * gpts, npts = pbase + gpts;
+  const unsigned nbase = g * (gpts / (unsigned)(Ho * Wo));
   constexpr int NV = 4 * CK;                       // dz values per lane per tile: (ch, r)
   __shared__ ProjWeights<CK, COM> sw;
   // dW1 (/ db1) accumulators in MFMA D layout.  CK == 4: v_mfma_f32_4x4x1f32, 16 blocks of
@@ -257,24 +280,25 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
 #pragma unroll
   for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
   const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C};
-  const unsigned ngroups = (npts + 16 * NP - 1) / (16 * NP);
+  const unsigned ngroups = (gpts + 16 * NP - 1) / (16 * NP);
   for (unsigned grp = blockIdx.x * kWaves + wave; grp < ngroups; grp += gridDim.x * kWaves) {
     float az[NP][KS], zb[NP][4], gv[NP][4][COM];
     int zo4[NP][4];                                 // element offsets (< 2^31, checked)
 #pragma unroll
     for (int np = 0; np < NP; ++np) {
       const unsigned tile = grp * NP + np;
-      load_az<KS>(z, pm, tile * 16 + c16, npts, g4, az[np]);
+      load_az<KS>(z, pm, pbase + tile * 16 + c16, npts, g4, az[np]);
       // this lane's 4 points (D layout rows): z column c16 (1.0 at c16 == C: db1), dout
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const unsigned p = tile * 16 + 4 * g4 + r;
+        const unsigned p = pbase + tile * 16 + 4 * g4 + r;
         const bool ok = p < npts;
         unsigned n, q;
         zo4[np][r] = (int)pm.zoff(ok ? p : 0, n, q);
         const int zc = kGW44 ? (c16 & 3) : c16;
         zb[np][r] = !ok ? 0.f : (zc < C ? z[zo4[np][r] + (int64_t)zc * pm.HW] : (zc == C ? 1.f : 0.f));
-        const float* gp = dout + ((int64_t)(n / (unsigned)dout_div) * pm.HoWo + q) * ostride + ooff;
+        const float* gp = dout + ((int64_t)((n - nbase) / (unsigned)dout_div) * pm.HoWo + q) * ostride +
+                          ooff + g * gr.goff;
 #pragma unroll
         for (int c = 0; c < COM; ++c) gv[np][r][c] = (ok && c < Cout) ? gp[c] : 0.f;
       }
@@ -371,7 +395,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
         }
       }
       const int r = c16 & 3;
-      const unsigned p = (grp * NP + np) * 16 + 4 * g4 + r;
+      const unsigned p = pbase + (grp * NP + np) * 16 + 4 * g4 + r;
       if (p < npts) {
 #pragma unroll
         for (int m = 0; m < NV / 16; ++m) {
@@ -391,7 +415,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
   }
   __syncthreads();
   const int np_ = kHd * C + kHd + Cout * kHd + Cout;
-  float* pp = partial + (int64_t)blockIdx.x * np_;
+  float* pp = partial + ((int64_t)blockIdx.x * gridDim.y + g) * np_;
   for (int e = threadIdx.x; e < np_; e += blockDim.x) {
     float v = 0.f;
     if (e < kHd * C + kHd) {
@@ -440,16 +464,20 @@ bool project_mfma_ok(int C, int Hd, int Cout, int64_t field_elems) {
 
 int project_fwd_mfma(const float* z, const float* w1, const float* b1, const float* w2,
                      const float* b2, float* out, int Bn, int C, int P1, int P2, int Ho, int Wo,
-                     int Cout, int ostride, int ooff, hipStream_t st) {
+                     int Cout, int ostride, int ooff, int G, int64_t wgs, hipStream_t st) {
+  if (G < 1 || G > kMaxGroups || Bn % G) return (int)hipErrorInvalidValue;
   const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
+  const Groups gr{G, npts / (unsigned)G, G > 1 ? wgs : 0, Cout};
   const unsigned ntiles = (npts + 15) / 16;
   unsigned blocks = (ntiles + kWaves * PF_TPW - 1) / (kWaves * PF_TPW);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-#define PF(CK_, CO_)                                                                           \
-  project_fwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kFwdNP4 : (CK_ <= 8 ? 4 : 2))><<<blocks, 256, 0, st>>>(z, w1, b1, w2, b2, out, C, P1, P2, \
-                                                            Ho, Wo, Cout, ostride, ooff, npts)
   const int ck = (C + 3) / 4 * 4;
+  const int np = ck <= 4 ? kFwdNP4 : (ck <= 8 ? 4 : 2);
+  if (G > 1 && gr.gpts % (16u * np)) return (int)hipErrorInvalidValue;   // steps within a group
+#define PF(CK_, CO_)                                                                           \
+  project_fwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kFwdNP4 : (CK_ <= 8 ? 4 : 2))><<<blocks, 256, 0, st>>>( \
+      z, w1, b1, w2, b2, out, C, P1, P2, Ho, Wo, Cout, ostride, ooff, npts, gr)
   if (Cout == 1) {
     if (ck == 4) PF(4, 1); else if (ck == 8) PF(8, 1); else if (ck == 12) PF(12, 1); else PF(16, 1);
   } else {
@@ -468,12 +496,14 @@ int project_bwd_mfma_nchunk(int64_t npts) {
 int project_bwd_mfma(const float* z, const float* w1, const float* b1, const float* w2,
                      const float* dout, float* dz, float* partial, int nchunk, int Bn, int C,
                      int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff,
-                     int dout_div, hipStream_t st) {
-  const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
+                     int dout_div, int G, int64_t wgs, hipStream_t st) {
+  if (G < 1 || G > kMaxGroups || Bn % G) return (int)hipErrorInvalidValue;
+  const unsigned gpts = (unsigned)((int64_t)(Bn / G) * Ho * Wo);
+  const Groups gr{G, gpts, G > 1 ? wgs : 0, Cout};
+  const dim3 grid(nchunk, G);
 #define PB(CK_, CO_)                                                                          \
-  project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kBwdNP4 : 1)><<<nchunk, 256, 0, st>>>(z, w1, b1, w2, dout, dz, partial, \
-                                                            C, P1, P2, Ho, Wo, Cout, ostride,  \
-                                                            ooff, dout_div, npts)
+  project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kBwdNP4 : 1)><<<grid, 256, 0, st>>>(            \
+      z, w1, b1, w2, dout, dz, partial, C, P1, P2, Ho, Wo, Cout, ostride, ooff, dout_div, gpts, gr)
   const int ck = (C + 3) / 4 * 4;
   if (Cout == 1) {
     if (ck == 4) PB(4, 1); else if (ck == 8) PB(8, 1); else if (ck == 12) PB(12, 1); else PB(16, 1);

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int C, int P1, int P2,
-    int m2, int TPW, BagLift bl) {
+    int m2, int TPW, BagLift bl, int Bg, int64_t wgs) {
   extern __shared__ float sTB[];                    // [KS][NT][64] when LDSB
   const int KS = (m2 + 1) >> 1;
   const int NT = (P2 + 15) >> 4;
@@ -96,6 +96,12 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     const bool rok = ro < nrows;
     const int n = rok ? ro / P1 : 0, h = rok ? ro - (ro / P1) * P1 : 0;
     const int64_t rbase = (int64_t)n * C * HW + (int64_t)h * P2;
+    // weight group of this quad of rows (two heads batched over one launch: wc / bc at + g wgs;
+    // wave-uniform -- the launcher requires P1 % 4 == 0 when grouped -- so the weights stay
+    // scalar loads)
+    const int64_t goff = wgs ? (int64_t)uniform_int((4 * quad) / P1 / Bg) * wgs : 0;
+    const float* wcg = wc + goff;
+    const float* bcg = bc + goff;
     const float* urow = nullptr;                    // LIFT: snapshot row / grid row
     const float* grow = nullptr;
     if (LIFT && rok && h < bl.N1) {
@@ -149,10 +155,10 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
           for (int r = 0; r < 4; ++r) {
             const int o = c0 + r;
             if (o >= C) continue;
-            float v = d[r] + bc[o];
+            float v = d[r] + bcg[o];
 #pragma unroll
             for (int i = 0; i < CM; ++i)
-              if (i < C) v = fmaf(wc[o * C + i], xv[i], v);
+              if (i < C) v = fmaf(wcg[o * C + i], xv[i], v);
             out[rbase + o * HW + w] = v;
           }
         } else {
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
             const int i = c0 + r;
             float gi = d[r];
 #pragma unroll
-            for (int o = 0; o < CM; ++o) gi = fmaf((o < C && i < C) ? wc[o * C + i] : 0.f, fv[o], gi);
+            for (int o = 0; o < CM; ++o) gi = fmaf((o < C && i < C) ? wcg[o * C + i] : 0.f, fv[o], gi);
             xa[r] = sv[r];
             if (ACT) {
               float a, dg;
@@ -259,7 +265,10 @@ RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   // reuses it over several items (otherwise every MFMA step reads it from L1/L2)
   const int b = (g.nitems + kW - 1) / kW;
   const size_t tbytes = sizeof(float) * (size_t)KS * NT * 64;
-  g.ldsb = tbytes <= 48 * 1024 && g.nitems >= 8192;
+  // staging pays when a workgroup's items read the table at least twice over (each item reads
+  // TPW of its NT column tiles)
+  const int64_t items_per_block = (g.nitems + 1023) / 1024;
+  g.ldsb = tbytes <= 48 * 1024 && g.nitems >= 8192 && items_per_block * tpw >= 2 * NT;
   const int cap = g.ldsb ? 1024 : 2048;
   g.blocks = b < cap ? b : cap;
   g.lds = g.ldsb ? tbytes : 0;
@@ -269,7 +278,11 @@ RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
 template <int MODE, int ACT, int WG, int LIFT = 0>
 int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
                   const float* bc, float* out, const float* TB, float* partial, int nblocks,
-                  int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{}) {
+                  int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{},
+                  int G = 1, int64_t wgs = 0) {
+  if (G < 1 || Bn % G || (G > 1 && (WG || LIFT || P1 % 4))) return (int)hipErrorInvalidValue;
+  const int Bg = Bn / G;
+  if (G == 1) wgs = 0;
   if (Bn <= 0 || C <= 0 || C > 32 || m2 <= 0 || P2 <= 0) return (int)hipErrorInvalidValue;
   if (WG && C > 4) return (int)hipErrorInvalidValue;
   const int64_t zel = (int64_t)Bn * P1 * m2 * C * 2, fel = (int64_t)Bn * C * P1 * P2;
@@ -288,10 +301,10 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   do {                                                                                       \
     if (g.ldsb)                                                                              \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 1, LIFT><<<nblocks, 256, sh, st>>>(        \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl);                \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs);       \
     else                                                                                     \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 0, LIFT><<<nblocks, 256, sh, st>>>(        \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl);                \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs);       \
   } while (0)
 #define RI_K(CM_) \
   if (ks <= 8) RI(CM_, 8); else if (ks <= 16) RI(CM_, 16); else RI(CM_, 24);
@@ -309,18 +322,40 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
 
 }  // namespace
 
-BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float* wc,
-                                    const float* bc, float* z, const float* tb, int Bn, int C,
-                                    int P1, int P2, int m2, int act, void* stream) {
+BLINDNO_API int blindno_rowidft_epi_g(const float* Z, const float* x, const float* wc,
+                                      const float* bc, float* z, const float* tb, int G,
+                                      int64_t wgs, int Bn, int C, int P1, int P2, int m2, int act,
+                                      void* stream) {
   const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
   hipStream_t st = (hipStream_t)stream;
   if (act)
-    return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
-  return rowinv_launch<0, 0, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
+    return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                  BagLift{}, G, wgs);
+  return rowinv_launch<0, 0, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                BagLift{}, G, wgs);
+}
+
+BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float* wc,
+                                    const float* bc, float* z, const float* tb, int Bn, int C,
+                                    int P1, int P2, int m2, int act, void* stream) {
+  return blindno_rowidft_epi_g(Z, x, wc, bc, z, tb, 1, 0, Bn, C, P1, P2, m2, act, stream);
 }
 
 BLINDNO_API int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2) {
   return C <= 4 ? rowinv_geom(Bn, C, P1, P2, m2).blocks : 0;
+}
+
+BLINDNO_API int blindno_rowidft_bwd_g(const float* Gs, const float* dz, const float* wc,
+                                      const float* xsrc, float* dx, const float* tb, int G,
+                                      int64_t wgs, int Bn, int C, int P1, int P2, int m2, int act,
+                                      void* stream) {
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  hipStream_t st = (hipStream_t)stream;
+  if (act)
+    return rowinv_launch<1, 1, 0>(Gs, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2,
+                                  st, BagLift{}, G, wgs);
+  return rowinv_launch<1, 0, 0>(Gs, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2,
+                                st, BagLift{}, G, wgs);
 }
 
 BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc,

@@ -234,7 +234,9 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
                                                          float2* __restrict__ Xs,
                                                          float2* __restrict__ Y, int npairs,
                                                          int Ci, int Co, int P1, int m1, int m2,
-                                                         int P2, int G, int vec) {
+                                                         int P2, int G, int vec, int Bg,
+                                                         int64_t wtgs) {
+  // grouped launches: samples n of weight group n / Bg use Wt + (n / Bg) wtgs (in floats)
   extern __shared__ float2 sX[];                  // [G Cin][K1p + 1]
   const int K1 = kept_rows_count(m1, P1);
   const int Jt = (K1 + 15) >> 4, K1p = Jt * 16, LDX = K1p + 1;
@@ -296,7 +298,10 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
     const int k = (q0 + p) % m2;
     float re = 0.f, im = 0.f;
     if (j < K1) {
-      const float2* wj = Wt + ((int64_t)k * K1 + j) * Ci * Co;
+      const float2* wg = wtgs ? reinterpret_cast<const float2*>(
+                                    reinterpret_cast<const float*>(Wt) + ((q0 + p) / m2 / Bg) * wtgs)
+                              : Wt;
+      const float2* wj = wg + ((int64_t)k * K1 + j) * Ci * Co;
       const float2* xp = sX + p * Cin * LDX + j;
 #pragma unroll 4
       for (int c = 0; c < Cin; ++c) {
@@ -369,9 +374,11 @@ __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restr
                                                            int Ci, int Co, int K1, int m2) {
   // blockIdx.y = sample slice: out[y][idx] = sum over this slice's samples (partials when
   // gridDim.y > 1, reduced in fixed order afterwards)
+  // blockIdx.z = weight group: its Bn / gridDim.z samples only; out[(y G + g)][idx]
   const int total = m2 * K1 * Ci * Co;
-  const int ns = (Bn + gridDim.y - 1) / gridDim.y;
-  const int n0 = blockIdx.y * ns, n1 = min(Bn, n0 + ns);
+  const int Bg = Bn / gridDim.z, grp = blockIdx.z;
+  const int ns = (Bg + gridDim.y - 1) / gridDim.y;
+  const int n0 = grp * Bg + blockIdx.y * ns, n1 = min(grp * Bg + Bg, n0 + ns);
   const int sX = m2 * Ci * K1, sG = m2 * Co * K1;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += gridDim.x * blockDim.x) {
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restr
       re = fmaf(a.x, g.x, fmaf(a.y, g.y, re));
       im = fmaf(a.x, g.y, fmaf(-a.y, g.x, im));
     }
-    out[(int64_t)blockIdx.y * total + idx] = make_float2(re, im);
+    out[((int64_t)blockIdx.y * gridDim.z + grp) * total + idx] = make_float2(re, im);
   }
 }
 
@@ -595,11 +602,15 @@ BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const fl
   return (int)hipGetLastError();
 }
 
-BLINDNO_API int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
-                                const float* FB, const float* GB, int Bn, int Ci, int Co, int P1,
-                                int m1, int m2, int P2, int dir, void* stream) {
-  if (Bn <= 0 || m1 <= 0 || m1 > P1 || m2 <= 0 || m2 > P2 / 2 + 1 || (dir != 0 && dir != 1))
+BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
+                                  const float* FB, const float* GB, int Gw, int64_t wtgs, int Bn,
+                                  int Ci, int Co, int P1, int m1, int m2, int P2, int dir,
+                                  void* stream) {
+  if (Bn <= 0 || m1 <= 0 || m1 > P1 || m2 <= 0 || m2 > P2 / 2 + 1 || (dir != 0 && dir != 1) ||
+      Gw < 1 || Bn % Gw)
     return (int)hipErrorInvalidValue;
+  const int Bg = Bn / Gw;
+  if (Gw == 1) wtgs = 0;
   const int K1 = kept_rows_count(m1, P1);
   const int Jt = (K1 + 15) / 16, K1p = Jt * 16;
   const int cin = dir == 0 ? Ci : Co, cout = dir == 0 ? Co : Ci;
@@ -619,11 +630,13 @@ BLINDNO_API int blindno_colpass(const float* At, const float* Wt, float* Xs, flo
   if (dir == 0)
     coldft_mix_kernel<0><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,
                                               (const f32x4*)FB, (float2*)Xs, (float2*)Y,
-                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec);
+                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg,
+                                              wtgs);
   else
     coldft_mix_kernel<1><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,
                                               (const f32x4*)FB, (float2*)Xs, (float2*)Y,
-                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec);
+                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg,
+                                              wtgs);
   int e = (int)hipGetLastError();
   if (e) return e;
   const int Ht = (P1 + 15) / 16;
@@ -632,6 +645,12 @@ BLINDNO_API int blindno_colpass(const float* At, const float* Wt, float* Xs, flo
   colidft_kernel<<<g2, 256, 0, st>>>((const float2*)Y, (const f32x4*)GB, (float2*)Z, cout, P1, m1,
                                      m2);
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
+                                const float* FB, const float* GB, int Bn, int Ci, int Co, int P1,
+                                int m1, int m2, int P2, int dir, void* stream) {
+  return blindno_colpass_g(At, Wt, Xs, Y, Z, FB, GB, 1, 0, Bn, Ci, Co, P1, m1, m2, P2, dir, stream);
 }
 
 BLINDNO_API int blindno_mix_wgrad_nsplit(int Bn, int Ci, int Co, int K1, int m2) {
@@ -644,23 +663,29 @@ BLINDNO_API int blindno_mix_wgrad_nsplit(int Bn, int Ci, int Co, int K1, int m2)
   return (int)(ns > 1024 ? 1024 : ns);
 }
 
-BLINDNO_API int blindno_mix_wgrad(const float* X, const float* G, float* dWt, float* partial,
-                                  int nsplit, int Bn, int Ci, int Co, int K1, int m2,
-                                  void* stream) {
+BLINDNO_API int blindno_mix_wgrad_g(const float* X, const float* G, float* dWt, float* partial,
+                                    int nsplit, int Gw, int Bn, int Ci, int Co, int K1, int m2,
+                                    void* stream) {
   const int64_t total = (int64_t)m2 * K1 * Ci * Co;
-  if (total >= INT32_MAX / 2 || nsplit < 1 || (nsplit > 1 && !partial))
+  if (total >= INT32_MAX / 2 || nsplit < 1 || (nsplit > 1 && !partial) || Gw < 1 || Bn % Gw)
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 g((unsigned)cdiv(total, kBlock), nsplit);
+  const dim3 g((unsigned)cdiv(total, kBlock), nsplit, Gw);
   mix_wgrad_kernel<<<g, kBlock, 0, st>>>((const float2*)X, (const float2*)G,
                                          (float2*)(nsplit > 1 ? partial : dWt), Bn, Ci, Co, K1,
                                          m2);
   if (nsplit > 1) {
     const int e = (int)hipGetLastError();
     if (e) return e;
-    return blindno_reduce_partials(partial, dWt, nsplit, (int)(2 * total), stream);
+    return blindno_reduce_partials(partial, dWt, nsplit, (int)(2 * total * Gw), stream);
   }
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_mix_wgrad(const float* X, const float* G, float* dWt, float* partial,
+                                  int nsplit, int Bn, int Ci, int Co, int K1, int m2,
+                                  void* stream) {
+  return blindno_mix_wgrad_g(X, G, dWt, partial, nsplit, 1, Bn, Ci, Co, K1, m2, stream);
 }
 
 BLINDNO_API int blindno_mix1d(const float* At, const float* Wt, float* Xs, float* Z, int Bn,

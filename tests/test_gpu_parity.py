@@ -240,3 +240,34 @@ def test_niofp2d_fno_fused_encoder(case, heads, train):
             assert e <= GRAD_TOL, (k, e)
             n += 1
     assert n > 20
+
+
+@pytest.mark.parametrize("width,modes,N,B", [(12, 16, 64, 3), (6, 5, 16, 2)])
+def test_head_pair_grouped_matches_separate_heads(width, modes, N, B):
+    """The two heads batched into one chain of grouped launches (ops.fno_forward_grouped)
+    against the same heads run one after the other through ops.FNOFn (tolerance: the
+    reduction order of the weight gradients differs)."""
+    from blindno import FNO2d, ops
+    torch.manual_seed(21)
+    heads = [FNO2d(modes, width, 3, width, 1).cuda() for _ in range(2)]
+    h = torch.randn(B, N, N, width, device="cuda", requires_grad=True)
+    side = torch.cuda.Stream()
+    from blindno.fno import fno_params
+    p0, p1 = fno_params(heads[0], 2), fno_params(heads[1], 2)
+    assert ops.grouped_ok(heads[0].meta(width), h, [p0, p1])
+    out = ops.HeadPairFn.apply(heads[0].meta(width), heads[1].meta(width), len(p0), side, h, *p0, *p1)
+    cot = torch.randn_like(out)
+    (out * cot).sum().backward()
+    got = [p.grad.clone() for hd in heads for p in hd.parameters()]
+    gh = h.grad.clone()
+    for hd in heads:
+        for p in hd.parameters():
+            p.grad = None
+    h.grad = None
+    ref = torch.cat([heads[0](h), heads[1](h)], dim=-1)
+    assert rel_l2(out.detach().cpu().numpy(), ref.detach().cpu().numpy()) <= 1e-6
+    (ref * cot).sum().backward()
+    want = [p.grad for hd in heads for p in hd.parameters()]
+    for a, b in zip(got, want):
+        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-5
+    assert rel_l2(gh.cpu().numpy(), h.grad.cpu().numpy()) <= 1e-6
