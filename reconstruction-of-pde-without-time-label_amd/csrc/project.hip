@@ -80,7 +80,7 @@ __device__ __forceinline__ float sum16(float v) {
 constexpr float kK = 0.84932180028801904f;        // sqrt(log2(e) / 2)
 constexpr float kInvK = 1.1774100225154747f;
 constexpr float kT = 0.27273748087922245f;        // A&S p / (sqrt2 k)
-constexpr float kPdfK = 0.46971863934982566f;     // 1 / (sqrt(2 pi) k)
+// kp = 1 / (sqrt(2 pi) k) = 0.46971863934982566 (folded into norm_cdf_pair_pdf)
 
 // Two GELUs per lane-instruction: the polynomial / product steps as packed fp32 (v_pk_fma_f32,
 // v_pk_mul_f32 on <2 x float>); the transcendentals, |hk| (a free VOP3 source modifier on the
@@ -106,6 +106,24 @@ __device__ __forceinline__ f32x2 norm_cdf_pair(f32x2 hk, f32x2& e) {
   q = pk_fma(t, q, splat2(-0.142248368f));
   q = pk_fma(t, q, splat2(0.127414796f));
   const f32x2 m = pk_fma(-(q * t), e, splat2(0.5f));          // 1/2 - half
+  const f32x2 sgn = {copysignf(m.x, hk.x), copysignf(m.y, hk.y)};
+  return sgn + splat2(0.5f);
+}
+
+// Backward variant: Phi(h) and ep = phi_k(h) = kp e^{-h^2/2} (kp = 1/(sqrt(2 pi) k)), so that
+// GELU'(h) = Phi + hk ep is one fma: the exp argument carries log2(kp) and the polynomial
+// coefficients carry 1/kp (half = q' t ep).
+constexpr float kLog2Kp = -1.0901312512086083f;
+__device__ __forceinline__ f32x2 norm_cdf_pair_pdf(f32x2 hk, f32x2& ep) {
+  const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(hk.x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk.y), kT, 1.0f))};
+  const f32x2 ea = pk_fma(-hk, hk, splat2(kLog2Kp));
+  ep = (f32x2){__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  f32x2 q = pk_fma(t, splat2(1.129831073415752f), splat2(-1.5468324069611348f));
+  q = pk_fma(t, q, splat2(1.513048048260859f));
+  q = pk_fma(t, q, splat2(-0.3028373926078324f));
+  q = pk_fma(t, q, splat2(0.27125769625911544f));
+  const f32x2 m = pk_fma(-(q * t), ep, splat2(0.5f));         // 1/2 - half
   const f32x2 sgn = {copysignf(m.x, hk.x), copysignf(m.y, hk.y)};
   return sgn + splat2(0.5f);
 }
@@ -262,6 +280,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
   // c16 & 3, K = one point of group g4 per instruction; db1 then sums on the VALU (sgb1).
   // CK > 4: v_mfma_f32_16x16x4f32 against [Z^T | 1] (column C = db1).
   constexpr bool kGW44 = CK == 4;
+  constexpr bool kFoldW2 = COM == 1;
   __shared__ f32x4 sgw1[kWaves][kNT][64];
   __shared__ float sgb1[kWaves][kNT][64];
   __shared__ float sgw2[kWaves][kNT][COM][64];     // dW2 accumulators (lane = hidden c16)
@@ -318,10 +337,13 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
       float bw[KS], wr[CK];
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) bw[kk] = sw.w1[j][4 * kk + g4];
+      // Cout == 1: W1 rows pre-multiplied by w2_j, so dz = (W1 w2)^T (gout GELU') with no
+      // per-value w2 product; dW1 / db1 take the w2_j factor at the fold
+      const float w2f = kFoldW2 ? sw.w2[0][j] : 1.0f;
 #pragma unroll
       for (int i = 0; i < CK; i += 4) {
         const float4 v = *reinterpret_cast<const float4*>(&sw.w1[j][i]);
-        wr[i] = v.x; wr[i + 1] = v.y; wr[i + 2] = v.z; wr[i + 3] = v.w;
+        wr[i] = v.x * w2f; wr[i + 1] = v.y * w2f; wr[i + 2] = v.z * w2f; wr[i + 3] = v.w * w2f;
       }
       const float bb = sw.b1[j];
       float w2v[COM];
@@ -339,23 +361,27 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x4f32(az[np][kk], bw[kk], d, 0, 0, 0);
         const f32x2 h01 = {d[0], d[1]}, h23 = {d[2], d[3]};
-        f32x2 e01, e23;
-        const f32x2 cdf01 = norm_cdf_pair(h01, e01), cdf23 = norm_cdf_pair(h23, e23);
+        f32x2 ep01, ep23;
+        const f32x2 cdf01 = norm_cdf_pair_pdf(h01, ep01), cdf23 = norm_cdf_pair_pdf(h23, ep23);
         f32x2 da01 = {0.f, 0.f}, da23 = {0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < COM; ++c) {
-          const f32x2 wv = splat2(w2v[c]);
           const f32x2 g01v = {gv[np][0][c], gv[np][1][c]}, g23v = {gv[np][2][c], gv[np][3][c]};
-          da01 = pk_fma(wv, g01v, da01);
-          da23 = pk_fma(wv, g23v, da23);
+          if constexpr (kFoldW2) {
+            da01 = g01v;
+            da23 = g23v;
+          } else {
+            const f32x2 wv = splat2(w2v[c]);
+            da01 = pk_fma(wv, g01v, da01);
+            da23 = pk_fma(wv, g23v, da23);
+          }
           // k dW2 (scaled at the fold), pair accumulators
           gw2[c] = pk_fma(g01v, h01 * cdf01, gw2[c]);
           gw2[c] = pk_fma(g23v, h23 * cdf23, gw2[c]);
         }
-        // GELU' = Phi + h phi
-        const f32x2 kp = splat2(kPdfK);
-        const f32x2 dh01 = da01 * pk_fma(h01 * kp, e01, cdf01);
-        const f32x2 dh23 = da23 * pk_fma(h23 * kp, e23, cdf23);
+        // GELU' = Phi + h phi  (dh / w2_j when folded)
+        const f32x2 dh01 = da01 * pk_fma(h01, ep01, cdf01);
+        const f32x2 dh23 = da23 * pk_fma(h23, ep23, cdf23);
         const float dh[4] = {dh01.x, dh01.y, dh23.x, dh23.y};
 #pragma unroll
         for (int i = 0; i < CK; ++i) {                                 // k dz (scaled at the store)
@@ -437,6 +463,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v += sgw1[w][t][ln][r];
       }
+      if (kFoldW2) v *= sw.w2[0][j];
     } else if (e < kHd * C + kHd + Cout * kHd) {
       const int q = e - kHd * C - kHd, c = q / kHd, j = q % kHd;
       const int t = j >> 4, cl = j & 15;
