@@ -31,6 +31,9 @@ def draw_bag(T: int):
 
 
 def _select(module, x, bag_idx):
+    if torch.is_tensor(bag_idx) and bag_idx.is_cuda:
+        # device-resident index list (graph replays): gather on the device
+        return x.index_select(1, bag_idx), bag_idx.numel()
     if bag_idx is not None:
         idx = np.asarray(bag_idx)
         return x[:, torch.as_tensor(idx, device=x.device)], len(idx)
