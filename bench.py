@@ -145,7 +145,9 @@ def main():
         graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc)
         torch.index_select(X, 0, order[:B], out=xb)
         torch.index_select(Y, 0, order[:B], out=yb)
-        for L in range(50, T):
+        # keys: the bag size L, or with deduplicated bags the number of distinct snapshots
+        # (U <= L; a randint(50, T) draw with replacement from T has U >= ~0.3 T in practice)
+        for L in range(min(50, T // 5) if graphed.dedup else 50, T):
             graphed.capture(L)
         torch.cuda.synchronize()
 

@@ -76,6 +76,12 @@ int blindno_project_bwd(const float* z, const float* w1, const float* b1, const 
                         int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout,
                         int ostride, int ooff, int dout_div, blindno_stream_t stream);
 int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo);
+/* blindno_project_bwd (matrix-core path) with dout of sample n scaled by lscale[n % dout_div]
+ * (the multiplicity weights of a deduplicated bag). */
+int blindno_project_bwd_w(const float* z, const float* w1, const float* b1, const float* w2,
+                          const float* dout, const float* lscale, float* dz, float* partial,
+                          int nchunk, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd,
+                          int Cout, int ostride, int ooff, int dout_div, blindno_stream_t stream);
 
 /* --- truncated spectral transforms --------------------------------------------------- */
 
@@ -199,6 +205,11 @@ int blindno_pack_w1d(const float* w, float* Wt, int Ci, int Co, int m, int dir,
 int blindno_bagmean_fwd(const float* u, const float* grid, const float* w, const float* bias,
                         float* y, int B, int L, int S, int d, int width,
                         blindno_stream_t stream);
+/* As blindno_bagmean_fwd with per-snapshot weights lw (L) replacing 1/L: the bag of a step
+ * given as its unique snapshots with multiplicities, lw[l] = count_l / L_drawn. */
+int blindno_bagmean_fwd_w(const float* u, const float* grid, const float* w, const float* bias,
+                          const float* lw, float* y, int B, int L, int S, int d, int width,
+                          blindno_stream_t stream);
 /* s[b,s] = sum_c (W[c,d]/L) dy[b,s,c]   (the gradient of every u[b,l,s]). */
 int blindno_bagmean_bwd(const float* dy, const float* w, float* s, int B, int S, int d,
                         int width, int L, blindno_stream_t stream);

@@ -59,6 +59,8 @@ SIGNATURES = {
     "blindno_rowidft_epi_g": "ppppppiliiiiiis",
     "blindno_rowidft_bwd_g": "ppppppiliiiiiis",
     "blindno_conv_wgrad_g": "pppiiiiiiis",
+    "blindno_bagmean_fwd_w": "pppppp" + "iiiii" + "s",
+    "blindno_project_bwd_w": "pppppppp" + "i" + "iiiiiiiiiii" + "s",
     "blindno_bn_act_nslices": "iii",
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",

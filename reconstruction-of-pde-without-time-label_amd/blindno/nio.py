@@ -47,6 +47,20 @@ _SIDE = {}
 
 
 HEAD_STREAMS = True     # fork the two heads over two streams (ops.HeadPairFn)
+DEDUP_BAGS = True       # run the snapshot encoder once per distinct snapshot of a bag
+
+
+def dedup_bag(idx):
+    """(unique indices int32, multiplicity / L float32) of a with-replacement bag draw, or
+    (idx, None) when every index is distinct (or DEDUP_BAGS is off).  The encoder output of a
+    repeated snapshot is identical, so the bag mean sum_l u_l = sum_u count_u u_u."""
+    idx = np.asarray(idx, dtype=np.int32)
+    if not DEDUP_BAGS:
+        return idx, None
+    uniq, counts = np.unique(idx, return_counts=True)
+    if len(uniq) == len(idx):
+        return idx, None
+    return uniq.astype(np.int32), (counts / float(len(idx))).astype(np.float32)
 
 
 def _run_heads(module, h):
@@ -99,6 +113,8 @@ class NIOFP2D_FNO(nn.Module):
             setattr(self, name, FNO2d(modes=modes, width=width, n_layers=self.fno_layers,
                                       input_dim=width, output_dim=1))
 
+    accepts_dedup_bag = True    # forward(bag_idx=(unique idx, weights)) on the fused path
+
     def _fused_ok(self, x, grid):
         return (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and
                 grid.dtype == torch.float32 and tuple(grid.shape) == (x.shape[2], x.shape[3], 2) and
@@ -112,22 +128,26 @@ class NIOFP2D_FNO(nn.Module):
         (ops.BagEncoderFn: snapshots read from x through the bag's indices); otherwise as the
         generic composition below (same numerics, gradients for x and grid)."""
         if self._fused_ok(x, grid):
-            if torch.is_tensor(bag_idx) and bag_idx.is_cuda and bag_idx.dtype == torch.int32:
-                # device-resident bag indices (graph-captured training steps, train.GraphedBagStep)
-                idx_t = bag_idx
-                fno = self.FNO_input
-                h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, grid, self.fc0.weight.data,
-                                           self.fc0.bias.data, *fno_params(fno, 2))
-                return _run_heads(self, h)
-            if bag_idx is not None:
-                idx = np.asarray(bag_idx)
-            elif self.training:
-                _, idx = draw_bag(x.shape[1])
-            else:
-                idx = np.arange(x.shape[1])
-            idx_t = torch.as_tensor(np.asarray(idx, dtype=np.int32), device=x.device)
             fno = self.FNO_input
-            h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, grid, self.fc0.weight.data,
+            lw = None
+            if isinstance(bag_idx, tuple):
+                # device-resident deduplicated bag (train.GraphedBagStep): unique indices and
+                # multiplicity weights
+                idx_t, lw = bag_idx
+            elif torch.is_tensor(bag_idx) and bag_idx.is_cuda and bag_idx.dtype == torch.int32:
+                idx_t = bag_idx                  # device-resident bag indices
+            else:
+                if bag_idx is not None:
+                    idx = np.asarray(bag_idx)
+                elif self.training:
+                    _, idx = draw_bag(x.shape[1])
+                else:
+                    idx = np.arange(x.shape[1])
+                idx, w = dedup_bag(idx)
+                idx_t = torch.as_tensor(idx, device=x.device)
+                if w is not None:
+                    lw = torch.as_tensor(w, device=x.device)
+            h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, lw, grid, self.fc0.weight.data,
                                        self.fc0.bias.data, *fno_params(fno, 2))
             return _run_heads(self, h)
         x, L = _select(self, x, bag_idx)

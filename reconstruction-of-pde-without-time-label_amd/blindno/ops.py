@@ -751,10 +751,16 @@ class BagEncoderFn(torch.autograd.Function):
     row DFT and recomputed in the first layer's epilogue / adjoint, which also reduces fc0's
     gradient).  The bag mean's gradient reaches the projection as a per-bag field (dout_div =
     L) instead of an L-fold broadcast copy.  No gradient flows to X or grid (the caller uses
-    the generic path when they require one)."""
+    the generic path when they require one).
+
+    ``lw`` (optional, device float (L,)): the bag is given as its UNIQUE snapshots idx_t with
+    weights lw = multiplicity / L_drawn (the draw is with replacement, so ~30% of a bag repeats
+    a snapshot whose FNO_input output is identical): every encoder kernel runs on the unique
+    snapshots only, the bag mean weights them by lw, and the projection backward scales the
+    per-bag gradient by lw (exact up to fp32 summation order)."""
 
     @staticmethod
-    def forward(ctx, meta, X, idx_t, grid, bw, bb, *prm):
+    def forward(ctx, meta, X, idx_t, lw, grid, bw, bb, *prm):
         require_device(X, grid, *prm)
         X, grid = _c(X), _c(grid)
         prm = [_c(p) for p in prm]
@@ -801,9 +807,10 @@ class BagEncoderFn(torch.autograd.Function):
         S = Ho * Wo
         width = bw.shape[0]
         h = _empty(B, S, width, like=X)
-        call("blindno_bagmean_fwd", ptr(u), ptr(grid), ptr(bw), ptr(bb), ptr(h), B, L, S, 2, width,
-             stream_ptr())
+        call("blindno_bagmean_fwd_w", ptr(u), ptr(grid), ptr(bw), ptr(bb), ptr(lw), ptr(h), B, L, S, 2,
+             width, stream_ptr())
         ctx.meta, ctx.n, ctx.dims = meta, n, (B, T, L, N1, N2, C, P1, P2, Ho, Wo, Hd, Cout, width)
+        ctx.lw = lw
         ctx.save_for_backward(X, idx_t, grid, bw, *Xs, *Wts, *zs, *prm)
         return h.view(B, N1, N2, width)
 
@@ -820,7 +827,9 @@ class BagEncoderFn(torch.autograd.Function):
         grads = [None] * len(prm)
         # bag mean: every snapshot of bag b receives the same gradient s[b]
         sgr = _empty(B, S, like=gh)
-        call("blindno_bagmean_bwd", ptr(gh), ptr(bw), ptr(sgr), B, S, 2, width, L, stream_ptr())
+        lw = ctx.lw
+        call("blindno_bagmean_bwd", ptr(gh), ptr(bw), ptr(sgr), B, S, 2, width, 1 if lw is not None else L,
+             stream_ptr())
         # projection (dout read per bag: dout_div = L)
         off_fc1 = 2 + 4 * n
         fc1w, fc1b, fc2w = prm[off_fc1:off_fc1 + 3]
@@ -828,8 +837,12 @@ class BagEncoderFn(torch.autograd.Function):
         np_p = Hd * C + Hd + Cout * Hd + Cout
         nchunk = query("blindno_project_bwd_nchunk", Bn, Ho, Wo)
         partial = _empty(nchunk, np_p, like=gh)
-        call("blindno_project_bwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(sgr), ptr(dz),
-             ptr(partial), nchunk, Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, L, stream_ptr())
+        if lw is not None:
+            call("blindno_project_bwd_w", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(sgr), ptr(lw),
+                 ptr(dz), ptr(partial), nchunk, Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, L, stream_ptr())
+        else:
+            call("blindno_project_bwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(sgr), ptr(dz),
+                 ptr(partial), nchunk, Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, L, stream_ptr())
         gp = reduce_partials(partial, nchunk, np_p)
         o = 0
         grads[off_fc1] = gp[o:o + Hd * C].view(Hd, C); o += Hd * C
@@ -858,8 +871,9 @@ class BagEncoderFn(torch.autograd.Function):
                 grads[off + 3] = g[C * C:C * C + C]
                 grads[0] = g[C * C + C:C * C + 4 * C].view(C, 3)
                 grads[1] = g[C * C + 4 * C:]
-        grads = [gr if ctx.needs_input_grad[6 + i] else None for i, gr in enumerate(grads)]
-        return (None, None, None, None, None, None, *grads)
+        ctx.lw = None
+        grads = [gr if ctx.needs_input_grad[7 + i] else None for i, gr in enumerate(grads)]
+        return (None, None, None, None, None, None, None, *grads)
 
 
 # ---------------------------------------------------------------------------- bag mean

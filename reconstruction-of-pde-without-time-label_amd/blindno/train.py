@@ -166,19 +166,26 @@ class GraphedBagStep:
 
     def __init__(self, model, loss_fn, opt: "FlatAdam", dp: "DataParallel", x, y, grid,
                  loss_acc: Optional[torch.Tensor] = None):
+        from . import nio
         self.model, self.loss_fn, self.opt, self.dp = model, loss_fn, opt, dp
         self.x, self.y, self.grid = x, y, grid
         self.loss_acc = loss_acc
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs = {}
         self.idx = {}
+        self.lw = {}
         self.T = x.shape[1]
+        # deduplicated bags (NIOFP2D_FNO's fused encoder): graphs keyed by the number U of
+        # distinct snapshots, fed the unique indices and multiplicity weights
+        self.dedup = bool(getattr(model, "accepts_dedup_bag", False)) and nio.DEDUP_BAGS
         self._ring = [torch.empty(self.T, dtype=torch.int32).pin_memory() for _ in range(4)]
+        self._ringw = [torch.empty(self.T, dtype=torch.float32).pin_memory() for _ in range(4)]
         self._ev = [None] * len(self._ring)
         self._k = 0
 
     def _body(self, L):
-        out = self.model(self.x, self.grid, bag_idx=self.idx[L])
+        bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
+        out = self.model(self.x, self.grid, bag_idx=bag)
         loss = self.loss_fn(out, self.y)
         loss.backward()
         self.opt.gather_grads()
@@ -189,6 +196,7 @@ class GraphedBagStep:
         if L in self.graphs:
             return
         self.idx[L] = torch.zeros(L, dtype=torch.int32, device=self.x.device)
+        self.lw[L] = torch.zeros(L, dtype=torch.float32, device=self.x.device)
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                 # eager warm-up: caches, lazy init
@@ -203,6 +211,13 @@ class GraphedBagStep:
 
     def step(self, idx) -> None:
         idx = np.asarray(idx, dtype=np.int32)
+        w = None
+        if self.dedup:
+            from .nio import dedup_bag
+            n_drawn = len(idx)
+            idx, w = dedup_bag(idx)
+            if w is None:
+                w = np.full(len(idx), 1.0 / n_drawn, dtype=np.float32)
         L = len(idx)
         if L not in self.graphs:
             self.capture(L)
@@ -213,6 +228,10 @@ class GraphedBagStep:
         buf = self._ring[k]
         buf[:L].numpy()[:] = idx
         self.idx[L].copy_(buf[:L], non_blocking=True)
+        if w is not None:
+            bw = self._ringw[k]
+            bw[:L].numpy()[:] = w
+            self.lw[L].copy_(bw[:L], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._ev[k] = ev

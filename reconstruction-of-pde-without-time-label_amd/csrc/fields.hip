@@ -477,16 +477,23 @@ __global__ __launch_bounds__(kBlock) void bagmean_fwd_kernel(const float* __rest
                                                              const float* __restrict__ grid,
                                                              const float* __restrict__ w,
                                                              const float* __restrict__ bias,
+                                                             const float* __restrict__ lw,
                                                              float* __restrict__ y, int B, int L,
                                                              int S, int d, int width) {
+  // lw (nullable): per-snapshot weights replacing 1/L (a bag of unique snapshots with
+  // multiplicities: lw[l] = count_l / L_drawn)
   const int64_t total = (int64_t)B * S;
-  const float invL = 1.0f / (float)L;
+  const float invL = lw ? 1.0f : 1.0f / (float)L;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int s = (int)(idx % S);
     const int b = (int)(idx / S);
     float sum = 0.f;
-    for (int l = 0; l < L; ++l) sum += u[((int64_t)b * L + l) * S + s];
+    if (lw) {
+      for (int l = 0; l < L; ++l) sum = fmaf(lw[l], u[((int64_t)b * L + l) * S + s], sum);
+    } else {
+      for (int l = 0; l < L; ++l) sum += u[((int64_t)b * L + l) * S + s];
+    }
     for (int c = 0; c < width; ++c) {
       float v = bias[c];
       for (int e = 0; e < d; ++e) v = fmaf(w[c * (d + 1) + e], grid[(int64_t)s * d + e], v);
@@ -752,6 +759,19 @@ BLINDNO_API int blindno_project_bwd_g(const float* z, const float* w1, const flo
                           ostride, ooff, 1, G, wgs, (hipStream_t)stream);
 }
 
+BLINDNO_API int blindno_project_bwd_w(const float* z, const float* w1, const float* b1,
+                                      const float* w2, const float* dout, const float* lscale,
+                                      float* dz, float* partial, int nchunk, int Bn, int C,
+                                      int P1, int P2, int Ho, int Wo, int Hd, int Cout,
+                                      int ostride, int ooff, int dout_div, void* stream) {
+  if (Ho > P1 || Wo > P2 || dout_div < 1 || C > 32 || Cout > 4 || !dz || !partial ||
+      nchunk < 1 || (int64_t)Bn * Ho * Wo >= INT32_MAX ||
+      !project_mfma_ok(C, Hd, Cout, (int64_t)Bn * C * P1 * P2))
+    return (int)hipErrorInvalidValue;
+  return project_bwd_mfma(z, w1, b1, w2, dout, dz, partial, nchunk, Bn, C, P1, P2, Ho, Wo, Cout,
+                          ostride, ooff, dout_div, 1, 0, (hipStream_t)stream, lscale);
+}
+
 BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float* b1,
                                     const float* w2, const float* dout, float* dz,
                                     float* partial, int nchunk, int Bn, int C, int P1, int P2,
@@ -787,12 +807,18 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
   return (int)hipGetLastError();
 }
 
+BLINDNO_API int blindno_bagmean_fwd_w(const float* u, const float* grid, const float* w,
+                                      const float* bias, const float* lw, float* y, int B, int L,
+                                      int S, int d, int width, void* stream) {
+  bagmean_fwd_kernel<<<grid_for((int64_t)B * S), kBlock, 0, (hipStream_t)stream>>>(
+      u, grid, w, bias, lw, y, B, L, S, d, width);
+  return (int)hipGetLastError();
+}
+
 BLINDNO_API int blindno_bagmean_fwd(const float* u, const float* grid, const float* w,
                                     const float* bias, float* y, int B, int L, int S, int d,
                                     int width, void* stream) {
-  bagmean_fwd_kernel<<<grid_for((int64_t)B * S), kBlock, 0, (hipStream_t)stream>>>(
-      u, grid, w, bias, y, B, L, S, d, width);
-  return (int)hipGetLastError();
+  return blindno_bagmean_fwd_w(u, grid, w, bias, nullptr, y, B, L, S, d, width, stream);
 }
 
 BLINDNO_API int blindno_bagmean_bwd(const float* dy, const float* w, float* s, int B, int S,

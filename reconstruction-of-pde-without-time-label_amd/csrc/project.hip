@@ -52,6 +52,7 @@ struct Groups {
   unsigned gpts;
   int64_t wgs;
   int goff;
+  const float* lscale;   // backward: dout of sample n scaled by lscale[n % dout_div] (nullable)
 };
 
 struct PointMap {
@@ -318,8 +319,9 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
         zb[np][r] = !ok ? 0.f : (zc < C ? z[zo4[np][r] + (int64_t)zc * pm.HW] : (zc == C ? 1.f : 0.f));
         const float* gp = dout + ((int64_t)((n - nbase) / (unsigned)dout_div) * pm.HoWo + q) * ostride +
                           ooff + g * gr.goff;
+        const float ls = gr.lscale ? gr.lscale[(n - nbase) % (unsigned)dout_div] : 1.0f;
 #pragma unroll
-        for (int c = 0; c < COM; ++c) gv[np][r][c] = (ok && c < Cout) ? gp[c] : 0.f;
+        for (int c = 0; c < COM; ++c) gv[np][r][c] = (ok && c < Cout) ? gp[c] * ls : 0.f;
       }
       if (c16 == 0) {
 #pragma unroll
@@ -494,7 +496,7 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
                      int Cout, int ostride, int ooff, int G, int64_t wgs, hipStream_t st) {
   if (G < 1 || G > kMaxGroups || Bn % G) return (int)hipErrorInvalidValue;
   const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
-  const Groups gr{G, npts / (unsigned)G, G > 1 ? wgs : 0, Cout};
+  const Groups gr{G, npts / (unsigned)G, G > 1 ? wgs : 0, Cout, nullptr};
   const unsigned ntiles = (npts + 15) / 16;
   unsigned blocks = (ntiles + kWaves * PF_TPW - 1) / (kWaves * PF_TPW);
   if (blocks > 2048) blocks = 2048;
@@ -523,10 +525,10 @@ int project_bwd_mfma_nchunk(int64_t npts) {
 int project_bwd_mfma(const float* z, const float* w1, const float* b1, const float* w2,
                      const float* dout, float* dz, float* partial, int nchunk, int Bn, int C,
                      int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff,
-                     int dout_div, int G, int64_t wgs, hipStream_t st) {
+                     int dout_div, int G, int64_t wgs, hipStream_t st, const float* lscale) {
   if (G < 1 || G > kMaxGroups || Bn % G) return (int)hipErrorInvalidValue;
   const unsigned gpts = (unsigned)((int64_t)(Bn / G) * Ho * Wo);
-  const Groups gr{G, gpts, G > 1 ? wgs : 0, Cout};
+  const Groups gr{G, gpts, G > 1 ? wgs : 0, Cout, lscale};
   const dim3 grid(nchunk, G);
 #define PB(CK_, CO_)                                                                          \
   project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kBwdNP4 : 1)><<<grid, 256, 0, st>>>(            \

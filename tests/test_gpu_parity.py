@@ -271,3 +271,30 @@ def test_head_pair_grouped_matches_separate_heads(width, modes, N, B):
     for a, b in zip(got, want):
         assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-5
     assert rel_l2(gh.cpu().numpy(), h.grad.cpu().numpy()) <= 1e-6
+
+
+def test_dedup_bag_matches_full_bag():
+    """A with-replacement bag run once per distinct snapshot (multiplicity weights in the bag
+    mean and its gradient, nio.dedup_bag) against the same bag run snapshot by snapshot."""
+    from blindno import NIOFP2D_FNO, nio
+    torch.manual_seed(8)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 6, 8, 2).cuda().train()
+    x = torch.randn(3, 60, 32, 32, device="cuda")
+    gx, gy = np.meshgrid(np.linspace(-1, 1, 32, dtype=np.float32), np.linspace(-1, 1, 32, dtype=np.float32),
+                         indexing="ij")
+    grid = torch.tensor(np.stack([gx, gy], 2)).cuda()
+    idx = np.random.RandomState(2).choice(60, 55)
+    assert len(np.unique(idx)) < len(idx)
+    res = []
+    for dedup in (True, False):
+        nio.DEDUP_BAGS = dedup
+        try:
+            m.zero_grad()
+            out = m(x, grid, bag_idx=idx)
+            (out * torch.linspace(-1, 1, out.numel(), device="cuda").view_as(out)).sum().backward()
+            res.append((out.detach().cpu().numpy(), [p.grad.cpu().numpy() for p in m.FNO_input.parameters()]))
+        finally:
+            nio.DEDUP_BAGS = True
+    assert rel_l2(res[0][0], res[1][0]) <= 1e-6
+    for a, b in zip(res[0][1], res[1][1]):
+        assert rel_l2(a, b) <= 1e-5
