@@ -30,17 +30,28 @@ def draw_bag(T: int):
     return L, idx
 
 
-def _select(module, x, bag_idx):
+def _select(module, x, bag_idx, dedup=False):
+    """The bag of this step: (x[:, idx], L, lw).  With ``dedup`` (models whose per-snapshot
+    encoder output does not depend on the rest of the batch -- not the BatchNorm'd NIO branch)
+    the bag is reduced to its distinct snapshots and lw holds multiplicity / L."""
+    if isinstance(bag_idx, tuple):
+        idx_t, lw = bag_idx                       # device-resident deduplicated bag
+        return x.index_select(1, idx_t), idx_t.numel(), lw
     if torch.is_tensor(bag_idx) and bag_idx.is_cuda:
         # device-resident index list (graph replays): gather on the device
-        return x.index_select(1, bag_idx), bag_idx.numel()
+        return x.index_select(1, bag_idx), bag_idx.numel(), None
     if bag_idx is not None:
         idx = np.asarray(bag_idx)
-        return x[:, torch.as_tensor(idx, device=x.device)], len(idx)
-    if module.training:
-        L, idx = draw_bag(x.shape[1])
-        return x[:, torch.as_tensor(idx, device=x.device)], L
-    return x, x.shape[1]
+    elif module.training:
+        _, idx = draw_bag(x.shape[1])
+    else:
+        return x, x.shape[1], None
+    lw = None
+    if dedup:
+        idx, w = dedup_bag(idx)
+        if w is not None:
+            lw = torch.as_tensor(w, device=x.device)
+    return x[:, torch.as_tensor(idx, device=x.device)], len(idx), lw
 
 
 _SIDE = {}
@@ -80,16 +91,16 @@ def _run_heads(module, h):
                                 h, *p0, *p1)
 
 
-def _bag_mean_2d(module, u, grid, B, L, nx, ny):
+def _bag_mean_2d(module, u, grid, B, L, nx, ny, lw=None):
     g = grid.reshape(nx * ny, 2)
     h = ops.BagMeanFn.apply(u.reshape(B, L, nx * ny), g, module.fc0.weight.data,
-                            module.fc0.bias.data)
+                            module.fc0.bias.data, lw)
     return h.view(B, nx, ny, -1)
 
 
-def _bag_mean_1d(module, u, grid, B, L, nx):
+def _bag_mean_1d(module, u, grid, B, L, nx, lw=None):
     h = ops.BagMeanFn.apply(u.reshape(B, L, nx), grid.reshape(nx, 1), module.fc0.weight.data,
-                            module.fc0.bias.data)
+                            module.fc0.bias.data, lw)
     return h
 
 
@@ -150,19 +161,21 @@ class NIOFP2D_FNO(nn.Module):
             h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, lw, grid, self.fc0.weight.data,
                                        self.fc0.bias.data, *fno_params(fno, 2))
             return _run_heads(self, h)
-        x, L = _select(self, x, bag_idx)
+        x, L, lw = _select(self, x, bag_idx, dedup=True)
         B, _, nx, ny = x.shape
         x_in = x.reshape(B * L, 1, nx, ny)
         grid_r = grid.permute(2, 0, 1).unsqueeze(0).expand(B * L, 2, nx, ny)
         inp = torch.cat((x_in, grid_r), dim=1).permute(0, 2, 3, 1).contiguous()
         u = self.FNO_input(inp)                       # (B*L, nx, ny, 1)
-        h = _bag_mean_2d(self, u, grid, B, L, nx, ny)
+        h = _bag_mean_2d(self, u, grid, B, L, nx, ny, lw)
         return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
 
 
 class NIOFP_FNO(nn.Module):
     """1D FNO-NIO: 1d_FPE/NIOModules.py:87-155 (heads fno_drift/fno_diffusion) or
     1d_GPE/NIOModules.py:228-289 (single head ``fno_V``: ``heads=("fno_V",)``)."""
+
+    accepts_dedup_bag = True    # forward(bag_idx=(unique idx, weights)): deduplicated bag
 
     def __init__(self, fno_layers, width, modes, output_dim, device,
                  heads: Sequence[str] = ("fno_drift", "fno_diffusion")):
@@ -179,13 +192,13 @@ class NIOFP_FNO(nn.Module):
 
     def forward(self, x, grid, bag_idx=None):
         """x (B, T, Nx), grid (Nx, 1) -> (B, Nx, n_heads)."""
-        x, L = _select(self, x, bag_idx)
+        x, L, lw = _select(self, x, bag_idx, dedup=True)
         B, _, nx = x.shape
         x_in = x.reshape(B * L, nx, 1)
         grid_r = grid.unsqueeze(0).expand(B * L, nx, 1)
         inp = torch.cat((x_in, grid_r), dim=2).contiguous()
         u = self.FNO_input(inp)                       # (B*L, nx, 1)
-        h = _bag_mean_1d(self, u, grid, B, L, nx)
+        h = _bag_mean_1d(self, u, grid, B, L, nx, lw)
         outs = [getattr(self, n)(h) for n in self._heads]
         return torch.cat(outs, dim=-1) if len(outs) > 1 else outs[0]
 
@@ -212,7 +225,7 @@ class NIOFP2D(nn.Module):
 
     def forward(self, x, grid, bag_idx=None):
         ops.require_device(x, grid)
-        x, L = _select(self, x, bag_idx)
+        x, L, _ = _select(self, x, bag_idx)
         B, _, nx, ny = x.shape
         u = self.deeponet(x.unsqueeze(2), grid.reshape(-1, 2))     # (B, L, nx*ny)
         h = _bag_mean_2d(self, u, grid, B, L, nx, ny)
@@ -244,7 +257,7 @@ class NIOFP(nn.Module):
 
     def forward(self, x, grid, bag_idx=None):
         ops.require_device(x, grid)
-        x, L = _select(self, x, bag_idx)
+        x, L, _ = _select(self, x, bag_idx)
         B, _, nx = x.shape
         u = self.deeponet(x, grid)                                   # (B, L, nx)
         h = _bag_mean_1d(self, u, grid, B, L, nx)

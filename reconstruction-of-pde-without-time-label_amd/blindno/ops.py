@@ -885,7 +885,8 @@ class BagMeanFn(torch.autograd.Function):
     reference, 2d_FPE/NIOModules.py:569-570)."""
 
     @staticmethod
-    def forward(ctx, u, grid, w, bias):
+    def forward(ctx, u, grid, w, bias, lw=None):
+        """lw (optional, (L,)): per-snapshot weights replacing 1/L (deduplicated bag)."""
         require_device(u, grid, w, bias)
         u, grid = _c(u), _c(grid)
         w, bias = _c(w.detach()), _c(bias.detach())
@@ -893,9 +894,10 @@ class BagMeanFn(torch.autograd.Function):
         d = grid.shape[1]
         width = w.shape[0]
         y = _empty(B, S, width, like=u)
-        call("blindno_bagmean_fwd", ptr(u), ptr(grid), ptr(w), ptr(bias), ptr(y), B, L, S, d,
+        call("blindno_bagmean_fwd_w", ptr(u), ptr(grid), ptr(w), ptr(bias), ptr(lw), ptr(y), B, L, S, d,
              width, stream_ptr())
         ctx.save_for_backward(w)
+        ctx.lw = lw
         ctx.dims = (B, L, S, d, width)
         return y
 
@@ -907,11 +909,14 @@ class BagMeanFn(torch.autograd.Function):
         gu = ggrid = None
         if ctx.needs_input_grad[0]:
             s = _empty(B, S, like=gy)
-            call("blindno_bagmean_bwd", ptr(gy), ptr(w), ptr(s), B, S, d, width, L, stream_ptr())
-            gu = s.unsqueeze(1).expand(B, L, S)
+            lw = ctx.lw
+            call("blindno_bagmean_bwd", ptr(gy), ptr(w), ptr(s), B, S, d, width,
+                 1 if lw is not None else L, stream_ptr())
+            gu = s.unsqueeze(1).expand(B, L, S) if lw is None else s.unsqueeze(1) * lw.view(1, L, 1)
         if ctx.needs_input_grad[1]:
             ggrid = torch.einsum("bsc,ce->se", gy, w[:, :d])
-        return gu, ggrid, None, None
+        ctx.lw = None
+        return gu, ggrid, None, None, None
 
 
 # ---------------------------------------------------------------------------- loss

@@ -273,16 +273,22 @@ def test_head_pair_grouped_matches_separate_heads(width, modes, N, B):
     assert rel_l2(gh.cpu().numpy(), h.grad.cpu().numpy()) <= 1e-6
 
 
-def test_dedup_bag_matches_full_bag():
+@pytest.mark.parametrize("dim", [2, 1])
+def test_dedup_bag_matches_full_bag(dim):
     """A with-replacement bag run once per distinct snapshot (multiplicity weights in the bag
     mean and its gradient, nio.dedup_bag) against the same bag run snapshot by snapshot."""
-    from blindno import NIOFP2D_FNO, nio
+    from blindno import NIOFP2D_FNO, NIOFP_FNO, nio
     torch.manual_seed(8)
-    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 6, 8, 2).cuda().train()
-    x = torch.randn(3, 60, 32, 32, device="cuda")
-    gx, gy = np.meshgrid(np.linspace(-1, 1, 32, dtype=np.float32), np.linspace(-1, 1, 32, dtype=np.float32),
-                         indexing="ij")
-    grid = torch.tensor(np.stack([gx, gy], 2)).cuda()
+    if dim == 2:
+        m = NIOFP2D_FNO(2, 3, 100, 25, 3, 6, 8, 2).cuda().train()
+        x = torch.randn(3, 60, 32, 32, device="cuda")
+        gx, gy = np.meshgrid(np.linspace(-1, 1, 32, dtype=np.float32),
+                             np.linspace(-1, 1, 32, dtype=np.float32), indexing="ij")
+        grid = torch.tensor(np.stack([gx, gy], 2)).cuda()
+    else:
+        m = NIOFP_FNO(3, 30, 15, 2, "cuda").cuda().train()
+        x = torch.randn(3, 60, 64, device="cuda")
+        grid = torch.linspace(0, 1, 64, device="cuda").unsqueeze(-1)
     idx = np.random.RandomState(2).choice(60, 55)
     assert len(np.unique(idx)) < len(idx)
     res = []
