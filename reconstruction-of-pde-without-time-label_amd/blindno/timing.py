@@ -14,7 +14,10 @@ import torch
 from . import _lib
 
 GELU_FLOPS = 20          # flop-equivalents charged per exact-erf GELU evaluation
+# the snapshot encoder's projection backward: blindno_project_bwd_w when the bag is
+# deduplicated (distinct snapshots + multiplicity weights), blindno_project_bwd otherwise
 DOMINANT = os.environ.get("BLINDNO_TIMED_KERNEL", "blindno_project_bwd")
+_VARIANTS = {"blindno_project_bwd": ("blindno_project_bwd", "blindno_project_bwd_w")}
 
 
 def _i(args, k):
@@ -45,9 +48,10 @@ def cost(name, args):
         Bn, C, P1, P2, Ho, Wo, Hd, Cout = (_i(args, k) for k in range(6, 14))
         pts = Bn * Ho * Wo
         return 4 * pts * (C + Cout), pts * Hd * (2 * C + 2 * Cout + GELU_FLOPS)
-    if name == "blindno_project_bwd":
-        Bn, C, P1, P2, Ho, Wo, Hd, Cout = (_i(args, k) for k in range(8, 16))
-        dout_div = _i(args, 18)
+    if name in ("blindno_project_bwd", "blindno_project_bwd_w"):
+        o = 8 if name == "blindno_project_bwd" else 9
+        Bn, C, P1, P2, Ho, Wo, Hd, Cout = (_i(args, k) for k in range(o, o + 8))
+        dout_div = _i(args, o + 10)
         pts = Bn * Ho * Wo
         # read z, write dz (crop), read dout (one value per bag and point when dout_div = L);
         # recompute h (2C) + GELU/GELU' + dh (2 Cout) + dz (2C) + weight grads (2C + 2 Cout + 1)
@@ -73,8 +77,8 @@ def pmc_traffic(root: str, name: str):
 
 
 def points(name, args):
-    if name in ("blindno_project_bwd", "blindno_project_fwd"):
-        o = 8 if name == "blindno_project_bwd" else 6
+    if name in ("blindno_project_bwd", "blindno_project_bwd_w", "blindno_project_fwd"):
+        o = {"blindno_project_bwd": 8, "blindno_project_bwd_w": 9, "blindno_project_fwd": 6}[name]
         Bn, Ho, Wo = _i(args, o), _i(args, o + 4), _i(args, o + 5)
         return Bn * Ho * Wo
     return 0
@@ -87,25 +91,32 @@ class KernelTimer:
 
     def __init__(self, name: str = DOMINANT):
         self.name = name
+        self.entries = _VARIANTS.get(name, (name,))
         self.recs = []            # (ev0, ev1, bytes, flops, points)
         self._pending = None
 
-    def before(self, args):
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        self._pending = ev
+    class _Hook:
+        def __init__(self, timer, entry):
+            self.timer, self.entry = timer, entry
 
-    def after(self, args):
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        b, f = cost(self.name, args)
-        self.recs.append((self._pending, ev, b, f, points(self.name, args)))
+        def before(self, args):
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.timer._pending = ev
+
+        def after(self, args):
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            b, f = cost(self.entry, args)
+            self.timer.recs.append((self.timer._pending, ev, b, f, points(self.entry, args)))
 
     def start(self):
-        _lib._HOOKS[self.name] = self
+        for e in self.entries:
+            _lib._HOOKS[e] = KernelTimer._Hook(self, e)
 
     def stop(self):
-        _lib._HOOKS.pop(self.name, None)
+        for e in self.entries:
+            _lib._HOOKS.pop(e, None)
         torch.cuda.synchronize()
 
     def roofline(self, hbm_peak_gbs: float, flop_peak_tflops: float, bound: str = None,
