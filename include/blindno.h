@@ -194,6 +194,11 @@ int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, int Ci, int Co
  * weights2 (overlapping rows) receive 0. */
 int blindno_unpack_w2d(const float* dWt, float* dw1, float* dw2, int Ci, int Co, int m1,
                        int m2, int P1, blindno_stream_t stream);
+/* The same for two weight sets in one launch (the two heads): Wt (2, m2, K1, Ci, Co) complex. */
+int blindno_pack_w2d_2(const float* w1a, const float* w2a, const float* w1b, const float* w2b,
+                       float* Wt, int Ci, int Co, int m1, int m2, int P1, blindno_stream_t stream);
+int blindno_unpack_w2d_2(const float* dWt, float* dw1a, float* dw2a, float* dw1b, float* dw2b,
+                         int Ci, int Co, int m1, int m2, int P1, blindno_stream_t stream);
 /* 1D: (Ci,Co,m) complex <-> Wt (m,Ci,Co) complex; dir 0 pack, 1 unpack. */
 int blindno_pack_w1d(const float* w, float* Wt, int Ci, int Co, int m, int dir,
                      blindno_stream_t stream);

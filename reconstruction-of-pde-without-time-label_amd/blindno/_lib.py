@@ -61,6 +61,8 @@ SIGNATURES = {
     "blindno_conv_wgrad_g": "pppiiiiiiis",
     "blindno_bagmean_fwd_w": "pppppp" + "iiiii" + "s",
     "blindno_project_bwd_w": "pppppppp" + "i" + "iiiiiiiiiii" + "s",
+    "blindno_pack_w2d_2": "ppppp" + "iiiii" + "s",
+    "blindno_unpack_w2d_2": "ppppp" + "iiiii" + "s",
     "blindno_bn_act_nslices": "iii",
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",

@@ -560,9 +560,8 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
     for k in range(n):
         off = 2 + 4 * k
         Wt = _empty(G, meta.m2, K1, C, C, 2, like=inp)
-        for g in range(G):
-            call("blindno_pack_w2d", ptr(_c(prms[g][off])), ptr(_c(prms[g][off + 1])), ptr(Wt[g]), C, C,
-                 meta.m1, meta.m2, P1, stream_ptr())
+        call("blindno_pack_w2d_2", ptr(_c(prms[0][off])), ptr(_c(prms[0][off + 1])), ptr(_c(prms[1][off])),
+             ptr(_c(prms[1][off + 1])), ptr(Wt), C, C, meta.m1, meta.m2, P1, stream_ptr())
         At = k_rowdft(src, Bn, C, P1, P2, meta.m2, act)
         X = _empty(Bn, meta.m2, C, K1, 2, like=inp)
         Y = _empty(Bn, meta.m2, C, K1p, 2, like=inp)
@@ -635,9 +634,11 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         part = _empty(ns, G, meta.m2 * K1 * C * C * 2, like=inp) if ns > 1 else None
         call("blindno_mix_wgrad_g", ptr(Xs[k]), ptr(Gs), ptr(dWt), ptr(part) if part is not None else None,
              ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
+        dws = [torch.empty_like(prms[g][off]) for g in range(G) for _ in range(2)]
+        call("blindno_unpack_w2d_2", ptr(dWt), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), C, C,
+             meta.m1, meta.m2, P1, stream_ptr())
         for g in range(G):
-            dw1, dw2 = k_unpack_w2d(dWt[g], prms[g][off], P1)
-            grads[g][off], grads[g][off + 1] = dw1, dw2
+            grads[g][off], grads[g][off + 1] = dws[2 * g], dws[2 * g + 1]
         nch = query("blindno_conv_wgrad_nchunk", Bg, P1, P2)
         pc = _empty(nch, G, np_c, like=inp)
         call("blindno_conv_wgrad_g", ptr(dz), ptr(src), ptr(pc), nch, G, Bn, C, P1, P2, act, stream_ptr())

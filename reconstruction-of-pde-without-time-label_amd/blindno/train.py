@@ -178,8 +178,8 @@ class GraphedBagStep:
         # deduplicated bags (NIOFP2D_FNO's fused encoder): graphs keyed by the number U of
         # distinct snapshots, fed the unique indices and multiplicity weights
         self.dedup = bool(getattr(model, "accepts_dedup_bag", False)) and nio.DEDUP_BAGS
-        self._ring = [torch.empty(self.T, dtype=torch.int32).pin_memory() for _ in range(4)]
-        self._ringw = [torch.empty(self.T, dtype=torch.float32).pin_memory() for _ in range(4)]
+        # pinned ring of [idx (int32) | weights (float32 bits)] slots: one H2D copy per step
+        self._ring = [torch.empty(2 * self.T, dtype=torch.int32).pin_memory() for _ in range(4)]
         self._ev = [None] * len(self._ring)
         self._k = 0
 
@@ -195,8 +195,11 @@ class GraphedBagStep:
     def capture(self, L: int):
         if L in self.graphs:
             return
-        self.idx[L] = torch.zeros(L, dtype=torch.int32, device=self.x.device)
-        self.lw[L] = torch.zeros(L, dtype=torch.float32, device=self.x.device)
+        blob = torch.zeros(2 * L, dtype=torch.int32, device=self.x.device)
+        self.blob = getattr(self, "blob", {})
+        self.blob[L] = blob
+        self.idx[L] = blob[:L]
+        self.lw[L] = blob[L:].view(torch.float32)
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                 # eager warm-up: caches, lazy init
@@ -225,13 +228,13 @@ class GraphedBagStep:
         self._k = (k + 1) % len(self._ring)
         if self._ev[k] is not None:
             self._ev[k].synchronize()                 # ring slot's previous copy has landed
-        buf = self._ring[k]
-        buf[:L].numpy()[:] = idx
-        self.idx[L].copy_(buf[:L], non_blocking=True)
+        buf = self._ring[k].numpy()
+        buf[:L] = idx
+        n = L
         if w is not None:
-            bw = self._ringw[k]
-            bw[:L].numpy()[:] = w
-            self.lw[L].copy_(bw[:L], non_blocking=True)
+            buf[L:2 * L] = np.asarray(w, dtype=np.float32).view(np.int32)
+            n = 2 * L
+        self.blob[L][:n].copy_(self._ring[k][:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._ev[k] = ev

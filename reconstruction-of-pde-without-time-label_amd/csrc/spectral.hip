@@ -451,11 +451,16 @@ __global__ __launch_bounds__(kBlock) void mix1d_kernel(const float2* __restrict_
 }
 
 // ------------------------------------------------------------------------------ weight packing
-__global__ void pack_w2d_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
+// blockIdx.y selects one of up to two weight sets (the two heads, packed in one launch)
+__global__ void pack_w2d_kernel(const float* __restrict__ w1a, const float* __restrict__ w2a,
+                                const float* __restrict__ w1b, const float* __restrict__ w2b,
                                 float2* __restrict__ Wt, int Ci, int Co, int m1, int m2,
                                 int P1) {
   const int K1 = kept_rows_count(m1, P1);
   const int64_t total = (int64_t)m2 * K1 * Ci * Co;
+  const float* w1 = blockIdx.y ? w1b : w1a;
+  const float* w2 = blockIdx.y ? w2b : w2a;
+  Wt += blockIdx.y * total;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int o = (int)(idx % Co);
@@ -473,11 +478,15 @@ __global__ void pack_w2d_kernel(const float* __restrict__ w1, const float* __res
   }
 }
 
-__global__ void unpack_w2d_kernel(const float2* __restrict__ dWt, float* __restrict__ dw1,
-                                  float* __restrict__ dw2, int Ci, int Co, int m1, int m2,
+__global__ void unpack_w2d_kernel(const float2* __restrict__ dWt, float* __restrict__ dw1a,
+                                  float* __restrict__ dw2a, float* __restrict__ dw1b,
+                                  float* __restrict__ dw2b, int Ci, int Co, int m1, int m2,
                                   int P1) {
   const int K1 = kept_rows_count(m1, P1);
   const int64_t per = (int64_t)Ci * Co * m1 * m2;
+  float* dw1 = blockIdx.y ? dw1b : dw1a;
+  float* dw2 = blockIdx.y ? dw2b : dw2a;
+  dWt += blockIdx.y * (int64_t)m2 * K1 * Ci * Co;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < 2 * per;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int which = idx >= per;
@@ -708,8 +717,18 @@ BLINDNO_API int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, in
                                  int m1, int m2, int P1, void* stream) {
   if (m1 > P1) return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)m2 * kept_rows_count(m1, P1) * Ci * Co;
-  pack_w2d_kernel<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(w1, w2, (float2*)Wt, Ci,
-                                                                       Co, m1, m2, P1);
+  pack_w2d_kernel<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(w1, w2, w1, w2, (float2*)Wt,
+                                                                       Ci, Co, m1, m2, P1);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_pack_w2d_2(const float* w1a, const float* w2a, const float* w1b,
+                                   const float* w2b, float* Wt, int Ci, int Co, int m1, int m2,
+                                   int P1, void* stream) {
+  if (m1 > P1) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)m2 * kept_rows_count(m1, P1) * Ci * Co;
+  pack_w2d_kernel<<<dim3(grid_for(total), 2), kBlock, 0, (hipStream_t)stream>>>(
+      w1a, w2a, w1b, w2b, (float2*)Wt, Ci, Co, m1, m2, P1);
   return (int)hipGetLastError();
 }
 
@@ -718,7 +737,17 @@ BLINDNO_API int blindno_unpack_w2d(const float* dWt, float* dw1, float* dw2, int
   if (m1 > P1) return (int)hipErrorInvalidValue;
   const int64_t total = 2 * (int64_t)Ci * Co * m1 * m2;
   unpack_w2d_kernel<<<grid_for(total), kBlock, 0, (hipStream_t)stream>>>(
-      (const float2*)dWt, dw1, dw2, Ci, Co, m1, m2, P1);
+      (const float2*)dWt, dw1, dw2, dw1, dw2, Ci, Co, m1, m2, P1);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_unpack_w2d_2(const float* dWt, float* dw1a, float* dw2a, float* dw1b,
+                                     float* dw2b, int Ci, int Co, int m1, int m2, int P1,
+                                     void* stream) {
+  if (m1 > P1) return (int)hipErrorInvalidValue;
+  const int64_t total = 2 * (int64_t)Ci * Co * m1 * m2;
+  unpack_w2d_kernel<<<dim3(grid_for(total), 2), kBlock, 0, (hipStream_t)stream>>>(
+      (const float2*)dWt, dw1a, dw2a, dw1b, dw2b, Ci, Co, m1, m2, P1);
   return (int)hipGetLastError();
 }
 
