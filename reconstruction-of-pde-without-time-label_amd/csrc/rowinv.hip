@@ -110,35 +110,85 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
       grow = bl.grid + (int64_t)h * bl.N2 * 2;
     }
     const int t0 = chunk * TPW, t1 = min(NT, t0 + TPW);
+    // epilogue operands of a column tile (raw loads), fetched one tile ahead so their latency
+    // overlaps the previous tile's MFMA chain and epilogue
+    struct Ops {
+      float fv[CM];        // MODE 0: x of every input channel; MODE 1: dz of every output channel
+      float sv[4];         // MODE 1: xsrc of this group's channels
+      float lin[3];        // LIFT: [u, gx, gy] at this point
+      bool lok;
+    };
+    auto load_ops = [&](int tile, Ops& o) {
+      const int w = 16 * tile + c16;
+      const bool pok = rok && w < P2;
+      o.lok = false;
+      o.lin[0] = o.lin[1] = o.lin[2] = 0.f;
+      if (LIFT) {
+        o.lok = pok && urow != nullptr && w < bl.N2;
+        if (o.lok) {
+          o.lin[0] = urow[w];
+          o.lin[1] = grow[2 * w];
+          o.lin[2] = grow[2 * w + 1];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CM; ++i)
+        o.fv[i] = (!(LIFT && MODE == 0) && pok && has_wc && i < C)
+                      ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        o.sv[r] = (!LIFT && MODE == 1 && (ACT || WG) && pok && c0 + r < C) ? xs[rbase + (c0 + r) * HW + w] : 0.f;
+    };
+    // (forward epilogue of narrow fields only: the adjoint's and the 12-channel heads' larger
+    // operand sets cost more occupancy than the lookahead gains -- measured)
+    constexpr bool kPre = MODE == 0 && CM <= 8;
+    Ops nx;
+    if (kPre) load_ops(t0, nx);
     for (int tile = t0; tile < t1; ++tile) {
       const int w = 16 * tile + c16;
       const bool pok = rok && w < P2;
-      // epilogue operands first: their loads fly while the MFMA chain runs
-      float fv[CM];        // MODE 0: x of every input channel; MODE 1: dz of every output channel
-      float sv[4];         // MODE 1: xsrc of this group's channels
-      float lin[3] = {0.f, 0.f, 0.f};               // LIFT: [u, gx, gy] at this point
+      float fv[CM], sv[4];
       bool lok = false;
-      if (LIFT) {
-        lok = pok && urow != nullptr && w < bl.N2;
-        if (lok) {
-          lin[0] = urow[w];
-          lin[1] = grow[2 * w];
-          lin[2] = grow[2 * w + 1];
+      float lin[3] = {0.f, 0.f, 0.f};
+      if constexpr (kPre) {
+        const Ops cur = nx;
+        if (tile + 1 < t1) load_ops(tile + 1, nx);
+        lok = cur.lok;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) lin[j] = cur.lin[j];
+#pragma unroll
+        for (int i = 0; i < CM; ++i) fv[i] = cur.fv[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sv[r] = cur.sv[r];
+      } else {
+        // operands of this tile, loaded in place (as before the lookahead variant)
+        if (LIFT) {
+          lok = pok && urow != nullptr && w < bl.N2;
+          if (lok) {
+            lin[0] = urow[w];
+            lin[1] = grow[2 * w];
+            lin[2] = grow[2 * w + 1];
+          }
         }
+#pragma unroll
+        for (int i = 0; i < CM; ++i)
+          fv[i] = (!(LIFT && MODE == 0) && pok && has_wc && i < C)
+                      ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sv[r] = (!LIFT && MODE == 1 && (ACT || WG) && pok && c0 + r < C) ? xs[rbase + (c0 + r) * HW + w] : 0.f;
       }
       auto x0 = [&](int c) -> float {               // the lifted field (0 outside the crop)
         return lok ? fmaf(bl.w0[c * 3], lin[0], fmaf(bl.w0[c * 3 + 1], lin[1],
                                                      fmaf(bl.w0[c * 3 + 2], lin[2], bl.b0[c]))) : 0.f;
       };
+      if (LIFT) {
 #pragma unroll
-      for (int i = 0; i < CM; ++i) {
-        if (LIFT && MODE == 0) fv[i] = (has_wc && i < C) ? x0(i) : 0.f;
-        else fv[i] = (pok && has_wc && i < C) ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
-      }
+        for (int i = 0; i < CM; ++i)
+          if (MODE == 0) fv[i] = (has_wc && i < C) ? x0(i) : 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (LIFT && MODE == 1) sv[r] = c0 + r < C ? x0(c0 + r) : 0.f;
-        else sv[r] = (MODE == 1 && (ACT || WG) && pok && c0 + r < C) ? xs[rbase + (c0 + r) * HW + w] : 0.f;
+        for (int r = 0; r < 4; ++r)
+          if (MODE == 1) sv[r] = c0 + r < C ? x0(c0 + r) : 0.f;
       }
       f32x4 d = {0.f, 0.f, 0.f, 0.f};
       const float* tb = (LDSB ? (const float*)sTB : TB) + tile * 64 + lane;
