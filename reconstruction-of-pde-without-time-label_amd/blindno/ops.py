@@ -533,7 +533,8 @@ def grouped_ok(meta: FNOMeta, inp, prms) -> bool:
     if any(a.shape != b.shape for a, b in zip(prms[0], prms[1])):
         return False
     Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
-    return (Bg * Ho * Wo) % 64 == 0
+    # grouped projection steps stay within one head; grouped row-inverse quads within a sample
+    return (Bg * Ho * Wo) % 64 == 0 and P1 % 4 == 0
 
 
 def _sub(buf, off):
