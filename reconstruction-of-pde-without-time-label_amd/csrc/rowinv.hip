@@ -300,6 +300,10 @@ struct RowinvGeom {
   size_t lds;
 };
 
+#ifndef ROWINV_MIN_ITEMS
+#define ROWINV_MIN_ITEMS 4096
+#endif
+
 RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   RowinvGeom g;
   const int KS = (m2 + 1) / 2, NT = (P2 + 15) / 16;
@@ -308,7 +312,7 @@ RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   // columns per work item: all of a row group when there is plenty of row parallelism,
   // split down to one tile for the small head layers
   int tpw = NT;
-  while (tpw > 1 && base * ((NT + tpw - 1) / tpw) < 8192) tpw = (tpw + 1) / 2;
+  while (tpw > 1 && base * ((NT + tpw - 1) / tpw) < ROWINV_MIN_ITEMS) tpw = (tpw + 1) / 2;
   g.TPW = tpw;
   g.nitems = (int)(base * ((NT + tpw - 1) / tpw));
   // persistent workgroups; the twiddle image is staged in LDS only when each workgroup

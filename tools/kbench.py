@@ -49,7 +49,7 @@ def main():
         res.append((name, us, nbytes / (us * 1e-6) / 1e9))
         print(f"{name:40s} {us:9.1f} us  {nbytes / (us * 1e-6) / 1e9:8.0f} GB/s", flush=True)
 
-    for tag, Bn, C, m, Cout in (("input", 300, 4, 12, 1), ("head", 4, 12, 32, 1)):
+    for tag, Bn, C, m, Cout in (("input", 300, 4, 12, 1), ("head", 4, 12, 32, 1), ("head2", 8, 12, 32, 1)):
         P, N = 160, 128
         z = torch.randn(Bn, C, P, P, device=dev)
         w1 = torch.randn(128, C, device=dev) * 0.3
