@@ -219,6 +219,24 @@ int blindno_bagmean_fwd_w(const float* u, const float* grid, const float* w, con
 int blindno_bagmean_bwd(const float* dy, const float* w, float* s, int B, int S, int d,
                         int width, int L, blindno_stream_t stream);
 
+/* --- token self-attention over the bag (NIOFP2D_FNO_attn, 2d_FPE/NIOModules.py:365-399;
+ *     2d_Non_conservative_FPE/NIOModules.py:364-398) ------------------------------------
+ * Tokens X[b] = [gx, gy, u_1..u_L] (T = L + 2 <= 256 rows of S points); grid (S, 2)
+ * channels-last, u (B, L, S), fc0 weight w (width) and bias (width), y (B, S, width).
+ * Forward: A = softmax(X X^T / sqrt(S)) (B,T,T), c = column sums of A (B,T),
+ * y[b,p,:] = w (1/T) sum_s c_s X[s,p] + bias  (= the reference's (A X)^T w / T + bias).
+ * partial: caller scratch of B * nchunk * T * T floats, nchunk = blindno_bagattn_nchunk(S). */
+int blindno_bagattn_nchunk(int S);
+int blindno_bagattn_fwd(const float* grid, const float* u, const float* w, const float* bias,
+                        float* partial, float* A, float* cs, float* y, int B, int L, int S,
+                        int width, blindno_stream_t stream);
+/* Backward from dy (B,S,width) and the forward's A, cs: du (B,L,S) and, if dgt is non-NULL,
+ * the grid tokens' gradient dgt (B,2,S).  Scratch: partial B*nchunk*T, dm B*S, M B*T*T. */
+int blindno_bagattn_bwd(const float* grid, const float* u, const float* dy, const float* w,
+                        const float* A, const float* cs, float* partial, float* dm, float* M,
+                        float* du, float* dgt, int B, int L, int S, int width,
+                        blindno_stream_t stream);
+
 /* --- loss / metrics / optimiser -------------------------------------------------------- */
 
 /* nn.MSELoss (2d_FPE/train_fno.py:116,142): partial sums of (p-t)^2 per block into

@@ -30,7 +30,7 @@ def set_precision(name: str = "fp64") -> None:
 
 __all__ = ["set_precision", 
     "pad_amount", "gelu", "c2r_weights", "spectral_conv2d", "spectral_conv1d",
-    "fno2d", "fno1d", "bag_mean", "niofp2d_fno", "niofp_fno", "encoder2d",
+    "fno2d", "fno1d", "bag_mean", "bag_attention", "niofp2d_fno", "niofp2d_fno_attn", "niofp_fno", "encoder2d",
     "ffn", "deeponet_nobias", "niofp2d", "mse", "train_rel_l2_2ch", "rel_l2",
     "time_averaged_relative_l2", "time_averaged_L2_error", "adam_step",
     "sub_params", "n_layers_of",
@@ -250,6 +250,43 @@ def niofp2d_fno(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
     h = bag_mean(u, gcf, p["fc0.weight"], p["fc0.bias"])
     outs = [fno2d(sub_params(p, hd), h) for hd in heads]
     return torch.cat(outs, dim=-1)
+
+
+def bag_attention(u: torch.Tensor, grid_cf: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Token self-attention + fixed-weight fusion of NIOFP2D_FNO_attn
+    (2d_FPE/NIOModules.py:365-399; NC copy 2d_Non_conservative_FPE/NIOModules.py:364-398).
+
+    Tokens X = [gx, gy, u_1..u_L] flattened to d = nx*ny (:369-375); scores X X^T / sqrt(d)
+    (:376-378), row softmax (:379), Z = A X (:381); fused = Z^T w[:, 0] / T + bias with
+    T = L + 2 (:391-399; fc0 = Linear(1, width), ``.data``: no gradient).
+    u: (B, L, nx, ny); grid_cf: (B, 2, nx, ny).  Returns (B, nx, ny, width)."""
+    xt = torch.cat((grid_cf.to(DT), u.to(DT)), 1)
+    B, T, nx, ny = xt.shape
+    d = nx * ny
+    xf = xt.reshape(B, T, d)
+    a = torch.softmax(xf @ xf.transpose(1, 2) / math.sqrt(d), dim=-1)
+    z = (a @ xf).view(B, T, nx, ny)
+    wt = w.detach().to(DT)[:, 0:1].repeat(1, T) / T
+    return z.permute(0, 2, 3, 1) @ wt.T + b.detach().to(DT)
+
+
+def niofp2d_fno_attn(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
+                     idx: Optional[Sequence[int]] = None,
+                     heads: Sequence[str] = ("fno_drift", "fno_diffusion")) -> torch.Tensor:
+    """NIOFP2D_FNO_attn.forward, 2d_FPE/NIOModules.py:338-408 (NC: fno_Fx/fno_Fy).
+    ``idx`` replaces the train-mode draw (:343-346, WITHOUT replacement); None = eval."""
+    x = x.to(DT)
+    if idx is not None:
+        x = x[:, list(idx)]
+    B, L, nx, ny = x.shape
+    g = grid.to(DT)
+    x_in = x.reshape(B * L, 1, nx, ny)
+    grid_r = g.permute(2, 0, 1).unsqueeze(0).repeat(B * L, 1, 1, 1)
+    inp = torch.cat((x_in, grid_r), 1).permute(0, 2, 3, 1)
+    u = fno2d(sub_params(p, "FNO_input"), inp).view(B, L, nx, ny)
+    gcf = g.unsqueeze(0).repeat(B, 1, 1, 1).permute(0, 3, 1, 2)
+    h = bag_attention(u, gcf, p["fc0.weight"], p["fc0.bias"])
+    return torch.cat([fno2d(sub_params(p, hd), h) for hd in heads], dim=-1)
 
 
 def niofp_fno(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,

@@ -8,7 +8,8 @@ there is no CPU fallback.
 from . import _lib  # noqa: F401
 from ._lib import BlindnoError, load as load_library  # noqa: F401
 from .fno import FNO1d, FNO2d, FNO3d, MLP, SpectralConv1d, SpectralConv2d, SpectralConv3d  # noqa: F401
-from .nio import NIOFP, NIOFP2D, NIOFP2D_FNO, NIOFP_FNO, NIOFP_schrodinger, draw_bag  # noqa: F401
+from .nio import (NIOFP, NIOFP2D, NIOFP2D_FNO, NIOFP2D_FNO_attn, NIOFP_FNO,  # noqa: F401
+                  NIOFP_schrodinger, draw_bag)
 from .deeponet import FFN, DeepOnetNoBiasOrg, FeedForwardNN  # noqa: F401
 from .encoders import ConvBlock, Encoder, Encoder2D  # noqa: F401
 from .ops import mse_loss, pad_amount  # noqa: F401

@@ -66,6 +66,9 @@ SIGNATURES = {
     "blindno_bn_act_nslices": "iii",
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",
+    "blindno_bagattn_nchunk": "i",
+    "blindno_bagattn_fwd": "pppppppp" + "iiii" + "s",
+    "blindno_bagattn_bwd": "ppppppppppp" + "iiii" + "s",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,

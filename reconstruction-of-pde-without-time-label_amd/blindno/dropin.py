@@ -69,6 +69,20 @@ class _NIOFP2D_nc(_nio.NIOFP2D):
                          branch_last_kernel=(3, 2))
 
 
+class _NIOFP2D_FNO_attn_2d(_nio.NIOFP2D_FNO_attn):
+    def __init__(self, input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                 width, modes, output_dim, nx, ny):
+        super().__init__(input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                         width, modes, output_dim, nx, ny, heads=("fno_drift", "fno_diffusion"))
+
+
+class _NIOFP2D_FNO_attn_nc(_nio.NIOFP2D_FNO_attn):
+    def __init__(self, input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                 width, modes, output_dim, nx, ny):
+        super().__init__(input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                         width, modes, output_dim, nx, ny, heads=("fno_Fx", "fno_Fy"))
+
+
 # ------------------------------------------------------------------------------- 1D
 class _NIOFP_FNO_1d(_nio.NIOFP_FNO):
     def __init__(self, fno_layers, width, modes, output_dim, device):
@@ -103,17 +117,19 @@ def _oos(where, *names):
     return {n: _out_of_scope(n, where) for n in names}
 
 
-_2D_OOS = ("NIOFP2D_Trans", "NIOFP2D_Trans_attn", "NIOFP2D_FNO_attn", "NIOFP2D_attn",
+_2D_OOS = ("NIOFP2D_Trans", "NIOFP2D_Trans_attn", "NIOFP2D_attn",
            "NIOFP_ode", "NIOFP3D", "PermInvUNet", "PermInvUNet_attn", "ConvNeXtBlock",
            "TemporalSelfAttention")
 
 EXPERIMENTS = {
     "2d_FPE": dict(
         NIOModules=dict(NIOFP2D=_NIOFP2D_2d, NIOFP2D_FNO=_NIOFP2D_FNO_2d, NIOFP=_NIOFP_1d,
+                        NIOFP2D_FNO_attn=_NIOFP2D_FNO_attn_2d,
                         draw_bag=_nio.draw_bag, **_oos("2d_FPE/NIOModules.py", *_2D_OOS)),
     ),
     "2d_Non_conservative_FPE": dict(
         NIOModules=dict(NIOFP2D=_NIOFP2D_nc, NIOFP2D_FNO=_NIOFP2D_FNO_nc, NIOFP=_NIOFP_1d,
+                        NIOFP2D_FNO_attn=_NIOFP2D_FNO_attn_nc,
                         draw_bag=_nio.draw_bag,
                         **_oos("2d_Non_conservative_FPE/NIOModules.py", *_2D_OOS)),
     ),

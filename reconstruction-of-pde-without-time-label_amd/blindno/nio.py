@@ -171,6 +171,59 @@ class NIOFP2D_FNO(nn.Module):
         return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
 
 
+def draw_bag_distinct(T: int):
+    """Train-mode draw of the attention variant: WITHOUT replacement
+    (2d_FPE/NIOModules.py:344-345)."""
+    L = np.random.randint(50, T)
+    idx = np.random.choice(T, L, replace=False)
+    return L, idx
+
+
+class NIOFP2D_FNO_attn(nn.Module):
+    """FNO-NIO with token self-attention over the bag, 2d_FPE/NIOModules.py:300-408
+    (NC copy with heads fno_Fx/fno_Fy: 2d_Non_conservative_FPE/NIOModules.py:299-407).
+
+    The snapshot encoder FNO_input runs on every snapshot of the bag (HIP FNO2d), then
+    ops.BagAttnFn forms the tokens [gx, gy, u_1..u_L], their softmax(X X^T / sqrt(nx ny))
+    attention and the fc0-weighted token mean (fc0 = Linear(1, width), ``.data``), and the
+    two FNO heads run as in NIOFP2D_FNO.  Registration order (FNO_input, heads, fc0) follows
+    the reference, so a seeded construction gives the reference's initial weights."""
+
+    def __init__(self, input_dimensions_trunk, n_hidden_layers, neurons, n_basis, fno_layers,
+                 width, modes, output_dim, nx, ny,
+                 heads: Sequence[str] = ("fno_drift", "fno_diffusion")):
+        super().__init__()
+        self.fno_layers = fno_layers
+        self.FNO_input = FNO2d(modes=12, width=4, n_layers=2, input_dim=3, output_dim=1)
+        self._heads = tuple(heads)
+        for name in self._heads:
+            setattr(self, name, FNO2d(modes=modes, width=width, n_layers=self.fno_layers,
+                                      input_dim=width, output_dim=1))
+        self.fc0 = nn.Linear(1, width)
+        self.nx = nx
+        self.ny = ny
+
+    def forward(self, x, grid, bag_idx=None):
+        """x (B, T, nx, ny), grid (nx, ny, 2) -> (B, nx, ny, 2).  ``bag_idx`` overrides the
+        train-mode draw (a host index list or a device int tensor)."""
+        ops.require_device(x, grid)
+        if torch.is_tensor(bag_idx) and bag_idx.is_cuda:
+            x = x.index_select(1, bag_idx)
+        elif bag_idx is not None:
+            x = x[:, torch.as_tensor(np.asarray(bag_idx), device=x.device)]
+        elif self.training:
+            _, idx = draw_bag_distinct(x.shape[1])
+            x = x[:, torch.as_tensor(idx, device=x.device)]
+        B, L, nx, ny = x.shape
+        x_in = x.reshape(B * L, 1, nx, ny)
+        grid_r = grid.permute(2, 0, 1).unsqueeze(0).expand(B * L, 2, nx, ny)
+        inp = torch.cat((x_in, grid_r), dim=1).permute(0, 2, 3, 1).contiguous()
+        u = self.FNO_input(inp)                                      # (B*L, nx, ny, 1)
+        h = ops.BagAttnFn.apply(u.reshape(B, L, nx * ny), grid.reshape(nx * ny, 2),
+                                self.fc0.weight.data, self.fc0.bias.data)
+        return _run_heads(self, h.view(B, nx, ny, -1))
+
+
 class NIOFP_FNO(nn.Module):
     """1D FNO-NIO: 1d_FPE/NIOModules.py:87-155 (heads fno_drift/fno_diffusion) or
     1d_GPE/NIOModules.py:228-289 (single head ``fno_V``: ``heads=("fno_V",)``)."""

@@ -921,6 +921,54 @@ class BagMeanFn(torch.autograd.Function):
         return gu, ggrid, None, None, None
 
 
+class BagAttnFn(torch.autograd.Function):
+    """Token self-attention + fixed-weight fusion of NIOFP2D_FNO_attn
+    (2d_FPE/NIOModules.py:365-399): u (B, L, S) encoded snapshots, grid (S, 2) -> (B, S, width).
+    Tokens are [gx, gy, u_1..u_L]; ``w``/``bias`` are ``fc0.weight.data``/``.bias.data``
+    (fc0 = Linear(1, width), never trained).  csrc/attn.hip: Gram matrix, softmax + column
+    sums, and the column-sum-weighted bag mean (the reference's Z = A X collapses to it)."""
+
+    @staticmethod
+    def forward(ctx, u, grid, w, bias):
+        require_device(u, grid, w, bias)
+        u, grid = _c(u), _c(grid)
+        w, bias = _c(w.detach()).view(-1), _c(bias.detach())
+        B, L, S = u.shape
+        T = L + 2
+        if T > 256:
+            raise BlindnoError(f"bag attention supports at most 256 tokens (L + 2), got {T}")
+        if tuple(grid.shape) != (S, 2) or w.numel() != bias.numel():
+            raise BlindnoError(f"bag attention: grid {tuple(grid.shape)} / fc0 {tuple(w.shape)} "
+                               f"do not match S={S}")
+        width = w.numel()
+        nch = query("blindno_bagattn_nchunk", S)
+        partial = _empty(B, nch, T, T, like=u)
+        A = _empty(B, T, T, like=u)
+        cs = _empty(B, T, like=u)
+        y = _empty(B, S, width, like=u)
+        call("blindno_bagattn_fwd", ptr(grid), ptr(u), ptr(w), ptr(bias), ptr(partial), ptr(A),
+             ptr(cs), ptr(y), B, L, S, width, stream_ptr())
+        ctx.save_for_backward(u, grid, w, A, cs)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        u, grid, w, A, cs = ctx.saved_tensors
+        B, L, S = u.shape
+        T = L + 2
+        gy = _c(gy)
+        nch = query("blindno_bagattn_nchunk", S)
+        partial = _empty(B, nch, T, like=gy)
+        dm = _empty(B, S, like=gy)
+        M = _empty(B, T, T, like=gy)
+        du = _empty(B, L, S, like=gy)
+        dgt = _empty(B, 2, S, like=gy) if ctx.needs_input_grad[1] else None
+        call("blindno_bagattn_bwd", ptr(grid), ptr(u), ptr(gy), ptr(w), ptr(A), ptr(cs),
+             ptr(partial), ptr(dm), ptr(M), ptr(du), ptr(dgt), B, L, S, w.numel(), stream_ptr())
+        ggrid = dgt.sum(0).t() if dgt is not None else None
+        return (du if ctx.needs_input_grad[0] else None), ggrid, None, None
+
+
 # ---------------------------------------------------------------------------- loss
 
 

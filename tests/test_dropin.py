@@ -57,9 +57,17 @@ def test_reference_import_lines_work(exp):
 
 
 def test_out_of_scope_classes_raise():
-    r = _run("from NIOModules import NIOFP2D_FNO_attn\ntry:\n    NIOFP2D_FNO_attn(2,3,100,25,3,12,32,2)\n"
+    r = _run("from NIOModules import NIOFP2D_Trans_attn\ntry:\n    NIOFP2D_Trans_attn(2,3,100,25,3,12,32,2)\n"
              "except NotImplementedError as e:\n    print('raised', 'SURVEY' in str(e))\n", "2d_FPE")
     assert r.stdout.strip() == "raised True", r.stderr
+
+
+def test_attention_variant_is_served():
+    r = _run("from NIOModules import NIOFP2D_FNO_attn\n"
+             "m = NIOFP2D_FNO_attn(2,3,100,25,3,12,32,2,64,64)\n"
+             "print(type(m).__mro__[1].__name__, sorted(n for n, _ in m.named_children()))\n",
+             "2d_Non_conservative_FPE")
+    assert r.stdout.strip() == "NIOFP2D_FNO_attn ['FNO_input', 'fc0', 'fno_Fx', 'fno_Fy']", r.stderr
 
 
 def test_launcher_runs_script_with_shims(tmp_path):

@@ -57,6 +57,10 @@ def test_state_dict_layouts_match_reference():
     assert got(blindno.NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, **nc)) == lay["2d_NC.NIOFP2D(2,3,100,25,3,12,32,2)"]
     assert got(blindno.NIOFP_FNO(3, 30, 15, 2, "cpu")) == lay["1d_FPE.NIOFP_FNO(3,30,15,2)"]
     assert got(blindno.NIOFP_FNO(3, 20, 40, 1, "cpu", heads=("fno_V",))) == lay["1d_GPE.NIOFP_FNO(3,20,40,1)"]
+    assert (got(blindno.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 12, 32, 2, 128, 128))
+            == lay["2d.NIOFP2D_FNO_attn(2,3,100,25,3,12,32,2,128,128)"])
+    assert (got(blindno.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 12, 32, 2, 128, 128, heads=("fno_Fx", "fno_Fy")))
+            == lay["2d_NC.NIOFP2D_FNO_attn(2,3,100,25,3,12,32,2,128,128)"])
 
 
 @pytest.mark.parametrize("case,seed,ctor", [
@@ -67,6 +71,9 @@ def test_state_dict_layouts_match_reference():
     ("fno1d", 103, lambda b: b.FNO1d(5, 6, 3, 2, 2)),
     ("nio1d_fno_train", 105, lambda b: b.NIOFP_FNO(3, 6, 5, 2, "cpu")),
     ("gpe_nio_fno_train", 201, lambda b: b.NIOFP_FNO(3, 5, 8, 1, "cpu", heads=("fno_V",))),
+    ("nio2d_fno_attn_train", 401, lambda b: b.NIOFP2D_FNO_attn(2, 3, 100, 25, 2, 6, 5, 2, 20, 20)),
+    ("nc_nio2d_fno_attn_train", 402,
+     lambda b: b.NIOFP2D_FNO_attn(2, 3, 100, 25, 2, 6, 5, 2, 20, 20, heads=("fno_Fx", "fno_Fy"))),
 ])
 def test_same_seed_same_initial_weights(case, seed, ctor):
     """Parameters are created in the reference's order with the reference's init, so a
@@ -111,6 +118,21 @@ def test_bag_draw_matches_reference_semantics():
     assert L == L2 and np.array_equal(idx, idx2)
     g = load_golden("nio2d_fno_train")   # the draw the reference made under seed 13
     assert L == int(g["L"]) and np.array_equal(idx, g["idx"])
+
+
+def test_attn_bag_draw_is_without_replacement():
+    """NIOFP2D_FNO_attn draws its bag WITHOUT replacement (2d_FPE/NIOModules.py:344-345);
+    the recorded reference draw of the golden fixture is reproduced from the same seed."""
+    from blindno.nio import draw_bag_distinct
+    g = load_golden("nio2d_fno_attn_train")
+    np.random.seed(19)
+    L, idx = draw_bag_distinct(60)
+    assert L == int(g["L"]) and np.array_equal(idx, g["idx"])
+    assert len(set(idx.tolist())) == L
+    import blindno
+    m = blindno.NIOFP2D_FNO_attn(2, 3, 100, 25, 2, 6, 5, 2, 16, 16).eval()
+    with pytest.raises(blindno.BlindnoError):
+        m(torch.randn(1, 60, 16, 16), torch.zeros(16, 16, 2))
 
 
 def test_steplr_and_accelerate_quirk():

@@ -98,6 +98,23 @@ def test_niofp2d_fno(case, heads):
     _check(g, y, p, {"x": x, "grid": grid})
 
 
+@pytest.mark.parametrize("case,heads", [("nio2d_fno_attn_train", ("fno_drift", "fno_diffusion")),
+                                        ("nio2d_fno_attn_eval", ("fno_drift", "fno_diffusion")),
+                                        ("nc_nio2d_fno_attn_train", ("fno_Fx", "fno_Fy"))])
+def test_niofp2d_fno_attn(case, heads):
+    """Token self-attention variant (2d_FPE/NIOModules.py:300-408): bag drawn WITHOUT
+    replacement in train mode, fc0 = Linear(1, width)."""
+    g = load_golden(case)
+    p = _leaf(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    grid = torch.from_numpy(g["in.grid"]).double().requires_grad_(True)
+    idx = g["idx"].tolist() if "idx" in g else None
+    if idx is not None:
+        assert len(idx) == int(g["L"]) and len(set(idx)) == len(idx)
+    y = oracle.niofp2d_fno_attn(p, x, grid, idx=idx, heads=heads)
+    _check(g, y, p, {"x": x, "grid": grid})
+
+
 @pytest.mark.parametrize("case,heads", [("nio1d_fno_train", ("fno_drift", "fno_diffusion")),
                                         ("nio1d_fno_eval", ("fno_drift", "fno_diffusion")),
                                         ("gpe_nio_fno_train", ("fno_V",))])
