@@ -1,0 +1,209 @@
+"""Batched evaluation / inference of the 2D snapshot-bag models -- the eval_fno.py path.
+
+Reference: 2d_FPE/eval_fno.py:34-281 (drift / diffusion, npz keys potential + drag) and
+2d_Non_conservative_FPE/eval_fno.py:33-300 (Fx / Fy, npz key F).  The reference evaluates one
+test trajectory at a time: normalise with the TRAIN statistics (:34-54, :66-70), eval-mode
+forward with L = T (every snapshot), de-normalise (:72-99), relative L2 per field (:124-128),
+one ``sample_XXXX_predictions.npy`` dict per index (:228-236) and a ``metrics.csv`` row
+(:180-181, :275).
+
+Here the eval-mode forward -- the only GPU work -- runs on ``batch`` test samples per launch
+chain (eval mode has no batch coupling: FNO layers are per sample and the NIO branch's
+BatchNorm uses running statistics), on the HIP path.  Normalisation, de-normalisation and the
+metrics keep the reference's own float32 numpy sequences, so the numbers written match what
+eval_fno.py writes for the same predictions.  The figures (matplotlib) are out of scope.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import os
+from collections import OrderedDict
+from typing import Dict, Iterable, List, Optional
+
+import numpy as np
+import torch
+
+TRAJ_SCALE = 1e10
+KINDS = {
+    # kind: (target npz keys / scales, output names, metric header)
+    "2d_FPE": dict(fields=("drift", "diffusion"), header=["index", "rel_l2_drift", "rel_l2_diffusion"]),
+    "2d_Non_conservative_FPE": dict(fields=("Fx", "Fy"), header=["index", "rel_l2_Fx", "rel_l2_Fy"]),
+}
+DRIFT_SCALE, DIFFUSION_SCALE, F_SCALE = 1e21, 1e6, 1e12
+
+
+def load_checkpoint_robust(ckpt_path: str, device="cpu") -> "OrderedDict[str, torch.Tensor]":
+    """eval_fno.py:104-122: a raw state_dict or {'state_dict': ...}; leading 'module.'
+    stripped.  Loaded with ``weights_only=True`` (tensors only, nothing executed)."""
+    raw = torch.load(ckpt_path, map_location=device, weights_only=True)
+    if isinstance(raw, dict) and isinstance(raw.get("state_dict"), dict):
+        sd = raw["state_dict"]
+    elif isinstance(raw, dict):
+        sd = raw
+    else:
+        raise RuntimeError(f"Unrecognized checkpoint format at {ckpt_path}")
+    return OrderedDict((k[len("module."):] if k.startswith("module.") else k, v) for k, v in sd.items())
+
+
+def rel_l2(a: np.ndarray, b: np.ndarray, eps: float = 1e-12) -> float:
+    """eval_fno.py:124-128."""
+    return float(np.linalg.norm((a - b).ravel(), 2) / (np.linalg.norm(b.ravel(), 2) + eps))
+
+
+def compute_train_stats(kind: str, train) -> Dict[str, np.ndarray]:
+    """eval_fno.py:34-54 (2d_FPE) / 2d_Non_conservative_FPE/eval_fno.py:37-58.  ``train`` is an
+    npz path or a dict of arrays."""
+    data = np.load(train) if isinstance(train, str) else train
+    traj = np.array(data["trajectories"], dtype=np.float32) * TRAJ_SCALE
+    st = {"traj_mean": traj.mean(axis=(0, 1), keepdims=True),
+          "traj_std": traj.std(axis=(0, 1), keepdims=True) + 1e-8}
+    if kind == "2d_FPE":
+        drift = np.array(data["potential"], dtype=np.float32) * DRIFT_SCALE
+        diff = np.array(data["drag"], dtype=np.float32) * DIFFUSION_SCALE
+        st.update(drift_mean=drift.mean(axis=0, keepdims=True), drift_std=drift.std(axis=0, keepdims=True) + 1e-8,
+                  diff_mean=diff.mean(axis=0, keepdims=True), diff_std=diff.std(axis=0, keepdims=True) + 1e-8)
+    else:
+        F = np.array(data["F"], dtype=np.float32) * F_SCALE
+        st.update(F_mean=F.mean(axis=0, keepdims=True), F_std=F.std(axis=0, keepdims=True) + 1e-8)
+    return st
+
+
+def normalize_input(traj_raw: np.ndarray, stats) -> np.ndarray:
+    """eval_fno.py:66-70 for one (T, Nx, Ny) trajectory."""
+    return (traj_raw * TRAJ_SCALE - stats["traj_mean"].squeeze(0)) / stats["traj_std"].squeeze(0)
+
+
+def denormalize(kind: str, pred: np.ndarray, stats):
+    """eval_fno.py:72-99 for one (Nx, Ny, 2) prediction -> two fields in original units."""
+    if kind == "2d_FPE":
+        a = (pred[..., 0] * stats["drift_std"].squeeze(0) + stats["drift_mean"].squeeze(0)) / DRIFT_SCALE
+        b = (pred[..., 1] * stats["diff_std"].squeeze(0) + stats["diff_mean"].squeeze(0)) / DIFFUSION_SCALE
+        return a, b
+    mean = np.transpose(stats["F_mean"].squeeze(0), (1, 2, 0))
+    std = np.transpose(stats["F_std"].squeeze(0), (1, 2, 0))
+    return ((pred[..., 0] * std[..., 0] + mean[..., 0]) / F_SCALE,
+            (pred[..., 1] * std[..., 1] + mean[..., 1]) / F_SCALE)
+
+
+def true_fields(kind: str, data, index: int, stats):
+    """The reference's normalise -> de-normalise round trip of the true fields
+    (eval_fno.py:218-223; 2d_Non_conservative_FPE/eval_fno.py:261-267)."""
+    if kind == "2d_FPE":
+        out = []
+        for key, scale, m, s in (("potential", DRIFT_SCALE, "drift_mean", "drift_std"),
+                                 ("drag", DIFFUSION_SCALE, "diff_mean", "diff_std")):
+            raw = np.array(data[key][index], dtype=np.float32)
+            mu, sd = stats[m].squeeze(0), stats[s].squeeze(0)
+            out.append(((raw * scale - mu) / sd * sd + mu) / scale)
+        return tuple(out)
+    F = np.array(data["F"][index], dtype=np.float32)
+    mu, sd = stats["F_mean"].squeeze(0), stats["F_std"].squeeze(0)
+    return tuple(((F[c] * F_SCALE - mu[c]) / sd[c] * sd[c] + mu[c]) / F_SCALE for c in (0, 1))
+
+
+def grid2d(nx: int, ny: int, device) -> torch.Tensor:
+    gx, gy = np.meshgrid(np.linspace(-1, 1, nx, dtype=np.float32),
+                         np.linspace(-1, 1, ny, dtype=np.float32), indexing="ij")
+    return torch.tensor(np.stack([gx, gy], axis=2), device=device)
+
+
+@torch.no_grad()
+def predict(model: torch.nn.Module, x: torch.Tensor, grid: torch.Tensor, batch: int = 8) -> torch.Tensor:
+    """Eval-mode predictions (n, Nx, Ny, 2) of normalised bags x (n, T, Nx, Ny) in HBM,
+    ``batch`` samples per forward."""
+    was = model.training
+    model.eval()
+    try:
+        outs = [model(x[i:i + batch], grid) for i in range(0, x.shape[0], batch)]
+    finally:
+        model.train(was)
+    out = torch.cat(outs, 0)
+    if out.shape[1] == 2 and out.shape[-1] != 2:
+        out = out.permute(0, 2, 3, 1)
+    return out.contiguous()
+
+
+def evaluate(kind: str, model: torch.nn.Module, train, test, indices: Iterable[int],
+             outdir: Optional[str] = None, batch: int = 8, device="cuda") -> List[list]:
+    """The eval_fno.py loop over ``indices`` (out-of-range ones skipped, :196-201).  Returns the
+    metrics rows [index, rel_l2_a, rel_l2_b]; with ``outdir`` also writes the per-sample .npy
+    dicts and appends metrics.csv exactly as the reference does."""
+    names = KINDS[kind]["fields"]
+    stats = compute_train_stats(kind, train)
+    data = np.load(test) if isinstance(test, str) else test
+    traj = np.asarray(data["trajectories"])
+    M = traj.shape[0]
+    idx = [i for i in indices if 0 <= i < M]
+    nx, ny = traj.shape[2], traj.shape[3]
+    x = np.stack([normalize_input(np.array(traj[i], dtype=np.float32), stats) for i in idx]) if idx else \
+        np.zeros((0,) + traj.shape[1:], np.float32)
+    xd = torch.tensor(x, dtype=torch.float32, device=device)
+    pred = predict(model, xd, grid2d(nx, ny, device), batch).cpu().numpy() if idx else None
+    rows = []
+    writer = f_csv = None
+    if outdir is not None:
+        os.makedirs(outdir, exist_ok=True)
+        path = os.path.join(outdir, "metrics.csv")
+        header = not os.path.exists(path)
+        f_csv = open(path, "a", newline="")
+        writer = csv.writer(f_csv)
+        if header:
+            writer.writerow(KINDS[kind]["header"])
+    try:
+        for k, i in enumerate(idx):
+            pa, pb = denormalize(kind, pred[k], stats)
+            ta, tb = true_fields(kind, data, i, stats)
+            row = [i, rel_l2(pa, ta), rel_l2(pb, tb)]
+            rows.append(row)
+            if writer is not None:
+                np.save(os.path.join(outdir, f"sample_{i:04d}_predictions.npy"), {
+                    "index": i,
+                    f"{names[0]}_pred": pa.astype(np.float32), f"{names[1]}_pred": pb.astype(np.float32),
+                    f"{names[0]}_true": ta.astype(np.float32), f"{names[1]}_true": tb.astype(np.float32)})
+                writer.writerow(row)
+    finally:
+        if f_csv is not None:
+            f_csv.close()
+    return rows
+
+
+def main(argv=None):
+    """CLI mirroring eval_fno.py's arguments (:131-150) plus --experiment, --model, --batch."""
+    from . import nio
+    ap = argparse.ArgumentParser(description="Batched evaluation of a trained 2D snapshot-bag model.")
+    ap.add_argument("--experiment", choices=sorted(KINDS), default="2d_FPE")
+    ap.add_argument("--model", choices=["NIOFP2D_FNO", "NIOFP2D_FNO_attn", "NIOFP2D"], default="NIOFP2D_FNO")
+    ap.add_argument("--train_data", required=True)
+    ap.add_argument("--test_data", required=True)
+    ap.add_argument("--ckpt", required=True)
+    ap.add_argument("--outdir", default="result_fig/fno")
+    ap.add_argument("--start", type=int, default=33)
+    ap.add_argument("--end", type=int, default=64)
+    ap.add_argument("--nx", type=int, default=61)
+    ap.add_argument("--ny", type=int, default=61)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--strict", action="store_true")
+    a = ap.parse_args(argv)
+    heads = ("fno_drift", "fno_diffusion") if a.experiment == "2d_FPE" else ("fno_Fx", "fno_Fy")
+    if a.model == "NIOFP2D_FNO_attn":
+        model = nio.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 12, 32, 2, a.nx, a.ny, heads=heads)
+    else:
+        cls = getattr(nio, a.model)
+        model = cls(2, 3, 100, 25, 3, 12, 32, 2, heads=heads,
+                    branch_last_kernel=(2, 1) if a.experiment == "2d_FPE" else (3, 2))
+    ret = model.load_state_dict(load_checkpoint_robust(a.ckpt), strict=a.strict)
+    if ret.missing_keys or ret.unexpected_keys:
+        print("[Warn] Incompatible keys when loading:", ret.missing_keys, ret.unexpected_keys)
+    model = model.to(a.device)
+    rows = evaluate(a.experiment, model, a.train_data, a.test_data, range(a.start, a.end + 1),
+                    outdir=a.outdir, batch=a.batch, device=a.device)
+    for r in rows:
+        print(f"[Metrics] index={r[0]}  {KINDS[a.experiment]['header'][1]}={r[1]:.6f}  "
+              f"{KINDS[a.experiment]['header'][2]}={r[2]:.6f}")
+    print(f"[Info] Metrics saved to: {os.path.join(a.outdir, 'metrics.csv')}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,93 @@
+"""The eval_fno.py path (blindno.evaluate): host math pinned to the reference's own functions
+(golden eval_2d_*.npz from tests/golden/make_golden_eval.py), checkpoint loading, and the
+batched GPU evaluation against the float64 oracle run sample by sample, as the reference
+loops (GPU part marked)."""
+import csv
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+KINDS = [("2d_FPE", "eval_2d_fpe"), ("2d_Non_conservative_FPE", "eval_2d_nc")]
+
+
+def _split(g, prefix):
+    return {k[len(prefix):]: v for k, v in g.items() if k.startswith(prefix)}
+
+
+@pytest.mark.parametrize("kind,case", KINDS)
+def test_host_math_matches_reference(kind, case):
+    from blindno import evaluate as ev
+    g = load_golden(case)
+    st = ev.compute_train_stats(kind, _split(g, "train."))
+    ref = _split(g, "stats.")
+    assert sorted(st) == sorted(ref)
+    for k in ref:
+        assert np.array_equal(st[k], ref[k]), k
+    te = _split(g, "test.")
+    for i in range(2):
+        assert np.array_equal(ev.normalize_input(te["trajectories"][i], st), g[f"x_norm{i}"])
+        pa, pb = ev.denormalize(kind, g["pred"][i], st)
+        assert np.array_equal(pa, g[f"pred_a{i}"]) and np.array_equal(pb, g[f"pred_b{i}"])
+        ta, tb = ev.true_fields(kind, te, i, st)
+        assert np.array_equal(ta, g[f"true_a{i}"]) and np.array_equal(tb, g[f"true_b{i}"])
+        assert ev.rel_l2(pa, ta) == float(g[f"rel_a{i}"])
+        assert ev.rel_l2(pb, tb) == float(g[f"rel_b{i}"])
+
+
+def test_checkpoint_robust_loading(tmp_path):
+    from blindno import evaluate as ev
+    sd = {"module.fc0.weight": torch.ones(2, 3), "module.fc0.bias": torch.zeros(2)}
+    p1, p2 = tmp_path / "a.pt", tmp_path / "b.pt"
+    torch.save(sd, p1)
+    torch.save({"state_dict": sd, "epoch": 3}, p2)
+    for p in (p1, p2):
+        out = ev.load_checkpoint_robust(str(p))
+        assert list(out) == ["fc0.weight", "fc0.bias"]
+    torch.save([1, 2], tmp_path / "c.pt")
+    with pytest.raises(RuntimeError):
+        ev.load_checkpoint_robust(str(tmp_path / "c.pt"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["2d_FPE", "2d_Non_conservative_FPE"])
+def test_batched_gpu_eval_matches_per_sample_oracle(kind, tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import oracle
+    from blindno import NIOFP2D_FNO
+    from blindno import evaluate as ev
+    heads = ("fno_drift", "fno_diffusion") if kind == "2d_FPE" else ("fno_Fx", "fno_Fy")
+    rs = np.random.RandomState(3)
+    M, T, N = 6, 60, 20
+    mk = (lambda m: dict(trajectories=(rs.rand(m, T, N, N) * 1e-10).astype(np.float32),
+                         potential=(rs.randn(m, N, N) * 1e-21).astype(np.float32),
+                         drag=(rs.rand(m, N, N) * 1e-6).astype(np.float32))) if kind == "2d_FPE" else \
+         (lambda m: dict(trajectories=(rs.rand(m, T, N, N) * 1e-10).astype(np.float32),
+                         F=(rs.randn(m, 2, N, N) * 1e-12).astype(np.float32)))
+    train, test = mk(M), mk(5)
+    torch.manual_seed(2)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 2, 6, 5, 2, heads=heads).cuda()
+    rows = ev.evaluate(kind, m, train, test, range(-1, 7), outdir=str(tmp_path), batch=2)
+    assert [r[0] for r in rows] == [0, 1, 2, 3, 4]            # out-of-range indices skipped
+    assert m.training                                          # mode restored
+    st = ev.compute_train_stats(kind, train)
+    p = {k: v.detach().cpu().double() for k, v in m.state_dict().items() if not k.startswith("branch.")}
+    grid = ev.grid2d(N, N, "cpu")
+    for r in rows:
+        i = r[0]
+        x = torch.tensor(ev.normalize_input(test["trajectories"][i], st)[None])
+        ref = oracle.niofp2d_fno(p, x, grid, idx=None, heads=heads)[0].numpy().astype(np.float32)
+        ra, rb = ev.denormalize(kind, ref, st)
+        ta, tb = ev.true_fields(kind, test, i, st)
+        assert abs(r[1] - ev.rel_l2(ra, ta)) <= 1e-5 * abs(ev.rel_l2(ra, ta))
+        assert abs(r[2] - ev.rel_l2(rb, tb)) <= 1e-5 * abs(ev.rel_l2(rb, tb))
+    with open(tmp_path / "metrics.csv") as f:
+        got = list(csv.reader(f))
+    assert got[0] == ev.KINDS[kind]["header"] and len(got) == 6
+    d = np.load(tmp_path / "sample_0003_predictions.npy", allow_pickle=True).item()   # our own file
+    assert d["index"] == 3 and d[f"{ev.KINDS[kind]['fields'][0]}_pred"].shape == (N, N)
+    assert os.path.exists(tmp_path / "sample_0000_predictions.npy")
