@@ -47,23 +47,45 @@ constexpr int kBwdNP4 = PROJ_BWD_NP4;
 // consecutive points (Bg samples); group g's weights sit at + g wgs and its outputs at channel
 // offset ooff + g goff of the shared output sample.
 constexpr int kMaxGroups = 2;
+
+// Division by a launch-invariant divisor as one v_mul_hi_u32 + add + shift (Granlund-Montgomery
+// round-up multiplier): exact for every n < 2^31.  The point -> (sample, row, column) mapping of
+// the projection divides each lane's point index by Ho*Wo and Wo; as generic 32-bit divisions
+// those cost ~25 VALU each and were a third of project_bwd's instruction stream.
+struct FastDiv {
+  unsigned m, s;
+  static FastDiv make(unsigned d) {
+    unsigned l = 0;
+    while ((1ull << l) < d) ++l;
+    const uint64_t m = (((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1;
+    return FastDiv{(unsigned)m, l};
+  }
+  __device__ __forceinline__ unsigned div(unsigned n) const {
+    return (__umulhi(n, m) + n) >> s;
+  }
+};
+
 struct Groups {
   int G;
   unsigned gpts;
   int64_t wgs;
   int goff;
   const float* lscale;   // backward: dout of sample n scaled by lscale[n % dout_div] (nullable)
+  FastDiv dHoWo, dWo, dDoutDiv;   // divisors Ho*Wo, Wo, dout_div (backward)
 };
 
 struct PointMap {
   unsigned HoWo, Wo;
   int64_t HW;
   int P2, C;
-  __device__ __forceinline__ int64_t zoff(unsigned p, unsigned& n, unsigned& q) const {
-    n = p / HoWo;
+  FastDiv dHoWo, dWo;
+  // 32-bit offsets: the launchers require the field to hold < 2^31 elements
+  // (project_mfma_ok), so n C HW + h P2 + w never wraps
+  __device__ __forceinline__ unsigned zoff(unsigned p, unsigned& n, unsigned& q) const {
+    n = dHoWo.div(p);
     q = p - n * HoWo;
-    const unsigned h = q / Wo, w = q - (q / Wo) * Wo;
-    return (int64_t)n * C * HW + (int64_t)h * P2 + w;
+    const unsigned h = dWo.div(q), w = q - h * Wo;
+    return n * (unsigned)(C * HW) + h * (unsigned)P2 + w;
   }
 };
 
@@ -157,11 +179,11 @@ template <int KS>
 __device__ __forceinline__ void load_az(const float* __restrict__ z, const PointMap& pm,
                                         unsigned p, unsigned npts, int g4, float (&az)[KS]) {
   unsigned n, q;
-  const int64_t zo = pm.zoff(p < npts ? p : 0, n, q);
+  const unsigned zo = pm.zoff(p < npts ? p : 0, n, q);
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk) {
     const int ch = 4 * kk + g4;
-    az[kk] = (p < npts && ch < pm.C) ? z[zo + (int64_t)ch * pm.HW] : 0.f;
+    az[kk] = (p < npts && ch < pm.C) ? z[zo + (unsigned)ch * (unsigned)pm.HW] : 0.f;
   }
 }
 
@@ -180,7 +202,7 @@ __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
-  const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C};
+  const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C, gr.dHoWo, gr.dWo};
   const unsigned ngroups = (npts + 16 * NP - 1) / (16 * NP);
   for (unsigned grp = blockIdx.x * kWaves + wave; grp < ngroups; grp += gridDim.x * kWaves) {
     // weight group of this step's points (uniform: the launcher checks group alignment)
@@ -299,7 +321,8 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
   float gb2[COM];
 #pragma unroll
   for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
-  const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C};
+  const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C, gr.dHoWo, gr.dWo};
+  const bool row4 = (Wo & 3) == 0;
   const unsigned ngroups = (gpts + 16 * NP - 1) / (16 * NP);
   for (unsigned grp = blockIdx.x * kWaves + wave; grp < ngroups; grp += gridDim.x * kWaves) {
     float az[NP][KS], zb[NP][4], gv[NP][4][COM];
@@ -309,17 +332,27 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
       const unsigned tile = grp * NP + np;
       load_az<KS>(z, pm, pbase + tile * 16 + c16, npts, g4, az[np]);
       // this lane's 4 points (D layout rows): z column c16 (1.0 at c16 == C: db1), dout
+      // When Wo % 4 == 0 the lane's 4 points (4-aligned) share one sample and grid row, so one
+      // point -> offset mapping serves all four (row4, kernel-uniform)
+      unsigned zo = 0, n = 0, q = 0;
+      const float* gp = dout;
+      float ls = 1.0f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const unsigned p = pbase + tile * 16 + 4 * g4 + r;
         const bool ok = p < npts;
-        unsigned n, q;
-        zo4[np][r] = (int)pm.zoff(ok ? p : 0, n, q);
+        if (r == 0 || !row4) {
+          zo = pm.zoff(ok ? p : 0, n, q);
+          const unsigned nb = gr.dDoutDiv.div(n - nbase);
+          gp = dout + ((nb * pm.HoWo + q) * (unsigned)ostride + (unsigned)(ooff + g * gr.goff));
+          ls = gr.lscale ? gr.lscale[(n - nbase) - nb * (unsigned)dout_div] : 1.0f;
+        } else {
+          zo += 1;
+          gp += ostride;
+        }
+        zo4[np][r] = (int)zo;
         const int zc = kGW44 ? (c16 & 3) : c16;
-        zb[np][r] = !ok ? 0.f : (zc < C ? z[zo4[np][r] + (int64_t)zc * pm.HW] : (zc == C ? 1.f : 0.f));
-        const float* gp = dout + ((int64_t)((n - nbase) / (unsigned)dout_div) * pm.HoWo + q) * ostride +
-                          ooff + g * gr.goff;
-        const float ls = gr.lscale ? gr.lscale[(n - nbase) % (unsigned)dout_div] : 1.0f;
+        zb[np][r] = !ok ? 0.f : (zc < C ? z[zo + (unsigned)zc * (unsigned)pm.HW] : (zc == C ? 1.f : 0.f));
 #pragma unroll
         for (int c = 0; c < COM; ++c) gv[np][r][c] = (ok && c < Cout) ? gp[c] * ls : 0.f;
       }
@@ -428,7 +461,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
 #pragma unroll
         for (int m = 0; m < NV / 16; ++m) {
           const int ch = 4 * m + (c16 >> 2);
-          if (ch < C) dz[zo4[np][r] + (int64_t)ch * pm.HW] = kInvK * dzp[np][16 * m];
+          if (ch < C) dz[(unsigned)zo4[np][r] + (unsigned)ch * (unsigned)pm.HW] = kInvK * dzp[np][16 * m];
         }
       }
     }
@@ -496,7 +529,8 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
                      int Cout, int ostride, int ooff, int G, int64_t wgs, hipStream_t st) {
   if (G < 1 || G > kMaxGroups || Bn % G) return (int)hipErrorInvalidValue;
   const unsigned npts = (unsigned)((int64_t)Bn * Ho * Wo);
-  const Groups gr{G, npts / (unsigned)G, G > 1 ? wgs : 0, Cout, nullptr};
+  const Groups gr{G, npts / (unsigned)G, G > 1 ? wgs : 0, Cout, nullptr,
+                  FastDiv::make((unsigned)(Ho * Wo)), FastDiv::make((unsigned)Wo), FastDiv::make(1)};
   const unsigned ntiles = (npts + 15) / 16;
   unsigned blocks = (ntiles + kWaves * PF_TPW - 1) / (kWaves * PF_TPW);
   if (blocks > 2048) blocks = 2048;
@@ -526,9 +560,13 @@ int project_bwd_mfma(const float* z, const float* w1, const float* b1, const flo
                      const float* dout, float* dz, float* partial, int nchunk, int Bn, int C,
                      int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff,
                      int dout_div, int G, int64_t wgs, hipStream_t st, const float* lscale) {
-  if (G < 1 || G > kMaxGroups || Bn % G) return (int)hipErrorInvalidValue;
+  if (G < 1 || G > kMaxGroups || Bn % G || dout_div < 1) return (int)hipErrorInvalidValue;
+  // 32-bit dout offsets (see PointMap)
+  if ((int64_t)(Bn / G / dout_div + 1) * Ho * Wo * ostride + ooff + Cout >= INT32_MAX)
+    return (int)hipErrorInvalidValue;
   const unsigned gpts = (unsigned)((int64_t)(Bn / G) * Ho * Wo);
-  const Groups gr{G, gpts, G > 1 ? wgs : 0, Cout, lscale};
+  const Groups gr{G, gpts, G > 1 ? wgs : 0, Cout, lscale, FastDiv::make((unsigned)(Ho * Wo)),
+                  FastDiv::make((unsigned)Wo), FastDiv::make((unsigned)dout_div)};
   const dim3 grid(nchunk, G);
 #define PB(CK_, CO_)                                                                          \
   project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kBwdNP4 : 1)><<<grid, 256, 0, st>>>(            \
