@@ -254,6 +254,12 @@ int blindno_rowsq(const float* a, const float* b, double* out, int rows, int n, 
 
 /* Fused Adam over a flat fp32 buffer (torch.optim.Adam, no weight decay / amsgrad):
  * step_size = lr / (1 - beta1^t), bc2s = sqrt(1 - beta2^t). grad is scaled by gscale. */
+/* Gather nseg gradient segments into one flat buffer: dst[offs[i] + j] = srcs[i][j], j < ns[i].
+ * srcs / offs / ns are HOST arrays (device pointers inside srcs), copied into the kernel
+ * arguments, so a HIP-graph capture keeps them.  Replaces FlatAdam's per-parameter gradient
+ * copy (the reference's DDP bucket flatten, 2d_FPE/train_fno.py:121,143). */
+int blindno_gather_flat(const void* const* srcs, const int64_t* offs, const int64_t* ns, int nseg,
+                        float* dst, blindno_stream_t stream);
 int blindno_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1,
                  float beta2, float eps, float step_size, float bc2s, float gscale,
                  blindno_stream_t stream);

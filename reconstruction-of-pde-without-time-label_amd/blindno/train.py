@@ -14,6 +14,7 @@ gradients give Adam updates of exactly zero.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Iterable, List, Optional
 
@@ -79,7 +80,14 @@ class FlatAdam:
             if p.grad is None:
                 raise RuntimeError("FlatAdam: a trained parameter received no gradient")
             gs.append(_real(p.grad).reshape(-1))
-        torch._foreach_copy_(self._gviews, gs)
+        if self.grad.is_cuda and all(g.is_contiguous() for g in gs):
+            # one blindno_gather_flat launch (segments as kernel arguments; graph-capturable)
+            srcs = (ctypes.c_void_p * len(gs))(*[g.data_ptr() for g in gs])
+            offs = (ctypes.c_int64 * len(gs))(*self.offsets)
+            ns = (ctypes.c_int64 * len(gs))(*[g.numel() for g in gs])
+            call("blindno_gather_flat", srcs, offs, ns, len(gs), ptr(self.grad), stream_ptr())
+        else:
+            torch._foreach_copy_(self._gviews, gs)
         return self.grad
 
     def step(self, grad_scale: float = 1.0, gather: bool = True):

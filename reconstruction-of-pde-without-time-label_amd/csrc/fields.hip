@@ -841,6 +841,59 @@ BLINDNO_API int blindno_rowsq(const float* a, const float* b, double* out, int r
   return (int)hipGetLastError();
 }
 
+// Flat gradient gather: up to kGatherSegs (src, dst offset, count) segments per launch, passed
+// by value in the kernel arguments (so a HIP-graph capture bakes them in).  Segment i owns
+// blocks [cum[i], cum[i+1]) of kGatherChunk elements, so the grid is proportional to the bytes
+// moved; replaces a torch multi-tensor copy of ~100 blocks.
+constexpr int kGatherSegs = 64;
+constexpr int kGatherChunk = 8 * kBlock;
+struct GatherSegs {
+  const float* src[kGatherSegs];
+  int64_t off[kGatherSegs];
+  int n[kGatherSegs];
+  int cum[kGatherSegs + 1];
+  int nseg;
+};
+
+__global__ __launch_bounds__(kBlock) void gather_flat_kernel(GatherSegs segs, float* __restrict__ dst) {
+  const int b = blockIdx.x;
+  int sg = 0;
+  while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;    // uniform scan
+  const float* __restrict__ src = segs.src[sg];
+  float* __restrict__ d = dst + segs.off[sg];
+  const int n = segs.n[sg];
+  const int i0 = (b - segs.cum[sg]) * kGatherChunk + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = i0 + k * kBlock;
+    if (i < n) d[i] = src[i];
+  }
+}
+
+BLINDNO_API int blindno_gather_flat(const void* const* srcs, const int64_t* offs, const int64_t* ns,
+                                    int nseg, float* dst, void* stream) {
+  if (nseg < 0) return (int)hipErrorInvalidValue;
+  for (int s0 = 0; s0 < nseg; s0 += kGatherSegs) {
+    GatherSegs segs{};
+    const int k = nseg - s0 < kGatherSegs ? nseg - s0 : kGatherSegs;
+    segs.nseg = k;
+    int64_t blocks = 0;
+    for (int i = 0; i < k; ++i) {
+      if (ns[s0 + i] < 0 || ns[s0 + i] >= INT32_MAX) return (int)hipErrorInvalidValue;
+      segs.src[i] = (const float*)srcs[s0 + i];
+      segs.off[i] = offs[s0 + i];
+      segs.n[i] = (int)ns[s0 + i];
+      segs.cum[i] = (int)blocks;
+      blocks += (ns[s0 + i] + kGatherChunk - 1) / kGatherChunk;
+    }
+    segs.cum[k] = (int)blocks;
+    if (blocks == 0) continue;
+    if (blocks >= INT32_MAX) return (int)hipErrorInvalidValue;
+    gather_flat_kernel<<<(unsigned)blocks, kBlock, 0, (hipStream_t)stream>>>(segs, dst);
+  }
+  return (int)hipGetLastError();
+}
+
 BLINDNO_API int blindno_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1,
                              float beta2, float eps, float step_size, float bc2s, float gscale,
                              void* stream) {

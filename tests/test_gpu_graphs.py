@@ -62,3 +62,26 @@ def test_graphed_steps_match_eager(case):
         ropt.zero_grad()
     torch.cuda.synchronize()
     assert rel_l2(opt.flat.cpu().numpy(), ropt.flat.cpu().numpy()) <= 1e-6
+
+
+def test_gather_flat_segments():
+    """blindno_gather_flat (FlatAdam's gradient gather): odd offsets, empty and multi-launch
+    (> 64 segments) lists, sizes straddling the 2048-element block chunk."""
+    import ctypes
+    from blindno._lib import call, ptr, stream_ptr
+    rs = np.random.RandomState(0)
+    sizes = [0, 1, 2047, 2048, 2049, 5000] + list(rs.randint(1, 3000, 70))
+    srcs = [torch.randn(n, device="cuda") for n in sizes]
+    offs, o = [], 3
+    for n in sizes:
+        offs.append(o)
+        o += n + 1
+    dst = torch.full((o,), -7.0, device="cuda")
+    k = len(sizes)
+    call("blindno_gather_flat", (ctypes.c_void_p * k)(*[t.data_ptr() for t in srcs]),
+         (ctypes.c_int64 * k)(*offs), (ctypes.c_int64 * k)(*sizes), k, ptr(dst), stream_ptr())
+    ref = torch.full((o,), -7.0, device="cuda")
+    for t, off in zip(srcs, offs):
+        ref[off:off + t.numel()] = t
+    torch.cuda.synchronize()
+    assert torch.equal(dst, ref)
