@@ -283,6 +283,18 @@ int blindno_gpe_solve(const double* psi0, const double* V, const double* g, cons
 int blindno_trapz_rows(const double* a, const double* b, const double* x, double* out, int rows,
                        int n, blindno_stream_t stream);
 
+/* Batched FPE master-equation propagation (fplanck fokker_planck.propagate_interval, used by
+ * 1d_FPE/compute_time_error.py:215-238 and 2d_Non_conservative_FPE/compute_time_error.py:
+ * 300-319; fplanck is not shipped: restated, parity unpinned).  One workgroup per trajectory,
+ * fp64, N = nx*ny <= 8192 cells (1D: ny = 1), cell i = ix*ny + iy.  coef (B, 5, N) =
+ * [diag, cxm, cxp, cym, cyp]: (M p)_i = cxm_i p_{i-ex} + cxp_i p_{i+ex} + cym_i p_{i-ey} +
+ * cyp_i p_{i+ey} - diag_i p_i (neighbour indices wrap; zero coefficients make a wall).
+ * out (B, nout, N): p at t = o*dt_out, o < nout, out[:,0] = p0.  Each interval is
+ * `substeps` steps of the degree-`degree` Taylor polynomial of exp(dt_out/substeps M). */
+int blindno_fp_propagate(const double* p0, const double* coef, double* out, int B, int nx,
+                         int ny, int nout, int substeps, int degree, double dt_out,
+                         blindno_stream_t stream);
+
 /* ---- grouped launches: two FNO heads over one field in one chain (ops.HeadPairFn) ----------
  * G weight groups over consecutive blocks of Bg = Bn/G samples.  Group g's small weights (fc0,
  * 1x1 convs, fc1/fc2 -- packed per head in one buffer) are read at + g*wgs floats from the

@@ -67,6 +67,7 @@ SIGNATURES = {
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",
     "blindno_gather_flat": "pppips",
+    "blindno_fp_propagate": "pppiiiiiids",
     "blindno_bagattn_nchunk": "i",
     "blindno_bagattn_fwd": "pppppppp" + "iiii" + "s",
     "blindno_bagattn_bwd": "ppppppppppp" + "iiii" + "s",

@@ -215,6 +215,80 @@ __global__ __launch_bounds__(kBlock) void trapz_rows_kernel(const double* __rest
   }
 }
 
+
+// ---------------------------------------------------------------- FPE master equation
+// dp/dt = M p on a 1D / 2D grid of N = nx*ny cells (x-major, cell i = ix*ny + iy), the
+// finite-volume master equation fplanck builds (fokker_planck.master_matrix; used by
+// 1d_FPE/compute_time_error.py:215-238, 2d_Non_conservative_FPE/compute_time_error.py:300-319):
+//   (M p)_i = cxm_i p_{i-ex} + cxp_i p_{i+ex} + cym_i p_{i-ey} + cyp_i p_{i+ey} - diag_i p_i
+// coef (B, 5, N) = [diag, cxm, cxp, cym, cyp] per trajectory (in-rates from the neighbours, zero
+// across a reflecting wall; neighbour indices wrap, which is the periodic case).
+// One workgroup per trajectory: p (CPT cells per thread) in registers, the Taylor iterate
+// ping-pongs in LDS.  Each output interval is s substeps of exp(h M) ~ degree-m Taylor polynomial
+// in Horner form  w <- p + (h/k) M w,  k = m..1.
+template <int CPT>
+__global__ __launch_bounds__(1024) void fp_propagate_kernel(const double* __restrict__ p0,
+                                                            const double* __restrict__ coef,
+                                                            double* __restrict__ out, int N,
+                                                            int nx, int ny, int nout, int s,
+                                                            int m, double h) {
+  extern __shared__ double fsm[];
+  double* wa = fsm;
+  double* wb = fsm + N;
+  const int b = blockIdx.x;
+  const double* cf = coef + (int64_t)b * 5 * N;
+  double p[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int i = threadIdx.x + c * blockDim.x;
+    p[c] = i < N ? p0[(int64_t)b * N + i] : 0.0;
+    if (i < N) out[(int64_t)b * nout * N + i] = p[c];
+  }
+  for (int o = 1; o < nout; ++o) {
+    for (int sub = 0; sub < s; ++sub) {
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const int i = threadIdx.x + c * blockDim.x;
+        if (i < N) wa[i] = p[c];
+      }
+      __syncthreads();
+      for (int k = m; k >= 1; --k) {
+        const double hk = h / (double)k;
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+          const int i = threadIdx.x + c * blockDim.x;
+          if (i < N) {
+            const int ix = i / ny, iy = i - ix * ny;
+            const int xm = (ix == 0 ? nx - 1 : ix - 1) * ny + iy;
+            const int xp = (ix == nx - 1 ? 0 : ix + 1) * ny + iy;
+            const int ym = ix * ny + (iy == 0 ? ny - 1 : iy - 1);
+            const int yp = ix * ny + (iy == ny - 1 ? 0 : iy + 1);
+            double mw = -cf[i] * wa[i];
+            mw = fma(cf[N + i], wa[xm], mw);
+            mw = fma(cf[2 * N + i], wa[xp], mw);
+            mw = fma(cf[3 * N + i], wa[ym], mw);
+            mw = fma(cf[4 * N + i], wa[yp], mw);
+            wb[i] = fma(hk, mw, p[c]);
+          }
+        }
+        __syncthreads();
+        double* t = wa; wa = wb; wb = t;
+      }
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const int i = threadIdx.x + c * blockDim.x;
+        if (i < N) p[c] = wa[i];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int i = threadIdx.x + c * blockDim.x;
+      if (i < N) out[((int64_t)b * nout + o) * N + i] = p[c];
+    }
+  }
+}
+
 }  // namespace
 
 BLINDNO_API int blindno_gpe_solve(const double* psi0, const double* V, const double* g,
@@ -240,5 +314,26 @@ BLINDNO_API int blindno_trapz_rows(const double* a, const double* b, const doubl
                                    int rows, int n, void* stream) {
   if (rows <= 0 || n < 1) return (int)hipErrorInvalidValue;
   trapz_rows_kernel<<<rows, kBlock, 0, (hipStream_t)stream>>>(a, b, x, out, n);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_fp_propagate(const double* p0, const double* coef, double* out, int B,
+                                     int nx, int ny, int nout, int substeps, int degree,
+                                     double dt_out, void* stream) {
+  const int64_t N = (int64_t)nx * ny;
+  if (B <= 0 || nx < 1 || ny < 1 || nout < 1 || substeps < 1 || degree < 1 || N > 8192)
+    return (int)hipErrorInvalidValue;
+  const size_t sh = sizeof(double) * 2 * (size_t)N;
+  const int threads = N <= 256 ? 256 : (N <= 1024 ? 1024 : 1024);
+  const int cpt = (int)((N + threads - 1) / threads);
+  const double h = dt_out / substeps;
+  hipStream_t st = (hipStream_t)stream;
+#define FPL(C_) fp_propagate_kernel<C_><<<B, threads, sh, st>>>(p0, coef, out, (int)N, nx, ny, nout, \
+                                                               substeps, degree, h)
+  if (cpt <= 1) FPL(1);
+  else if (cpt <= 2) FPL(2);
+  else if (cpt <= 4) FPL(4);
+  else FPL(8);
+#undef FPL
   return (int)hipGetLastError();
 }

@@ -83,3 +83,12 @@ def test_launcher_runs_script_with_shims(tmp_path):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "blindno.nio True"
+
+
+def test_fplanck_shim_names():
+    # compute_time_error.py's `from fplanck import fokker_planck, boundary, gaussian_pdf`
+    r = _run("from fplanck import fokker_planck, boundary, gaussian_pdf, potential_from_data\n"
+             "s = fokker_planck(temperature=300, drag=1e-9, extent=[100e-9, 80e-9], resolution=10e-9,\n"
+             "                  force=lambda x, y: [0 * x, 0 * y], boundary=boundary.reflecting)\n"
+             "print(s.grid.shape)\n", "2d_Non_conservative_FPE")
+    assert r.stdout.strip() == "(2, 10, 8)", r.stderr

@@ -1,0 +1,137 @@
+"""FPE density propagation (§8f2, blindno.fpe / blindno_fp_propagate).
+
+PARITY UNPINNED: fplanck is absent, so the checks are the oracle's independent
+cell-by-cell assembly of the same master equation (oracle/fpe_ref.py), its physical invariants
+(mass conservation, Boltzmann stationary state, detailed balance), and on the GPU the batched
+LDS-resident Taylor integrator against scipy.sparse.linalg.expm_multiply (rel-L2 <= 1e-9, fp64).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_l2
+
+NM = 1e-9
+
+
+def _sim2d(periodic_y=True, with_potential=True):
+    from blindno import fpe
+    kT = fpe.K_B * 300.0
+    pot = (lambda x, y: 0.8 * kT * np.cos(2 * np.pi * x / (200 * NM)) * np.sin(np.pi * y / (240 * NM))) \
+        if with_potential else None
+    force = lambda x, y: np.array([3e-14 * np.sin(2 * np.pi * y / (240 * NM)) + 0 * x,   # noqa: E731
+                                   -2e-14 * np.cos(2 * np.pi * x / (200 * NM)) + 0 * y])
+    drag = lambda x, y: 1e-9 * (1.0 + 0.3 * np.exp(-(x ** 2 + y ** 2) / (80 * NM) ** 2))   # noqa: E731
+    bnd = [fpe.boundary.reflecting, fpe.boundary.periodic if periodic_y else fpe.boundary.reflecting]
+    return fpe.fokker_planck(temperature=300, drag=drag, extent=[200 * NM, 240 * NM], resolution=10 * NM,
+                             potential=pot, force=force, boundary=bnd)
+
+
+def _sim1d():
+    from blindno import fpe
+    kT = fpe.K_B * 300.0
+    U = lambda x: 2.0 * kT * ((x / (250 * NM)) ** 2 - 1) ** 2    # noqa: E731  double well
+    return fpe.fokker_planck(temperature=300, drag=2e-9, extent=800 * NM, resolution=10 * NM,
+                             potential=U, boundary=fpe.boundary.reflecting)
+
+
+def _dense_from_coefficients(sim):
+    c = sim.coefficients()
+    nx, ny = sim.grid_dims()
+    N = nx * ny
+    M = np.zeros((N, N))
+    for i in range(N):
+        ix, iy = divmod(i, ny)
+        M[i, i] -= c[0, i]
+        M[i, ((ix - 1) % nx) * ny + iy] += c[1, i]
+        M[i, ((ix + 1) % nx) * ny + iy] += c[2, i]
+        if sim.ndim == 2:
+            M[i, ix * ny + (iy - 1) % ny] += c[3, i]
+            M[i, ix * ny + (iy + 1) % ny] += c[4, i]
+    return M
+
+
+def _oracle_matrix(sim):
+    from oracle import fpe_ref
+    periodic = [b.name == "periodic" for b in sim.boundary]
+    return fpe_ref.master_matrix(sim.potential_values, sim.force_values, sim.diffusion, sim.resolution,
+                                 sim.beta, periodic)
+
+
+@pytest.mark.parametrize("which", ["1d", "2d_periodic", "2d_reflecting"])
+def test_rates_match_oracle_assembly(which):
+    sim = _sim1d() if which == "1d" else _sim2d(periodic_y=(which == "2d_periodic"))
+    M = _dense_from_coefficients(sim)
+    Mo = _oracle_matrix(sim).toarray()
+    assert np.abs(M - Mo).max() <= 1e-12 * np.abs(Mo).max()
+
+
+def test_oracle_invariants():
+    from oracle import fpe_ref
+    sim = _sim2d()
+    M = _oracle_matrix(sim)
+    assert np.abs(np.asarray(M.sum(axis=0))).max() <= 1e-9 * abs(M.diagonal()).max()   # mass
+    # potential only, reflecting: Boltzmann exp(-beta U) is stationary and detailed balance holds
+    sim1 = _sim1d()
+    M1 = _oracle_matrix(sim1).toarray()
+    pb = np.exp(-sim1.beta * sim1.potential_values)
+    pb /= pb.sum()
+    assert np.abs(M1 @ pb).max() <= 1e-10 * np.abs(np.diag(M1)).max() * pb.max()
+    flux = M1 * pb[None, :]                       # flux[j, i] = rate(i -> j) p_i
+    off = flux - np.diag(np.diag(flux))
+    assert np.abs(off - off.T).max() <= 1e-12 * np.abs(off).max()
+    # expm_multiply keeps mass and relaxes toward Boltzmann
+    p0 = np.exp(-((sim1.grid[0] + 250 * NM) / (40 * NM)) ** 2)
+    p0 /= p0.sum()
+    Pt = fpe_ref.propagate(_oracle_matrix(sim1), p0, 5.0, 3)
+    assert abs(Pt[-1].sum() - 1.0) < 1e-10
+    assert rel_l2(Pt[-1], pb) < rel_l2(Pt[0], pb)
+
+
+def test_helpers():
+    from blindno import fpe
+    sim = _sim2d()
+    f = fpe.potential_from_data(sim.grid, sim.force_values[0])
+    assert np.allclose(f(*sim.grid), sim.force_values[0], rtol=1e-12, atol=0)
+    x = np.linspace(-1, 1, 11)
+    g = fpe.potential_from_data(x, x ** 2)
+    assert np.allclose(g(x), x ** 2)
+    pdf = fpe.gaussian_pdf(center=(0.1, -0.2), width=0.3)
+    assert np.isclose(pdf(np.array(0.1), np.array(-0.2)), 1.0)
+    with pytest.raises(Exception):
+        sim.propagate_interval(fpe.gaussian_pdf(0.0, 1.0), 1e-3, Nsteps=3, device="cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which,tf,nsteps", [("1d", 2.0, 41), ("2d_periodic", 0.05, 21),
+                                             ("2d_reflecting", 0.02, 11)])
+def test_gpu_propagation_matches_expm_multiply(which, tf, nsteps):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from blindno import fpe
+    from oracle import fpe_ref
+    sim = _sim1d() if which == "1d" else _sim2d(periodic_y=(which == "2d_periodic"))
+    center = (-250 * NM,) if sim.ndim == 1 else (-50 * NM, 40 * NM)
+    pdf = fpe.gaussian_pdf(center=center, width=30 * NM)
+    t, Pt = sim.propagate_interval(pdf, tf, Nsteps=nsteps)
+    assert np.allclose(t, np.linspace(0, tf, nsteps))
+    p0 = pdf(*sim.grid).reshape(-1)
+    p0 /= p0.sum()
+    ref = fpe_ref.propagate(_oracle_matrix(sim), p0, tf, nsteps)
+    got = Pt.reshape(nsteps, -1)
+    assert rel_l2(got, ref) <= 1e-9, rel_l2(got, ref)
+    assert np.abs(got.sum(axis=1) - 1.0).max() <= 1e-11
+
+
+@pytest.mark.gpu
+def test_gpu_batched_trajectories_match_single():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from blindno import fpe
+    sims = [_sim2d(), _sim2d(with_potential=False), _sim2d(periodic_y=False)]
+    pdfs = [fpe.gaussian_pdf(center=(c * NM, 0.0), width=30 * NM) for c in (-50, 0, 50)]
+    many = fpe.propagate_many(sims, pdfs, 0.01, Nsteps=6)
+    for sim, pdf, (t, Pt) in zip(sims, pdfs, many):
+        t1, P1 = sim.propagate_interval(pdf, 0.01, Nsteps=6)
+        # the batch shares one substep count (the stiffest trajectory's): same result to 1e-12
+        assert rel_l2(Pt, P1) <= 1e-12
