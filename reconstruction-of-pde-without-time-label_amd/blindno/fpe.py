@@ -56,6 +56,27 @@ def gaussian_pdf(center, width):
     return pdf
 
 
+def gaussian_potential(center, width, amplitude):
+    """A Gaussian well -amplitude * exp(-((x - c) / w)^2) per axis (fplanck's helper used by
+    1d_FPE/dataset_1d_drift_diffusion.py:45-49 and 2d_FPE/test_datagen.py:38-42)."""
+    center = np.atleast_1d(np.asarray(center, dtype=np.float64))
+    width = np.broadcast_to(np.asarray(width, dtype=np.float64), center.shape)
+
+    def U(*args):
+        v = np.ones_like(np.asarray(args[0], dtype=np.float64))
+        for i, a in enumerate(args):
+            v = v * np.exp(-np.square((np.asarray(a) - center[i]) / width[i]))
+        return -amplitude * v
+    return U
+
+
+def combine(*funcs):
+    """The sum of several potential / force callables (fplanck.combine)."""
+    def f(*args):
+        return sum(np.asarray(fn(*args), dtype=np.float64) for fn in funcs)
+    return f
+
+
 def potential_from_data(grid, data):
     """A callable interpolating ``data`` sampled on ``grid`` (an axis (N,) in 1D, or the
     simulator grid (ndim, *N)); evaluated on the same grid it returns ``data``."""
@@ -164,9 +185,10 @@ def substeps_for(coef: np.ndarray, dt_out: float, theta: float = THETA) -> int:
 
 
 def propagate_many(sims: Sequence[fokker_planck], initials, tf, Nsteps=None, dt=None,
-                   normalize=True, device="cuda"):
+                   normalize=True, device="cuda", select=None):
     """propagate_interval of several simulators (same grid) in ONE launch: one workgroup per
-    trajectory.  Returns [(time, Pt)] in the order given."""
+    trajectory.  Returns [(time, Pt)] in the order given; ``select`` (per trajectory, a list of
+    time indices) keeps only those records (gathered on the device before the host copy)."""
     if not sims:
         return []
     if Nsteps is None:
@@ -195,6 +217,13 @@ def propagate_many(sims: Sequence[fokker_planck], initials, tf, Nsteps=None, dt=
     out = torch.empty(len(sims), Nsteps, N, dtype=torch.float64, device=dev)
     call("blindno_fp_propagate", ptr(p0_d), ptr(coef_d), ptr(out), len(sims), nx, ny, Nsteps, s,
          TAYLOR_DEGREE, float(dt_out), stream_ptr(dev))
+    grid_shape = tuple(int(n) for n in sims[0].Ngrid)
+    if select is not None:
+        res = []
+        for k in range(len(sims)):
+            sel = np.asarray(select[k], dtype=np.int64)
+            rec = out[k].index_select(0, torch.from_numpy(sel).to(dev)).cpu().numpy()
+            res.append((time[sel], rec.reshape((len(sel),) + grid_shape)))
+        return res
     res = out.cpu().numpy()
-    shape = (Nsteps,) + tuple(int(n) for n in sims[0].Ngrid)
-    return [(time, res[k].reshape(shape)) for k in range(len(sims))]
+    return [(time, res[k].reshape((Nsteps,) + grid_shape)) for k in range(len(sims))]

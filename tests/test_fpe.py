@@ -135,3 +135,52 @@ def test_gpu_batched_trajectories_match_single():
         t1, P1 = sim.propagate_interval(pdf, 0.01, Nsteps=6)
         # the batch shares one substep count (the stiffest trajectory's): same result to 1e-12
         assert rel_l2(Pt, P1) <= 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gen,kw", [("fpe_1d_dataset", dict(nsteps=120, tf=2e-3)),
+                                    ("fpe_2d_dataset", dict(nsteps=110, tf=2e-4)),
+                                    ("fpe_2d_nc_dataset", dict(nsteps=105, tf=2e-3))])
+def test_dataset_generators(gen, kw, tmp_path):
+    """The reference generator scripts (1d_FPE/dataset_1d_drift_diffusion.py,
+    2d_FPE/test_datagen.py, 2d_Non_conservative_FPE/testdata_gen.py) at M = 2 and a shortened
+    time grid: reference keys and shapes, the numpy-RNG parameter order, mass conservation,
+    and (1D) the trajectory against expm_multiply of the oracle matrix."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from blindno import datagen, fpe
+    from oracle import fpe_ref
+    np.random.seed(5)
+    d = getattr(datagen, gen)(M=2, **kw)
+    nt = kw["nsteps"]
+    keys = {"time", "grid", "trajectories", "F"} if gen == "fpe_2d_nc_dataset" else \
+        {"time", "grid", "trajectories", "potential", "drag"}
+    assert set(d) == keys
+    assert d["time"].shape == (2, 100) and d["trajectories"].shape[:2] == (2, 100)
+    full_t = np.linspace(0, kw["tf"], nt)
+    for k in range(2):
+        assert np.all(np.diff(d["time"][k]) > 0) and np.all(np.isin(d["time"][k], full_t))
+        assert np.abs(d["trajectories"][k].reshape(100, -1).sum(-1) - 1.0).max() < 1e-10
+    datagen.save_npz(str(tmp_path / "ds.npz"), d)
+    assert set(np.load(tmp_path / "ds.npz").files) == keys
+    if gen == "fpe_1d_dataset":
+        # RNG order: sample 0's wells and its recorded indices come first
+        np.random.seed(5)
+        while True:
+            c = np.random.uniform(-150 * NM, 150 * NM, size=3)
+            if all(abs(c[i] - c[j]) > 80 * NM for i in range(3) for j in range(i + 1, 3)):
+                break
+        w = np.random.uniform(20 * NM, 80 * NM, size=3)
+        A = np.random.uniform(1e-20, 2e-20, size=3)
+        vf = np.random.uniform(1, 2, size=1)
+        sel = np.sort(np.random.choice(range(nt), size=100, replace=False))
+        g = d["grid"][0][0]
+        U = sum(-A[i] * vf[0] * np.exp(-((g - c[i]) / w[i]) ** 2) for i in range(3))
+        assert np.allclose(d["potential"][0], U, rtol=1e-12, atol=0)
+        assert np.isclose(d["drag"][0], datagen.DRAG * vf[0])
+        assert np.array_equal(d["time"][0], full_t[sel])
+        sim = fpe.fokker_planck(temperature=300, drag=d["drag"][0], extent=800 * NM, resolution=10 * NM,
+                                potential=fpe.potential_from_data(g, U))
+        p0 = np.exp(-(g / (50 * NM)) ** 2)
+        ref = fpe_ref.propagate(_oracle_matrix(sim), p0 / p0.sum(), kw["tf"], nt)[sel]
+        assert rel_l2(d["trajectories"][0], ref) <= 1e-9
