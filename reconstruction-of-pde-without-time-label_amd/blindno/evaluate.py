@@ -119,7 +119,7 @@ def predict(model: torch.nn.Module, x: torch.Tensor, grid: torch.Tensor, batch: 
     finally:
         model.train(was)
     out = torch.cat(outs, 0)
-    if out.shape[1] == 2 and out.shape[-1] != 2:
+    if out.dim() == 4 and out.shape[1] == 2 and out.shape[-1] != 2:
         out = out.permute(0, 2, 3, 1)
     return out.contiguous()
 
@@ -165,6 +165,67 @@ def evaluate(kind: str, model: torch.nn.Module, train, test, indices: Iterable[i
     finally:
         if f_csv is not None:
             f_csv.close()
+    return rows
+
+
+# ------------------------------------------------------------------------------- 1D FPE
+# 1d_FPE/eval_fno.py:23-190: scales 1e5 / 1e20 / 1e5, drag a per-sample scalar; the script
+# predicts one sample, saves pred_sample_<idx>.npy = stack(potential, drag per point) (Nx, 2) in
+# physical units and prints the x-mean of the predicted drag next to the true one.
+TRAJ_SCALE_1D, POTENTIAL_SCALE_1D, DRAG_SCALE_1D = 1e5, 1e20, 1e5
+
+
+def compute_train_stats_1d(train) -> Dict[str, np.ndarray]:
+    """1d_FPE/eval_fno.py:30-53."""
+    data = np.load(train) if isinstance(train, str) else train
+    traj = np.array(data["trajectories"], dtype=np.float32) * TRAJ_SCALE_1D
+    pot = np.array(data["potential"], dtype=np.float32) * POTENTIAL_SCALE_1D
+    drag = (np.array(data["drag"], dtype=np.float32) * DRAG_SCALE_1D)[:, np.newaxis]
+    return {"traj_mean": traj.mean(axis=(0, 1), keepdims=True),
+            "traj_std": traj.std(axis=(0, 1), keepdims=True) + 1e-8,
+            "pot_mean": pot.mean(axis=(0), keepdims=True), "pot_std": pot.std(axis=(0), keepdims=True) + 1e-8,
+            "drag_mean": drag.mean(axis=(0), keepdims=True), "drag_std": drag.std(axis=(0), keepdims=True) + 1e-8}
+
+
+def normalize_input_1d(traj_raw: np.ndarray, stats) -> np.ndarray:
+    """1d_FPE/eval_fno.py:74-80."""
+    t = traj_raw * TRAJ_SCALE_1D
+    return ((t - stats["traj_mean"].squeeze()) / stats["traj_std"].squeeze()).astype(np.float32)
+
+
+def denormalize_1d(pred: np.ndarray, stats):
+    """1d_FPE/eval_fno.py:86-97: (Nx, 2) -> potential (Nx,), drag per point (Nx,)."""
+    pot = (pred[:, 0] * stats["pot_std"].squeeze() + stats["pot_mean"].squeeze()) / POTENTIAL_SCALE_1D
+    drg = (pred[:, 1] * stats["drag_std"].squeeze() + stats["drag_mean"].squeeze()) / DRAG_SCALE_1D
+    return pot, drg
+
+
+def evaluate_1d_fpe(model: torch.nn.Module, train, test, indices: Iterable[int],
+                    outdir: Optional[str] = None, batch: int = 32, device="cuda") -> List[list]:
+    """1d_FPE/eval_fno.py:116-190 over ``indices`` with the forward batched on the HIP path.
+    Rows [index, predicted drag (x-mean), true drag, rel_l2(potential)]; with ``outdir`` also
+    the reference's pred_sample_<idx>.npy (Nx, 2) files."""
+    stats = compute_train_stats_1d(train)
+    data = np.load(test) if isinstance(test, str) else test
+    traj = np.asarray(data["trajectories"])
+    idx = [i for i in indices if 0 <= i < traj.shape[0]]
+    if not idx:
+        return []
+    nx = traj.shape[2]
+    x = torch.tensor(np.stack([normalize_input_1d(np.array(traj[i], dtype=np.float32), stats) for i in idx]),
+                     device=device)
+    grid = torch.linspace(0, 1, nx, device=device).unsqueeze(-1)     # 1d_FPE/eval_fno.py:138
+    pred = predict(model, x, grid, batch).cpu().numpy()
+    rows = []
+    if outdir is not None:
+        os.makedirs(outdir, exist_ok=True)
+    for k, i in enumerate(idx):
+        pot, drg = denormalize_1d(pred[k], stats)
+        pot_true = np.array(data["potential"][i], dtype=np.float32)
+        drag_true = float(np.array(data["drag"], dtype=np.float32)[i])
+        rows.append([i, float(drg.mean()), drag_true, rel_l2(pot, pot_true)])
+        if outdir is not None:
+            np.save(os.path.join(outdir, f"pred_sample_{i}.npy"), np.stack([pot, drg], axis=1))
     return rows
 
 

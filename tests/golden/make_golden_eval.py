@@ -85,6 +85,24 @@ def main():
             out[f"rel_a{i}"] = np.array(g["rel_l2"](pa, ta))
             out[f"rel_b{i}"] = np.array(g["rel_l2"](pb, tb))
         _save(tag, out)
+    # 1d_FPE/eval_fno.py: compute_train_stats, normalize_with_train_stats, denormalize_outputs
+    g = _namespace(os.path.join(a.ref, "1d_FPE", "eval_fno.py"),
+                   ("compute_train_stats", "normalize_with_train_stats", "denormalize_outputs"))
+    tr = dict(trajectories=(rs.rand(M, T, 16) * 1e-5).astype(np.float32),
+              potential=(rs.randn(M, 16) * 1e-20).astype(np.float32),
+              drag=(rs.rand(M) * 1e-5).astype(np.float32))
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "train.npz")
+        np.savez(p, **tr)
+        stats = g["compute_train_stats"](p)
+    out = {f"train.{k}": v for k, v in tr.items()}
+    out.update({f"stats.{k}": v for k, v in stats.items()})
+    test_traj = (rs.rand(T, 16) * 1e-5).astype(np.float32)
+    pred = rs.randn(16, 2).astype(np.float32)
+    pot, drg = g["denormalize_outputs"](pred, stats)
+    out.update({"test_traj": test_traj, "x_norm": g["normalize_with_train_stats"](test_traj, stats),
+                "pred": pred, "pot": pot, "drg": drg})
+    _save("eval_1d_fpe", out)
 
 
 if __name__ == "__main__":

@@ -91,3 +91,48 @@ def test_batched_gpu_eval_matches_per_sample_oracle(kind, tmp_path):
     d = np.load(tmp_path / "sample_0003_predictions.npy", allow_pickle=True).item()   # our own file
     assert d["index"] == 3 and d[f"{ev.KINDS[kind]['fields'][0]}_pred"].shape == (N, N)
     assert os.path.exists(tmp_path / "sample_0000_predictions.npy")
+
+
+def test_host_math_1d_matches_reference():
+    from blindno import evaluate as ev
+    g = load_golden("eval_1d_fpe")
+    st = ev.compute_train_stats_1d(_split(g, "train."))
+    ref = _split(g, "stats.")
+    assert sorted(st) == sorted(ref)
+    for k in ref:
+        assert np.array_equal(st[k], ref[k]), k
+    assert np.array_equal(ev.normalize_input_1d(g["test_traj"], st), g["x_norm"])
+    pot, drg = ev.denormalize_1d(g["pred"], st)
+    assert np.array_equal(pot, g["pot"]) and np.array_equal(drg, g["drg"])
+
+
+@pytest.mark.gpu
+def test_batched_gpu_eval_1d_matches_per_sample_oracle(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import oracle
+    from blindno import NIOFP_FNO
+    from blindno import evaluate as ev
+    rs = np.random.RandomState(4)
+    T, N = 100, 80
+    mk = lambda m: dict(trajectories=(rs.rand(m, T, N) * 1e-5).astype(np.float32),   # noqa: E731
+                        potential=(rs.randn(m, N) * 1e-20).astype(np.float32),
+                        drag=(rs.rand(m) * 1e-5).astype(np.float32))
+    train, test = mk(6), mk(5)
+    torch.manual_seed(3)
+    m = NIOFP_FNO(3, 6, 5, 2, "cpu").cuda()
+    rows = ev.evaluate_1d_fpe(m, train, test, range(0, 9), outdir=str(tmp_path), batch=2)
+    assert [r[0] for r in rows] == [0, 1, 2, 3, 4]
+    st = ev.compute_train_stats_1d(train)
+    p = {k: (v.detach().cpu().to(torch.complex128) if v.is_complex() else v.detach().cpu().double())
+         for k, v in m.state_dict().items()}
+    grid = torch.linspace(0, 1, N).unsqueeze(-1)
+    for r in rows:
+        i = r[0]
+        x = torch.tensor(ev.normalize_input_1d(test["trajectories"][i], st)[None])
+        ref = oracle.niofp_fno(p, x, grid, idx=None)[0].numpy().astype(np.float32)
+        pot, drg = ev.denormalize_1d(ref, st)
+        assert abs(r[1] - float(drg.mean())) <= 1e-4 * abs(float(drg.mean())) + 1e-12
+        assert abs(r[3] - ev.rel_l2(pot, test["potential"][i])) <= 1e-4 * ev.rel_l2(pot, test["potential"][i])
+        assert r[2] == float(test["drag"][i])
+    assert np.load(tmp_path / "pred_sample_3.npy").shape == (N, 2)
