@@ -48,6 +48,10 @@ CONFIGS = {
               N=128, T=100, B=4, lr=5e-4),
     "E": dict(desc="2D FNO-NIO NIOFP2D_FNO(2,3,100,25,3,12,32,2) on a 256x256 grid (no 2d_GPE in the "
                    "reference; real-valued synthetic bags)", dim=2, N=256, T=100, B=4, lr=5e-4),
+    # the token-attention variant (not a BASELINE.json config; bags drawn without
+    # replacement, 2d_FPE/NIOModules.py:344-345)
+    "C_attn": dict(desc="2d_FPE NIOFP2D_FNO_attn(2,3,100,25,3,12,32,2,128,128)", dim=2, N=128, T=100,
+                   B=4, lr=5e-4),
 }
 
 
@@ -60,6 +64,9 @@ def build_model(cfg_name, N, dev):
     if cfg_name == "B":
         m = blindno.NIOFP_FNO(3, 20, 40, 1, dev, heads=("fno_V",))
         return m.to(dev), trained_parameters(m), 1
+    if cfg_name == "C_attn":
+        m = blindno.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 12, 32, 2, N, N)
+        return m.to(dev), trained_parameters(m), 2
     if cfg_name == "D":
         m = blindno.NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, heads=("fno_Fx", "fno_Fy"),
                             branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N))
@@ -96,6 +103,7 @@ def main():
     a = parse()
     import blindno
     from blindno import timing
+    from blindno.nio import draw_bag_distinct as draw_distinct
     from blindno.train import (DataParallel, FlatAdam, GraphedBagStep, grid1d, grid2d,
                                synthetic_bags)
 
@@ -139,7 +147,7 @@ def main():
     graphed = None
     # one graph per bag size (device-resident bag indices); the NIO branch (D) stays eager: its
     # MIOpen convolutions allocate workspace per call
-    if not a.no_graph and a.config in ("A", "B", "C", "E"):
+    if not a.no_graph and a.config in ("A", "B", "C", "E", "C_attn"):
         # one HIP graph per bag size L = randint(50, T) (captured here, before the warm-up; the
         # numpy draw below stays the reference's: L and idx are drawn on the host every step)
         graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc)
@@ -157,7 +165,7 @@ def main():
         torch.index_select(X, 0, ids, out=xb)
         torch.index_select(Y, 0, ids, out=yb)
         if graphed is not None and not eager:
-            graphed.step(blindno.draw_bag(T)[1])
+            graphed.step((draw_distinct if a.config == "C_attn" else blindno.draw_bag)(T)[1])
             return
         out = model(xb, grid)
         loss = blindno.mse_loss(out, yb)
@@ -219,7 +227,8 @@ def main():
             "data": "synthetic (standardised N(0,1) bags resident in HBM; reference datasets not shipped)",
             "config": {"workload": f"{cfg['desc']} ({a.config}), grid {'x'.join([str(N)] * cfg['dim'])}",
                        "per_gpu_batch": B, "global_batch": B * world, "T": T,
-                       "bag_size": "L=randint(50,T) with replacement", "dataset_bags": a.bags,
+                       "bag_size": "L=randint(50,T) " + ("without" if a.config == "C_attn" else "with")
+                                   + " replacement", "dataset_bags": a.bags,
                        "parallelism": f"dp{world}", "optimizer": f"Adam lr {cfg['lr']} (fused flat)",
                        "launch": "hip-graph per bag size L (all kernels replayed each step)" if graphed else "eager"},
         }
