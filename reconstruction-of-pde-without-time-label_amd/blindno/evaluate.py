@@ -229,6 +229,53 @@ def evaluate_1d_fpe(model: torch.nn.Module, train, test, indices: Iterable[int],
     return rows
 
 
+# ------------------------------------------------------------------------------- 1D GPE
+def compute_train_scalers_gpe(train) -> Dict[str, float]:
+    """1d_GPE/eval_fno_GPE.py:32-57: divide-by-max scalers (no mean removal)."""
+    return {"y_max": train["y"].max() / 3.0, "V_max": train["V"].max() / 3.0,
+            "g_max": train["g"].max(), "kappa_max": train["kappa"].max()}
+
+
+def normalize_gpe(d, sc) -> Dict[str, np.ndarray]:
+    """1d_GPE/eval_fno_GPE.py:59-67."""
+    return {"y": d["y"] / sc["y_max"], "V": d["V"] / sc["V_max"], "g": d["g"] / sc["g_max"],
+            "kappa": d["kappa"] / sc["kappa_max"]}
+
+
+def evaluate_1d_gpe(model: torch.nn.Module, train, test, indices: Iterable[int],
+                    outdir: Optional[str] = None, batch: int = 32, device="cuda") -> List[list]:
+    """1d_GPE/eval_fno_GPE.py:95-171 over ``indices`` (the script takes one --sample_idx), with
+    the forward batched on the HIP path.  ``train`` / ``test`` are the generator's dicts
+    (y, g, kappa, V; blindno.gpe).  Rows [index, rel_l2(pred_V, true_V)]; with ``outdir`` also
+    the reference's save dict (x, pred_V, true_V, V_max_used, note) per index as
+    sample_pred_V_<idx>.npy."""
+    sc = compute_train_scalers_gpe(train)
+    tn = normalize_gpe(test, sc)
+    y = np.asarray(tn["y"])
+    idx = [i for i in indices if 0 <= i < y.shape[0]]
+    if not idx:
+        return []
+    nx = y.shape[2]
+    x = torch.tensor(np.stack([y[i] for i in idx]), dtype=torch.float32, device=device)
+    grid = torch.linspace(0, 1, nx, device=device).unsqueeze(-1)     # :126
+    pred = predict(model, x, grid, batch).cpu().numpy()
+    if pred.ndim == 3:
+        pred = pred[..., 0]
+    xs = np.linspace(0.0, 1.0, nx)
+    rows = []
+    if outdir is not None:
+        os.makedirs(outdir, exist_ok=True)
+    for k, i in enumerate(idx):
+        pred_V = pred[k] * sc["V_max"]
+        true_V = tn["V"][i] * sc["V_max"]
+        rows.append([i, rel_l2(pred_V, true_V)])
+        if outdir is not None:
+            np.save(os.path.join(outdir, f"sample_pred_V_{i}.npy"), {
+                "x": xs, "pred_V": pred_V, "true_V": true_V, "V_max_used": sc["V_max"],
+                "note": "Values are de-normalized using training set V_max (V_max = V_train.max()/3)."})
+    return rows
+
+
 def main(argv=None):
     """CLI mirroring eval_fno.py's arguments (:131-150) plus --experiment, --model, --batch."""
     from . import nio

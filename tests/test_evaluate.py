@@ -136,3 +136,34 @@ def test_batched_gpu_eval_1d_matches_per_sample_oracle(tmp_path):
         assert abs(r[3] - ev.rel_l2(pot, test["potential"][i])) <= 1e-4 * ev.rel_l2(pot, test["potential"][i])
         assert r[2] == float(test["drag"][i])
     assert np.load(tmp_path / "pred_sample_3.npy").shape == (N, 2)
+
+
+@pytest.mark.gpu
+def test_batched_gpu_eval_gpe_matches_per_sample_oracle(tmp_path):
+    """1d_GPE/eval_fno_GPE.py: divide-by-max scalers, NIOFP_FNO(3, 20, 40, 1) head fno_V."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import oracle
+    from blindno import NIOFP_FNO
+    from blindno import evaluate as ev
+    rs = np.random.RandomState(6)
+    T, N = 101, 128
+    mk = lambda m: dict(y=rs.rand(m, T, N), V=rs.rand(m, N) * 3, g=rs.rand(m), kappa=rs.rand(m))   # noqa: E731
+    train, test = mk(5), mk(4)
+    torch.manual_seed(4)
+    m = NIOFP_FNO(3, 20, 40, 1, "cpu", heads=("fno_V",)).cuda()
+    rows = ev.evaluate_1d_gpe(m, train, test, range(0, 4), outdir=str(tmp_path), batch=3)
+    sc = ev.compute_train_scalers_gpe(train)
+    assert sc["V_max"] == train["V"].max() / 3.0 and sc["g_max"] == train["g"].max()
+    tn = ev.normalize_gpe(test, sc)
+    p = {k: (v.detach().cpu().to(torch.complex128) if v.is_complex() else v.detach().cpu().double())
+         for k, v in m.state_dict().items()}
+    grid = torch.linspace(0, 1, N).unsqueeze(-1)
+    for r in rows:
+        i = r[0]
+        ref = oracle.niofp_fno(p, torch.tensor(tn["y"][i][None]), grid, idx=None, heads=("fno_V",))
+        pv = ref[0, :, 0].numpy().astype(np.float32) * sc["V_max"]
+        e = ev.rel_l2(pv, tn["V"][i] * sc["V_max"])
+        assert abs(r[1] - e) <= 1e-4 * e
+    d = np.load(tmp_path / "sample_pred_V_2.npy", allow_pickle=True).item()   # our own file
+    assert d["pred_V"].shape == (N,) and d["V_max_used"] == sc["V_max"]
