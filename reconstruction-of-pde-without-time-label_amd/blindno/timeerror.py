@@ -1,0 +1,94 @@
+"""Density-trajectory error of predicted force fields -- 2d_Non_conservative_FPE/
+compute_time_error.py:361-510 as one batched pipeline.
+
+Per test index the reference normalises the bag with the train statistics, predicts (Fx, Fy)
+with each model, de-normalises, propagates a Gaussian density (centre (-150, -150) nm, width
+30 nm) under the true and under each predicted force with fplanck (``propagate_density_with_
+force``, :300-319), and writes ``[index, model, rel_l2_Fx, rel_l2_Fy, ErrL2_density]`` to
+metrics_all.csv, ErrL2 being ``time_averaged_relative_l2`` (:321-333).
+
+Here every model's forward runs batched on the HIP path (blindno.evaluate.predict) and ALL
+density propagations -- the reference one and one per model, for every index -- go into ONE
+``blindno_fp_propagate`` launch (one workgroup per trajectory).  The propagator restates the
+absent fplanck (blindno.fpe): parity UNPINNED.  The figures are out of scope.
+"""
+from __future__ import annotations
+
+import csv
+import os
+from typing import Dict, Iterable, List, Optional
+
+import numpy as np
+import torch
+
+from . import evaluate, fpe
+
+NM = 1e-9
+KIND = "2d_Non_conservative_FPE"
+
+
+def time_averaged_relative_l2(pt_pred: np.ndarray, pt_ref: np.ndarray, eps: float = 1e-12) -> float:
+    """compute_time_error.py:321-333: mean over t of ||P_pred[t] - P_ref[t]|| / (||P_ref[t]|| + eps)."""
+    a = pt_pred.reshape(pt_pred.shape[0], -1)
+    b = pt_ref.reshape(pt_ref.shape[0], -1)
+    return float(np.mean(np.linalg.norm(a - b, axis=1) / (np.linalg.norm(b, axis=1) + eps)))
+
+
+def build_fokker_planck(force, temperature=300.0, viscosity=8e-4, radius_nm=50.0, extent_nm=800.0,
+                        resolution_nm=10.0):
+    """compute_time_error.py:266-286."""
+    drag = 6 * np.pi * viscosity * radius_nm * NM
+    return fpe.fokker_planck(temperature=temperature, drag=drag, extent=[extent_nm * NM, extent_nm * NM],
+                             resolution=resolution_nm * NM, boundary=fpe.boundary.reflecting, force=force)
+
+
+def force_from_array(grid, Fx, Fy):
+    """compute_time_error.py:288-298."""
+    fx, fy = fpe.potential_from_data(grid, Fx), fpe.potential_from_data(grid, Fy)
+    return lambda x, y: np.array([fx(x, y), fy(x, y)])
+
+
+def compute_time_error(models: Dict[str, torch.nn.Module], train, test, indices: Iterable[int],
+                       outdir: Optional[str] = None, nsteps: int = 500, dt: float = 10e-3,
+                       batch: int = 8, device="cuda", **phys) -> List[list]:
+    """Rows [index, model, rel_l2_Fx, rel_l2_Fy, ErrL2_density] in the reference's order (per
+    index: the models in the given order); with ``outdir`` appended to metrics_all.csv."""
+    stats = evaluate.compute_train_stats(KIND, train)
+    data = np.load(test) if isinstance(test, str) else test
+    traj = np.asarray(data["trajectories"])
+    idx = [i for i in indices if 0 <= i < traj.shape[0]]
+    if not idx:
+        return []
+    nx, ny = traj.shape[2], traj.shape[3]
+    x = torch.tensor(np.stack([evaluate.normalize_input(np.array(traj[i], dtype=np.float32), stats)
+                               for i in idx]), dtype=torch.float32, device=device)
+    grid_t = evaluate.grid2d(nx, ny, device)
+    preds = {name: evaluate.predict(m, x, grid_t, batch).cpu().numpy() for name, m in models.items()}
+    grid = build_fokker_planck(lambda xx, yy: np.array([0 * xx, 0 * yy]), **phys).grid
+    pdf = fpe.gaussian_pdf(center=(-150 * NM, -150 * NM), width=30 * NM)
+    sims, fields = [], []
+    for k, i in enumerate(idx):
+        F = np.array(data["F"][i], dtype=np.float32)
+        sims.append(build_fokker_planck(force_from_array(grid, F[0], F[1]), **phys))
+        for name in models:
+            pa, pb = evaluate.denormalize(KIND, preds[name][k], stats)
+            fields.append((i, name, evaluate.rel_l2(pa, F[0]), evaluate.rel_l2(pb, F[1])))
+            sims.append(build_fokker_planck(force_from_array(grid, pa, pb), **phys))
+    res = fpe.propagate_many(sims, [pdf] * len(sims), dt, Nsteps=nsteps, device=device)
+    rows = []
+    per = 1 + len(models)
+    for k in range(len(idx)):
+        ref = res[k * per][1]
+        for j in range(len(models)):
+            i, name, rfx, rfy = fields[k * len(models) + j]
+            rows.append([i, name, rfx, rfy, time_averaged_relative_l2(res[k * per + 1 + j][1], ref)])
+    if outdir is not None:
+        os.makedirs(outdir, exist_ok=True)
+        path = os.path.join(outdir, "metrics_all.csv")
+        header = not os.path.exists(path)
+        with open(path, "a", newline="") as f:
+            w = csv.writer(f)
+            if header:
+                w.writerow(["index", "model", "rel_l2_Fx", "rel_l2_Fy", "ErrL2_density"])
+            w.writerows(rows)
+    return rows

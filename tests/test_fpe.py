@@ -184,3 +184,53 @@ def test_dataset_generators(gen, kw, tmp_path):
         p0 = np.exp(-(g / (50 * NM)) ** 2)
         ref = fpe_ref.propagate(_oracle_matrix(sim), p0 / p0.sum(), kw["tf"], nt)[sel]
         assert rel_l2(d["trajectories"][0], ref) <= 1e-9
+
+
+def test_time_averaged_relative_l2_matches_reference_fixture():
+    from blindno import timeerror
+    from conftest import load_golden
+    g = load_golden("metric_time_avg_rel_l2_2d")
+    assert abs(timeerror.time_averaged_relative_l2(g["pt_pred"], g["pt_ref"]) - float(g["val"])) <= \
+        1e-12 * abs(float(g["val"]))
+
+
+@pytest.mark.gpu
+def test_compute_time_error_pipeline(tmp_path):
+    """2d_Non_conservative_FPE/compute_time_error.py as one batched pipeline vs the same steps
+    run one trajectory at a time (predict, de-normalise, propagate true and predicted force)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import csv
+    from blindno import NIOFP2D_FNO, evaluate, fpe, timeerror
+    rs = np.random.RandomState(8)
+    M, T, N = 3, 60, 80
+    mk = lambda m: dict(trajectories=(rs.rand(m, T, N, N) * 1e-10).astype(np.float32),   # noqa: E731
+                        F=(rs.randn(m, 2, N, N) * 1e-13).astype(np.float32))
+    train, test = mk(4), mk(M)
+    models = {}
+    for name, seed in (("fno", 1), ("fno_b", 2)):
+        torch.manual_seed(seed)
+        models[name] = NIOFP2D_FNO(2, 3, 100, 25, 2, 6, 5, 2, heads=("fno_Fx", "fno_Fy")).cuda()
+    kw = dict(nsteps=6, dt=1e-3)
+    rows = timeerror.compute_time_error(models, train, test, range(0, 5), outdir=str(tmp_path), batch=2, **kw)
+    assert [(r[0], r[1]) for r in rows] == [(i, n) for i in range(M) for n in models]
+    st = evaluate.compute_train_stats("2d_Non_conservative_FPE", train)
+    grid = timeerror.build_fokker_planck(lambda x, y: np.array([0 * x, 0 * y])).grid
+    pdf = fpe.gaussian_pdf(center=(-150 * NM, -150 * NM), width=30 * NM)
+    for r in rows[:2]:
+        i, name = r[0], r[1]
+        x = torch.tensor(evaluate.normalize_input(test["trajectories"][i], st)[None], device="cuda")
+        pred = evaluate.predict(models[name], x, evaluate.grid2d(N, N, "cuda")).cpu().numpy()[0]
+        pa, pb = evaluate.denormalize("2d_Non_conservative_FPE", pred, st)
+        F = test["F"][i]
+        assert abs(r[2] - evaluate.rel_l2(pa, F[0])) <= 1e-6 * r[2]
+        _, Pref = timeerror.build_fokker_planck(timeerror.force_from_array(grid, F[0], F[1])) \
+            .propagate_interval(pdf, kw["dt"], Nsteps=kw["nsteps"])
+        _, Ppred = timeerror.build_fokker_planck(timeerror.force_from_array(grid, pa, pb)) \
+            .propagate_interval(pdf, kw["dt"], Nsteps=kw["nsteps"])
+        e = timeerror.time_averaged_relative_l2(Ppred, Pref)
+        # the batched launch shares the stiffest trajectory's substep count: agreement ~1e-9
+        assert abs(r[4] - e) <= 1e-6 * e + 1e-12
+    with open(tmp_path / "metrics_all.csv") as f:
+        got = list(csv.reader(f))
+    assert got[0] == ["index", "model", "rel_l2_Fx", "rel_l2_Fy", "ErrL2_density"] and len(got) == 1 + 2 * M
