@@ -85,3 +85,27 @@ def test_gather_flat_segments():
         ref[off:off + t.numel()] = t
     torch.cuda.synchronize()
     assert torch.equal(dst, ref)
+
+
+def test_grid_spectrum_cache_follows_fc0_and_grid():
+    """The encoder's grid/bias spectrum is cached across steps (ops._grid_spectrum); an in-place
+    change of FNO_input.fc0 or of the grid must invalidate it."""
+    import blindno
+    torch.manual_seed(3)
+    m = blindno.NIOFP2D_FNO(2, 3, 100, 25, 2, 6, 5, 2).cuda().eval()
+    x = torch.randn(1, 60, 20, 20, device="cuda")
+    gx, gy = np.meshgrid(np.linspace(-1, 1, 20, dtype=np.float32), np.linspace(-1, 1, 20, dtype=np.float32),
+                         indexing="ij")
+    grid = torch.tensor(np.stack([gx, gy], 2), device="cuda")
+    with torch.no_grad():
+        a = m(x, grid)
+        m.FNO_input.fc0.weight.mul_(1.5)
+        b = m(x, grid)
+        grid.mul_(0.5)
+        c = m(x, grid)
+    m2 = blindno.NIOFP2D_FNO(2, 3, 100, 25, 2, 6, 5, 2).cuda().eval()
+    m2.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        c2 = m2(x, grid.clone())          # fresh grid storage: computed from scratch
+    assert not torch.equal(a, b) and not torch.equal(b, c)
+    assert rel_l2(c.cpu().numpy(), c2.cpu().numpy()) <= 1e-6
