@@ -1,4 +1,6 @@
-"""Batched evaluation / inference of the 2D snapshot-bag models -- the eval_fno.py path.
+"""Batched evaluation / inference of the snapshot-bag models -- the eval_fno.py paths of the
+2D experiments (``evaluate``), of 1d_FPE (``evaluate_1d_fpe``) and of 1d_GPE
+(``evaluate_1d_gpe``).
 
 Reference: 2d_FPE/eval_fno.py:34-281 (drift / diffusion, npz keys potential + drag) and
 2d_Non_conservative_FPE/eval_fno.py:33-300 (Fx / Fy, npz key F).  The reference evaluates one
