@@ -1,5 +1,7 @@
-"""Density-trajectory error of predicted force fields -- 2d_Non_conservative_FPE/
-compute_time_error.py:361-510 as one batched pipeline.
+"""Density-trajectory errors of predicted fields: 2d_Non_conservative_FPE/
+compute_time_error.py:361-510 (``compute_time_error``, FPE forces) and 1d_GPE/
+compute_time_error_GPE.py:208-330 (``compute_time_error_gpe``, GPE potentials), each as one
+batched pipeline.
 
 Per test index the reference normalises the bag with the train statistics, predicts (Fx, Fy)
 with each model, de-normalises, propagates a Gaussian density (centre (-150, -150) nm, width
@@ -92,3 +94,62 @@ def compute_time_error(models: Dict[str, torch.nn.Module], train, test, indices:
                 w.writerow(["index", "model", "rel_l2_Fx", "rel_l2_Fy", "ErrL2_density"])
             w.writerows(rows)
     return rows
+
+
+# ------------------------------------------------------------------------------- 1D GPE
+def compute_time_error_gpe(models: Dict[str, torch.nn.Module], train, test, indices: Iterable[int],
+                           outdir: Optional[str] = None, order: int = 2, dt: float = 0.005,
+                           t_final: float = 5.0, init_ic: int = 2, batch: int = 32,
+                           device="cuda") -> Dict[str, np.ndarray]:
+    """1d_GPE/compute_time_error_GPE.py:208-330: per test index, V predicted by each model
+    (de-normalised with the train V_max), |psi| propagated from initial condition ``init_ic`` on
+    x = linspace(-10, 10, Nx) under the true V and under each prediction (true g, kappa), and
+    time_averaged_L2_error of the densities.  All trajectories -- reference and every model's,
+    for every index -- run in ONE blindno_gpe_solve launch; the errors' spatial integrals run on
+    the GPU (blindno.gpe.time_averaged_L2_error).  Returns {model: errors in index order}; with
+    ``outdir`` writes the reference's per-sample dicts <outdir>/<model>/sample_<idx>_V_and_err.npy
+    and ErrL2_relative_<model>_Nsamples_<n>.npy."""
+    from . import gpe
+    sc = evaluate.compute_train_scalers_gpe(train)
+    tn = evaluate.normalize_gpe(test, sc)
+    y = np.asarray(tn["y"])
+    idx = [int(i) for i in indices if 0 <= int(i) < y.shape[0]]
+    if not idx:
+        return {name: np.zeros(0) for name in models}
+    nx = y.shape[2]
+    xin = torch.tensor(np.stack([y[i] for i in idx]), dtype=torch.float32, device=device)
+    grid_n = torch.linspace(0.0, 1.0, nx, device=device).unsqueeze(-1)
+    preds = {}
+    for name, m in models.items():
+        p = evaluate.predict(m, xin, grid_n, batch).cpu().numpy()
+        preds[name] = (p[..., 0] if p.ndim == 3 else p) * sc["V_max"]
+    x = np.linspace(-10, 10, nx)
+    V, g, kappa = [], [], []
+    for k, i in enumerate(idx):
+        gi = float(np.atleast_1d(test["g"][i])[0])
+        ki = float(np.atleast_1d(test["kappa"][i])[0])
+        for Vi in [tn["V"][i] * sc["V_max"]] + [preds[name][k] for name in models]:
+            V.append(Vi)
+            g.append(gi)
+            kappa.append(ki)
+    r = gpe.solve_batch(gpe.initial_condition(init_ic, x), x, dt, t_final, order, np.array(g),
+                        np.array(kappa), np.array(V), rec_every=1, device=device)
+    t, rho = r["t"], r["abs"]
+    per = 1 + len(models)
+    errs = {name: [] for name in models}
+    for k, i in enumerate(idx):
+        ref = rho[k * per]
+        for j, name in enumerate(models):
+            e = gpe.time_averaged_L2_error(t, ref, t, rho[k * per + 1 + j], x)
+            errs[name].append(e)
+            if outdir is not None:
+                d = os.path.join(outdir, name)
+                os.makedirs(d, exist_ok=True)
+                np.save(os.path.join(d, f"sample_{i}_V_and_err.npy"),
+                        {"x": x, "true_V": V[k * per], "pred_V": V[k * per + 1 + j], "g": g[k * per],
+                         "kappa": kappa[k * per], "Err_L2_rel": e})
+    out = {name: np.array(v, dtype=float) for name, v in errs.items()}
+    if outdir is not None:
+        for name, arr in out.items():
+            np.save(os.path.join(outdir, f"ErrL2_relative_{name}_Nsamples_{len(idx)}.npy"), arr)
+    return out

@@ -234,3 +234,38 @@ def test_compute_time_error_pipeline(tmp_path):
     with open(tmp_path / "metrics_all.csv") as f:
         got = list(csv.reader(f))
     assert got[0] == ["index", "model", "rel_l2_Fx", "rel_l2_Fy", "ErrL2_density"] and len(got) == 1 + 2 * M
+
+
+@pytest.mark.gpu
+def test_compute_time_error_gpe_pipeline(tmp_path):
+    """1d_GPE/compute_time_error_GPE.py as one batched pipeline vs per-trajectory
+    solve_GPE_custom + time_averaged_L2_error (GPE solver pinned by gpe_solve_* goldens)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from blindno import NIOFP_FNO, evaluate, gpe, timeerror
+    rs = np.random.RandomState(9)
+    T, N = 101, 128
+    mk = lambda m: dict(y=rs.rand(m, T, N), V=rs.rand(m, N) * 3, g=rs.rand(m), kappa=rs.rand(m) * 0.1)  # noqa: E731
+    train, test = mk(4), mk(3)
+    models = {}
+    for name, seed in (("fno", 1), ("fno_b", 2)):
+        torch.manual_seed(seed)
+        models[name] = NIOFP_FNO(3, 20, 40, 1, "cpu", heads=("fno_V",)).cuda()
+    kw = dict(t_final=0.5, dt=0.005)
+    errs = timeerror.compute_time_error_gpe(models, train, test, [2, 0, 7], outdir=str(tmp_path), **kw)
+    assert list(errs) == ["fno", "fno_b"] and errs["fno"].shape == (2,)
+    sc = evaluate.compute_train_scalers_gpe(train)
+    tn = evaluate.normalize_gpe(test, sc)
+    x = np.linspace(-10, 10, N)
+    i = 2
+    pv = evaluate.predict(models["fno_b"], torch.tensor(tn["y"][i][None], dtype=torch.float32, device="cuda"),
+                          torch.linspace(0, 1, N, device="cuda").unsqueeze(-1)).cpu().numpy()[0, :, 0] * sc["V_max"]
+    ic = lambda xx: gpe.initial_condition(2, xx)   # noqa: E731
+    t, pr = gpe.solve_GPE_custom(ic, x, kw["dt"], kw["t_final"], 2, test["g"][i], test["kappa"][i],
+                                 tn["V"][i] * sc["V_max"])
+    _, pp = gpe.solve_GPE_custom(ic, x, kw["dt"], kw["t_final"], 2, test["g"][i], test["kappa"][i], pv)
+    e = gpe.time_averaged_L2_error(t, np.abs(pr), t, np.abs(pp), x)
+    assert abs(errs["fno_b"][0] - e) <= 1e-9 * e + 1e-15
+    d = np.load(tmp_path / "fno" / "sample_0_V_and_err.npy", allow_pickle=True).item()   # our own file
+    assert d["Err_L2_rel"] == errs["fno"][1]
+    assert np.load(tmp_path / "ErrL2_relative_fno_Nsamples_2.npy").shape == (2,)
