@@ -1,5 +1,6 @@
 """Density-trajectory errors of predicted fields: 2d_Non_conservative_FPE/
-compute_time_error.py:361-510 (``compute_time_error``, FPE forces) and 1d_GPE/
+compute_time_error.py:361-510 (``compute_time_error``, FPE forces), 1d_FPE/
+compute_time_error.py:215-420 (``compute_time_error_1d``, potential + drag) and 1d_GPE/
 compute_time_error_GPE.py:208-330 (``compute_time_error_gpe``, GPE potentials), each as one
 batched pipeline.
 
@@ -152,4 +153,65 @@ def compute_time_error_gpe(models: Dict[str, torch.nn.Module], train, test, indi
     if outdir is not None:
         for name, arr in out.items():
             np.save(os.path.join(outdir, f"ErrL2_relative_{name}_Nsamples_{len(idx)}.npy"), arr)
+    return out
+
+
+# ------------------------------------------------------------------------------- 1D FPE
+def compute_time_error_1d(models: Dict[str, torch.nn.Module], train, test, indices: Iterable[int],
+                          outdir: Optional[str] = None, nsteps: int = 400, dt: float = 2e-3,
+                          batch: int = 32, device="cuda", temperature: float = 300.0,
+                          extent_nm: float = 800.0, resolution_nm: float = 10.0,
+                          init_width_nm: float = 50.0) -> Dict[str, np.ndarray]:
+    """1d_FPE/compute_time_error.py:215-420: per test index, (potential, drag) predicted by each
+    model (de-normalised with the train statistics, drag = x-mean of the per-point drag), the
+    density from a centred Gaussian (width 50 nm) propagated under the true and under each
+    predicted (U, drag) (``simulate_density_trajectory``, :215-238), and
+    time_averaged_L2_error (:240-295).  All trajectories go into ONE blindno_fp_propagate
+    launch.  Returns {model: errors in index order}; with ``outdir`` writes
+    <outdir>/<model>/pred_sample_<idx>.npy (Nx, 2) and ErrL2_<model>_Nsamples_<n>.npy."""
+    from . import gpe
+    stats = evaluate.compute_train_stats_1d(train)
+    data = np.load(test) if isinstance(test, str) else test
+    traj = np.asarray(data["trajectories"])
+    idx = [int(i) for i in indices if 0 <= int(i) < traj.shape[0]]
+    if not idx:
+        return {name: np.zeros(0) for name in models}
+    nx = traj.shape[2]
+    xin = torch.tensor(np.stack([evaluate.normalize_input_1d(np.array(traj[i], dtype=np.float32), stats)
+                                 for i in idx]), device=device)
+    grid_n = torch.linspace(0, 1, nx, device=device).unsqueeze(-1)
+    preds = {name: evaluate.predict(m, xin, grid_n, batch).cpu().numpy() for name, m in models.items()}
+
+    def sim(U, drag):
+        proto = fpe.fokker_planck(temperature=temperature, drag=drag, extent=extent_nm * NM,
+                                  resolution=resolution_nm * NM, boundary=fpe.boundary.reflecting)
+        return fpe.fokker_planck(temperature=temperature, drag=drag, extent=extent_nm * NM,
+                                 resolution=resolution_nm * NM, boundary=fpe.boundary.reflecting,
+                                 potential=fpe.potential_from_data(proto.grid[0], U))
+    sims, saved = [], []
+    for k, i in enumerate(idx):
+        sims.append(sim(np.asarray(data["potential"][i], dtype=np.float64), float(np.asarray(data["drag"])[i])))
+        for name in models:
+            pot, drg = evaluate.denormalize_1d(preds[name][k], stats)
+            saved.append((name, i, np.stack([pot, drg], axis=1)))
+            sims.append(sim(pot, float(drg.mean())))
+    pdf = fpe.gaussian_pdf(center=(0 * NM), width=init_width_nm * NM)
+    res = fpe.propagate_many(sims, [pdf] * len(sims), dt, Nsteps=nsteps, device=device)
+    grid = sims[0].grid
+    per = 1 + len(models)
+    errs = {name: [] for name in models}
+    for k in range(len(idx)):
+        t_ref, P_ref = res[k * per]
+        for j, name in enumerate(models):
+            t_p, P_p = res[k * per + 1 + j]
+            errs[name].append(gpe.time_averaged_L2_error(t_ref, P_ref, t_p, P_p, grid))
+    if outdir is not None:
+        for name, i, arr in saved:
+            d = os.path.join(outdir, name)
+            os.makedirs(d, exist_ok=True)
+            np.save(os.path.join(d, f"pred_sample_{i}.npy"), arr)
+    out = {name: np.array(v, dtype=float) for name, v in errs.items()}
+    if outdir is not None:
+        for name, arr in out.items():
+            np.save(os.path.join(outdir, f"ErrL2_{name}_Nsamples_{len(idx)}.npy"), arr)
     return out

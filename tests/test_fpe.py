@@ -269,3 +269,41 @@ def test_compute_time_error_gpe_pipeline(tmp_path):
     d = np.load(tmp_path / "fno" / "sample_0_V_and_err.npy", allow_pickle=True).item()   # our own file
     assert d["Err_L2_rel"] == errs["fno"][1]
     assert np.load(tmp_path / "ErrL2_relative_fno_Nsamples_2.npy").shape == (2,)
+
+
+@pytest.mark.gpu
+def test_compute_time_error_1d_pipeline(tmp_path):
+    """1d_FPE/compute_time_error.py as one batched pipeline vs per-trajectory propagation."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from blindno import NIOFP_FNO, evaluate, fpe, gpe, timeerror
+    rs = np.random.RandomState(10)
+    T, N = 100, 80
+    kT = fpe.K_B * 300
+    mk = lambda m: dict(trajectories=(rs.rand(m, T, N) * 1e-5).astype(np.float32),   # noqa: E731
+                        potential=(rs.randn(m, N) * 0.3 * kT).astype(np.float32),
+                        drag=(rs.rand(m) * 1e-9 + 1e-9).astype(np.float32))
+    train, test = mk(5), mk(3)
+    models = {}
+    for name, seed in (("fno", 1), ("fno_b", 2)):
+        torch.manual_seed(seed)
+        models[name] = NIOFP_FNO(3, 6, 5, 2, "cpu").cuda()
+    kw = dict(nsteps=11, dt=2e-4)
+    errs = timeerror.compute_time_error_1d(models, train, test, [1, 2], outdir=str(tmp_path), **kw)
+    st = evaluate.compute_train_stats_1d(train)
+    i = 1
+    x = torch.tensor(evaluate.normalize_input_1d(test["trajectories"][i], st)[None], device="cuda")
+    p = evaluate.predict(models["fno"], x, torch.linspace(0, 1, N, device="cuda").unsqueeze(-1)).cpu().numpy()[0]
+    pot, drg = evaluate.denormalize_1d(p, st)
+
+    def sim(U, drag):
+        s0 = fpe.fokker_planck(temperature=300, drag=drag, extent=800 * NM, resolution=10 * NM)
+        return fpe.fokker_planck(temperature=300, drag=drag, extent=800 * NM, resolution=10 * NM,
+                                 potential=fpe.potential_from_data(s0.grid[0], U))
+    pdf = fpe.gaussian_pdf(center=0.0, width=50 * NM)
+    t, Pr = sim(test["potential"][i].astype(np.float64), float(test["drag"][i])).propagate_interval(pdf, kw["dt"], Nsteps=kw["nsteps"])
+    _, Pp = sim(pot, float(drg.mean())).propagate_interval(pdf, kw["dt"], Nsteps=kw["nsteps"])
+    e = gpe.time_averaged_L2_error(t, Pr, t, Pp, sim(pot, 1e-9).grid)
+    assert abs(errs["fno"][0] - e) <= 1e-6 * e + 1e-15
+    assert np.load(tmp_path / "fno_b" / "pred_sample_2.npy").shape == (N, 2)
+    assert np.load(tmp_path / "ErrL2_fno_Nsamples_2.npy").shape == (2,)
