@@ -282,7 +282,7 @@ def main(argv=None):
     """CLI mirroring eval_fno.py's arguments (:131-150) plus --experiment, --model, --batch."""
     from . import nio
     ap = argparse.ArgumentParser(description="Batched evaluation of a trained 2D snapshot-bag model.")
-    ap.add_argument("--experiment", choices=sorted(KINDS), default="2d_FPE")
+    ap.add_argument("--experiment", choices=sorted(KINDS) + ["1d_FPE", "1d_GPE"], default="2d_FPE")
     ap.add_argument("--model", choices=["NIOFP2D_FNO", "NIOFP2D_FNO_attn", "NIOFP2D"], default="NIOFP2D_FNO")
     ap.add_argument("--train_data", required=True)
     ap.add_argument("--test_data", required=True)
@@ -297,6 +297,28 @@ def main(argv=None):
     ap.add_argument("--strict", action="store_true")
     a = ap.parse_args(argv)
     heads = ("fno_drift", "fno_diffusion") if a.experiment == "2d_FPE" else ("fno_Fx", "fno_Fy")
+    if a.experiment in ("1d_FPE", "1d_GPE"):
+        # the reference's 1D eval models: NIOFP_FNO(3, 30, 15, 2) (1d_FPE/eval_fno.py:100-114),
+        # NIOFP_FNO(3, 20, 40, 1) head fno_V (1d_GPE/eval_fno_GPE.py:69-83)
+        model = nio.NIOFP_FNO(3, 30, 15, 2, a.device) if a.experiment == "1d_FPE" else \
+            nio.NIOFP_FNO(3, 20, 40, 1, a.device, heads=("fno_V",))
+        ret = model.load_state_dict(load_checkpoint_robust(a.ckpt), strict=a.strict)
+        if ret.missing_keys or ret.unexpected_keys:
+            print("[Warn] Incompatible keys when loading:", ret.missing_keys, ret.unexpected_keys)
+        model = model.to(a.device)
+        idx = range(a.start, a.end + 1)
+        if a.experiment == "1d_FPE":
+            for r in evaluate_1d_fpe(model, a.train_data, a.test_data, idx, outdir=a.outdir,
+                                     batch=a.batch, device=a.device):
+                print(f"[Metrics] index={r[0]}  drag_pred={r[1]:.6g}  drag_true={r[2]:.6g}  "
+                      f"rel_l2_potential={r[3]:.6f}")
+        else:
+            # the GPE generator's files are np.save'd dicts: our own format, allow_pickle
+            tr = np.load(a.train_data, allow_pickle=True).item()
+            te = np.load(a.test_data, allow_pickle=True).item()
+            for r in evaluate_1d_gpe(model, tr, te, idx, outdir=a.outdir, batch=a.batch, device=a.device):
+                print(f"[Metrics] index={r[0]}  rel_l2_V={r[1]:.6f}")
+        return
     if a.model == "NIOFP2D_FNO_attn":
         model = nio.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 12, 32, 2, a.nx, a.ny, heads=heads)
     else:

@@ -167,3 +167,26 @@ def test_batched_gpu_eval_gpe_matches_per_sample_oracle(tmp_path):
         assert abs(r[1] - e) <= 1e-4 * e
     d = np.load(tmp_path / "sample_pred_V_2.npy", allow_pickle=True).item()   # our own file
     assert d["pred_V"].shape == (N,) and d["V_max_used"] == sc["V_max"]
+
+
+@pytest.mark.gpu
+def test_cli_1d_fpe(tmp_path):
+    """python -m blindno.evaluate --experiment 1d_FPE: reference-size NIOFP_FNO(3, 30, 15, 2)
+    checkpoint with the DDP 'module.' prefix, npz train/test files, per-sample outputs."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from blindno import NIOFP_FNO
+    from blindno import evaluate as ev
+    rs = np.random.RandomState(12)
+    T, N = 100, 80
+    for name, m in (("train", 4), ("test", 3)):
+        np.savez(tmp_path / f"{name}.npz", trajectories=(rs.rand(m, T, N) * 1e-5).astype(np.float32),
+                 potential=(rs.randn(m, N) * 1e-20).astype(np.float32), drag=(rs.rand(m) * 1e-5).astype(np.float32))
+    torch.manual_seed(0)
+    m = NIOFP_FNO(3, 30, 15, 2, "cpu")
+    torch.save({"module." + k: v for k, v in m.state_dict().items()}, tmp_path / "ckpt.pt")
+    ev.main(["--experiment", "1d_FPE", "--train_data", str(tmp_path / "train.npz"),
+             "--test_data", str(tmp_path / "test.npz"), "--ckpt", str(tmp_path / "ckpt.pt"),
+             "--outdir", str(tmp_path / "out"), "--start", "0", "--end", "5", "--strict"])
+    for i in range(3):
+        assert np.load(tmp_path / "out" / f"pred_sample_{i}.npy").shape == (N, 2)
