@@ -51,13 +51,13 @@ def gelu(x: torch.Tensor) -> torch.Tensor:
     return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
 
 
-def c2r_weights(n: int, m: int) -> torch.Tensor:
+def c2r_weights(n: int, m: int, device=None) -> torch.Tensor:
     """Hermitian weights of a length-``n`` complex-to-real inverse over bins [0, m).
 
     irfft counts bin 0 (and the Nyquist bin n/2 for even n) once and every other
     bin twice; the imaginary part of the once-counted bins is ignored.
     """
-    c = torch.full((m,), 2.0, dtype=DT)
+    c = torch.full((m,), 2.0, dtype=DT, device=device)
     c[0] = 1.0
     if n % 2 == 0 and m > n // 2:
         c[n // 2] = 1.0
@@ -72,10 +72,10 @@ def _as_complex(w: torch.Tensor) -> torch.Tensor:
     return torch.complex(w[..., 0], w[..., 1])
 
 
-def _dft(n: int, k: int, sign: float) -> torch.Tensor:
+def _dft(n: int, k: int, sign: float, device=None) -> torch.Tensor:
     """(n, k) matrix exp(sign * 2*pi*i * j*kk / n) with exact integer phases."""
-    j = torch.arange(n, dtype=torch.int64)[:, None]
-    kk = torch.arange(k, dtype=torch.int64)[None, :]
+    j = torch.arange(n, dtype=torch.int64, device=device)[:, None]
+    kk = torch.arange(k, dtype=torch.int64, device=device)[None, :]
     ph = ((j * kk) % n).to(DT) * (2.0 * math.pi / n)
     return torch.complex(torch.cos(ph), sign * torch.sin(ph))
 
@@ -112,18 +112,19 @@ def spectral_conv2d(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> torc
     H, W = x.shape[-2], x.shape[-1]
     if m2 > W // 2 + 1:
         raise ValueError(f"modes2={m2} exceeds W//2+1={W // 2 + 1}")
+    dev = x.device
     rows = kept_rows(H, m1)
-    r_idx = torch.tensor([r for r, _, _ in rows], dtype=torch.int64)
+    r_idx = torch.tensor([r for r, _, _ in rows], dtype=torch.int64, device=dev)
     wt = torch.stack([(w1c if which == 1 else w2c)[:, :, j, :] for _, which, j in rows], 0)  # (K,Ci,Co,m2)
-    fw = _dft(W, m2, -1.0)                        # (W, m2)
+    fw = _dft(W, m2, -1.0, dev)                   # (W, m2)
     a = torch.einsum("bihw,wk->bihk", x.to(CDT), fw)
-    fh = _dft(H, H, -1.0)[:, r_idx].T             # (K, H): exp(-2 pi i r h / H)
+    fh = _dft(H, H, -1.0, dev)[:, r_idx].T        # (K, H): exp(-2 pi i r h / H)
     xh = torch.einsum("rh,bihk->birk", fh, a)
     yh = torch.einsum("birk,riok->bork", xh, wt)
-    gh = _dft(H, H, +1.0)[:, r_idx] / H          # (H, K)
+    gh = _dft(H, H, +1.0, dev)[:, r_idx] / H     # (H, K)
     z = torch.einsum("hr,bork->bohk", gh, yh)
-    c = c2r_weights(W, m2).to(CDT) / W
-    gw = _dft(W, m2, +1.0).T                      # (m2, W)
+    c = c2r_weights(W, m2, dev).to(CDT) / W
+    gw = _dft(W, m2, +1.0, dev).T                 # (m2, W)
     y = torch.einsum("bohk,kw->bohw", z * c, gw)
     return y.real
 
@@ -140,13 +141,14 @@ def spectral_conv1d(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     W = x.shape[-1]
     if m > W // 2 + 1:
         raise ValueError(f"modes={m} exceeds W//2+1={W // 2 + 1}")
-    xf = torch.einsum("biw,wk->bik", x.to(CDT), _dft(W, m, -1.0))
-    half = torch.ones(m, dtype=CDT)
+    dev = x.device
+    xf = torch.einsum("biw,wk->bik", x.to(CDT), _dft(W, m, -1.0, dev))
+    half = torch.ones(m, dtype=CDT, device=dev)
     half[0] = 0.5
     xf = xf * half
     yf = torch.einsum("bik,iok->bok", xf, wc)
-    c = c2r_weights(W, m).to(CDT) / W
-    y = torch.einsum("bok,kw->bow", yf * c, _dft(W, m, +1.0).T)
+    c = c2r_weights(W, m, dev).to(CDT) / W
+    y = torch.einsum("bok,kw->bow", yf * c, _dft(W, m, +1.0, dev).T)
     return y.real
 
 

@@ -182,6 +182,8 @@ class GraphedBagStep:
         self.graphs = {}
         self.idx = {}
         self.lw = {}
+        self.out = {}
+        self.loss = {}
         self.T = x.shape[1]
         # deduplicated bags (NIOFP2D_FNO's fused encoder): graphs keyed by the number U of
         # distinct snapshots, fed the unique indices and multiplicity weights
@@ -191,14 +193,15 @@ class GraphedBagStep:
         self._ev = [None] * len(self._ring)
         self._k = 0
 
-    def _body(self, L):
+    def _body(self, L, accumulate=True):
         bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
         out = self.model(self.x, self.grid, bag_idx=bag)
         loss = self.loss_fn(out, self.y)
         loss.backward()
         self.opt.gather_grads()
-        if self.loss_acc is not None:
+        if accumulate and self.loss_acc is not None:
             self.loss_acc.add_(loss.detach())
+        return out.detach(), loss.detach()
 
     def capture(self, L: int):
         if L in self.graphs:
@@ -211,16 +214,26 @@ class GraphedBagStep:
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                 # eager warm-up: caches, lazy init
-            self._body(L)
+            self._body(L, accumulate=False)           # (its loss is not a training step's)
             self.opt.zero_grad()
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.pool):
-            self._body(L)
+            # static output / loss of the graph: valid after each replay of this key
+            self.out[L], self.loss[L] = self._body(L)
         self.opt.zero_grad()
         self.graphs[L] = g
 
-    def step(self, idx) -> None:
+    def step(self, idx) -> int:
+        """One training step on the drawn bag ``idx``: replay, all-reduce, Adam.  Returns the
+        graph key (``self.out[key]`` / ``self.loss[key]`` hold this step's output and loss)."""
+        key = self.replay(idx)
+        self.dp.reduce_and_step()
+        return key
+
+    def replay(self, idx) -> int:
+        """Stage the bag and replay its graph (forward, loss, backward, gradient gather into
+        ``opt.grad``) without the optimizer step.  Returns the graph key."""
         idx = np.asarray(idx, dtype=np.int32)
         w = None
         if self.dedup:
@@ -247,7 +260,7 @@ class GraphedBagStep:
         ev.record()
         self._ev[k] = ev
         self.graphs[L].replay()
-        self.dp.reduce_and_step()
+        return L
 
 
 def synthetic_bags(n_bags: int, T: int, grid_shape, out_ch: int, seed: int, device,

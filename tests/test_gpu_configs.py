@@ -1,0 +1,211 @@
+"""Full-geometry parity at every BASELINE.json config, through the path bench.py times
+(needs a GPU).
+
+Each test builds the config's model at the reference's own sizes (SURVEY.md section 8 "Configs
+restated"), runs ONE training step on a recorded with-replacement bag draw exactly as
+``bench.py`` does -- for A, B, C, E: ``train.GraphedBagStep`` (HIP graph per distinct-count
+key, deduplicated bag with multiplicity weights, grouped heads, fused snapshot encoder); for
+D: the eager NIO step -- and compares the step's output and every trained parameter's
+gradient (MSE loss, the reference's criterion) with the float64 oracle (``oracle.fno_ref``)
+evaluated on the same inputs, weights and bag.  The oracle runs in fp64 on the GPU (plain
+torch ops; it shares nothing with the HIP kernels) so the 128^2 / 256^2 cases finish in
+seconds.
+
+Tolerances (fp32 HIP vs fp64): forward rel-L2 <= 1e-5, gradients rel-L2 <= 1e-4
+per parameter tensor.  Config D (ten train-mode BatchNorm'd convolutions) is held to a bar
+relative to what a plain fp32 evaluation of the same graph achieves against fp64 -- see
+``test_config_d_niofp2d``.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+FWD_TOL = 1e-5
+GRAD_TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import blindno
+    blindno.load_library()
+
+
+def _oracle_params(model, skip=("branch.",)):
+    out = {}
+    for k, v in model.state_dict().items():
+        if k.startswith(tuple(skip)) or not v.is_floating_point() and not v.is_complex():
+            continue
+        v = v.detach().to("cuda")
+        v = v.to(torch.complex128) if v.is_complex() else v.double()
+        out[k] = v.requires_grad_(True)
+    return out
+
+
+def _check_grads(model, opt, p64, min_count):
+    """Compare the flat gradient buffer the graph filled (``opt.grad``) per parameter tensor."""
+    names = {id(p): k for k, p in model.named_parameters()}
+    n = 0
+    worst = 0.0
+    for prm, off, sz in zip(opt.params, opt.offsets, opt.sizes):
+        k = names[id(prm)]
+        ref = p64[k].grad
+        assert ref is not None, k
+        ref = torch.view_as_real(ref) if ref.is_complex() else ref
+        got = opt.grad[off:off + sz].view(ref.shape)
+        e = rel_l2(got.cpu().numpy(), ref.cpu().numpy())
+        worst = max(worst, e)
+        assert e <= GRAD_TOL, (k, e)
+        n += 1
+    assert n >= min_count
+    return worst
+
+
+def _graphed_step_vs_oracle(model, x, y, grid, draws, oracle_fwd, min_params):
+    import blindno
+    from blindno.train import DataParallel, FlatAdam, GraphedBagStep, trained_parameters
+    model = model.cuda().train()
+    opt = FlatAdam(trained_parameters(model), lr=1e-3)
+    p64 = _oracle_params(model)
+    gs = GraphedBagStep(model, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+    res = []
+    for idx in draws:
+        key = gs.replay(idx)
+        torch.cuda.synchronize()
+        assert gs.dedup and key < len(idx), "bench path must run the deduplicated bag"
+        out = gs.out[key].clone()
+        for v in p64.values():
+            v.grad = None
+        ref = oracle_fwd(p64, x.double(), grid.double(), idx)
+        e_fwd = rel_l2(out.cpu().numpy(), ref.detach().cpu().numpy())
+        assert e_fwd <= FWD_TOL, e_fwd
+        loss = ((ref - y.double()) ** 2).mean()
+        assert abs(float(gs.loss[key]) - float(loss.detach())) <= 1e-5 * float(loss.detach())
+        loss.backward()
+        e_grad = _check_grads(model, opt, p64, min_params)
+        res.append((len(idx), key, e_fwd, e_grad))
+    return res
+
+
+def _grid2d(n):
+    from blindno.train import grid2d
+    return grid2d(n, n, "cuda")
+
+
+def _draws(T, seed, k=2):
+    rs = np.random.RandomState(seed)
+    return [rs.choice(T, rs.randint(50, T)) for _ in range(k)]
+
+
+def test_config_c_niofp2d_fno_128():
+    """Config C, the headline: NIOFP2D_FNO(2,3,100,25,3,12,32,2) at 128^2 (P = 160, FNO_input
+    m = 12 on ~55 distinct snapshots per bag, heads m = 32 width 12 as one grouped chain), B = 2,
+    T = 100, two recorded draws (two graph keys)."""
+    import oracle
+    from blindno import Encoder2D, NIOFP2D_FNO, ops
+    torch.manual_seed(0)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2, branch_last_kernel=Encoder2D.kernel_for_grid(128))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(2, 100, 128, 128, device="cuda", generator=g)
+    y = torch.randn(2, 128, 128, 2, device="cuda", generator=g)
+    assert ops.GROUPED_HEADS
+    res = _graphed_step_vs_oracle(m, x, y, _grid2d(128), _draws(100, 7),
+                                  lambda p, x, gr, idx: oracle.niofp2d_fno(p, x, gr, idx=idx.tolist()), 40)
+    print("config C", res)
+
+
+def test_config_e_niofp2d_fno_256():
+    """Config E geometry in fp32: NIOFP2D_FNO at 256^2 (P = 320), B = 1, T = 100."""
+    import oracle
+    from blindno import Encoder2D, NIOFP2D_FNO
+    torch.manual_seed(2)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2, branch_last_kernel=Encoder2D.kernel_for_grid(256))
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(1, 100, 256, 256, device="cuda", generator=g)
+    y = torch.randn(1, 256, 256, 2, device="cuda", generator=g)
+    res = _graphed_step_vs_oracle(m, x, y, _grid2d(256), _draws(100, 8, k=1),
+                                  lambda p, x, gr, idx: oracle.niofp2d_fno(p, x, gr, idx=idx.tolist()), 40)
+    print("config E", res)
+
+
+@pytest.mark.parametrize("cfg", ["A", "B"])
+def test_config_ab_niofp_fno_1d(cfg):
+    """Config A: 1d_FPE NIOFP_FNO(3,30,15,2), N = 64, T = 256, B = 32.  Config B: 1d_GPE
+    NIOFP_FNO(3,20,40,1) head fno_V, N = 256, T = 101, B = 32."""
+    import oracle
+    from blindno import NIOFP_FNO
+    from blindno.train import grid1d
+    if cfg == "A":
+        args, heads, N, T, cout = (3, 30, 15, 2), ("fno_drift", "fno_diffusion"), 64, 256, 2
+    else:
+        args, heads, N, T, cout = (3, 20, 40, 1), ("fno_V",), 256, 101, 1
+    torch.manual_seed(4)
+    m = NIOFP_FNO(*args, "cuda", heads=heads)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(32, T, N, device="cuda", generator=g)
+    y = torch.randn(32, N, cout, device="cuda", generator=g)
+    res = _graphed_step_vs_oracle(m, x, y, grid1d(N, "cuda"), _draws(T, 9),
+                                  lambda p, x, gr, idx: oracle.niofp_fno(p, x, gr, idx=idx.tolist(), heads=heads),
+                                  10)
+    print("config", cfg, res)
+
+
+def test_config_d_niofp2d_nc_128():
+    """Config D: 2d_Non_conservative_FPE NIOFP2D (Encoder2D branch with the grid-adaptive (4,2)
+    final kernel, FFN trunk, DeepONet combiner, heads fno_Fx/fno_Fy) at 128^2, B = 2, one
+    recorded draw, eager step as bench.py runs it.
+
+    Ten train-mode BatchNorm'd convolutions amplify fp32 rounding: the bar for each tensor is
+    max(4 x the error of the same graph evaluated in plain fp32 torch, the SURVEY 8c bar), both
+    measured against fp64 on the same inputs."""
+    import blindno
+    import oracle
+    from blindno import Encoder2D, NIOFP2D
+    torch.manual_seed(6)
+    m = NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, heads=("fno_Fx", "fno_Fy"),
+                branch_last_kernel=Encoder2D.kernel_for_grid(128)).cuda().train()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(2, 100, 128, 128, device="cuda", generator=g)
+    y = torch.randn(2, 128, 128, 2, device="cuda", generator=g)
+    grid = _grid2d(128)
+    idx = _draws(100, 10, k=1)[0]
+    heads = ("fno_Fx", "fno_Fy")
+    out = m(x, grid, bag_idx=idx)
+    blindno.mse_loss(out, y).backward()
+    torch.cuda.synchronize()
+
+    def oracle_run(prec):
+        oracle.set_precision(prec)
+        try:
+            dt = torch.float64 if prec == "fp64" else torch.float32
+            p = {k: v.detach().to(dt).requires_grad_(True) for k, v in m.state_dict().items()
+                 if v.is_floating_point() and not k.endswith(("running_mean", "running_var"))}
+            ref = oracle.niofp2d(p, x.to(dt), grid.to(dt), idx=idx.tolist(), heads=heads)
+            ((ref - y.to(dt)) ** 2).mean().backward()
+            return ref.detach().double(), {k: v.grad for k, v in p.items()}
+        finally:
+            oracle.set_precision("fp64")
+
+    ref64, g64 = oracle_run("fp64")
+    ref32, g32 = oracle_run("fp32")
+    e = rel_l2(out.detach().cpu().numpy(), ref64.cpu().numpy())
+    e32 = rel_l2(ref32.cpu().numpy(), ref64.cpu().numpy())
+    print(f"config D fwd {e:.2e} (fp32 torch {e32:.2e})")
+    assert e <= max(4 * e32, FWD_TOL), (e, e32)
+    n, worst = 0, []
+    for k, prm in m.named_parameters():
+        if k.startswith("fc0.") or k.endswith("layers.0.bias"):
+            continue     # fc0 is read through .data; a conv bias ahead of batch-stat BN has grad 0
+        assert prm.grad is not None and g64[k] is not None, k
+        e = rel_l2(prm.grad.cpu().numpy(), g64[k].cpu().numpy())
+        e32 = rel_l2(g32[k].double().cpu().numpy(), g64[k].cpu().numpy())
+        worst.append((e, e32, k))
+        assert e <= max(4 * e32, GRAD_TOL), (k, e, e32)
+        n += 1
+    assert n > 60
+    print("config D worst grads", sorted(worst)[-5:])
