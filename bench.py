@@ -34,6 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_PEAK_TFLOPS = 157.3       # fp32 vector = fp32 MFMA dense peak (same table)
+BASELINE_METRIC = "snapshot-bags/sec (train step) + rel-L2 drift error, 2D FPE 128\u00b2 @1/2/4/8 GPU"
 
 
 # BASELINE.json configs (SURVEY.md section 8 "Configs restated")
@@ -92,6 +93,7 @@ def parse():
     ap.add_argument("--bags", type=int, default=4096, help="dataset size (all ranks)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="cpu baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the GPU-vs-CPU-reference parity leg")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
     ap.add_argument("--timer-steps", type=int, default=4,
@@ -212,7 +214,7 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": ("snapshot-bags/sec (train step), 2D FPE 128^2 FNO-NIO" if a.config == "C" else
+            "metric": (BASELINE_METRIC if a.config == "C" else
                        f"snapshot-bags/sec (train step), config {a.config}"),
             "value": round(value, 3),
             "unit": "snapshot-bags/s",
@@ -238,8 +240,13 @@ def main():
                                              if a.config == "C" else None)
             if a.config in ("C", "E"):
                 res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
-        if world == 1 and not a.no_cpu and a.config == "C":
-            res["cpu_baseline"] = cpu_baseline(N, T, budget=a.cpu_seconds)
+        if world == 1 and a.config in ("A", "B", "C", "E"):
+            # the reference's CPU path on the same weights / inputs: accuracy parity of the
+            # benched step (the "rel-L2 drift error" half of BASELINE's metric), then its timing
+            if not a.no_parity:
+                res["parity"] = parity_check(a.config, model, graphed, opt, xb, yb, grid, T)
+            if a.config == "C" and not a.no_cpu:
+                res["cpu_baseline"] = cpu_baseline(a.config, model, xb, yb, grid, T, budget=a.cpu_seconds)
         res["loss_mean"] = float(loss_acc) / (a.warmup + a.steps)
         res["host_enqueue_ms_per_step"] = round(1000.0 * t_enq / a.steps, 4)
         print(json.dumps(res))
@@ -286,35 +293,128 @@ def spectral_roofline(model, grid, B, T, N, dev):
             "algorithmic_bytes": int(nbytes), "snapshots": Bn}
 
 
-def cpu_baseline(N, T, budget):
-    """float32 CPU oracle (oracle/ restates the reference's algorithm) timed on this host:
-    forward + backward of one bag per step (L = 75, the mean bag size), until ~budget s."""
-    import oracle
-    import blindno
-    oracle.set_precision("fp32")
+def _cpu_params(model):
+    """CPU fp32 leaves of the model's current weights (the reference's state_dict keys)."""
+    p = {}
+    for k, v in model.state_dict().items():
+        if k.startswith("branch.") or not (v.is_floating_point() or v.is_complex()):
+            continue
+        p[k] = v.detach().cpu().clone().requires_grad_(True)
+    return p
+
+
+def _cpu_step(cfg_name, p, x, y, grid, idx):
+    """The reference's train step in fp32 on the host (oracle.cpu_ref: rfft2/irfft2, F.gelu,
+    F.linear -- the reference's own CPU execution), forward + MSE + backward."""
+    from oracle import cpu_ref
+    if cfg_name in ("A", "B"):
+        heads = ("fno_V",) if cfg_name == "B" else ("fno_drift", "fno_diffusion")
+        out = cpu_ref.niofp_fno_fft(p, x, grid, idx=list(idx), heads=heads)
+    else:
+        out = cpu_ref.niofp2d_fno_fft(p, x, grid, idx=list(idx))
+    loss = ((out - y) ** 2).mean()
+    loss.backward()
+    return out.detach(), loss.detach()
+
+
+def parity_check(cfg_name, model, graphed, opt, xb, yb, grid, T, seed=4321):
+    """Accuracy of the benched GPU step (graph replay: deduplicated bag, grouped heads) on one
+    recorded bag draw, against (1) the reference's fp32 CPU step (oracle.cpu_ref: pocketfft,
+    F.gelu, F.linear -- how the reference computes) and (2) the same step in float64 (same
+    code, plain torch fp64 ops on the GPU) as the arbiter, on the same weights and inputs.
+    Reported: rel-L2 of the output fields (drift = channel 0, diffusion = channel 1), the loss,
+    and the worst per-tensor gradient rel-L2; also the reference fp32 path's own distance to
+    fp64 (its conditioning floor).  Pass: GPU vs fp64 within SURVEY.md 8c (fields 1e-5,
+    gradients 1e-4) and GPU vs the reference's fp32 fields within 1e-5."""
+    rs = np.random.RandomState(seed)
+    L = rs.randint(50, T)
+    idx = rs.choice(T, L)
+    if graphed is not None:
+        key = graphed.replay(idx)
+        out_gpu, loss_gpu = graphed.out[key], graphed.loss[key]
+    else:
+        import blindno
+        opt.zero_grad()
+        out_gpu = model(xb, grid, bag_idx=idx)
+        loss = blindno.mse_loss(out_gpu, yb)
+        loss.backward()
+        opt.gather_grads()
+        out_gpu, loss_gpu = out_gpu.detach(), loss.detach()
+        key = L
+    torch.cuda.synchronize()
+    grads_gpu = {}
+    names = {id(q): k for k, q in model.named_parameters()}
+    for prm, off, sz in zip(opt.params, opt.offsets, opt.sizes):
+        grads_gpu[names[id(prm)]] = opt.grad[off:off + sz].detach().clone()
+    p32 = _cpu_params(model)
+    out32, loss32 = _cpu_step(cfg_name, p32, xb.cpu(), yb.cpu(), grid.cpu(), idx)
+    p64 = {k: v.detach().to(xb.device, torch.complex128 if v.is_complex() else torch.float64)
+           .requires_grad_(True) for k, v in p32.items()}
+    out64, loss64 = _cpu_step(cfg_name, p64, xb.double(), yb.double(), grid.double(), idx)
+
+    def rel(a, b):
+        a, b = a.double().cpu(), b.double().cpu()
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+    def g(p, k):
+        t = p[k].grad
+        return torch.view_as_real(t) if t.is_complex() else t
+
+    def fields(out, ref):
+        r = {"fwd": rel(out, ref), "drift": rel(out[..., 0], ref[..., 0])}
+        if ref.shape[-1] > 1:
+            r["diffusion"] = rel(out[..., 1], ref[..., 1])
+        return r
+
+    def worst(get):
+        w = max(((rel(get(k), g(p64, k)), k) for k in grads_gpu), key=lambda t: t[0])
+        return w
+
+    gw, gk = worst(lambda k: grads_gpu[k].view(g(p64, k).shape))
+    rw, rk = worst(lambda k: g(p32, k))
+    gpu64 = fields(out_gpu, out64)
+    ref64 = fields(out32, out64)
+    gpu32 = fields(out_gpu, out32)
+    fmt = lambda d: {k: float(f"{v:.3e}") for k, v in d.items()}
+    res = {"bag": {"L": int(L), "distinct": int(len(np.unique(idx))), "graph_key": int(key)},
+           "reference": "the reference's fp32 CPU step (oracle.cpu_ref: rfft2/irfft2, F.gelu, F.linear) "
+                        "and the same step in fp64 as arbiter, same weights / inputs / bag",
+           "drift_rel_l2": float(f"{gpu32['drift']:.3e}"),
+           "gpu_vs_ref_fp32": fmt(gpu32),
+           "gpu_vs_fp64": dict(fmt(gpu64), grad_max=float(f"{gw:.3e}"), grad_worst=gk,
+                               loss=float(f"{abs(float(loss_gpu) - float(loss64)) / abs(float(loss64)):.3e}")),
+           "ref_fp32_vs_fp64": dict(fmt(ref64), grad_max=float(f"{rw:.3e}"), grad_worst=rk),
+           "tolerance": {"fields": 1e-5, "grads": 1e-4}}
+    res["pass"] = bool(gpu64["fwd"] <= 1e-5 and gw <= 1e-4 and gpu32["fwd"] <= 1e-5)
+    return res
+
+
+def cpu_baseline(cfg_name, model, xb, yb, grid, T, budget):
+    """The reference's fp32 CPU train step (oracle.cpu_ref, the reference's own execution:
+    pocketfft rfft2/irfft2, fused GELU, addmm linears) timed on this host's cores at the
+    benched batch (B bags, L = randint(50, T) with replacement, a fresh draw per step), on the
+    model's current weights, until ~``budget`` s."""
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
-    torch.manual_seed(0)
-    m = blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2,
-                            branch_last_kernel=blindno.Encoder2D.kernel_for_grid(N))
-    p = {k: v.detach().float().requires_grad_(True) for k, v in m.state_dict().items()
-         if not k.startswith("branch.")}
-    from blindno.train import grid2d
-    grid = grid2d(N, N, "cpu")
-    x = torch.randn(1, T, N, N)
-    y = torch.randn(1, N, N, 2)
-    n, t0 = 0, time.perf_counter()
+    p = _cpu_params(model)
+    x, y, g = xb.cpu(), yb.cpu(), grid.cpu()
+    rs = np.random.RandomState(99)
+    _cpu_step(cfg_name, p, x, y, g, rs.choice(T, 60))          # warm-up (allocator, fft plans)
+    n, Ls, t0 = 0, [], time.perf_counter()
     while True:
-        idx = np.random.RandomState(n).choice(T, 75)
-        out = oracle.niofp2d_fno(p, x, grid, idx=idx.tolist())
-        oracle.mse(out, y).backward()
+        for v in p.values():
+            v.grad = None
+        L = rs.randint(50, T)
+        _cpu_step(cfg_name, p, x, y, g, rs.choice(T, L))
+        Ls.append(int(L))
         n += 1
         el = time.perf_counter() - t0
-        if el >= budget or n >= 50:
+        if el >= budget or n >= 200:
             break
-    oracle.set_precision("fp64")
-    return {"value": round(n / el, 4), "unit": "snapshot-bags/s", "cores": threads, "kind": "port",
-            "sample": f"{n} train steps of 1 bag (L=75, {N}x{N}, fp32 oracle fwd+bwd) in {el:.1f}s"}
+    B = x.shape[0]
+    return {"value": round(n * B / el, 4), "unit": "snapshot-bags/s", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps x B={B} bags (L={Ls} with replacement, fp32 forward+MSE+backward, "
+                      f"no optimizer) in {el:.1f}s; reference measured 1.29 bags/s on 8 threads (BASELINE.md)"}
 
 
 if __name__ == "__main__":

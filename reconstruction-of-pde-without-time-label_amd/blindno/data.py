@@ -105,14 +105,49 @@ class TrajectoryDataset1D(Dataset):
         return np.stack([self.potential, np.repeat(self.drag, self.potential.shape[1], 1)], -1)
 
 
+_NUMPY_PICKLE_GLOBALS = {
+    ("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+    ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+    ("numpy", "ndarray"), ("numpy", "dtype"),
+}
+
+
+def load_npy_dict(path: str) -> dict:
+    """A dict of arrays / numbers saved with ``np.save(path, dict)`` (the GPE generator's
+    format, 1d_GPE/datagen_GPE.py:183-189), read WITHOUT ``allow_pickle``: the object payload
+    is unpickled by a restricted unpickler that resolves only numpy's array / dtype / scalar
+    reconstructors -- any other global in the file (code execution) raises."""
+    import pickle
+
+    class _Restricted(pickle.Unpickler):
+        def find_class(self, module, name):
+            if (module, name) in _NUMPY_PICKLE_GLOBALS:
+                return super().find_class(module, name)
+            raise pickle.UnpicklingError(f"{path}: refusing to load global {module}.{name}")
+
+    with open(path, "rb") as f:
+        version = np.lib.format.read_magic(f)
+        if version == (1, 0):
+            shape, _, dtype = np.lib.format.read_array_header_1_0(f)
+        else:
+            shape, _, dtype = np.lib.format.read_array_header_2_0(f)
+        if dtype != np.dtype(object):
+            raise ValueError(f"{path}: not an np.save'd object (dict) file")
+        arr = _Restricted(f).load()
+    obj = arr.item() if isinstance(arr, np.ndarray) else arr
+    if not isinstance(obj, dict):
+        raise ValueError(f"{path}: payload is {type(obj).__name__}, expected dict")
+    return obj
+
+
 class ParameterDataset(Dataset):
     """1D GPE bags (potential V target), 1d_GPE/train_fno_GPE.py:33-74.  ``file_path`` is the
-    generator's np.save'd dict (1d_GPE/datagen_GPE.py:183-189): loading it needs
-    ``allow_pickle=True``, so pass ``arrays=`` for data of unknown origin."""
+    generator's np.save'd dict (1d_GPE/datagen_GPE.py:183-189), read with ``load_npy_dict``
+    (restricted unpickler: numpy arrays and scalars only)."""
 
     def __init__(self, file_path: Optional[str] = None, *, arrays: Optional[dict] = None,
                  verbose: bool = False):
-        data = arrays if arrays is not None else np.load(file_path, allow_pickle=True).item()
+        data = arrays if arrays is not None else load_npy_dict(file_path)
         self.y = data["y"]
         self.g = data["g"]
         self.kappa = data["kappa"]

@@ -283,7 +283,7 @@ def main(argv=None):
     from . import nio
     ap = argparse.ArgumentParser(description="Batched evaluation of a trained 2D snapshot-bag model.")
     ap.add_argument("--experiment", choices=sorted(KINDS) + ["1d_FPE", "1d_GPE"], default="2d_FPE")
-    ap.add_argument("--model", choices=["NIOFP2D_FNO", "NIOFP2D_FNO_attn", "NIOFP2D"], default="NIOFP2D_FNO")
+    ap.add_argument("--model", choices=["NIOFP2D_FNO", "NIOFP2D_FNO_attn", "NIOFP2D"], default=None)
     ap.add_argument("--train_data", required=True)
     ap.add_argument("--test_data", required=True)
     ap.add_argument("--ckpt", required=True)
@@ -296,8 +296,13 @@ def main(argv=None):
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--strict", action="store_true")
     a = ap.parse_args(argv)
+    a.model_given = a.model is not None
+    a.model = a.model or "NIOFP2D_FNO"
     heads = ("fno_drift", "fno_diffusion") if a.experiment == "2d_FPE" else ("fno_Fx", "fno_Fy")
     if a.experiment in ("1d_FPE", "1d_GPE"):
+        if a.model_given:
+            ap.error(f"--model {a.model} is a 2D model; the {a.experiment} evaluation always builds the "
+                     f"reference's NIOFP_FNO (1d_FPE/eval_fno.py:100-114, 1d_GPE/eval_fno_GPE.py:69-83)")
         # the reference's 1D eval models: NIOFP_FNO(3, 30, 15, 2) (1d_FPE/eval_fno.py:100-114),
         # NIOFP_FNO(3, 20, 40, 1) head fno_V (1d_GPE/eval_fno_GPE.py:69-83)
         model = nio.NIOFP_FNO(3, 30, 15, 2, a.device) if a.experiment == "1d_FPE" else \
@@ -313,9 +318,11 @@ def main(argv=None):
                 print(f"[Metrics] index={r[0]}  drag_pred={r[1]:.6g}  drag_true={r[2]:.6g}  "
                       f"rel_l2_potential={r[3]:.6f}")
         else:
-            # the GPE generator's files are np.save'd dicts: our own format, allow_pickle
-            tr = np.load(a.train_data, allow_pickle=True).item()
-            te = np.load(a.test_data, allow_pickle=True).item()
+            # the GPE generator's files are np.save'd dicts: read by a restricted unpickler
+            # (numpy arrays / scalars only), never allow_pickle
+            from .data import load_npy_dict
+            tr = load_npy_dict(a.train_data)
+            te = load_npy_dict(a.test_data)
             for r in evaluate_1d_gpe(model, tr, te, idx, outdir=a.outdir, batch=a.batch, device=a.device):
                 print(f"[Metrics] index={r[0]}  rel_l2_V={r[1]:.6f}")
         return

@@ -178,9 +178,19 @@ class fokker_planck:
                               device=device)[0]
 
 
+# Upper bound on the Taylor substeps one launch may take in total (substeps per output interval
+# x output intervals).  The step count grows like exp(beta W / 2) with the rates, so one badly
+# predicted force could otherwise turn a launch into an effectively hung GPU job (or overflow
+# the kernel's int argument); such a request is refused before launching.
+MAX_TOTAL_SUBSTEPS = 1 << 24
+
+
 def substeps_for(coef: np.ndarray, dt_out: float, theta: float = THETA) -> int:
-    """Substeps per output interval so that ||h M||_1 <= theta (||M||_1 = 2 max diag)."""
+    """Substeps per output interval so that ||h M||_1 <= theta (||M||_1 = 2 max diag) for the
+    rate coefficients ``coef`` (5, N) of one trajectory (or a stack: the max over it)."""
     norm = 2.0 * float(np.max(coef[..., 0, :]))
+    if not math.isfinite(norm):
+        raise BlindnoError("fp propagation: non-finite hop rates (overflowing exp(-beta dU/2))")
     return max(1, int(math.ceil(norm * dt_out / theta)))
 
 
@@ -208,15 +218,30 @@ def propagate_many(sims: Sequence[fokker_planck], initials, tf, Nsteps=None, dt=
         coef[k] = sim.coefficients()
     time = np.linspace(0, tf, Nsteps)
     dt_out = tf / (Nsteps - 1) if Nsteps > 1 else 0.0
-    s = substeps_for(coef, dt_out) if dt_out > 0 else 1
+    # substeps per trajectory: one stiff trajectory must not multiply every other one's work, so
+    # trajectories are launched in groups of equal substep count
+    steps = [substeps_for(coef[k], dt_out) if dt_out > 0 else 1 for k in range(len(sims))]
+    worst = max(steps)
+    if worst * max(1, Nsteps - 1) > MAX_TOTAL_SUBSTEPS:
+        k = int(np.argmax(steps))
+        raise BlindnoError(
+            f"fp propagation: trajectory {k} needs {worst} Taylor substeps per output interval "
+            f"({worst * (Nsteps - 1)} in total, limit {MAX_TOTAL_SUBSTEPS}); its hop rates reach "
+            f"{float(np.max(coef[k, 0])):.3e}/s -- a force / potential far outside the physical "
+            f"range (e.g. a badly predicted field); refusing to launch")
     dev = torch.device(device)
     if dev.type != "cuda":
         raise BlindnoError("fp propagation runs on a HIP device (there is no CPU path)")
-    p0_d = torch.from_numpy(p0).to(dev)
-    coef_d = torch.from_numpy(coef).to(dev)
     out = torch.empty(len(sims), Nsteps, N, dtype=torch.float64, device=dev)
-    call("blindno_fp_propagate", ptr(p0_d), ptr(coef_d), ptr(out), len(sims), nx, ny, Nsteps, s,
-         TAYLOR_DEGREE, float(dt_out), stream_ptr(dev))
+    for s in sorted(set(steps)):
+        ks = [k for k in range(len(sims)) if steps[k] == s]
+        p0_d = torch.from_numpy(np.ascontiguousarray(p0[ks])).to(dev)
+        coef_d = torch.from_numpy(np.ascontiguousarray(coef[ks])).to(dev)
+        dst = out if len(ks) == len(sims) else torch.empty(len(ks), Nsteps, N, dtype=torch.float64, device=dev)
+        call("blindno_fp_propagate", ptr(p0_d), ptr(coef_d), ptr(dst), len(ks), nx, ny, Nsteps, s,
+             TAYLOR_DEGREE, float(dt_out), stream_ptr(dev))
+        if dst is not out:
+            out[torch.as_tensor(ks, device=dev)] = dst
     grid_shape = tuple(int(n) for n in sims[0].Ngrid)
     if select is not None:
         res = []

@@ -190,7 +190,9 @@ def compute_time_error_1d(models: Dict[str, torch.nn.Module], train, test, indic
                                  potential=fpe.potential_from_data(proto.grid[0], U))
     sims, saved = [], []
     for k, i in enumerate(idx):
-        sims.append(sim(np.asarray(data["potential"][i], dtype=np.float64), float(np.asarray(data["drag"])[i])))
+        # the reference reads potential / drag as float32 (1d_FPE/compute_time_error.py:112-117)
+        sims.append(sim(np.asarray(data["potential"][i], dtype=np.float32).astype(np.float64),
+                        float(np.asarray(data["drag"], dtype=np.float32)[i])))
         for name in models:
             pot, drg = evaluate.denormalize_1d(preds[name][k], stats)
             saved.append((name, i, np.stack([pot, drg], axis=1)))

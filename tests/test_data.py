@@ -55,3 +55,27 @@ def test_parameter_dataset_gpe(tmp_path):
     x, t = _items(ds)
     assert np.array_equal(x, g["x"]) and np.array_equal(t, g["t"])
     assert ds.y_max == g["y_max"] and ds.V_max == g["V_max"]
+
+
+def test_load_npy_dict_restricted(tmp_path):
+    """The GPE generator's np.save'd dict reads back through the restricted unpickler (arrays
+    and numpy scalars), and a file carrying any other global is refused."""
+    import pickle
+    import numpy as np
+    import pytest
+    from blindno.data import load_npy_dict
+    d = {"y": np.random.rand(3, 5, 8), "g": np.float64(2.0), "kappa": np.arange(3.0), "V": np.ones((3, 8))}
+    np.save(tmp_path / "ok.npy", d, allow_pickle=True)
+    got = load_npy_dict(str(tmp_path / "ok.npy"))
+    assert sorted(got) == sorted(d) and all(np.array_equal(got[k], d[k]) for k in d)
+
+    class Evil:
+        def __reduce__(self):
+            return (print, ("pwned",))
+    arr = np.empty((), dtype=object)
+    arr[()] = {"y": Evil()}
+    with open(tmp_path / "bad.npy", "wb") as f:
+        np.lib.format.write_array_header_1_0(f, {"descr": "|O", "fortran_order": False, "shape": ()})
+        pickle.dump(arr, f, protocol=3)
+    with pytest.raises(pickle.UnpicklingError, match="refusing"):
+        load_npy_dict(str(tmp_path / "bad.npy"))

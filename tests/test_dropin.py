@@ -92,3 +92,24 @@ def test_fplanck_shim_names():
              "                  force=lambda x, y: [0 * x, 0 * y], boundary=boundary.reflecting)\n"
              "print(s.grid.shape)\n", "2d_Non_conservative_FPE")
     assert r.stdout.strip() == "(2, 10, 8)", r.stderr
+
+
+# the fplanck import lines of the reference scripts, per experiment (1d_FPE/compute_time_error.py:8-15,
+# dataset_1d_drift_diffusion.py:3, cal_trajectory*.py:3; 2d_FPE/test_datagen.py:3, cal_traj.py:3;
+# 2d_Non_conservative_FPE/compute_time_error.py:44, testdata_gen.py:3)
+FPLANCK_IMPORTS = {
+    "1d_FPE": "from fplanck import fokker_planck, boundary, gaussian_pdf, combine, gaussian_potential, "
+              "potential_from_data",
+    "2d_FPE": "from fplanck import fokker_planck, boundary, gaussian_pdf, combine, gaussian_potential",
+    "2d_Non_conservative_FPE": "from fplanck import fokker_planck, boundary, gaussian_pdf",
+}
+
+
+@pytest.mark.parametrize("exp", sorted(FPLANCK_IMPORTS))
+def test_fplanck_shim_serves_every_reference_import(exp):
+    r = _run(FPLANCK_IMPORTS[exp] + "\nimport fplanck\n"
+             "U = fplanck.combine(fplanck.gaussian_potential(0.0, 1.0, 2.0), fplanck.gaussian_potential(1.0, 1.0, 1.0))\n"
+             "print(sorted(fplanck.__all__), float(U(0.0)) < 0)\n", exp)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == ("['boundary', 'combine', 'fokker_planck', 'gaussian_pdf', 'gaussian_potential', "
+                                "'potential_from_data'] True"), r.stdout

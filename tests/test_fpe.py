@@ -133,8 +133,25 @@ def test_gpu_batched_trajectories_match_single():
     many = fpe.propagate_many(sims, pdfs, 0.01, Nsteps=6)
     for sim, pdf, (t, Pt) in zip(sims, pdfs, many):
         t1, P1 = sim.propagate_interval(pdf, 0.01, Nsteps=6)
-        # the batch shares one substep count (the stiffest trajectory's): same result to 1e-12
+        # each trajectory keeps its own substep count (grouped launches): same result to 1e-12
         assert rel_l2(Pt, P1) <= 1e-12
+
+
+def test_outlier_force_is_refused_before_launch():
+    """A force far outside the physical range (rates ~ exp(beta W / 2)) would need an
+    effectively unbounded number of Taylor substeps: propagate_many refuses it with a clear
+    error before any launch, and a normal trajectory's substep count is its own."""
+    from blindno import fpe
+    from blindno._lib import BlindnoError
+    ok = _sim2d()
+    wild = fpe.fokker_planck(temperature=300, drag=1e-9, extent=[200 * NM, 240 * NM], resolution=10 * NM,
+                             force=lambda x, y: [1e-11 + 0 * x, 0 * y], boundary=fpe.boundary.reflecting)
+    dt = 0.01 / 5
+    s_ok = fpe.substeps_for(ok.coefficients(), dt)
+    assert s_ok < fpe.MAX_TOTAL_SUBSTEPS
+    pdf = fpe.gaussian_pdf(center=(0.0, 0.0), width=30 * NM)
+    with pytest.raises(BlindnoError, match="refusing to launch"):
+        fpe.propagate_many([ok, wild], [pdf, pdf], 0.01, Nsteps=6, device="cpu")
 
 
 @pytest.mark.gpu

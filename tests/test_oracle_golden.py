@@ -204,3 +204,73 @@ def test_gpe_datagen_oracle():
     assert np.array_equal(V, g["V"])
     _, rec = gpe_ref.solve(gpe_ref.initial_condition(2, x), x, 0.005, 5.0, 2, 2.0, 2.0, V[0])
     assert rel_l2(np.abs(rec)[::10], g["y"][0]) <= 1e-10
+
+
+# ---------------------------------------------------------------- fp32 torch.fft restatement
+# (oracle.cpu_ref: bench.py's CPU baseline and the GPU-vs-CPU parity leg), pinned to the
+# same reference goldens in the reference's own precision (fp32 vs fp32: fwd 1e-5, grads 1e-4)
+
+def _leaf32(g, prefix="p."):
+    out = {}
+    for k, v in _params(g, prefix).items():
+        t = v.to(torch.complex64 if v.is_complex() else torch.float32)
+        out[k] = t.requires_grad_(True)
+    return out
+
+
+def _check32(g, out, params, inputs):
+    assert rel_l2(out.detach().numpy(), g["out"]) <= FWD_TOL
+    (out * torch.from_numpy(g["cot"]).float()).sum().backward()
+    n = 0
+    for k, v in g.items():
+        if k.startswith("g."):
+            assert rel_l2(params[k[2:]].grad.numpy(), v) <= GRAD_TOL, k
+            n += 1
+        elif k.startswith("gin."):
+            assert rel_l2(inputs[k[4:]].grad.numpy(), v) <= GRAD_TOL, k
+            n += 1
+    assert n > 0
+
+
+@pytest.mark.parametrize("case", ["sc2d_a", "sc2d_overlap", "sc2d_nyq"])
+def test_cpu_ref_spectral_conv2d(case):
+    from oracle import cpu_ref
+    g = load_golden(case)
+    p = _leaf32(g)
+    x = torch.from_numpy(g["in.x"]).float().requires_grad_(True)
+    _check32(g, cpu_ref.spectral_conv2d_fft(x, p["weights1"], p["weights2"]), p, {"x": x})
+
+
+@pytest.mark.parametrize("case", ["sc1d", "sc1d_nyq"])
+def test_cpu_ref_spectral_conv1d(case):
+    from oracle import cpu_ref
+    g = load_golden(case)
+    p = _leaf32(g)
+    x = torch.from_numpy(g["in.x"]).float().requires_grad_(True)
+    _check32(g, cpu_ref.spectral_conv1d_fft(x, p["weights1"]), p, {"x": x})
+
+
+@pytest.mark.parametrize("case,heads", [("nio2d_fno_train", ("fno_drift", "fno_diffusion")),
+                                        ("nio2d_fno_eval", ("fno_drift", "fno_diffusion")),
+                                        ("nc_nio2d_fno_eval", ("fno_Fx", "fno_Fy"))])
+def test_cpu_ref_niofp2d_fno(case, heads):
+    from oracle import cpu_ref
+    g = load_golden(case)
+    p = _leaf32(g)
+    x = torch.from_numpy(g["in.x"]).float().requires_grad_(True)
+    grid = torch.from_numpy(g["in.grid"]).float().requires_grad_(True)
+    idx = g["idx"].tolist() if "idx" in g else None
+    _check32(g, cpu_ref.niofp2d_fno_fft(p, x, grid, idx=idx, heads=heads), p, {"x": x, "grid": grid})
+
+
+@pytest.mark.parametrize("case,heads", [("nio1d_fno_train", ("fno_drift", "fno_diffusion")),
+                                        ("nio1d_fno_eval", ("fno_drift", "fno_diffusion")),
+                                        ("gpe_nio_fno_train", ("fno_V",))])
+def test_cpu_ref_niofp_fno_1d(case, heads):
+    from oracle import cpu_ref
+    g = load_golden(case)
+    p = _leaf32(g)
+    x = torch.from_numpy(g["in.x"]).float().requires_grad_(True)
+    grid = torch.from_numpy(g["in.grid"]).float().requires_grad_(True)
+    idx = g["idx"].tolist() if "idx" in g else None
+    _check32(g, cpu_ref.niofp_fno_fft(p, x, grid, idx=idx, heads=heads), p, {"x": x, "grid": grid})
