@@ -346,6 +346,9 @@ def parity_check(cfg_name, model, graphed, opt, xb, yb, grid, T, seed=4321):
     names = {id(q): k for k, q in model.named_parameters()}
     for prm, off, sz in zip(opt.params, opt.offsets, opt.sizes):
         grads_gpu[names[id(prm)]] = opt.grad[off:off + sz].detach().clone()
+    out_gpu, loss_gpu = out_gpu.clone(), loss_gpu.clone()
+    if graphed is not None:
+        graphed.release()            # the timed region is over: free the graph pool for fp64
     p32 = _cpu_params(model)
     out32, loss32 = _cpu_step(cfg_name, p32, xb.cpu(), yb.cpu(), grid.cpu(), idx)
     p64 = {k: v.detach().to(xb.device, torch.complex128 if v.is_complex() else torch.float64)

@@ -747,15 +747,23 @@ def k_rowdft_bag_lift(X, idx_t, w0, Gt, B, T, L, N1, N2, C, P1, P2, m2):
 _GT_CACHE = {}
 
 
-def _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, m2):
+def _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, m2, cacheable=True):
     """Row DFT of the grid / bias part of the encoder's lifted input (x0 of an all-zero
-    snapshot).  It depends only on the grid and on FNO_input.fc0, which change rarely (the
-    grid never during training), so it is cached keyed by their storage and version counters:
-    a training step (and its HIP graph) reuses the cached spectrum instead of re-running the
-    concat, lift and row DFT every step."""
+    snapshot).  It depends only on the grid and on FNO_input.fc0.
+
+    With frozen weights (eval / inference: ``cacheable``) it is cached, keyed by the storage
+    and version counters of grid, fc0.weight and fc0.bias.  In training it is recomputed every
+    step (a lift and a one-sample row DFT, ~17 us): fc0 is a trained parameter, and a HIP graph
+    captured around a cached tensor would replay the capture-time spectrum after the optimizer
+    has moved fc0 (that was a bug: a stale spectrum, 4e-3 rel-L2 on the first layer's weight
+    gradients after 25 steps).  Writers of the weights outside torch ops (FlatAdam's fused
+    kernel) bump the version counters (torch.autograd.graph.increment_version), so a cached
+    entry never outlives the weights it was computed from."""
     key = (grid.device, grid.data_ptr(), grid._version, fc0w.data_ptr(), fc0w._version,
            fc0b.data_ptr(), fc0b._version, N1, N2, C, P1, P2, m2)
-    hit = _GT_CACHE.get(key)
+    capturing = torch.cuda.is_current_stream_capturing()
+    cacheable = cacheable and not capturing
+    hit = _GT_CACHE.get(key) if cacheable else None
     Gt = hit[-1] if hit is not None else None
     if Gt is None:
         inp0 = torch.cat([torch.zeros(1, N1, N2, 1, device=grid.device), grid.view(1, N1, N2, 2)], -1)
@@ -763,7 +771,7 @@ def _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, m2):
         call("blindno_lift_fwd", ptr(inp0), ptr(fc0w), ptr(fc0b), ptr(g0), 1, N1, N2, 3, C, P1, P2,
              stream_ptr())
         Gt = k_rowdft(g0, 1, C, P1, P2, m2, 0)
-        if not torch.cuda.is_current_stream_capturing():
+        if cacheable:
             if len(_GT_CACHE) > 16:
                 _GT_CACHE.clear()
             # the entry holds the inputs too, so their storage (part of the key) is never
@@ -804,7 +812,9 @@ class BagEncoderFn(torch.autograd.Function):
         if C > 4 or meta.dim != 2 or n < 1:
             raise BlindnoError("BagEncoderFn: needs a 2D FNO of width <= 4")
         fc0w, fc0b = prm[0], prm[1]
-        Gt = _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, meta.m2)
+        # cached only when no parameter of the encoder is being trained (frozen weights)
+        frozen = not any(ctx.needs_input_grad[7:])
+        Gt = _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, meta.m2, cacheable=frozen)
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         Xs, Wts, zs = [], [], []
         for k in range(n):

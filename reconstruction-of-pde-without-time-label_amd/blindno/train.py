@@ -99,6 +99,10 @@ class FlatAdam:
         bc2s = math.sqrt(1.0 - b2 ** self.t)
         call("blindno_adam", ptr(self.flat), ptr(self.grad), ptr(self.m), ptr(self.v), self.n,
              b1, b2, self.eps, step_size, bc2s, grad_scale, stream_ptr())
+        # the kernel wrote the parameters behind autograd's back: bump their version counters
+        # (host-side, ~10 us for 150 tensors) so anything keyed on them (caches, saved tensors)
+        # sees the update
+        torch.autograd.graph.increment_version(self.params)
 
     def state_dict(self):
         return {"t": self.t, "m": self.m.clone(), "v": self.v.clone(), "lr": self.lr}
@@ -223,6 +227,17 @@ class GraphedBagStep:
             self.out[L], self.loss[L] = self._body(L)
         self.opt.zero_grad()
         self.graphs[L] = g
+
+    def release(self):
+        """Drop every captured graph and its static buffers (frees the shared graph pool)."""
+        self.graphs.clear()
+        self.out.clear()
+        self.loss.clear()
+        self.idx.clear()
+        self.lw.clear()
+        getattr(self, "blob", {}).clear()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
 
     def step(self, idx) -> int:
         """One training step on the drawn bag ``idx``: replay, all-reduce, Adam.  Returns the

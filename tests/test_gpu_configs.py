@@ -209,3 +209,35 @@ def test_config_d_niofp2d_nc_128():
         n += 1
     assert n > 60
     print("config D worst grads", sorted(worst)[-5:])
+
+
+def test_config_c_after_training_steps():
+    """Config C after 30 Adam steps (lr 5e-4) of the benched graphed step: trained weights make
+    the spectral weight-gradient sums over the bag cancel heavily (the encoder's first layer),
+    which an accumulation that is merely fp32-adequate at initialisation no longer survives.
+    Same bar as above against the fp64 oracle."""
+    import blindno
+    import oracle
+    from blindno import Encoder2D, NIOFP2D_FNO
+    from blindno.train import DataParallel, FlatAdam, GraphedBagStep, trained_parameters
+    torch.manual_seed(0)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2, branch_last_kernel=Encoder2D.kernel_for_grid(128)).cuda().train()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(2, 100, 128, 128, device="cuda", generator=g)
+    y = torch.randn(2, 128, 128, 2, device="cuda", generator=g)
+    grid = _grid2d(128)
+    opt = FlatAdam(trained_parameters(m), lr=5e-4)
+    gs = GraphedBagStep(m, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+    for idx in _draws(100, 11, k=30):
+        gs.step(idx)
+    idx = _draws(100, 12, k=1)[0]
+    key = gs.replay(idx)
+    torch.cuda.synchronize()
+    out = gs.out[key].clone()
+    p64 = _oracle_params(m)
+    ref = oracle.niofp2d_fno(p64, x.double(), grid.double(), idx=idx.tolist())
+    e = rel_l2(out.cpu().numpy(), ref.detach().cpu().numpy())
+    assert e <= FWD_TOL, e
+    ((ref - y.double()) ** 2).mean().backward()
+    worst = _check_grads(m, opt, p64, 40)
+    print("config C trained: fwd", e, "worst grad", worst)

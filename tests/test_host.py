@@ -172,3 +172,15 @@ def test_ctypes_signatures_match_header_arity():
         assert m, name
         args = [a for a in m.group(1).split(",") if a.strip() and a.strip() != "void"]
         assert len(args) == len(sig), (name, len(args), len(sig))
+
+
+def test_trainer_split_is_random_split():
+    """blindno.trainer's 80/20 split = torch's random_split (2d_FPE/train_fno.py:67-69) with a
+    seeded generator (the reference's own split is unseeded: it differs run to run)."""
+    import torch
+    from torch.utils.data import random_split
+    from blindno import trainer
+    for seed in (0, 5):
+        a, b = random_split(range(37), [29, 8], generator=torch.Generator().manual_seed(seed))
+        tr, te = trainer.split_indices(37, seed)
+        assert list(a) == tr and list(b) == te
