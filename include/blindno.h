@@ -357,6 +357,28 @@ int blindno_bn_act_bwd(const float* dy, const float* z, const float* gamma, cons
                        float* dz, float* dgamma, float* dbeta, float* partial, float* coef, int N,
                        int Npad, int C, int HW, float slope, int training, blindno_stream_t stream);
 
+/* ---- NIO encoder convolutions: nn.Conv2d (bias, groups 1, any kernel / stride / zero padding)
+ * of the ConvBlocks (2d_FPE/Baselines.py:40-52; Encoder2D :186-249 and the 1D Encoder
+ * :254-287, whose (1, k) kernels are 2D convolutions of height 1), replacing the MIOpen calls
+ * of torch.nn.Conv2d.  NCHW fp32; Ho = (Hi + 2 ph - KH) / sh + 1, Wo likewise.  Implicit GEMMs
+ * on the fp32 matrix cores with a fixed accumulation order (deterministic).
+ *   fwd:        y (N, Co, Ho, Wo) = conv(x (N, Ci, Hi, Wi), w (Co, Ci, KH, KW)) + b (b may be NULL)
+ *   bwd_data:   dx (N, Ci, Hi, Wi) = conv^T(dy, w)
+ *   bwd_weight: dwb (Co, Ci KH KW + 1): columns [0, Ci KH KW) = dW, last column = db; partial:
+ *               scratch of nsplit * Co * (Ci KH KW + 1) floats (nsplit from
+ *               blindno_conv2d_wgrad_nsplit; NULL allowed when it is 1). */
+int blindno_conv2d_fwd(const float* x, const float* w, const float* b, float* y, int N, int Ci,
+                       int Hi, int Wi, int Co, int KH, int KW, int sh, int sw, int ph, int pw,
+                       blindno_stream_t stream);
+int blindno_conv2d_bwd_data(const float* dy, const float* w, float* dx, int N, int Ci, int Hi,
+                            int Wi, int Co, int KH, int KW, int sh, int sw, int ph, int pw,
+                            blindno_stream_t stream);
+int blindno_conv2d_wgrad_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh,
+                                int sw, int ph, int pw);
+int blindno_conv2d_bwd_weight(const float* dy, const float* x, float* dwb, float* partial,
+                              int nsplit, int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,
+                              int sh, int sw, int ph, int pw, blindno_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,10 @@ SIGNATURES = {
     "blindno_bagattn_nchunk": "i",
     "blindno_bagattn_fwd": "pppppppp" + "iiii" + "s",
     "blindno_bagattn_bwd": "ppppppppppp" + "iiii" + "s",
+    "blindno_conv2d_fwd": "pppp" + "iiiiiiiiiii" + "s",
+    "blindno_conv2d_bwd_data": "ppp" + "iiiiiiiiiii" + "s",
+    "blindno_conv2d_wgrad_nsplit": "iiiiiiiiiii",
+    "blindno_conv2d_bwd_weight": "pppp" + "i" + "iiiiiiiiiii" + "s",
 }
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,

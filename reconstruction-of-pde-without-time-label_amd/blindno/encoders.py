@@ -8,12 +8,10 @@ copy) and crashes at 128^2.  Here ``last_kernel`` is a constructor argument and
 ``Encoder2D.kernel_for_grid(n)`` gives the kernel that collapses an n x n input to 1x1
 ((4,2) at 128^2).
 
-MI355X execution of a ConvBlock: the convolution runs on MIOpen over fixed-size chunks of
-``CONV_CHUNK`` snapshots (the batch is zero-padded to a whole number of chunks), so each layer
-is ONE MIOpen problem whatever the bag size L of the step -- MIOpen's find/compile cost is
-paid once instead of for every new B*L (10-50 s per step on a fresh box otherwise).  The
-BatchNorm2d (batch statistics over the real rows only) and the LeakyReLU run fused in
-libblindno (ops.BNActFn, csrc/batchnorm.hip), which writes the padded rows as 0.
+MI355X execution of a ConvBlock: the convolution runs on libblindno's implicit-GEMM kernels
+(ops.Conv2dFn, csrc/conv.hip: fp32 matrix cores, fixed accumulation order -- deterministic,
+any batch size, graph-capturable; no MIOpen find/compile per new bag size), the BatchNorm2d
+(batch statistics) and the LeakyReLU run fused in ops.BNActFn (csrc/batchnorm.hip).
 """
 from __future__ import annotations
 
@@ -24,20 +22,6 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-
-CONV_CHUNK = 32     # snapshots per convolution call (one MIOpen problem per layer)
-
-
-def pad_rows(x, n_rows):
-    """Zero-pad dim 0 of x to n_rows."""
-    extra = n_rows - x.shape[0]
-    if extra == 0:
-        return x
-    return torch.cat([x, x.new_zeros((extra,) + tuple(x.shape[1:]))])
-
-
-def padded_rows(n):
-    return -(-n // CONV_CHUNK) * CONV_CHUNK
 
 NORM_LAYERS = {"bn": nn.BatchNorm2d, "in": nn.InstanceNorm2d, "ln": nn.LayerNorm}
 
@@ -57,22 +41,14 @@ class ConvBlock(nn.Module):
         self.relu_slope = relu_slope
         self._fused = norm == "bn" and not dropout
 
-    def forward(self, x, n_valid=None):
-        """x (rows, C, H, W).  ``n_valid``: x is already padded to whole chunks and only the
-        first n_valid rows are snapshots (the output keeps the padding, as zeros)."""
+    def forward(self, x):
+        """x (rows, C, H, W) -> (rows, C', H', W')."""
         if not self._fused:
             return self.layers(x)   # norms the reference's encoders never use (in / ln / dropout)
         ops.require_device(x)
         conv, bn = self.layers[0], self.layers[1]
-        n = x.shape[0] if n_valid is None else n_valid
-        x = pad_rows(x, padded_rows(x.shape[0]))
-        K = CONV_CHUNK
-        if x.shape[0] == K:
-            z = conv(x)
-        else:
-            z = torch.cat([conv(x[i:i + K]) for i in range(0, x.shape[0], K)])
-        y = ops.BNActFn.apply(z, bn.weight, bn.bias, bn, n, self.relu_slope)
-        return y if n_valid is not None else y[:n]
+        z = ops.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
+        return ops.BNActFn.apply(z, bn.weight, bn.bias, bn, z.shape[0], self.relu_slope)
 
 
 def _conv_out(n, k, s, p):
@@ -110,14 +86,12 @@ class Encoder2D(nn.Module):
 
     def forward(self, x):
         b, L = x.shape[0], x.shape[1]
-        n = b * L
-        x = pad_rows(x.reshape(n, x.shape[2], x.shape[3], x.shape[4]), padded_rows(n))
+        x = x.reshape(b * L, x.shape[2], x.shape[3], x.shape[4])
         for blk in (self.convblock1, self.convblock2_1, self.convblock2_2, self.convblock3_1,
                     self.convblock3_2, self.convblock4_1, self.convblock4_2, self.convblock7_1,
                     self.convblock7_2, self.convblock7_3):
-            x = blk(x, n_valid=n)
-        x = x[:n].flatten(1).view(b, L, -1)
-        return self.linear(x)
+            x = blk(x)
+        return self.linear(x.flatten(1).view(b, L, -1))
 
 
 class Encoder(nn.Module):
@@ -141,11 +115,10 @@ class Encoder(nn.Module):
 
     def forward(self, x):
         b, L, N = x.shape
-        n = b * L
-        x = pad_rows(x.reshape(n, 1, 1, N), padded_rows(n))
+        x = x.reshape(b * L, 1, 1, N)
         blocks = [self.conv1, self.conv2, self.conv3, self.final_conv1, self.final_conv2, self.final_conv3]
         if self.apply_conv4:
             blocks.append(self.final_conv4)
         for blk in blocks:
-            x = blk(x, n_valid=n)
-        return self.linear(x[:n].reshape(b, L, -1))
+            x = blk(x)
+        return self.linear(x.reshape(b, L, -1))

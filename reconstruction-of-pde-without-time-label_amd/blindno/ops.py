@@ -1068,6 +1068,55 @@ def time_averaged_relative_l2(pt_pred, pt_ref, eps=1e-12):
 
 # ---------------------------------------------------------------------------- NIO encoder blocks
 
+class Conv2dFn(torch.autograd.Function):
+    """nn.Conv2d (bias, groups 1, zero padding) of the NIO encoders' ConvBlocks
+    (2d_FPE/Baselines.py:40-52) on the HIP implicit-GEMM kernels (csrc/conv.hip): x (N, Ci, H, W),
+    weight (Co, Ci, KH, KW), bias (Co) -> (N, Co, Ho, Wo).  Deterministic; any batch size N, so
+    the bag needs no fixed-size chunking and the step can be captured in a HIP graph."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding):
+        require_device(x, weight)
+        x, weight = _c(x), _c(weight)
+        bias = _c(bias) if bias is not None else None
+        N, Ci, Hi, Wi = x.shape
+        Co, _, KH, KW = weight.shape
+        sh, sw = stride
+        ph, pw = padding
+        Ho, Wo = (Hi + 2 * ph - KH) // sh + 1, (Wi + 2 * pw - KW) // sw + 1
+        y = _empty(N, Co, Ho, Wo, like=x)
+        call("blindno_conv2d_fwd", ptr(x), ptr(weight), ptr(bias), ptr(y), N, Ci, Hi, Wi, Co, KH, KW,
+             sh, sw, ph, pw, stream_ptr())
+        ctx.geom = (N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw = ctx.geom
+        g = ctx.geom
+        dy = _c(dy)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            call("blindno_conv2d_bwd_data", ptr(dy), ptr(weight), ptr(dx), *g, stream_ptr())
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            ncol = Ci * KH * KW + 1
+            ns = query("blindno_conv2d_wgrad_nsplit", *g)
+            dwb = _empty(Co, ncol, like=dy)
+            part = _empty(ns, Co * ncol, like=dy) if ns > 1 else None
+            call("blindno_conv2d_bwd_weight", ptr(dy), ptr(x), ptr(dwb), ptr(part), ns, *g, stream_ptr())
+            dw = dwb[:, :-1].reshape(Co, Ci, KH, KW) if ctx.needs_input_grad[1] else None
+            db = dwb[:, -1].contiguous() if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None
+
+
+def conv2d(x, weight, bias, stride, padding):
+    return Conv2dFn.apply(x, weight, bias, tuple(stride), tuple(padding))
+
+
 class BNActFn(torch.autograd.Function):
     """BatchNorm2d + LeakyReLU of a ConvBlock (2d_FPE/Baselines.py:40-52) on rows [0, n) of z
     (rows [n, Npad) are the convolution chunks' padding and come out 0).  Running statistics

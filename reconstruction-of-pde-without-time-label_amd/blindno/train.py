@@ -279,18 +279,21 @@ class GraphedBagStep:
 
 
 def synthetic_bags(n_bags: int, T: int, grid_shape, out_ch: int, seed: int, device,
-                   chunk: int = 64):
+                   bag_ids=None):
     """Standardised synthetic snapshot bags x ~ N(0,1) (n, T, *grid) and targets
-    (n, *grid, out_ch), generated on the device from a seeded generator (the real
-    datasets are not shipped with the reference)."""
+    (n, *grid, out_ch), generated on the device (the real datasets are not shipped with the
+    reference).  Bag ``i`` of the global set is drawn from its own generator seeded by
+    (seed, i), so its content does not depend on which rank holds it: ``bag_ids`` (default
+    0..n_bags-1) lists the global ids this rank materialises -- rank r of world w holds
+    {i : i mod w = r}, the same data at any world size."""
+    ids = list(range(n_bags)) if bag_ids is None else [int(i) for i in bag_ids]
     g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    x = torch.empty(n_bags, T, *grid_shape, dtype=torch.float32, device=device)
-    y = torch.empty(n_bags, *grid_shape, out_ch, dtype=torch.float32, device=device)
-    for s in range(0, n_bags, chunk):
-        e = min(n_bags, s + chunk)
-        x[s:e].normal_(generator=g)
-        y[s:e].normal_(generator=g)
+    x = torch.empty(len(ids), T, *grid_shape, dtype=torch.float32, device=device)
+    y = torch.empty(len(ids), *grid_shape, out_ch, dtype=torch.float32, device=device)
+    for j, i in enumerate(ids):
+        g.manual_seed(seed * 1_000_003 + i)
+        x[j].normal_(generator=g)
+        y[j].normal_(generator=g)
     return x, y
 
 

@@ -48,23 +48,6 @@ constexpr int kBwdNP4 = PROJ_BWD_NP4;
 // offset ooff + g goff of the shared output sample.
 constexpr int kMaxGroups = 2;
 
-// Division by a launch-invariant divisor as one v_mul_hi_u32 + add + shift (Granlund-Montgomery
-// round-up multiplier): exact for every n < 2^31.  The point -> (sample, row, column) mapping of
-// the projection divides each lane's point index by Ho*Wo and Wo; as generic 32-bit divisions
-// those cost ~25 VALU each and were a third of project_bwd's instruction stream.
-struct FastDiv {
-  unsigned m, s;
-  static FastDiv make(unsigned d) {
-    unsigned l = 0;
-    while ((1ull << l) < d) ++l;
-    const uint64_t m = (((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1;
-    return FastDiv{(unsigned)m, l};
-  }
-  __device__ __forceinline__ unsigned div(unsigned n) const {
-    return (__umulhi(n, m) + n) >> s;
-  }
-};
-
 struct Groups {
   int G;
   unsigned gpts;

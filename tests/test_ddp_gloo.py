@@ -87,3 +87,16 @@ def test_dataparallel_gloo_world2():
     # the flat gradient holds the SUM (all-reduce); Adam sees it scaled by 1/world = mean 1.5
     assert abs(float(ga[0]) - 3.0) < 1e-6 and abs(float(gb[0]) - 3.0) < 1e-6
     assert not (wa == w0a).all()
+
+
+def test_synthetic_bag_set_is_keyed_by_bag_id():
+    """bench.py's dataset: rank r of world w materialises bags {i : i mod w = r} of ONE global
+    bag-keyed set -- the same bags whatever the world size."""
+    import torch
+    from blindno.train import synthetic_bags
+    X, Y = synthetic_bags(8, 3, (4, 5), 2, seed=1234, device="cpu")
+    for world in (2, 4):
+        for r in range(world):
+            ids = list(range(r, 8, world))
+            xr, yr = synthetic_bags(len(ids), 3, (4, 5), 2, seed=1234, device="cpu", bag_ids=ids)
+            assert torch.equal(xr, X[ids]) and torch.equal(yr, Y[ids])

@@ -1,10 +1,11 @@
 """NIO snapshot-encoder ConvBlocks on the HIP path vs plain PyTorch fp32 (needs a GPU).
 
-ops.BNActFn (csrc/batchnorm.hip) replaces BatchNorm2d + LeakyReLU(0.2) of ConvBlock
-(2d_FPE/Baselines.py:40-52); the convolution runs on MIOpen over fixed-size chunks of
-encoders.CONV_CHUNK snapshots.  Reference: torch.nn.BatchNorm2d / F.leaky_relu in fp64 on the
-same inputs.  Tolerances: outputs and gradients rel-L2 <= 1e-5 (one normalisation of fp32
-data), running statistics 1e-6.
+ops.Conv2dFn (csrc/conv.hip, implicit GEMM on the fp32 matrix cores) replaces nn.Conv2d and
+ops.BNActFn (csrc/batchnorm.hip) BatchNorm2d + LeakyReLU(0.2) of ConvBlock
+(2d_FPE/Baselines.py:40-52).  References: F.conv2d / torch.nn.BatchNorm2d / F.leaky_relu in
+fp64 on the same inputs.  Tolerances: one convolution or normalisation of fp32 data, rel-L2
+<= 1e-5 (outputs and gradients), running statistics 1e-6; the whole ten-block encoder: see
+test_encoder2d_matches_fp64.
 """
 import pytest
 import torch
@@ -76,15 +77,57 @@ def test_bn_act_matches_torch(shape, n):
     assert torch.equal(rm, bn.running_mean)
 
 
-def test_encoder2d_chunked_matches_torch_modules():
-    """Encoder2D (64x64 snapshots, 2 bags of 37: 74 rows -> 3 chunks of 32) through the
-    chunked HIP path vs the same modules run as plain torch (nn.Sequential).  Both fp32 paths
-    are measured against the torch modules in fp64; the HIP path's error must stay within the
-    plain fp32 torch's own order (ten train-mode BatchNorm'd conv layers amplify fp32 rounding: the
-    first layer's weight gradient differs by ~1e-3 between any two fp32 convolution algorithms,
-    and MIOpen's solver choice -- Winograd for some 3x3 chunk shapes, fp32 error ~1e-4 -- varies
-    run to run): within 4x of torch fp32's error, or <= 1e-3 for gradients (the bar of the
-    reference golden test for this model, tests/test_gpu_evaluators.py)."""
+# every convolution shape of Encoder2D at 128^2 and 61^2 (the reference grid, odd sizes), of the
+# 1D Encoder ((1, k) kernels), plus odd channel counts / strides / paddings
+CONV_CASES = [
+    # (N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)
+    (6, 1, 128, 128, 64, 1, 7, 1, 2, 0, 3),
+    (5, 64, 128, 64, 128, 3, 3, 2, 2, 1, 1),
+    (5, 128, 64, 32, 128, 3, 3, 1, 1, 1, 1),
+    (7, 256, 16, 8, 512, 3, 3, 2, 2, 1, 1),
+    (7, 512, 8, 4, 512, 3, 3, 1, 1, 1, 1),
+    (9, 512, 4, 2, 512, 3, 3, 2, 2, 1, 1),
+    (9, 512, 4, 2, 512, 4, 2, 1, 1, 0, 0),
+    (4, 1, 61, 61, 64, 1, 7, 1, 2, 0, 3),
+    (3, 64, 61, 31, 128, 3, 3, 2, 2, 1, 1),
+    (11, 256, 1, 20, 256, 1, 5, 1, 1, 0, 1),
+    (3, 5, 13, 11, 7, 3, 2, 3, 2, 2, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_matches_fp64(case):
+    from blindno import ops
+    N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw = case
+    torch.manual_seed(sum(case))
+    x = torch.randn(N, Ci, Hi, Wi, device="cuda", dtype=torch.float64)
+    w = torch.randn(Co, Ci, KH, KW, device="cuda", dtype=torch.float64) / (Ci * KH * KW) ** 0.5
+    b = torch.randn(Co, device="cuda", dtype=torch.float64)
+    xs, ws, bs = (t.float().requires_grad_(True) for t in (x, w, b))
+    y = ops.conv2d(xs, ws, bs, (sh, sw), (ph, pw))
+    x64, w64, b64 = (t.clone().requires_grad_(True) for t in (x, w, b))
+    y64 = F.conv2d(x64, w64, b64, stride=(sh, sw), padding=(ph, pw))
+    assert y.shape == y64.shape
+    assert rel_l2(y.detach().cpu().numpy(), y64.detach().cpu().numpy()) <= 1e-5
+    cot = torch.randn_like(y64)
+    (y * cot.float()).sum().backward()
+    (y64 * cot).sum().backward()
+    for got, ref in ((xs.grad, x64.grad), (ws.grad, w64.grad), (bs.grad, b64.grad)):
+        assert rel_l2(got.cpu().numpy(), ref.cpu().numpy()) <= 1e-5
+    # deterministic: a second evaluation is bit-identical
+    y2 = ops.conv2d(xs.detach(), ws.detach(), bs.detach(), (sh, sw), (ph, pw))
+    assert torch.equal(y.detach(), y2)
+
+
+def test_encoder2d_matches_fp64():
+    """Encoder2D (64x64 snapshots, 2 bags of 37) on the HIP path vs the same modules in fp64,
+    and plain fp32 torch (MIOpen) measured the same way.  Ten train-mode BatchNorm'd conv blocks
+    make this model's gradients ill-conditioned in fp32 (plain fp32 torch sits at 1e-6 .. 5e-3
+    rel-L2 from fp64 depending on the tensor and the run's MIOpen solvers), so the bar is the
+    fp32 error level of the model itself, measured in the same run: per tensor
+    e <= max(1e-4, 4 e32[tensor], 4 median(e32)), and over the model median(e) <= 2 median(e32)
+    and max(e) <= 2 max(e32)."""
+    import numpy as np
     import blindno
     torch.manual_seed(1)
     enc = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().train()
@@ -107,23 +150,24 @@ def test_encoder2d_chunked_matches_torch_modules():
     out64 = ref_fwd(ref64, x.double())
     e_out = rel_l2(out.detach().cpu().numpy(), out64.detach().cpu().numpy())
     e_out32 = rel_l2(out32.detach().cpu().numpy(), out64.detach().cpu().numpy())
-    assert e_out <= max(4 * e_out32, 1e-4), (e_out, e_out32)
+    assert e_out <= max(4 * e_out32, 1e-5), (e_out, e_out32)
     cot = torch.randn_like(out64)
     (out * cot.float()).sum().backward()
     (out32 * cot.float()).sum().backward()
     (out64 * cot).sum().backward()
     p32, p64 = dict(ref32.named_parameters()), dict(ref64.named_parameters())
+    es, e32s, keys = [], [], []
     for k, p in enc.named_parameters():
         if k.endswith("layers.0.bias"):
             continue    # conv bias ahead of a batch-statistics BatchNorm: true gradient is exactly 0
         g64 = p64[k].grad.cpu().numpy()
-        e = rel_l2(p.grad.cpu().numpy(), g64)
-        e32 = rel_l2(p32[k].grad.cpu().numpy(), g64)
-        # deep blocks (7_x) normalise over B*L*2*1 values per channel: their BatchNorm weight
-        # gradients amplify the conv algorithm's rounding most (measured 0.3e-3 .. 2.1e-3 over
-        # runs, by the Winograd / direct solver MIOpen picks for a chunk): bar 5e-3 there
-        bar = 5e-3 if k.startswith("convblock7_") else 1e-3
-        assert e <= max(4 * e32, bar), (k, e, e32)
+        es.append(rel_l2(p.grad.cpu().numpy(), g64))
+        e32s.append(rel_l2(p32[k].grad.cpu().numpy(), g64))
+        keys.append(k)
+    med32 = float(np.median(e32s))
+    for k, e, e32 in zip(keys, es, e32s):
+        assert e <= max(1e-4, 4 * e32, 4 * med32), (k, e, e32, med32)
+    assert np.median(es) <= 2 * med32 and max(es) <= 2 * max(e32s), (np.median(es), med32, max(es), max(e32s))
     b64 = dict(ref64.named_buffers())
     for k, b in enc.named_buffers():
         if b.dtype.is_floating_point:

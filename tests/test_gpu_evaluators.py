@@ -2,8 +2,8 @@
 
   a14  GPE split-step solver (blindno_gpe_solve)           tol: rel-L2 1e-10 (fp64)
   a13  1D time-averaged L2 error (blindno_trapz_rows)       tol: 1e-12 relative
-  a8   NIOFP2D (Encoder2D branch + FFN trunk + FNO heads)    tol: fwd 1e-4, param grads 1e-3,
-       input grad 5e-3 (train-mode BatchNorm over the bag, fp32 MIOpen convolutions)
+  a8   NIOFP2D (Encoder2D branch + FFN trunk + FNO heads)    against the fp64 oracle; bar per
+       tensor max(SURVEY 8c bar, 2 x the reference fp32 run's own error, 2 x its median)
   a9   Adam (FlatAdam fused kernel)                          tol: 1e-6
 """
 import json
@@ -86,7 +86,14 @@ def test_time_averaged_L2_error_1d():
 
 
 def test_niofp2d_nio_branch_trunk():
-    """NIOFP2D (config D's model) at the reference grid 80^2, recipe parameters."""
+    """NIOFP2D (config D's model) at the reference grid 80^2, recipe parameters, against the
+    float64 oracle (oracle.niofp2d, itself pinned to this golden on CPU).  The golden is the
+    reference's own fp32 evaluation; its distance to fp64 measures how ill-conditioned this
+    model is in fp32 (ten train-mode BatchNorm'd convolutions): the HIP path must be at least
+    as close to fp64 as the reference itself, within 2x, or within SURVEY 8c's bars (fwd 1e-5,
+    grads 1e-4)."""
+    import numpy as np
+    import oracle
     from blindno import NIOFP2D
     from recipe import make_state
     g = load_golden("nio2d_nc_train")
@@ -98,24 +105,35 @@ def test_niofp2d_nio_branch_trunk():
     x = torch.from_numpy(g["in.x"]).cuda().requires_grad_(True)
     grid = torch.from_numpy(g["in.grid"]).cuda()
     out = m(x, grid, bag_idx=g["idx"])
-    assert rel_l2(out.detach().cpu().numpy(), g["out"]) <= 1e-4
-    (out * torch.from_numpy(g["cot"]).cuda()).sum().backward()
+    cot = torch.from_numpy(g["cot"]).cuda()
+    (out * cot).sum().backward()
+    p64 = {k: torch.from_numpy(v).cuda().double().requires_grad_(v.dtype.kind == "f") for k, v in st.items()}
+    x64 = x.detach().double().requires_grad_(True)
+    ref = oracle.niofp2d(p64, x64, grid.double(), idx=g["idx"].tolist(), heads=("fno_Fx", "fno_Fy"))
+    (ref * cot.double()).sum().backward()
+    e = rel_l2(out.detach().cpu().numpy(), ref.detach().cpu().numpy())
+    e_ref = rel_l2(g["out"], ref.detach().cpu().numpy())
+    assert e <= max(1e-5, 2 * e_ref), (e, e_ref)
     named = dict(m.named_parameters())
-    gmax = max(float(v) for k, v in g.items() if k.startswith("gnorm."))
-    n = 0
+    rows = []                                   # (name, gpu error, reference fp32 error)
+    gmax = max(float(p64[k[6:]].grad.norm()) for k in g if k.startswith("gnorm."))
     for k, v in g.items():
         if k.startswith("g."):
-            assert rel_l2(named[k[2:]].grad.cpu().numpy(), v) <= 1e-3, k
-            n += 1
+            ref_g = p64[k[2:]].grad.cpu().numpy()
+            rows.append((k, rel_l2(named[k[2:]].grad.cpu().numpy(), ref_g), rel_l2(v, ref_g)))
         elif k.startswith("gnorm."):
+            # tensors the fixture keeps only by norm (conv biases ahead of batch-stat BN have
+            # exactly zero gradient: absolute term)
+            want = float(p64[k[6:]].grad.norm())
             got = float(named[k[6:]].grad.double().norm())
-            assert abs(got - float(v)) <= 1e-3 * abs(float(v)) + 1e-5 * gmax, k
-            n += 1
-    assert n > 60
-    # the input gradient crosses all ten train-mode BatchNorm'd conv blocks (MIOpen fp32 vs the
-    # reference's CPU fp32 convolutions): measured 1.6e-3, bounded at 5e-3
-    e = float(rel_l2(x.grad.cpu().numpy(), g["gin.x"]))
-    assert e <= 5e-3, e
+            assert abs(got - want) <= max(2 * abs(float(v) - want), 1e-4 * want) + 1e-5 * gmax, k
+    med = float(np.median([r[2] for r in rows]))
+    for k, eg, er in rows:
+        assert eg <= max(1e-4, 2 * er, 2 * med), (k, eg, er, med)
+    assert len(rows) > 30
+    eg = rel_l2(x.grad.cpu().numpy(), x64.grad.cpu().numpy())
+    er = rel_l2(g["gin.x"], x64.grad.cpu().numpy())
+    assert eg <= max(1e-4, 2 * er), (eg, er)
 
 
 def test_flat_adam_matches_reference_two_steps():
