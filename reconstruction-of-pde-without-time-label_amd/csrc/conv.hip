@@ -6,8 +6,11 @@
 //   FWD   y[n][co][p]   = b[co] + sum_{ci,kh,kw} W[co][ci][kh][kw] x[n][ci][tap(p,kh,kw)]
 //         GEMM  M = Co, N = pixels (n, ho, wo), K = Ci KH KW
 //   BWD_D dx[n][ci][q]  = sum_{co,kh,kw} W[co][ci][kh][kw] dy[n][co][(q + pad - k) / stride]
-//         GEMM  M = Ci, N = input pixels (n, hi, wi), K = Co KH KW (taps that do not land on
-//         an output pixel -- off the grid or off the stride lattice -- contribute 0)
+//         split into stride-phase classes (sub-pixel decomposition): input pixels with
+//         (hi + ph) % sh = ah, (wi + pw) % sw = aw only meet taps kh = ah + sh j, kw = aw + sw j',
+//         so each class (blockIdx.z) is its own GEMM  M = Ci, N = class pixels,
+//         K = Co x (its taps) -- a stride-2 3x3 layer does 9/4 taps per pixel, not 9 (the taps
+//         off the stride lattice are never visited)
 //   BWD_W dW[co][ci][kh][kw] = sum_{n,p} dy[n][co][p] x[n][ci][tap(p,kh,kw)],  db[co] = sum dy
 //         GEMM  M = Co, N = Ci KH KW + 1 (the extra column is the bias: B = 1), K = pixels,
 //         split over blockIdx.z into fixed K ranges; the partials are reduced in a fixed order
@@ -34,23 +37,35 @@ constexpr int SA = BM + 16, SB = BN + 16;      // LDS row strides (floats)
 
 enum { FWD = 0, BWD_D = 1, BWD_W = 2 };
 
+// one stride-phase class of BWD_D: input pixels hi = hi0 + sh t (t < Hc), wi = wi0 + sw u (u < Wc),
+// taps kh = ah + sh jh (jh < nKh), kw = aw + sw jw (jw < nKw); output pixel ho = oh0 + t - jh,
+// wo = ow0 + u - jw
+constexpr int kMaxPhases = 16;   // sh, sw <= 4
+struct Phase {
+  int hi0, wi0, Hc, Wc, ah, aw, nKh, nKw, oh0, ow0, Ncol, K;
+  FastDiv dHcWc, dWc, dKhw, dKw;
+};
+
 struct ConvArgs {
   int N, Ci, Hi, Wi, Co, Ho, Wo, KH, KW, sh, sw, ph, pw;
   int M, Ncol, K;               // GEMM sizes of this mode
   int kchunk;                   // BWD_W: K per split (multiple of BK)
   FastDiv dKHW, dKW, dHoWo, dWo, dHiWi, dWi;
+  Phase phase[kMaxPhases];      // BWD_D
 };
 
 // ---- A operand (BM x BK tile), element (m, k) of global (m0 + m, k0 + k)
 template <int MODE>
-__device__ __forceinline__ float load_a(const float* __restrict__ pa, const ConvArgs& g, int mg,
-                                        int kg, int kend) {
+__device__ __forceinline__ float load_a(const float* __restrict__ pa, const ConvArgs& g,
+                                        const Phase& ph, int mg, int kg, int kend) {
   if (mg >= g.M || kg >= kend) return 0.f;
   const int KHW = g.KH * g.KW;
   if (MODE == FWD) return pa[(int64_t)mg * g.K + kg];                       // W[co][k]
-  if (MODE == BWD_D) {                                                         // W[co][ci][khw]
-    const int co = (int)g.dKHW.div((unsigned)kg), khw = kg - co * KHW;
-    return pa[((int64_t)co * g.Ci + mg) * KHW + khw];
+  if (MODE == BWD_D) {                                    // W[co][ci][ah + sh jh][aw + sw jw]
+    const int nkk = ph.nKh * ph.nKw;
+    const int co = (int)ph.dKhw.div((unsigned)kg), j = kg - co * nkk;
+    const int jh = (int)ph.dKw.div((unsigned)j), jw = j - jh * ph.nKw;
+    return pa[((int64_t)co * g.Ci + mg) * KHW + (ph.ah + g.sh * jh) * g.KW + ph.aw + g.sw * jw];
   }
   // BWD_W: dy[n][co][q], k = pixel
   const int HoWo = g.Ho * g.Wo;
@@ -66,9 +81,9 @@ struct Pix {
 };
 
 template <int MODE>
-__device__ __forceinline__ Pix decode_pix(const ConvArgs& g, int ng) {
+__device__ __forceinline__ Pix decode_pix(const ConvArgs& g, const Phase& ph, int ng) {
   Pix p;
-  p.ok = ng < g.Ncol;
+  p.ok = ng < (MODE == BWD_D ? ph.Ncol : g.Ncol);
   const int v = p.ok ? ng : 0;
   if (MODE == FWD) {
     const int HoWo = g.Ho * g.Wo;
@@ -78,42 +93,44 @@ __device__ __forceinline__ Pix decode_pix(const ConvArgs& g, int ng) {
     p.r = ho * g.sh - g.ph;
     p.c = wo * g.sw - g.pw;
   } else {
-    const int HiWi = g.Hi * g.Wi;
-    const int n = (int)g.dHiWi.div((unsigned)v), q = v - n * HiWi;
-    const int hi = (int)g.dWi.div((unsigned)q), wi = q - hi * g.Wi;
+    // class-local pixel (n, t, u): output rows of its taps ho = oh0 + t - jh, wo = ow0 + u - jw
+    const int HcWc = ph.Hc * ph.Wc;
+    const int n = (int)ph.dHcWc.div((unsigned)v), q = v - n * HcWc;
+    const int t = (int)ph.dWc.div((unsigned)q), u = q - t * ph.Wc;
     p.base = (int64_t)n * g.Co * g.Ho * g.Wo;
-    p.r = hi + g.ph;
-    p.c = wi + g.pw;
+    p.r = ph.oh0 + t;
+    p.c = ph.ow0 + u;
   }
   return p;
+}
+
+// output offset of BWD_D's class-local pixel
+__device__ __forceinline__ int64_t dx_offset(const ConvArgs& g, const Phase& ph, int ng, int ci) {
+  const int HcWc = ph.Hc * ph.Wc;
+  const int n = (int)ph.dHcWc.div((unsigned)ng), q = ng - n * HcWc;
+  const int t = (int)ph.dWc.div((unsigned)q), u = q - t * ph.Wc;
+  return (((int64_t)n * g.Ci + ci) * g.Hi + ph.hi0 + g.sh * t) * g.Wi + ph.wi0 + g.sw * u;
 }
 
 // B element (k, pixel) for FWD / BWD_D
 template <int MODE>
 __device__ __forceinline__ float load_b_pix(const float* __restrict__ pb, const ConvArgs& g,
-                                            const Pix& p, int kg) {
-  if (!p.ok || kg >= g.K) return 0.f;
-  const int KHW = g.KH * g.KW;
-  const int ch = (int)g.dKHW.div((unsigned)kg), khw = kg - ch * KHW;
-  const int kh = (int)g.dKW.div((unsigned)khw), kw = khw - kh * g.KW;
+                                            const Phase& ph, const Pix& p, int kg, int kend) {
+  if (!p.ok || kg >= kend) return 0.f;
   if (MODE == FWD) {
+    const int KHW = g.KH * g.KW;
+    const int ch = (int)g.dKHW.div((unsigned)kg), khw = kg - ch * KHW;
+    const int kh = (int)g.dKW.div((unsigned)khw), kw = khw - kh * g.KW;
     const int hi = p.r + kh, wi = p.c + kw;
     if ((unsigned)hi >= (unsigned)g.Hi || (unsigned)wi >= (unsigned)g.Wi) return 0.f;
     return pb[p.base + ((int64_t)ch * g.Hi + hi) * g.Wi + wi];
   }
-  int th = p.r - kh, tw = p.c - kw;                    // = ho sh, wo sw when on the lattice
-  if (th < 0 || tw < 0) return 0.f;
-  int ho = th, wo = tw;
-  if (g.sh != 1) {
-    ho = th / g.sh;
-    if (ho * g.sh != th) return 0.f;
-  }
-  if (g.sw != 1) {
-    wo = tw / g.sw;
-    if (wo * g.sw != tw) return 0.f;
-  }
-  if (ho >= g.Ho || wo >= g.Wo) return 0.f;
-  return pb[p.base + ((int64_t)ch * g.Ho + ho) * g.Wo + wo];
+  const int nkk = ph.nKh * ph.nKw;
+  const int co = (int)ph.dKhw.div((unsigned)kg), j = kg - co * nkk;
+  const int jh = (int)ph.dKw.div((unsigned)j), jw = j - jh * ph.nKw;
+  const int ho = p.r - jh, wo = p.c - jw;
+  if ((unsigned)ho >= (unsigned)g.Ho || (unsigned)wo >= (unsigned)g.Wo) return 0.f;
+  return pb[p.base + ((int64_t)co * g.Ho + ho) * g.Wo + wo];
 }
 
 // BWD_W B operand: column n = (ci, kh, kw) (or the bias column) fixed per thread and tile
@@ -151,7 +168,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   const int wm = wave >> 1, wn = wave & 1;
   const int c16 = lane & 15, g4 = lane >> 4;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  int kbeg = 0, kend = g.K;
+  const Phase& ph = g.phase[MODE == BWD_D ? blockIdx.z : 0];
+  if (MODE == BWD_D && n0 >= ph.Ncol) return;        // this class has fewer pixels (whole block)
+  int kbeg = 0, kend = MODE == BWD_D ? ph.K : g.K;
   if (MODE == BWD_W) {
     kbeg = blockIdx.z * g.kchunk;
     kend = min(g.K, kbeg + g.kchunk);
@@ -166,7 +185,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   Pix pix{};
   Tap taps[4];
   if (MODE != BWD_W) {
-    pix = decode_pix<MODE>(g, n0 + bn);
+    pix = decode_pix<MODE>(g, ph, n0 + bn);
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) taps[e] = decode_tap(g, n0 + (tid >> 4) + 16 * e);
@@ -176,10 +195,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) ra[e] = load_a<MODE>(pa, g, m0 + am + 16 * e, k0 + ak, kend);
+    for (int e = 0; e < 4; ++e) ra[e] = load_a<MODE>(pa, g, ph, m0 + am + 16 * e, k0 + ak, kend);
     if (MODE != BWD_W) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) rb[e] = load_b_pix<MODE>(pb, g, pix, k0 + bk + 4 * e);
+      for (int e = 0; e < 4; ++e) rb[e] = load_b_pix<MODE>(pb, g, ph, pix, k0 + bk + 4 * e, kend);
     } else {
       const int kg = k0 + ak;                          // this thread's pixel
       const bool kok = kg < kend;
@@ -261,19 +280,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
           const int mg = m0 + wm * 32 + i * 16 + 4 * g4 + r;
           if (mg < g.M) out[((int64_t)blockIdx.z * g.M + mg) * g.Ncol + ng] = acc[i][j][r];
         }
-    } else {
-      const int HW = MODE == FWD ? g.Ho * g.Wo : g.Hi * g.Wi;
-      const int n = (int)(MODE == FWD ? g.dHoWo : g.dHiWi).div((unsigned)ng), q = ng - n * HW;
+    } else if (MODE == FWD) {
+      const int HW = g.Ho * g.Wo;
+      const int n = (int)g.dHoWo.div((unsigned)ng), q = ng - n * HW;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int mg = m0 + wm * 32 + i * 16 + 4 * g4 + r;
-          if (mg < g.M) {
-            float v = acc[i][j][r];
-            if (MODE == FWD && bias) v += bias[mg];
-            out[((int64_t)n * g.M + mg) * HW + q] = v;
-          }
+          if (mg < g.M) out[((int64_t)n * g.M + mg) * HW + q] = acc[i][j][r] + (bias ? bias[mg] : 0.f);
+        }
+    } else {
+      if (ng >= ph.Ncol) continue;
+      const int64_t o0 = dx_offset(g, ph, ng, 0), cs = (int64_t)g.Hi * g.Wi;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int mg = m0 + wm * 32 + i * 16 + 4 * g4 + r;
+          if (mg < g.M) out[o0 + mg * cs] = acc[i][j][r];
         }
     }
   }
@@ -331,13 +356,47 @@ BLINDNO_API int blindno_conv2d_bwd_data(const float* dy, const float* w, float* 
                                         int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
                                         int ph, int pw, void* stream) {
   ConvArgs g;
-  if (!dy || !w || !dx || !make_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw))
+  if (!dy || !w || !dx || sh * sw > kMaxPhases ||
+      !make_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw))
     return (int)hipErrorInvalidValue;
   g.M = Ci;
   g.Ncol = N * Hi * Wi;
   g.K = Co * KH * KW;
-  const dim3 grid(cdiv(g.Ncol, BN), cdiv(g.M, BM), 1);
-  conv_igemm_kernel<BWD_D><<<grid, 256, 0, (hipStream_t)stream>>>(w, dy, nullptr, dx, g);
+  // stride-phase classes; pixels of a class whose taps are all off the kernel (nKh or nKw = 0)
+  // receive no gradient, so they are zeroed first (only possible when the stride exceeds the
+  // kernel extent)
+  int maxcol = 1;
+  bool uncovered = false;
+  for (int ah = 0; ah < sh; ++ah)
+    for (int aw = 0; aw < sw; ++aw) {
+      Phase& p = g.phase[ah * sw + aw];
+      p.ah = ah;
+      p.aw = aw;
+      p.hi0 = ((ah - ph) % sh + sh) % sh;
+      p.wi0 = ((aw - pw) % sw + sw) % sw;
+      p.Hc = p.hi0 < Hi ? (Hi - p.hi0 + sh - 1) / sh : 0;
+      p.Wc = p.wi0 < Wi ? (Wi - p.wi0 + sw - 1) / sw : 0;
+      p.nKh = ah < KH ? (KH - ah + sh - 1) / sh : 0;
+      p.nKw = aw < KW ? (KW - aw + sw - 1) / sw : 0;
+      p.oh0 = (p.hi0 + ph - ah) / sh;
+      p.ow0 = (p.wi0 + pw - aw) / sw;
+      p.Ncol = N * p.Hc * p.Wc;
+      p.K = Co * p.nKh * p.nKw;
+      if (p.K == 0 && p.Ncol > 0) uncovered = true;
+      if (p.K == 0) p.Ncol = 0;
+      p.dHcWc = FastDiv::make((unsigned)(p.Hc * p.Wc > 0 ? p.Hc * p.Wc : 1));
+      p.dWc = FastDiv::make((unsigned)(p.Wc > 0 ? p.Wc : 1));
+      p.dKhw = FastDiv::make((unsigned)(p.nKh * p.nKw > 0 ? p.nKh * p.nKw : 1));
+      p.dKw = FastDiv::make((unsigned)(p.nKw > 0 ? p.nKw : 1));
+      if (p.Ncol > maxcol) maxcol = p.Ncol;
+    }
+  hipStream_t st = (hipStream_t)stream;
+  if (uncovered) {
+    const hipError_t e = hipMemsetAsync(dx, 0, sizeof(float) * (size_t)N * Ci * Hi * Wi, st);
+    if (e != hipSuccess) return (int)e;
+  }
+  const dim3 grid(cdiv(maxcol, BN), cdiv(g.M, BM), sh * sw);
+  conv_igemm_kernel<BWD_D><<<grid, 256, 0, st>>>(w, dy, nullptr, dx, g);
   return (int)hipGetLastError();
 }
 
