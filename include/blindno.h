@@ -379,6 +379,42 @@ int blindno_conv2d_bwd_weight(const float* dy, const float* x, float* dwb, float
                               int nsplit, int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,
                               int sh, int sw, int ph, int pw, blindno_stream_t stream);
 
+/* ---- whole-op spectral convolutions for C / C++ hosts (no Python needed) ---------------
+ * SpectralConv2d.forward / backward (2d_FPE/FNOModules.py:156-178: rfft2 -> corner mix with
+ * weights1/weights2 -> irfft2) and SpectralConv1d (1d_FPE/FNOModules.py:47-59, DC bin x0.5)
+ * as ONE call each, over the stage kernels above.  The library never allocates: the caller
+ * owns
+ *   tables: twiddle images of one shape, blindno_spectral{2,1}d_tables_bytes bytes, filled once
+ *           by blindno_spectral{2,1}d_tables_init (host-built in double, blocking copy);
+ *   work:   scratch, blindno_spectral_conv{2,1}d_workspace_bytes(..., bwd) bytes;
+ *   saved:  the forward's spectrum, read by the backward (..._saved_bytes).
+ * Shapes: x (Bn, Ci, P1, P2) / (Bn, Ci, P2); w1, w2 (Ci, Co, m1, m2, 2) real view; 1D w
+ * (Ci, Co, m) complex64 interleaved; y (Bn, Co, P1, P2) / (Bn, Co, P2).  Ci, Co <= 32,
+ * m2 <= min(48, P2/2 + 1).  Backward: dx may be NULL (no input gradient).  Byte queries
+ * return -1 on an invalid shape. */
+int64_t blindno_spectral2d_tables_bytes(int P1, int P2, int m1, int m2);
+int blindno_spectral2d_tables_init(void* tables, int P1, int P2, int m1, int m2);
+int64_t blindno_spectral_conv2d_workspace_bytes(int Bn, int Ci, int Co, int P1, int P2, int m1,
+                                                int m2, int bwd);
+int64_t blindno_spectral_conv2d_saved_bytes(int Bn, int Ci, int P1, int m1, int m2);
+int blindno_spectral_conv2d_fwd(const float* x, const float* w1, const float* w2, float* y,
+                                float* saved, void* work, const void* tables, int Bn, int Ci,
+                                int Co, int P1, int P2, int m1, int m2, blindno_stream_t stream);
+int blindno_spectral_conv2d_bwd(const float* dy, const float* saved, const float* w1,
+                                const float* w2, float* dx, float* dw1, float* dw2, void* work,
+                                const void* tables, int Bn, int Ci, int Co, int P1, int P2,
+                                int m1, int m2, blindno_stream_t stream);
+int64_t blindno_spectral1d_tables_bytes(int P2, int m);
+int blindno_spectral1d_tables_init(void* tables, int P2, int m);
+int64_t blindno_spectral_conv1d_workspace_bytes(int Bn, int Ci, int Co, int P2, int m, int bwd);
+int64_t blindno_spectral_conv1d_saved_bytes(int Bn, int Ci, int m);
+int blindno_spectral_conv1d_fwd(const float* x, const float* w, float* y, float* saved,
+                                void* work, const void* tables, int Bn, int Ci, int Co, int P2,
+                                int m, blindno_stream_t stream);
+int blindno_spectral_conv1d_bwd(const float* dy, const float* saved, const float* w, float* dx,
+                                float* dw, void* work, const void* tables, int Bn, int Ci,
+                                int Co, int P2, int m, blindno_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

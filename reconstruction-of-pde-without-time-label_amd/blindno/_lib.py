@@ -75,7 +75,23 @@ SIGNATURES = {
     "blindno_conv2d_bwd_data": "ppp" + "iiiiiiiiiii" + "s",
     "blindno_conv2d_wgrad_nsplit": "iiiiiiiiiii",
     "blindno_conv2d_bwd_weight": "pppp" + "i" + "iiiiiiiiiii" + "s",
+    # whole-op spectral convolutions (C hosts); int64_t byte queries
+    "blindno_spectral2d_tables_bytes": "iiii",
+    "blindno_spectral2d_tables_init": "piiii",
+    "blindno_spectral_conv2d_workspace_bytes": "iiiiiiii",
+    "blindno_spectral_conv2d_saved_bytes": "iiiii",
+    "blindno_spectral_conv2d_fwd": "ppppppp" + "iiiiiii" + "s",
+    "blindno_spectral_conv2d_bwd": "ppppppppp" + "iiiiiii" + "s",
+    "blindno_spectral1d_tables_bytes": "ii",
+    "blindno_spectral1d_tables_init": "pii",
+    "blindno_spectral_conv1d_workspace_bytes": "iiiiii",
+    "blindno_spectral_conv1d_saved_bytes": "iii",
+    "blindno_spectral_conv1d_fwd": "pppppp" + "iiiii" + "s",
+    "blindno_spectral_conv1d_bwd": "ppppppp" + "iiiii" + "s",
 }
+
+# entry points returning int64_t (byte counts) instead of an error code / int count
+RET64 = {n for n in SIGNATURES if n.endswith("_bytes")}
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,
        "d": ctypes.c_double, "s": ctypes.c_void_p}
@@ -103,7 +119,7 @@ def load():
         for name, sig in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.argtypes = [_CT[c] for c in sig]
-            fn.restype = ctypes.c_int
+            fn.restype = ctypes.c_int64 if name in RET64 else ctypes.c_int
         lib.blindno_error_string.argtypes = [ctypes.c_int]
         lib.blindno_error_string.restype = ctypes.c_char_p
         _lib = lib

@@ -81,7 +81,31 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
             raise RuntimeError(f"link failed:\n{r.stderr}")
         if verbose:
             print(f"[blindno build] linked {OUT}", file=sys.stderr)
+    build_cabi_test(hipcc, force, verbose)
     return OUT
+
+
+CABI_SRC = os.path.join(os.path.dirname(HERE), "tests", "cabi", "test_cabi.cpp")
+CABI_BIN = os.path.join(os.path.dirname(HERE), "tests", "cabi", "test_cabi")
+
+
+def build_cabi_test(hipcc: str, force: bool = False, verbose: bool = True) -> str:
+    """The C++ caller of the C ABI (tests/cabi/test_cabi.cpp -> tests/cabi/test_cabi), linked
+    against the in-tree libblindno.so through an $ORIGIN-relative rpath (the tree moves to the
+    GPU box as a whole)."""
+    if not os.path.exists(CABI_SRC):
+        return ""
+    if not force and not _newer([CABI_SRC, OUT, os.path.join(INCLUDE, "blindno.h")], CABI_BIN):
+        return CABI_BIN
+    rel = os.path.relpath(os.path.dirname(OUT), os.path.dirname(CABI_BIN))
+    cmd = [hipcc, "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE, CABI_SRC,
+           "-L", os.path.dirname(OUT), "-lblindno", f"-Wl,-rpath,$ORIGIN/{rel}", "-o", CABI_BIN]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"C ABI test build failed:\n{r.stderr}")
+    if verbose:
+        print(f"[blindno build] built {CABI_BIN}", file=sys.stderr)
+    return CABI_BIN
 
 
 if __name__ == "__main__":

@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "blindno.h")
 
 def _declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(blindno_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(blindno_\w+)\(", txt, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -168,7 +168,7 @@ def test_ctypes_signatures_match_header_arity():
     from blindno import _lib
     txt = open(HEADER).read()
     for name, sig in _lib.SIGNATURES.items():
-        m = re.search(r"^(?:int|const char\*)\s+" + name + r"\(([^)]*)\)", txt, re.M | re.S)
+        m = re.search(r"^(?:int|int64_t|const char\*)\s+" + name + r"\(([^)]*)\)", txt, re.M | re.S)
         assert m, name
         args = [a for a in m.group(1).split(",") if a.strip() and a.strip() != "void"]
         assert len(args) == len(sig), (name, len(args), len(sig))
