@@ -3,7 +3,8 @@ path, drop-in for yl602019618/Reconstruction-of-PDE-without-Time-Label's
 FNOModules / NIOModules / DeepONetModules / Baselines surface.
 
 All numerics run in libblindno.so (HIP kernels behind the C ABI of include/blindno.h);
-there is no CPU fallback.
+there is no CPU fallback.  Importing the package registers the hot-path operators as
+``torch.ops.blindno.*`` (blindno/torch_ops.py).
 """
 from . import _lib  # noqa: F401
 from ._lib import BlindnoError, load as load_library  # noqa: F401
@@ -13,5 +14,6 @@ from .nio import (NIOFP, NIOFP2D, NIOFP2D_FNO, NIOFP2D_FNO_attn, NIOFP_FNO,  # n
 from .deeponet import FFN, DeepOnetNoBiasOrg, FeedForwardNN  # noqa: F401
 from .encoders import ConvBlock, Encoder, Encoder2D  # noqa: F401
 from .ops import mse_loss, pad_amount  # noqa: F401
+from . import torch_ops  # noqa: F401  (registers torch.ops.blindno.*)
 
 __version__ = "0.1.0"

@@ -134,10 +134,19 @@ def stream_ptr(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+class _TensorPtr(ctypes.c_void_p):
+    """A device pointer that keeps its tensor alive: ``call(name, ptr(x.contiguous()), ...)``
+    must not hand the kernel a block the caching allocator already took back (and gave to the
+    next temporary in the same argument list) before the launch is enqueued."""
+    __slots__ = ("tensor",)
+
+
 def ptr(t):
     if t is None:
         return None
-    return ctypes.c_void_p(t.data_ptr())
+    p = _TensorPtr(t.data_ptr())
+    p.tensor = t
+    return p
 
 
 _HOOKS = {}   # kernel name -> object with before(args) / after(args) (blindno.timing)
