@@ -327,20 +327,27 @@ _ENC2D_BLOCKS = [
 ]
 
 
-def encoder2d(p: Dict[str, torch.Tensor], x: torch.Tensor) -> torch.Tensor:
+def encoder2d(p: Dict[str, torch.Tensor], x: torch.Tensor,
+              masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
     """Encoder2D.forward (train-mode BatchNorm), 2d_FPE/Baselines.py:203-249.
 
     ConvBlock = Conv2d -> BatchNorm2d (batch statistics) -> LeakyReLU(0.2)
     (2d_FPE/Baselines.py:40-52).  x (B, L, 1, nx, ny) -> (B, L, n_out).
+
+    ``masks`` (optional, one bool tensor per block, True where the pre-activation is > 0): take
+    each LeakyReLU's branch from the path under test instead of from this evaluation.  The model
+    is piecewise linear, its gradient jumps across a branch, and a pre-activation within fp32
+    rounding of 0 can land on either side in two correct evaluations; with the checked path's own
+    branches the comparison is of one linear piece (tests/test_gpu_encoder.py, test_gpu_configs.py).
     """
     B, L = x.shape[:2]
     h = x.reshape(B * L, *x.shape[2:]).to(DT)
-    for name, stride, pad in _ENC2D_BLOCKS:
+    for k, (name, stride, pad) in enumerate(_ENC2D_BLOCKS):
         h = F.conv2d(h, p[f"{name}.layers.0.weight"].to(DT), p[f"{name}.layers.0.bias"].to(DT),
                      stride=stride, padding=pad)
         h = F.batch_norm(h, None, None, p[f"{name}.layers.1.weight"].to(DT),
                          p[f"{name}.layers.1.bias"].to(DT), training=True, eps=1e-5)
-        h = F.leaky_relu(h, 0.2)
+        h = F.leaky_relu(h, 0.2) if masks is None else torch.where(masks[k], h, 0.2 * h)
     h = h.flatten(1).view(B, L, -1)
     return _linear(h, p, "linear")
 
@@ -365,15 +372,16 @@ def deeponet_nobias(weights: torch.Tensor, basis: torch.Tensor, b0: torch.Tensor
 
 def niofp2d(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
             idx: Optional[Sequence[int]] = None, n_hidden_layers: int = 3,
-            heads: Sequence[str] = ("fno_drift", "fno_diffusion")) -> torch.Tensor:
+            heads: Sequence[str] = ("fno_drift", "fno_diffusion"),
+            branch_masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
     """NIOFP2D.forward, 2d_FPE/NIOModules.py:47-83 (NC: heads fno_Fx/fno_Fy,
-    2d_Non_conservative_FPE/NIOModules.py:46-82)."""
+    2d_Non_conservative_FPE/NIOModules.py:46-82).  ``branch_masks``: see encoder2d."""
     x = x.to(DT)
     if idx is not None:
         x = x[:, list(idx)]
     B, L, nx, ny = x.shape
     g = grid.to(DT)
-    w = encoder2d(sub_params(p, "branch"), x.unsqueeze(2))
+    w = encoder2d(sub_params(p, "branch"), x.unsqueeze(2), branch_masks)
     basis = ffn(sub_params(p, "trunk"), g.reshape(-1, 2), n_hidden_layers)
     u = deeponet_nobias(w, basis, p["deeponet.b0"]).view(B, L, nx, ny)
     gcf = g.unsqueeze(0).repeat(B, 1, 1, 1).permute(0, 3, 1, 2)

@@ -26,7 +26,11 @@ namespace {
 constexpr int kBnThreads = 256;
 
 // per-channel coefficient record (save buffer, [C][kSave]):
-//   0 mean, 1 invstd, 2 a = gamma invstd, 3 b = beta - mean a  (forward, y = act(a z + b))
+//   0 mean, 1 invstd, 2 a = gamma invstd, 3 beta   (forward, y = act(a (z - mean) + beta))
+// The affine is applied to the CENTRED value: folding it into a z + (beta - mean a) loses
+// eps |mean| / std of the pre-activation to cancellation, which for the deep 1x1 / 2x1 blocks
+// of the encoders (|mean| >> std over the batch) flips LeakyReLU branches and costs ~1e-3 of
+// gradient accuracy (tools/diag_encoder_bwd.py).
 constexpr int kSave = 4;
 
 __device__ __forceinline__ float leaky(float v, float slope) { return v > 0.f ? v : v * slope; }
@@ -115,7 +119,7 @@ __global__ void bn_finalize_kernel(const float* __restrict__ z, const float* __r
   save[c * kSave + 0] = mean;
   save[c * kSave + 1] = invstd;
   save[c * kSave + 2] = a;
-  save[c * kSave + 3] = b - mean * a;
+  save[c * kSave + 3] = b;
 }
 
 template <bool VEC>
@@ -132,12 +136,12 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const float* __res
       float4 o = {0.f, 0.f, 0.f, 0.f};
       if (e < valid) {
         const int c = (int)((e / HW) % C);
-        const float a = save[c * kSave + 2], b = save[c * kSave + 3];
+        const float m = save[c * kSave + 0], a = save[c * kSave + 2], b = save[c * kSave + 3];
         const float4 v = *reinterpret_cast<const float4*>(z + e);
-        o.x = leaky(fmaf(a, v.x, b), slope);
-        o.y = leaky(fmaf(a, v.y, b), slope);
-        o.z = leaky(fmaf(a, v.z, b), slope);
-        o.w = leaky(fmaf(a, v.w, b), slope);
+        o.x = leaky(fmaf(a, v.x - m, b), slope);
+        o.y = leaky(fmaf(a, v.y - m, b), slope);
+        o.z = leaky(fmaf(a, v.z - m, b), slope);
+        o.w = leaky(fmaf(a, v.w - m, b), slope);
       }
       *reinterpret_cast<float4*>(y + e) = o;
     }
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const float* __res
       float o = 0.f;
       if (e < valid) {
         const int c = (int)((e / HW) % C);
-        o = leaky(fmaf(save[c * kSave + 2], z[e], save[c * kSave + 3]), slope);
+        o = leaky(fmaf(save[c * kSave + 2], z[e] - save[c * kSave + 0], save[c * kSave + 3]), slope);
       }
       y[e] = o;
     }
@@ -164,9 +168,10 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_stats_kernel(
   const float a = save[c * kSave + 2], b = save[c * kSave + 3];
   float sg = 0.f, sgx = 0.f;
   auto acc = [&](float zv, float dv) {
-    const float g = fmaf(a, zv, b) > 0.f ? dv : dv * slope;
+    const float zc = zv - mean;
+    const float g = fmaf(a, zc, b) > 0.f ? dv : dv * slope;
     sg += g;
-    sgx = fmaf(g, (zv - mean) * invstd, sgx);
+    sgx = fmaf(g, zc * invstd, sgx);
   };
   if (VEC) {
     const int HW4 = HW >> 2;
@@ -235,8 +240,9 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(
         const float4 v = *reinterpret_cast<const float4*>(z + e);
         const float4 d = *reinterpret_cast<const float4*>(dy + e);
         auto one = [&](float zv, float dv) {
-          const float g = fmaf(a, zv, b) > 0.f ? dv : dv * slope;
-          return k1 * (g - mg - (zv - mean) * invstd * mgx);
+          const float zc = zv - mean;
+          const float g = fmaf(a, zc, b) > 0.f ? dv : dv * slope;
+          return k1 * (g - mg - zc * invstd * mgx);
         };
         o.x = one(v.x, d.x); o.y = one(v.y, d.y); o.z = one(v.z, d.z); o.w = one(v.w, d.w);
       }
@@ -247,9 +253,9 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(
       float o = 0.f;
       if (e < valid) {
         const int c = (int)((e / HW) % C);
-        const float zv = z[e], dv = dy[e];
-        const float g = fmaf(save[c * kSave + 2], zv, save[c * kSave + 3]) > 0.f ? dv : dv * slope;
-        o = coef[c * 3 + 0] * (g - coef[c * 3 + 1] - (zv - save[c * kSave]) * save[c * kSave + 1] * coef[c * 3 + 2]);
+        const float zc = z[e] - save[c * kSave], dv = dy[e];
+        const float g = fmaf(save[c * kSave + 2], zc, save[c * kSave + 3]) > 0.f ? dv : dv * slope;
+        o = coef[c * 3 + 0] * (g - coef[c * 3 + 1] - zc * save[c * kSave + 1] * coef[c * 3 + 2]);
       }
       dz[e] = o;
     }

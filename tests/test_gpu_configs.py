@@ -160,12 +160,15 @@ def test_config_d_niofp2d_nc_128():
     final kernel, FFN trunk, DeepONet combiner, heads fno_Fx/fno_Fy) at 128^2, B = 2, one
     recorded draw, eager step as bench.py runs it.
 
-    Ten train-mode BatchNorm'd convolutions amplify fp32 rounding: the bar for each tensor is
-    max(4 x the error of the same graph evaluated in plain fp32 torch, the SURVEY 8c bar), both
-    measured against fp64 on the same inputs."""
+    The branch is piecewise linear (ten Conv -> BatchNorm -> LeakyReLU blocks): a pre-activation
+    within fp32 rounding of 0 can take either branch in two correct evaluations, and one flip
+    moves a gradient by ~1e-3.  The fp64 oracle therefore takes every branch LeakyReLU's side
+    from the HIP forward (``branch_masks``, recorded by hooks) -- the same linear piece -- and the
+    SURVEY 8c bars hold as fixed numbers (forward 1e-5, gradients 1e-4)."""
     import blindno
     import oracle
     from blindno import Encoder2D, NIOFP2D
+    from test_gpu_encoder import _branch_masks
     torch.manual_seed(6)
     m = NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, heads=("fno_Fx", "fno_Fy"),
                 branch_last_kernel=Encoder2D.kernel_for_grid(128)).cuda().train()
@@ -175,37 +178,28 @@ def test_config_d_niofp2d_nc_128():
     grid = _grid2d(128)
     idx = _draws(100, 10, k=1)[0]
     heads = ("fno_Fx", "fno_Fy")
+    masks, hooks = _branch_masks(m.branch)
     out = m(x, grid, bag_idx=idx)
+    for h in hooks:
+        h.remove()
+    assert len(masks) == 10
     blindno.mse_loss(out, y).backward()
     torch.cuda.synchronize()
-
-    def oracle_run(prec):
-        oracle.set_precision(prec)
-        try:
-            dt = torch.float64 if prec == "fp64" else torch.float32
-            p = {k: v.detach().to(dt).requires_grad_(True) for k, v in m.state_dict().items()
-                 if v.is_floating_point() and not k.endswith(("running_mean", "running_var"))}
-            ref = oracle.niofp2d(p, x.to(dt), grid.to(dt), idx=idx.tolist(), heads=heads)
-            ((ref - y.to(dt)) ** 2).mean().backward()
-            return ref.detach().double(), {k: v.grad for k, v in p.items()}
-        finally:
-            oracle.set_precision("fp64")
-
-    ref64, g64 = oracle_run("fp64")
-    ref32, g32 = oracle_run("fp32")
-    e = rel_l2(out.detach().cpu().numpy(), ref64.cpu().numpy())
-    e32 = rel_l2(ref32.cpu().numpy(), ref64.cpu().numpy())
-    print(f"config D fwd {e:.2e} (fp32 torch {e32:.2e})")
-    assert e <= max(4 * e32, FWD_TOL), (e, e32)
+    p = {k: v.detach().double().requires_grad_(True) for k, v in m.state_dict().items()
+         if v.is_floating_point() and not k.endswith(("running_mean", "running_var"))}
+    ref64 = oracle.niofp2d(p, x.double(), grid.double(), idx=idx.tolist(), heads=heads, branch_masks=masks)
+    ((ref64 - y.double()) ** 2).mean().backward()
+    e = rel_l2(out.detach().cpu().numpy(), ref64.detach().cpu().numpy())
+    print(f"config D fwd {e:.2e}")
+    assert e <= FWD_TOL, e
     n, worst = 0, []
     for k, prm in m.named_parameters():
         if k.startswith("fc0.") or k.endswith("layers.0.bias"):
             continue     # fc0 is read through .data; a conv bias ahead of batch-stat BN has grad 0
-        assert prm.grad is not None and g64[k] is not None, k
-        e = rel_l2(prm.grad.cpu().numpy(), g64[k].cpu().numpy())
-        e32 = rel_l2(g32[k].double().cpu().numpy(), g64[k].cpu().numpy())
-        worst.append((e, e32, k))
-        assert e <= max(4 * e32, GRAD_TOL), (k, e, e32)
+        assert prm.grad is not None and p[k].grad is not None, k
+        e = rel_l2(prm.grad.cpu().numpy(), p[k].grad.cpu().numpy())
+        worst.append((e, k))
+        assert e <= GRAD_TOL, (k, e)
         n += 1
     assert n > 60
     print("config D worst grads", sorted(worst)[-5:])

@@ -119,58 +119,60 @@ def test_conv2d_matches_fp64(case):
     assert torch.equal(y.detach(), y2)
 
 
+def _branch_masks(enc):
+    """Forward hooks recording each ConvBlock's LeakyReLU branch (output > 0 <=> pre-activation > 0)."""
+    masks, hooks = [], []
+    for name in ("convblock1", "convblock2_1", "convblock2_2", "convblock3_1", "convblock3_2", "convblock4_1",
+                 "convblock4_2", "convblock7_1", "convblock7_2", "convblock7_3"):
+        hooks.append(getattr(enc, name).register_forward_hook(lambda mod, i, o: masks.append(o.detach() > 0)))
+    return masks, hooks
+
+
 def test_encoder2d_matches_fp64():
-    """Encoder2D (64x64 snapshots, 2 bags of 37) on the HIP path vs the same modules in fp64,
-    and plain fp32 torch (MIOpen) measured the same way.  Ten train-mode BatchNorm'd conv blocks
-    make this model's gradients ill-conditioned in fp32 (plain fp32 torch sits at 1e-6 .. 5e-3
-    rel-L2 from fp64 depending on the tensor and the run's MIOpen solvers), so the bar is the
-    fp32 error level of the model itself, measured in the same run: per tensor
-    e <= max(1e-4, 4 e32[tensor], 4 median(e32)), and over the model median(e) <= 4 median(e32)
-    and max(e) <= 4 max(e32).  Two exact-fp32 implementations land a factor ~2-3 apart either way
-    on such a model (measured: this test 2.4e-3 vs torch's 1.0e-3 median; at config D's 128^2,
-    tests/test_gpu_configs.py, the HIP path's worst tensors are 2-2.5x CLOSER to fp64 than
-    torch's), which is what the factor 4 covers."""
-    import numpy as np
+    """Encoder2D (64x64 snapshots, 2 bags of 37, train-mode BatchNorm) on the HIP path vs the same
+    modules in fp64.  The model is piecewise linear (LeakyReLU): a pre-activation within fp32
+    rounding of 0 may take either branch in two correct evaluations, and one such flip moves a
+    gradient by ~1e-3 rel-L2 (tools/diag_encoder_bwd.py / diag_bn.py: plain fp32 torch lands at
+    1e-6 or 2e-3 on the same tensor depending on whether it flipped).  So the fp64 evaluation takes
+    every LeakyReLU branch from the HIP forward (hooks on the blocks) -- the same linear piece --
+    and the SURVEY 8c bars then hold as fixed numbers: output <= 1e-5, every gradient <= 1e-4."""
     import blindno
     torch.manual_seed(1)
     enc = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().train()
-    ref32 = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().train()
     ref64 = blindno.Encoder2D(25, last_kernel=blindno.Encoder2D.kernel_for_grid(64)).cuda().double().train()
-    ref32.load_state_dict(enc.state_dict())
     ref64.load_state_dict(enc.state_dict())
     x = torch.randn(2, 37, 1, 64, 64, device="cuda")
+    masks, hooks = _branch_masks(enc)
+    out = enc(x)
+    for h in hooks:
+        h.remove()
+    assert len(masks) == 10
 
     def ref_fwd(m, x):
         b, L = x.shape[:2]
         h = x.reshape(b * L, 1, 64, 64)
-        for blk in (m.convblock1, m.convblock2_1, m.convblock2_2, m.convblock3_1, m.convblock3_2,
-                    m.convblock4_1, m.convblock4_2, m.convblock7_1, m.convblock7_2, m.convblock7_3):
-            h = blk.layers(h)
+        for blk, mask in zip((m.convblock1, m.convblock2_1, m.convblock2_2, m.convblock3_1, m.convblock3_2,
+                              m.convblock4_1, m.convblock4_2, m.convblock7_1, m.convblock7_2, m.convblock7_3),
+                             masks):
+            z = blk.layers[1](blk.layers[0](h))
+            h = torch.where(mask, z, blk.relu_slope * z)
         return m.linear(h.flatten(1).view(b, L, -1))
 
-    out = enc(x)
-    out32 = ref_fwd(ref32, x)
     out64 = ref_fwd(ref64, x.double())
     e_out = rel_l2(out.detach().cpu().numpy(), out64.detach().cpu().numpy())
-    e_out32 = rel_l2(out32.detach().cpu().numpy(), out64.detach().cpu().numpy())
-    assert e_out <= max(4 * e_out32, 1e-5), (e_out, e_out32)
+    assert e_out <= 1e-5, e_out
     cot = torch.randn_like(out64)
     (out * cot.float()).sum().backward()
-    (out32 * cot.float()).sum().backward()
     (out64 * cot).sum().backward()
-    p32, p64 = dict(ref32.named_parameters()), dict(ref64.named_parameters())
-    es, e32s, keys = [], [], []
+    p64 = dict(ref64.named_parameters())
+    worst = []
     for k, p in enc.named_parameters():
         if k.endswith("layers.0.bias"):
             continue    # conv bias ahead of a batch-statistics BatchNorm: true gradient is exactly 0
-        g64 = p64[k].grad.cpu().numpy()
-        es.append(rel_l2(p.grad.cpu().numpy(), g64))
-        e32s.append(rel_l2(p32[k].grad.cpu().numpy(), g64))
-        keys.append(k)
-    med32 = float(np.median(e32s))
-    for k, e, e32 in zip(keys, es, e32s):
-        assert e <= max(1e-4, 4 * e32, 4 * med32), (k, e, e32, med32)
-    assert np.median(es) <= 4 * med32 and max(es) <= 4 * max(e32s), (np.median(es), med32, max(es), max(e32s))
+        e = rel_l2(p.grad.cpu().numpy(), p64[k].grad.cpu().numpy())
+        worst.append((e, k))
+        assert e <= 1e-4, (k, e)
+    print("encoder2d fwd", e_out, "worst grads", sorted(worst)[-3:])
     b64 = dict(ref64.named_buffers())
     for k, b in enc.named_buffers():
         if b.dtype.is_floating_point:
