@@ -42,6 +42,10 @@ constexpr int kFwdNP4 = PROJ_FWD_NP4;
 #define PB_TPW 2
 #endif
 constexpr int kBwdNP4 = PROJ_BWD_NP4;
+// hidden-tile loop unroll of the backward (1: rolled)
+#ifndef PB_TUNROLL
+#define PB_TUNROLL 1
+#endif
 
 // Grouped launches: G weight groups (two FNO heads over one field), each owning gpts
 // consecutive points (Bg samples); group g's weights sit at + g wgs and its outputs at channel
@@ -172,7 +176,7 @@ __device__ __forceinline__ void load_az(const float* __restrict__ z, const Point
 
 // Forward: each wave owns NP point tiles (16 points each) per step and sweeps the 8 hidden
 // tiles in a rolled loop (weights from LDS), so NP independent MFMA -> GELU chains overlap.
-template <int CK, int COM, int NP>
+template <int CK, int COM, int NP, bool T16>
 __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ out, int C,
@@ -196,7 +200,21 @@ __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
     for (int c = 0; c < COM; ++c) b2v[c] = c < Cout ? b2[g * gr.wgs + c] : 0.f;
     float az[NP][KS];
 #pragma unroll
-    for (int np = 0; np < NP; ++np) load_az<KS>(z, pm, (grp * NP + np) * 16 + c16, npts, g4, az[np]);
+    for (int np = 0; np < NP; ++np) {
+      const unsigned tile = grp * NP + np;
+      if constexpr (T16) {           // tile in one grid row: map its first point once (uniform)
+        const bool live = tile * 16 < npts;
+        unsigned n0, q0;
+        const unsigned zo0 = pm.zoff(live ? tile * 16 : 0u, n0, q0);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int ch = 4 * kk + g4;
+          az[np][kk] = (live && ch < C) ? z[zo0 + (unsigned)c16 + (unsigned)ch * (unsigned)pm.HW] : 0.f;
+        }
+      } else {
+        load_az<KS>(z, pm, tile * 16 + c16, npts, g4, az[np]);
+      }
+    }
     f32x2 acc[NP][COM][2];                        // (r0, r1), (r2, r3)
 #pragma unroll
     for (int np = 0; np < NP; ++np)
@@ -264,7 +282,7 @@ __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
 // summed over the 16 hidden lanes by a reduce-scatter of four shuffles per value block).
 // The four waves of a workgroup fold their accumulators into one partial per workgroup
 // (fixed order; reduced afterwards by blindno_reduce_partials).
-template <int CK, int COM, int NP>
+template <int CK, int COM, int NP, bool T16>
 __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ dout, float* __restrict__ dz,
@@ -306,6 +324,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
   for (int c = 0; c < COM; ++c) gb2[c] = 0.f;
   const PointMap pm{(unsigned)(Ho * Wo), (unsigned)Wo, (int64_t)P1 * P2, P2, C, gr.dHoWo, gr.dWo};
   const bool row4 = (Wo & 3) == 0;
+  const unsigned ntiles = (gpts + 15) / 16;
   const unsigned ngroups = (gpts + 16 * NP - 1) / (16 * NP);
   for (unsigned grp = blockIdx.x * kWaves + wave; grp < ngroups; grp += gridDim.x * kWaves) {
     float az[NP][KS], zb[NP][4], gv[NP][4][COM];
@@ -313,6 +332,37 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
 #pragma unroll
     for (int np = 0; np < NP; ++np) {
       const unsigned tile = grp * NP + np;
+      if constexpr (T16) {
+        // Wo % 16 == 0: the tile's 16 points lie in one grid row of one sample, so its first
+        // point is mapped once, wave-uniformly (scalar unit), and every lane point is an offset
+        // (lane c16 for the A operand, 4 g4 + r for the D-layout rows).  A tile past the end
+        // (last step, odd tile count) is uniformly dead.
+        const bool live = tile < ntiles;
+        unsigned n0, q0;
+        const unsigned zo0 = pm.zoff(pbase + (live ? tile : 0u) * 16u, n0, q0);
+        const unsigned nb = gr.dDoutDiv.div(n0 - nbase);
+        const float ls = gr.lscale ? gr.lscale[(n0 - nbase) - nb * (unsigned)dout_div] : 1.0f;
+        const float* gp0 = dout + ((nb * pm.HoWo + q0) * (unsigned)ostride + (unsigned)(ooff + g * gr.goff));
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int ch = 4 * kk + g4;
+          az[np][kk] = (live && ch < C) ? z[zo0 + (unsigned)c16 + (unsigned)ch * (unsigned)pm.HW] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const unsigned off = 4u * g4 + r;
+          zo4[np][r] = (int)(zo0 + off);
+          const int zc = kGW44 ? (c16 & 3) : c16;
+          zb[np][r] = !live ? 0.f : (zc < C ? z[zo0 + off + (unsigned)zc * (unsigned)pm.HW] : (zc == C ? 1.f : 0.f));
+#pragma unroll
+          for (int c = 0; c < COM; ++c) gv[np][r][c] = (live && c < Cout) ? gp0[off * (unsigned)ostride + c] * ls : 0.f;
+        }
+        if (c16 == 0) {
+#pragma unroll
+          for (int c = 0; c < COM; ++c) gb2[c] += (gv[np][0][c] + gv[np][1][c]) + (gv[np][2][c] + gv[np][3][c]);
+        }
+        continue;
+      }
       load_az<KS>(z, pm, pbase + tile * 16 + c16, npts, g4, az[np]);
       // this lane's 4 points (D layout rows): z column c16 (1.0 at c16 == C: db1), dout
       // When Wo % 4 == 0 the lane's 4 points (4-aligned) share one sample and grid row, so one
@@ -349,7 +399,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
     for (int np = 0; np < NP; ++np)
 #pragma unroll
       for (int e = 0; e < NV; ++e) dzp[np][e] = 0.f;
-#pragma unroll 1
+#pragma unroll PB_TUNROLL
     for (int t = 0; t < kNT; ++t) {
       const int j = 16 * t + c16;
       float bw[KS], wr[CK];
@@ -440,7 +490,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
       }
       const int r = c16 & 3;
       const unsigned p = pbase + (grp * NP + np) * 16 + 4 * g4 + r;
-      if (p < npts) {
+      if (T16 ? (grp * NP + np) < ntiles : p < npts) {
 #pragma unroll
         for (int m = 0; m < NV / 16; ++m) {
           const int ch = 4 * m + (c16 >> 2);
@@ -521,15 +571,18 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
   const int ck = (C + 3) / 4 * 4;
   const int np = ck <= 4 ? kFwdNP4 : (ck <= 8 ? 4 : 2);
   if (G > 1 && gr.gpts % (16u * np)) return (int)hipErrorInvalidValue;   // steps within a group
-#define PF(CK_, CO_)                                                                           \
-  project_fwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kFwdNP4 : (CK_ <= 8 ? 4 : 2))><<<blocks, 256, 0, st>>>( \
+  const bool t16 = Wo % 16 == 0;
+#define PF2(CK_, CO_, T_)                                                                      \
+  project_fwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kFwdNP4 : (CK_ <= 8 ? 4 : 2)), T_><<<blocks, 256, 0, st>>>( \
       z, w1, b1, w2, b2, out, C, P1, P2, Ho, Wo, Cout, ostride, ooff, npts, gr)
+#define PF(CK_, CO_) do { if (t16) PF2(CK_, CO_, true); else PF2(CK_, CO_, false); } while (0)
   if (Cout == 1) {
     if (ck == 4) PF(4, 1); else if (ck == 8) PF(8, 1); else if (ck == 12) PF(12, 1); else PF(16, 1);
   } else {
     if (ck == 4) PF(4, 2); else if (ck == 8) PF(8, 2); else if (ck == 12) PF(12, 2); else PF(16, 2);
   }
 #undef PF
+#undef PF2
   return (int)hipGetLastError();
 }
 
@@ -551,9 +604,11 @@ int project_bwd_mfma(const float* z, const float* w1, const float* b1, const flo
   const Groups gr{G, gpts, G > 1 ? wgs : 0, Cout, lscale, FastDiv::make((unsigned)(Ho * Wo)),
                   FastDiv::make((unsigned)Wo), FastDiv::make((unsigned)dout_div)};
   const dim3 grid(nchunk, G);
-#define PB(CK_, CO_)                                                                          \
-  project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kBwdNP4 : 1)><<<grid, 256, 0, st>>>(            \
+  const bool t16 = Wo % 16 == 0;
+#define PB2(CK_, CO_, T_)                                                                     \
+  project_bwd_mfma_kernel<CK_, CO_, (CK_ <= 4 ? kBwdNP4 : 1), T_><<<grid, 256, 0, st>>>(        \
       z, w1, b1, w2, dout, dz, partial, C, P1, P2, Ho, Wo, Cout, ostride, ooff, dout_div, gpts, gr)
+#define PB(CK_, CO_) do { if (t16) PB2(CK_, CO_, true); else PB2(CK_, CO_, false); } while (0)
   const int ck = (C + 3) / 4 * 4;
   if (Cout == 1) {
     if (ck == 4) PB(4, 1); else if (ck == 8) PB(8, 1); else if (ck == 12) PB(12, 1); else PB(16, 1);
@@ -561,6 +616,7 @@ int project_bwd_mfma(const float* z, const float* w1, const float* b1, const flo
     if (ck == 4) PB(4, 2); else if (ck == 8) PB(8, 2); else if (ck == 12) PB(12, 2); else PB(16, 2);
   }
 #undef PB
+#undef PB2
   return (int)hipGetLastError();
 }
 
