@@ -20,3 +20,4 @@ importing the reference itself in the build container
 """
 from .fno_ref import *  # noqa: F401,F403
 from . import gpe_ref  # noqa: F401,E402
+from . import unet_ref  # noqa: F401,E402

@@ -36,7 +36,7 @@ def make_param(name: str, shape, seed: int, complex_: bool = False) -> np.ndarra
     if name.endswith("num_batches_tracked"):
         return np.zeros(shape, np.int64)
     if len(shape) <= 1:
-        is_bn = ".layers.1." in name or "batch_layers" in name
+        is_bn = ".layers.1." in name or "batch_layers" in name or any("norm" in c for c in name.split(".")[:-1])
         if is_bn and name.endswith("weight"):
             return (1.0 + 0.1 * rs.uniform(-1, 1, shape)).astype(np.float32)
         return (0.1 * rs.uniform(-1, 1, shape)).astype(np.float32)

@@ -274,3 +274,80 @@ def test_cpu_ref_niofp_fno_1d(case, heads):
     grid = torch.from_numpy(g["in.grid"]).float().requires_grad_(True)
     idx = g["idx"].tolist() if "idx" in g else None
     _check32(g, cpu_ref.niofp_fno_fft(p, x, grid, idx=idx, heads=heads), p, {"x": x, "grid": grid})
+
+
+# ---------------------------------------------------------------- PermInvUNet_attn
+def unet_recipe_params(g):
+    """The golden's parameters, regenerated from recipe.py (make_golden_unet.py loads the same
+    values into the reference module)."""
+    import json
+    shapes = [(k, tuple(s)) for k, s in json.loads(str(g["layout_json"]))]
+    cplx = json.loads(str(g["complex_json"]))
+    return make_state(shapes, seed=int(g["recipe_seed"]), complex_names=cplx)
+
+
+def unet_oracle_run(g, dim, variant, train, prec="fp64"):
+    """(out, {name: grad}, dx) of the oracle on a UNet golden's inputs and cotangent."""
+    st = unet_recipe_params(g)
+    if "run_mean" in g:                      # eval: running stats after the train forward
+        depth = int(g["depth"])
+        chs = [int(g["base_ch"]) * 2 ** i for i in range(depth + 1)]
+        off = np.cumsum([0] + chs)
+        for i in range(depth + 1):
+            st[f"skip_norms.{i}.running_mean"] = g["run_mean"][off[i]:off[i + 1]]
+            st[f"skip_norms.{i}.running_var"] = g["run_var"][off[i]:off[i + 1]]
+    rdt, cdt = (torch.float64, torch.complex128) if prec == "fp64" else (torch.float32, torch.complex64)
+    oracle.set_precision(prec)
+    try:
+        p = {k: torch.from_numpy(np.asarray(v)).to(cdt if np.iscomplexobj(v) else rdt)
+             .requires_grad_(np.asarray(v).dtype.kind in "fc") for k, v in st.items()}
+        x = torch.from_numpy(g["in.x"]).to(rdt).requires_grad_(True)
+        idx = g["idx"].tolist() if "idx" in g else None
+        y = oracle.unet_ref.perminv_unet_attn(p, x, int(g["depth"]), dim, idx=idx, bn_train=train,
+                                              variant=variant)
+        (y * torch.from_numpy(g["cot"]).to(rdt)).sum().backward()
+    finally:
+        oracle.set_precision("fp64")
+    grads = {k: v.grad.detach().to(torch.complex128 if v.is_complex() else torch.float64).numpy()
+             for k, v in p.items() if v.grad is not None}
+    return y.detach().double().numpy(), grads, x.grad.double().numpy()
+
+
+def unet_grad_bar(e32):
+    """Gradient tolerance of one parameter: 1e-4 or, where the model's own fp32
+    evaluation is further from fp64 than that (bias / LayerNorm sums with cancellation), three
+    times the fp32 oracle's own distance."""
+    return max(GRAD_TOL, 3.0 * e32)
+
+
+@pytest.mark.parametrize("case,dim,variant,train", [
+    ("unet2d_train", 2, "fpe", True), ("unet2d_eval", 2, "fpe", False),
+    ("nc_unet2d_train", 2, "nc", True), ("unet1d_bag_train", 1, "fpe", True),
+    ("unet1d_all", 1, "fpe", True)])
+def test_perminv_unet_attn(case, dim, variant, train):
+    """PermInvUNet_attn (2d_FPE/NIOModules.py:1062-1181), its NC copy with ConvBlocks
+    (2d_Non_conservative_FPE/NIOModules.py:932-1053) and the 1D models
+    (1d_FPE/NIOModules.py:209-443): the fp64 oracle against the reference's fp32 outputs and
+    gradients; gradient bars per unet_grad_bar (the fp32 oracle run gives the conditioning)."""
+    g = load_golden(case)
+    o64, g64, x64 = unet_oracle_run(g, dim, variant, train)
+    o32, g32, x32 = unet_oracle_run(g, dim, variant, train, "fp32")
+    assert rel_l2(g["out"], o64) <= FWD_TOL
+    n = 0
+    scale = max(float(np.linalg.norm(v)) for v in g64.values())
+    for k, v in g.items():
+        if k.startswith("g."):
+            name = k[2:]
+            if np.linalg.norm(g64[name]) <= 1e-10 * scale:
+                # structurally zero (a conv bias in front of a train-mode BatchNorm): fp32 noise
+                assert np.linalg.norm(v) <= 1e-5 * scale, name
+            else:
+                e, e32 = rel_l2(v, g64[name]), rel_l2(g32[name], g64[name])
+                assert e <= unet_grad_bar(e32), (name, e, e32)
+            n += 1
+        elif k.startswith("gnorm."):
+            name = k[6:]
+            assert abs(np.linalg.norm(g64[name]) - float(v)) <= GRAD_TOL * float(v), name
+            n += 1
+    assert rel_l2(g["gin.x"], x64) <= unet_grad_bar(rel_l2(x32, x64))
+    assert n > 20
