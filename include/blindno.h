@@ -415,6 +415,74 @@ int blindno_spectral_conv1d_bwd(const float* dy, const float* saved, const float
                                 float* dw, void* work, const void* tables, int Bn, int Ci,
                                 int Co, int P2, int m, blindno_stream_t stream);
 
+/* ---- permutation-invariant attention UNet, PermInvUNet_attn ("BlinDNO")
+ * 2d_FPE/NIOModules.py:1014-1181 (2D), 1d_FPE/NIOModules.py:163-443 (1D: height-1 fields,
+ * KH = 1).  The 3x3 convolutions and the 1x1 final_conv use blindno_conv2d_*, the skip
+ * BatchNorms (and the NC copy's ConvBlock BN + ReLU) blindno_bn_act_* (slope 1 / 0).
+ *
+ * Depthwise convolution of ConvNeXtBlock (nn.Conv2d(C, C, 7, padding=3, groups=C), :1016;
+ * Conv1d(C, C, 7, padding=3, groups=C), 1d_FPE/NIOModules.py:167): x, y (N, C, H, W), w (C, KH, KW),
+ * padding (KH/2, KW/2), KH KW <= 49.  bwd_weight: dwb (C, KH KW + 1), last column = db; partial:
+ * nsplit x C x (KH KW + 1) floats (nsplit = blindno_dwconv_wgrad_nsplit; NULL when 1). */
+int blindno_dwconv_fwd(const float* x, const float* w, const float* b, float* y, int N, int C,
+                       int H, int W, int KH, int KW, blindno_stream_t stream);
+int blindno_dwconv_bwd_data(const float* dy, const float* w, float* dx, int N, int C, int H,
+                            int W, int KH, int KW, blindno_stream_t stream);
+int blindno_dwconv_wgrad_nsplit(int N, int C, int H, int W);
+int blindno_dwconv_bwd_weight(const float* dy, const float* x, float* dwb, float* partial,
+                              int nsplit, int N, int C, int H, int W, int KH, int KW,
+                              blindno_stream_t stream);
+/* Rest of ConvNeXtBlock.forward (2d_FPE/NIOModules.py:1023-1032): per pixel of xd (the depthwise
+ * output, (N, C, HW)) LayerNorm over C (eps 1e-6, gamma lw / beta lb) -> Linear(C, 4C) (w1, b1)
+ * -> exact GELU -> Linear(4C, C) (w2, b2) -> + sc (the shortcut).  C in {1,2,4,...,64}.
+ * bwd: dxd = gradient at xd (the shortcut's is dy itself); dparams = [dw1 (4C x C) | db1 (4C) |
+ * dw2 (C x 4C) | db2 (C) | dlw (C) | dlb (C)]; partial: nblk x (8 C^2 + 7 C) floats,
+ * nblk = blindno_cnx_pw_bwd_nblk(N, C, HW). */
+int blindno_cnx_pw_fwd(const float* xd, const float* sc, const float* lw, const float* lb,
+                       const float* w1, const float* b1, const float* w2, const float* b2, float* y,
+                       int N, int C, int HW, blindno_stream_t stream);
+int blindno_cnx_pw_bwd_nblk(int N, int C, int HW);
+int blindno_cnx_pw_bwd(const float* dy, const float* xd, const float* lw, const float* lb,
+                       const float* w1, const float* b1, const float* w2, float* dxd,
+                       float* dparams, float* partial, int nblk, int N, int C, int HW,
+                       blindno_stream_t stream);
+/* MaxPool2d(2) / MaxPool1d(2) (:1092, 1d :239): window = stride = KH x KW, floor; arg (NC, Ho, Wo)
+ * uint8 index of the window's maximum (first in scan order; a NaN wins). */
+int blindno_maxpool_fwd(const float* x, float* y, uint8_t* arg, int NC, int H, int W, int KH,
+                        int KW, blindno_stream_t stream);
+int blindno_maxpool_bwd(const float* dy, const uint8_t* arg, float* dx, int NC, int H, int W,
+                        int KH, int KW, blindno_stream_t stream);
+/* ConvTranspose2d(Ci, Co, kernel = stride = 2, output_padding) of the up path (:1106-1110;
+ * 1d :258-261 with KH = 1): x (N, Ci, Hi, Wi), w (Ci, Co, KH, KW), y (N, Co, Ho, Wo) with
+ * KH Hi <= Ho < KH (Hi + 1) (the extra rows / columns are output_padding).  bwd_weight:
+ * dwb = [dW (Ci Co KH KW) | db (Co)], partial N x (Ci Co KH KW + Co) floats (NULL when N = 1). */
+int blindno_convt_fwd(const float* x, const float* w, const float* b, float* y, int N, int Ci,
+                      int Hi, int Wi, int Co, int KH, int KW, int Ho, int Wo,
+                      blindno_stream_t stream);
+int blindno_convt_bwd_data(const float* dy, const float* w, float* dx, int N, int Ci, int Hi,
+                           int Wi, int Co, int KH, int KW, int Ho, int Wo, blindno_stream_t stream);
+int blindno_convt_bwd_weight(const float* dy, const float* x, float* dwb, float* partial, int N,
+                             int Ci, int Hi, int Wi, int Co, int KH, int KW, int Ho, int Wo,
+                             blindno_stream_t stream);
+/* TemporalSelfAttention + the bag mean that follows it (:1035-1054 and :1152-1153 / :1160-1162):
+ * Y (B, D) = mean_l LayerNorm_D(A X + X)_l, A = softmax(X X^T / sqrt D), X (B, L, D) the bag's L
+ * snapshot features flattened to D = C H W, LayerNorm eps `eps` with gamma lw / beta lb (D).
+ * Collapsed to a centred Gram matrix per bag (see csrc/unet.hip).  L <= 480.
+ *   save: blindno_tok_attn_save_floats(B, L, D) floats (16-B aligned), written by the forward,
+ *         read by the backward; gram: B L L floats; gram_partial: blindno_tok_gram_nchunk(D)
+ *         x B L L floats (NULL when that is 1).
+ *   bwd:  dX (B, L, D) (NULL: none), dlw / dlb (D) (NULL: none); scratch:
+ *         blindno_tok_attn_bwd_scratch_floats(B, L) floats (8-B aligned). */
+int blindno_tok_gram_nchunk(int64_t D);
+int64_t blindno_tok_attn_save_floats(int B, int L, int64_t D);
+int blindno_tok_attn_fwd(const float* X, const float* lw, const float* lb, float* Y, float* save,
+                         float* gram_partial, float* gram, int B, int L, int64_t D, float eps,
+                         blindno_stream_t stream);
+int64_t blindno_tok_attn_bwd_scratch_floats(int B, int L);
+int blindno_tok_attn_bwd(const float* dY, const float* X, const float* lw, const float* save,
+                         float* dX, float* dlw, float* dlb, float* scratch, int B, int L,
+                         int64_t D, blindno_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

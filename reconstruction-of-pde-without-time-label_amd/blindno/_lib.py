@@ -88,10 +88,28 @@ SIGNATURES = {
     "blindno_spectral_conv1d_saved_bytes": "iii",
     "blindno_spectral_conv1d_fwd": "pppppp" + "iiiii" + "s",
     "blindno_spectral_conv1d_bwd": "ppppppp" + "iiiii" + "s",
+    # PermInvUNet_attn (csrc/unet.hip)
+    "blindno_dwconv_fwd": "pppp" + "iiiiii" + "s",
+    "blindno_dwconv_bwd_data": "ppp" + "iiiiii" + "s",
+    "blindno_dwconv_wgrad_nsplit": "iiii",
+    "blindno_dwconv_bwd_weight": "pppp" + "i" + "iiiiii" + "s",
+    "blindno_cnx_pw_fwd": "ppppppppp" + "iii" + "s",
+    "blindno_cnx_pw_bwd_nblk": "iii",
+    "blindno_cnx_pw_bwd": "pppppppppp" + "iiii" + "s",
+    "blindno_maxpool_fwd": "ppp" + "iiiii" + "s",
+    "blindno_maxpool_bwd": "ppp" + "iiiii" + "s",
+    "blindno_convt_fwd": "pppp" + "iiiiiiiii" + "s",
+    "blindno_convt_bwd_data": "ppp" + "iiiiiiiii" + "s",
+    "blindno_convt_bwd_weight": "pppp" + "iiiiiiiii" + "s",
+    "blindno_tok_gram_nchunk": "l",
+    "blindno_tok_attn_save_floats": "iil",
+    "blindno_tok_attn_fwd": "ppppppp" + "iil" + "f" + "s",
+    "blindno_tok_attn_bwd_scratch_floats": "ii",
+    "blindno_tok_attn_bwd": "pppppppp" + "iil" + "s",
 }
 
 # entry points returning int64_t (byte counts) instead of an error code / int count
-RET64 = {n for n in SIGNATURES if n.endswith("_bytes")}
+RET64 = {n for n in SIGNATURES if n.endswith(("_bytes", "_floats"))}
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_int64, "f": ctypes.c_float,
        "d": ctypes.c_double, "s": ctypes.c_void_p}

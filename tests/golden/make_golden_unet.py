@@ -39,6 +39,23 @@ def _load_recipe(m, seed):
             "complex_json": json.dumps(cplx)}
 
 
+def _init_fingerprint(tag, ctor, seed):
+    """Seeded construction -> per-parameter (sum, sum of squares, first four values) in float64:
+    pins the creation order and init of the drop-in classes without storing 3.5M weights."""
+    import numpy as np
+    import torch
+    torch.manual_seed(seed)
+    m = ctor()
+    out = {}
+    for k, v in m.state_dict().items():
+        a = v.detach().double().reshape(-1).numpy() if not v.is_complex() else \
+            torch.view_as_real(v.detach()).double().reshape(-1).numpy()
+        head = np.zeros(4)
+        head[:min(4, a.size)] = a[:4]
+        out[f"{tag}|{k}"] = np.concatenate([[a.sum(), (a * a).sum()], head])
+    return out
+
+
 def group(exp):
     import numpy as np
     import torch
@@ -74,6 +91,9 @@ def group(exp):
                      grad_norm_prefixes=SPEC, extra={"base_ch": base, "depth": depth, **run, **rec})
         else:
             np.savez(os.path.join(HERE, f"{tag}_train_run.npz"), **run)
+        fp = _init_fingerprint(tag, lambda: NM.PermInvUNet_attn(in_ch=1, out_ch=2, base_ch=1, depth=4,
+                                                                input_size=(61, 61)), 531)
+        np.savez(os.path.join(HERE, f"{tag}_init.npz"), **fp)
         key = f"{'2d' if exp == '2d_FPE' else '2d_NC'}.PermInvUNet_attn(1,2,1,4,(61,61))"
         out[key] = _layout(NM.PermInvUNet_attn(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=(61, 61)))
     else:  # 1d_FPE
@@ -93,6 +113,11 @@ def group(exp):
         m.train()
         _capture("unet1d_all", m, {"x": x}, lambda: m(x), seed=512, save_params=False,
                  extra={"base_ch": 2, "depth": 3, **rec})
+        fp = _init_fingerprint("unet1d_bag", lambda: NM.PermInvUNet_attn1D_bag(
+            in_ch=1, out_ch=2, base_ch=1, depth=5, input_size=80, device="cpu"), 532)
+        fp.update(_init_fingerprint("unet1d", lambda: NM.PermInvUNet_attn1D(
+            in_ch=1, out_ch=2, base_ch=1, depth=6, input_size=80, device="cpu"), 533))
+        np.savez(os.path.join(HERE, "unet1d_init.npz"), **fp)
         out["1d.PermInvUNet_attn1D_bag(1,2,1,5,80)"] = _layout(
             NM.PermInvUNet_attn1D_bag(in_ch=1, out_ch=2, base_ch=1, depth=5, input_size=80, device="cpu"))
         out["1d.PermInvUNet_attn1D(1,2,1,6,80)"] = _layout(

@@ -184,3 +184,37 @@ def test_trainer_split_is_random_split():
         a, b = random_split(range(37), [29, 8], generator=torch.Generator().manual_seed(seed))
         tr, te = trainer.split_indices(37, seed)
         assert list(a) == tr and list(b) == te
+
+
+# ---------------------------------------------------------------- PermInvUNet_attn
+def _unet_ctors():
+    from blindno import unet
+    return {
+        "2d.PermInvUNet_attn(1,2,1,4,(61,61))": ("unet2d", 531, lambda: unet.PermInvUNet_attn(1, 2, 1, 4, (61, 61))),
+        "2d_NC.PermInvUNet_attn(1,2,1,4,(61,61))": ("nc_unet2d", 531,
+                                                    lambda: unet.PermInvUNet_attn_NC(1, 2, 1, 4, (61, 61))),
+        "1d.PermInvUNet_attn1D_bag(1,2,1,5,80)": ("unet1d_bag", 532,
+                                                  lambda: unet.PermInvUNet_attn1D_bag(1, 2, 1, 5, 80, device="cpu")),
+        "1d.PermInvUNet_attn1D(1,2,1,6,80)": ("unet1d", 533,
+                                              lambda: unet.PermInvUNet_attn1D(1, 2, 1, 6, 80, device="cpu")),
+    }
+
+
+@pytest.mark.parametrize("key", list(_unet_ctors()))
+def test_unet_layout_and_seeded_init_match_reference(key):
+    """The UNet drop-ins (blindno.unet) have the reference's state_dict layout and, seeded, its
+    initial weights (fingerprints captured by tests/golden/make_golden_unet.py)."""
+    lay = json.load(open(os.path.join(GOLDEN, "layouts.json")))
+    tag, seed, ctor = _unet_ctors()[key]
+    torch.manual_seed(seed)
+    m = ctor()
+    got = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in m.state_dict().items()]
+    assert got == lay[key]
+    fp = np.load(os.path.join(GOLDEN, ("unet1d" if tag.startswith("unet1d") else tag) + "_init.npz"))
+    for k, v in m.state_dict().items():
+        a = (torch.view_as_real(v) if v.is_complex() else v).double().reshape(-1).numpy()
+        ref = fp[f"{tag}|{k}"]
+        head = np.zeros(4)
+        head[:min(4, a.size)] = a[:4]
+        np.testing.assert_array_equal(head, ref[2:], err_msg=k)
+        np.testing.assert_allclose([a.sum(), (a * a).sum()], ref[:2], rtol=1e-12, atol=1e-12, err_msg=k)
