@@ -114,13 +114,19 @@ def _bn(p, prefix, x, bn_train):
 
 def perminv_unet_attn(p: Dict[str, torch.Tensor], x: torch.Tensor, depth: int, dim: int,
                       idx: Optional[Sequence[int]] = None, bn_train: bool = True,
-                      variant: str = "fpe") -> torch.Tensor:
+                      variant: str = "fpe", taps: Optional[list] = None) -> torch.Tensor:
     """PermInvUNet_attn.forward (2d_FPE/NIOModules.py:1129-1181) for dim 2, x (B, T, H, W);
     PermInvUNet_attn1D(_bag).forward (1d_FPE/NIOModules.py:283-322, 398-443) for dim 1,
     x (B, T, L); ``variant="nc"``: the 2d_Non_conservative_FPE model (ConvBlocks, heads
     fno_Fx/fno_Fy; 2d_Non_conservative_FPE/NIOModules.py:1009-1053).  ``idx`` is the
     train-mode bag (drawn with replacement by the reference); ``bn_train`` selects batch
     statistics (train mode) or running ones for every BatchNorm."""
+    def tap(name, t):
+        if taps is not None:
+            t.retain_grad()
+            taps.append((name, t))
+        return t
+
     x = x.to(_dt())
     p = {k: (v.to(_dt()) if v.is_floating_point() else v) for k, v in p.items()}
     if idx is not None:
@@ -138,14 +144,14 @@ def perminv_unet_attn(p: Dict[str, torch.Tensor], x: torch.Tensor, depth: int, d
             h = torch.relu(_bn(p, f"down_convs.{i}.1", h, bn_train))
         else:
             h = convnext(sub_params(p, f"down_convs.{i}.1"), h, dim)
-        feats.append(h)
+        feats.append(tap(f"feat{i}", h))
         if i < depth:
             h = pool(h, 2)
 
     def agg(level):
         f = feats[level]
         seq = f.reshape(B, L, *f.shape[1:])
-        return temporal_attention(sub_params(p, f"temp_atts.{level}"), seq).mean(1)
+        return tap(f"agg{level}", temporal_attention(sub_params(p, f"temp_atts.{level}"), seq).mean(1))
 
     h = agg(depth)
     sizes = [skip_sizes(n, depth) for n in spatial]
@@ -162,7 +168,8 @@ def perminv_unet_attn(p: Dict[str, torch.Tensor], x: torch.Tensor, depth: int, d
             h = torch.relu(_bn(p, f"up_convs.{i}.1", h, bn_train))
         else:
             h = convnext(sub_params(p, f"up_convs.{i}.1"), h, dim)
-    fused = conv(h, p["final_conv.weight"], p["final_conv.bias"])
+        tap(f"up{i}", h)
+    fused = tap("fused", conv(h, p["final_conv.weight"], p["final_conv.bias"]))
     names = ("fno_Fx", "fno_Fy") if variant == "nc" else ("fno_drift", "fno_diffusion")
     if dim == 2:
         fused = fused.permute(0, 2, 3, 1)

@@ -117,8 +117,8 @@ class FlatAdam:
 def trained_parameters(model: torch.nn.Module, exclude_prefixes=("branch.", "fc0.")):
     """Parameters the reference actually trains for the FNO-NIO models (no gradient ever
     reaches ``branch.*``; ``fc0`` is read through ``.data``)."""
-    return [p for n, p in model.named_parameters()
-            if p.requires_grad and not n.startswith(tuple(exclude_prefixes))]
+    excl = tuple(exclude_prefixes) + tuple(getattr(model, "unused_prefixes", ()))
+    return [p for n, p in model.named_parameters() if p.requires_grad and not n.startswith(excl)]
 
 
 class StepLR:

@@ -329,6 +329,23 @@ class _UNetBase(nn.Module):
     _block = "convnext"
     _heads = ("fno_drift", "fno_diffusion")
     _bag = True
+    _taps = None        # diagnostics: a list collects (name, tensor) of the per-level activations
+
+    @property
+    def unused_prefixes(self):
+        """Registered parameters the forward never uses (no gradient; the reference trains with
+        find_unused_parameters=True): the bottom level's skip BatchNorm and, in the NC copy,
+        the fno_drift / fno_diffusion heads."""
+        p = [f"skip_norms.{self.depth}."]
+        if tuple(self._heads) != ("fno_drift", "fno_diffusion"):
+            p += ["fno_drift.", "fno_diffusion."]
+        return tuple(p)
+
+    def _tap(self, name, t):
+        if self._taps is not None:
+            t.retain_grad()
+            self._taps.append((name, t))
+        return t
 
     def _block_fwd(self, seq, h):
         if self._block == "convbn":
@@ -357,7 +374,7 @@ class _UNetBase(nn.Module):
         feats = []
         kpool = (2, 2) if self.dim == 2 else (1, 2)
         for i in range(self.depth + 1):
-            h = self._block_fwd(self.down_convs[i], h)
+            h = self._tap(f"feat{i}", self._block_fwd(self.down_convs[i], h))
             feats.append(h)
             if i < self.depth:
                 h = MaxPoolFn.apply(_as4(h), *kpool)
@@ -366,7 +383,7 @@ class _UNetBase(nn.Module):
 
         def agg(level):
             f = feats[level]
-            return self.temp_atts[level].bag_mean(f.view(B, L, *f.shape[1:]))
+            return self._tap(f"agg{level}", self.temp_atts[level].bag_mean(f.view(B, L, *f.shape[1:])))
 
         h = agg(self.depth)
         for i in range(self.depth):
@@ -379,8 +396,8 @@ class _UNetBase(nn.Module):
             h = h4 if self.dim == 2 else h4.squeeze(2)
             s = _bn(self.skip_norms[lv], agg(lv), 1.0)
             h = torch.cat([h, s], dim=1)
-            h = self._block_fwd(self.up_convs[i], h)
-        fused = _conv3(self.final_conv, h)
+            h = self._tap(f"up{i}", self._block_fwd(self.up_convs[i], h))
+        fused = self._tap("fused", _conv3(self.final_conv, h))
         fused = fused.permute(0, 2, 3, 1) if self.dim == 2 else fused.permute(0, 2, 1)
         return _run_heads(self, fused.contiguous())
 

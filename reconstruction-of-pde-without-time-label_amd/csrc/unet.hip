@@ -14,16 +14,18 @@
 // LayerNorm and then averages over the L tokens.  With M = A + I, x_t the token means and
 // Gc the CENTRED Gram matrix (Gc_ts = (X_t - x_t).(X_s - x_s)):
 //   mu_l   = sum_t M_lt x_t,       var_l = (1/D) m_l^T Gc m_l,     r_l = (var_l + eps)^-1/2
-//   Ybar   = gamma (sum_t c_t X_t - kappa) + beta,   c_t = (1/L) sum_l r_l M_lt,
-//   kappa  = (1/L) sum_l r_l mu_l,   and the scores are (Gc + D x x^T) / sqrt D.
-// So the forward is: token means, one centred Gram matrix per bag (L x L, reduced over D),
-// O(L^3) bag-local algebra, and a c-weighted token sum -- nothing of size L x D is written.
-// The backward is the exact adjoint.  With g = gamma dYbar, h_t = g.X_t, gb = mean(g),
-// a_l = r_l / L, P = M Gc (saved by the forward), gO_l = sum_t M_lt h_t and
-//   b_l  = a_l r_l^2 (gO_l - mu_l D gb) / D
-//   dA_lt = a_l (h_t - gb D x_t) - b_l P_lt,   dS = A o (dA - rowsum(A o dA)),
+//   Ybar   = gamma sum_t c_t (X_t - x_t) + beta,   c_t = (1/L) sum_l r_l M_lt,
+// (the token means cancel exactly: sum_t c_t x_t = (1/L) sum_l r_l mu_l), and the scores are
+// (Gc + D x x^T) / sqrt D.  So the forward is: token means, one centred Gram matrix per bag
+// (L x L, reduced over D), O(L^3) bag-local algebra, and a c-weighted sum of centred tokens --
+// nothing of size L x D is written.  Everything is kept in centred quantities (tokens whose
+// mean is large against their spread would otherwise cancel catastrophically).
+// The backward is the exact adjoint.  With g = gamma dYbar, gb = mean(g), centred dots
+// h_t = g.(X_t - x_t), a_l = r_l / L and P = M Gc (saved by the forward):
+//   b_l  = a_l r_l^2 (sum_t M_lt h_t) / D
+//   dA_lt = a_l h_t - b_l P_lt,   dS = A o (dA - rowsum(A o dA)),
 //   Q = (dS + dS^T) / sqrt D,   N = M^T diag(b) M,   R = Q - N,
-//   dX_t = (sum_l M_lt a_l) g + sum_s R_ts X_s + (sum_s N_ts x_s - (sum_l M_lt a_l) gb).
+//   dX_t = (sum_l M_lt a_l) g + sum_s R_ts (X_s - x_s) + (sum_s Q_ts x_s - (sum_l M_lt a_l) gb).
 // Every reduction is a fixed-order tree or a fixed-order sum of per-chunk partials
 // (blindno_reduce_partials): deterministic, no float atomics.
 #include "common.h"
@@ -63,7 +65,7 @@ __device__ __forceinline__ float gelu_exact(float z) {
 
 __device__ __forceinline__ float gelu_exact_grad(float z) {
   return 0.5f * (1.0f + erff(z * 0.70710678118654752f)) +
-         z * 0.39894228040143268f * __expf(-0.5f * z * z);
+         z * 0.39894228040143268f * expf(-0.5f * z * z);
 }
 
 // ---------------------------------------------------------------------- depthwise conv
@@ -214,9 +216,19 @@ __device__ __forceinline__ void stage_cnx(CnxW<C>& s, const float* w1, const flo
   }
 }
 
-// LayerNorm over the C channels of one pixel (biased variance, eps 1e-6): x <- (x - mean) r
+// LayerNorm over the C channels of one pixel (biased variance, eps 1e-6): x <- (x - mean) r.
+// C = 2 is evaluated in closed form, u = (x0 - x1) / 2, x = (u r, -u r): the generic
+// x - mean cancels catastrophically when x0 ~ x1 (and the UNet's base_ch = 1 models have a
+// C = 2 level in both paths).
 template <int C>
 __device__ __forceinline__ float cnx_norm(float (&x)[C]) {
+  if constexpr (C == 2) {
+    const float u = 0.5f * (x[0] - x[1]);
+    const float r = 1.0f / sqrtf(fmaf(u, u, 1e-6f));
+    x[0] = u * r;
+    x[1] = -x[0];
+    return r;
+  }
   float m = 0.f;
 #pragma unroll
   for (int c = 0; c < C; ++c) m += x[c];
@@ -323,7 +335,21 @@ __global__ __launch_bounds__(kBlock) void cnx_pw_bwd_kernel(
 #pragma unroll
         for (int c = 0; c < C; ++c) dln[c] = fmaf(W.W1(k, c), dh, dln[c]);
       }
-      // LayerNorm backward: dxh = gamma dln; dx = r (dxh - mean(dxh) - xh mean(dxh xh))
+      // LayerNorm backward: dxh = gamma dln; dx = r (dxh - mean(dxh) - xh mean(dxh xh)).
+      // C = 1: exactly 0.  C = 2 in closed form: with d = (dxh0 - dxh1) / 2 and xh0 = u r,
+      // dx0 = r d (1 - xh0^2) = d eps r^3 = -dx1 (no cancellation of 1 - xh0^2)
+      if constexpr (C <= 2) {
+        float dx0 = 0.f;
+        if constexpr (C == 2) dx0 = 0.5f * (W.LW(0) * dln[0] - W.LW(1) * dln[1]) * (1e-6f * r * r * r);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          dxd[base + (int64_t)c * HW] = c == 0 ? dx0 : -dx0;
+          sdy[c][tp] = g[c];
+          sln[c][tp] = fmaf(W.LW(c), xh[c], W.LB(c));
+          sdln[c][tp] = dln[c];
+          sxh[c][tp] = xh[c];
+        }
+      } else {
       float m1 = 0.f, m2 = 0.f;
 #pragma unroll
       for (int c = 0; c < C; ++c) {
@@ -341,6 +367,7 @@ __global__ __launch_bounds__(kBlock) void cnx_pw_bwd_kernel(
         sdln[c][tp] = dln[c];
         sxh[c][tp] = xh[c];
       }
+      }
     } else {
       for (int k = 0; k < H4; ++k) sg[k][tp] = sdh[k][tp] = 0.f;
 #pragma unroll
@@ -351,27 +378,27 @@ __global__ __launch_bounds__(kBlock) void cnx_pw_bwd_kernel(
   constexpr int E = 8 * C * C + 7 * C;
   float* out = partial + (int64_t)blockIdx.x * E;
   for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    float acc = 0.f;
+    double acc = 0.0;      // fp64: a PB-long sequential sum per entry (cancellation-prone biases)
     if (e < H4 * C) {                                   // dW1[k][c] = sum dh_k ln_c
       const int k = e / C, c = e % C;
-      for (int p = 0; p < PB; ++p) acc = fmaf(sdh[k][p], sln[c][p], acc);
+      for (int p = 0; p < PB; ++p) acc += (double)sdh[k][p] * sln[c][p];
     } else if (e < H4 * C + H4) {                       // db1[k]
       const int k = e - H4 * C;
       for (int p = 0; p < PB; ++p) acc += sdh[k][p];
     } else if (e < 2 * H4 * C + H4) {                   // dW2[c][k] = sum dy_c g_k
       const int q = e - H4 * C - H4, c = q / H4, k = q % H4;
-      for (int p = 0; p < PB; ++p) acc = fmaf(sdy[c][p], sg[k][p], acc);
+      for (int p = 0; p < PB; ++p) acc += (double)sdy[c][p] * sg[k][p];
     } else if (e < 2 * H4 * C + H4 + C) {               // db2[c]
       const int c = e - 2 * H4 * C - H4;
       for (int p = 0; p < PB; ++p) acc += sdy[c][p];
     } else if (e < 2 * H4 * C + H4 + 2 * C) {           // dgamma[c] = sum dln_c xh_c
       const int c = e - 2 * H4 * C - H4 - C;
-      for (int p = 0; p < PB; ++p) acc = fmaf(sdln[c][p], sxh[c][p], acc);
+      for (int p = 0; p < PB; ++p) acc += (double)sdln[c][p] * sxh[c][p];
     } else {                                            // dbeta[c]
       const int c = e - 2 * H4 * C - H4 - 2 * C;
       for (int p = 0; p < PB; ++p) acc += sdln[c][p];
     }
-    out[e] = acc;
+    out[e] = (float)acc;
   }
 }
 
@@ -638,10 +665,10 @@ __global__ __launch_bounds__(kBlock) void tok_stats_kernel(const float* __restri
   if (threadIdx.x == 0) kap[b] = k * iL;
 }
 
-// Ybar[b][d] = gamma[d] (U[b][d]) + beta[d],  U = sum_t c_t X_t[d] - kappa (saved for dgamma)
+// Ybar[b][d] = gamma[d] U[b][d] + beta[d],  U = sum_t c_t (X_t[d] - xbar_t) (saved for dgamma)
 __global__ __launch_bounds__(kBlock) void tok_out_kernel(const float* __restrict__ X,
                                                          const float4* __restrict__ st,
-                                                         const float* __restrict__ kap,
+                                                         const float* __restrict__ xbar,
                                                          const float* __restrict__ lw,
                                                          const float* __restrict__ lb,
                                                          float* __restrict__ Y,
@@ -651,15 +678,17 @@ __global__ __launch_bounds__(kBlock) void tok_out_kernel(const float* __restrict
   if (d >= D) return;
   const float* Xb = X + (int64_t)b * L * D + d;
   float acc = 0.f;
-  for (int t = 0; t < L; ++t) acc = fmaf(st[(int64_t)b * L + t].z, Xb[(int64_t)t * D], acc);
-  const float u = acc - kap[b];
+  for (int t = 0; t < L; ++t)
+    acc = fmaf(st[(int64_t)b * L + t].z, Xb[(int64_t)t * D] - xbar[(int64_t)b * L + t], acc);
+  const float u = acc;
   U[(int64_t)b * D + d] = u;
   Y[(int64_t)b * D + d] = fmaf(lw[d], u, lb[d]);
 }
 
-// backward prep: h[b][t] = sum_d gamma[d] dY[b][d] X_t[d] (one workgroup per token; token
-// b L is also the one that forms gb[b] = mean_d gamma dY)
+// backward prep: h[b][t] = sum_d gamma[d] dY[b][d] (X_t[d] - xbar_t) (one workgroup per token;
+// token b L is also the one that forms gb[b] = mean_d gamma dY)
 __global__ __launch_bounds__(kBlock) void tok_bwd_dot_kernel(const float* __restrict__ X,
+                                                             const float* __restrict__ xbar,
                                                              const float* __restrict__ dY,
                                                              const float* __restrict__ lw,
                                                              float* __restrict__ h,
@@ -669,11 +698,12 @@ __global__ __launch_bounds__(kBlock) void tok_bwd_dot_kernel(const float* __rest
   const int bt = blockIdx.x, b = bt / L;
   const float* xp = X + (int64_t)bt * D;
   const float* gp = dY + (int64_t)b * D;
+  const float xm = xbar[bt];
   float s = 0.f, s2 = 0.f;
   const bool first = bt % L == 0;
   for (int64_t d = threadIdx.x; d < D; d += blockDim.x) {
     const float g = lw[d] * gp[d];
-    s = fmaf(g, xp[d], s);
+    s = fmaf(g, xp[d] - xm, s);
     if (first) s2 += g;
   }
   s = block_sum(s, red);
@@ -722,21 +752,21 @@ __global__ __launch_bounds__(kBlock) void tok_bwd_stats_kernel(
     sx[t] = xbar[(int64_t)b * L + t];
   }
   __syncthreads();
-  // alpha_l = r_l / L, gO_l = sum_t M_lt h_t, beta_l
+  // alpha_l = r_l / L, beta_l = alpha_l r_l^2 (sum_t M_lt h_t) / D  (h centred)
   for (int l = threadIdx.x; l < L; l += blockDim.x) {
     const float4 s4 = st[(int64_t)b * L + l];
     float go = sh[l];
     for (int t = 0; t < L; ++t) go = fmaf(Ab[(int64_t)l * L + t], sh[t], go);
     const float al = s4.y * iL;
     sa[l] = al;
-    sbt[l] = al * s4.y * s4.y * (go - s4.x * Df * gb) / Df;
+    sbt[l] = al * s4.y * s4.y * go / Df;
   }
   __syncthreads();
   // dA_lt and softmax backward: dS_lt = A_lt (dA_lt - sum_s A_ls dA_ls)
   for (int l = 0; l < L; ++l) {
     float dot = 0.f;
     for (int t = threadIdx.x; t < L; t += blockDim.x) {
-      const float da = sa[l] * (sh[t] - gb * Df * sx[t]) - sbt[l] * Pb[(int64_t)l * L + t];
+      const float da = sa[l] * sh[t] - sbt[l] * Pb[(int64_t)l * L + t];
       Wb[(int64_t)l * L + t] = da;
       dot = fmaf(Ab[(int64_t)l * L + t], da, dot);
     }
@@ -759,23 +789,25 @@ __global__ __launch_bounds__(kBlock) void tok_bwd_stats_kernel(
     Rb[e] = (Wb[(int64_t)t * L + s] + Wb[(int64_t)s * L + t]) * isd - n;
   }
   __syncthreads();
-  // a_t = sum_l M_lt alpha_l,  k_t = sum_s N_ts xbar_s - a_t gb  (N_ts = Q_ts - R_ts)
+  // a_t = sum_l M_lt alpha_l,  k_t = sum_s Q_ts xbar_s - a_t gb  (dX is formed from centred
+  // tokens: sum_s R_ts X_s + sum_s N_ts xbar_s = sum_s R_ts (X_s - xbar_s) + sum_s Q_ts xbar_s)
   for (int t = threadIdx.x; t < L; t += blockDim.x) {
     float a = sa[t];
     for (int l = 0; l < L; ++l) a = fmaf(Ab[(int64_t)l * L + t], sa[l], a);
     float k = 0.f;
     for (int s = 0; s < L; ++s) {
       const float q = (Wb[(int64_t)t * L + s] + Wb[(int64_t)s * L + t]) * isd;
-      k = fmaf(q - Rb[(int64_t)t * L + s], sx[s], k);
+      k = fmaf(q, sx[s], k);
     }
     coef[(int64_t)b * L + t] = make_float2(a, k - a * gb);
   }
 }
 
-// dX[b][t][d] = a_t gamma[d] dY[b][d] + sum_s R_ts X_s[d] + k_t; a thread owns kTT tokens of
-// one point d (R loads are wave-uniform, X_s[d] coalesced over d)
+// dX[b][t][d] = a_t gamma[d] dY[b][d] + sum_s R_ts (X_s[d] - xbar_s) + k_t; a thread owns kTT
+// tokens of one point d (R loads are wave-uniform, X_s[d] coalesced over d)
 constexpr int kTT = 8;
 __global__ __launch_bounds__(kBlock) void tok_bwd_dx_kernel(const float* __restrict__ X,
+                                                            const float* __restrict__ xbar,
                                                             const float* __restrict__ R,
                                                             const float2* __restrict__ coef,
                                                             const float* __restrict__ lw,
@@ -789,7 +821,7 @@ __global__ __launch_bounds__(kBlock) void tok_bwd_dx_kernel(const float* __restr
   const float* Rb = R + (int64_t)b * L * L;
   float acc[kTT] = {};
   for (int s = 0; s < L; ++s) {
-    const float xs = Xb[(int64_t)s * D];
+    const float xs = Xb[(int64_t)s * D] - xbar[(int64_t)b * L + s];
 #pragma unroll
     for (int i = 0; i < kTT; ++i)
       if (t0 + i < L) acc[i] = fmaf(Rb[(int64_t)(t0 + i) * L + s], xs, acc[i]);
@@ -990,7 +1022,7 @@ BLINDNO_API int blindno_tok_attn_fwd(const float* X, const float* lw, const floa
     if (err) return err;
   }
   tok_stats_kernel<<<B, kBlock, 0, st>>>(gram, xbar, A, Pm, stt, kap, L, D, eps);
-  tok_out_kernel<<<dim3((unsigned)((D + kBlock - 1) / kBlock), B), kBlock, 0, st>>>(X, stt, kap, lw, lb,
+  tok_out_kernel<<<dim3((unsigned)((D + kBlock - 1) / kBlock), B), kBlock, 0, st>>>(X, stt, xbar, lw, lb,
                                                                                    Y, U, L, D);
   return (int)hipGetLastError();
 }
@@ -1022,10 +1054,10 @@ BLINDNO_API int blindno_tok_attn_bwd(const float* dY, const float* X, const floa
   if (dlw || dlb)
     tok_ln_wgrad_kernel<<<(unsigned)((D + kBlock - 1) / kBlock), kBlock, 0, st>>>(dY, U, dlw, dlb, B, D);
   if (dX) {
-    tok_bwd_dot_kernel<<<(unsigned)BL, kBlock, 0, st>>>(X, dY, lw, h, gb, L, D);
+    tok_bwd_dot_kernel<<<(unsigned)BL, kBlock, 0, st>>>(X, xbar, dY, lw, h, gb, L, D);
     tok_bwd_stats_kernel<<<B, kBlock, 0, st>>>(A, Pm, stt, xbar, h, gb, R, Wk, coef, L, D);
     tok_bwd_dx_kernel<<<dim3((unsigned)((D + kBlock - 1) / kBlock), (L + kTT - 1) / kTT, B), kBlock, 0,
-                        st>>>(X, R, coef, lw, dY, dX, L, D);
+                        st>>>(X, xbar, R, coef, lw, dY, dX, L, D);
   }
   return (int)hipGetLastError();
 }

@@ -5,8 +5,9 @@ functional ops in fp64 / oracle.unet_ref): one fp32 kernel, so outputs and gradi
 rel-L2 1e-5 (the temporal attention's fp32 Gram / softmax: 2e-5).  Model tests run the drop-in
 classes (blindno.unet) on the reference goldens' inputs and recipe parameters and compare with
 the float64 oracle (pinned to the reference by tests/test_oracle_golden.py) and the reference's
-fp32 outputs: forward 1e-5, gradients max(1e-4, 3 x the fp32 oracle's own distance from fp64)
--- the same conditioning-aware bar the oracle meets against the reference.
+fp32 outputs: forward 1e-5, gradients max(1e-4, 3 x the fp32 envelope: the largest distance
+from fp64 among fp32 evaluations of the same model -- the oracle in fp32, unperturbed and under
+three fp32-rounding-sized input perturbations, and the reference's own gradients).
 """
 import numpy as np
 import pytest
@@ -72,23 +73,26 @@ def test_convnext_pointwise(C, N, HW):
     w2, b2 = torch.randn(C, 4 * C, dtype=d) / (4 * C) ** 0.5, 0.1 * torch.randn(C, dtype=d)
     g = torch.randn(N, C, HW, dtype=d)
     args = (xd, sc, lw, lb, w1, b1, w2, b2)
-    ref = [t.clone().requires_grad_(True) for t in args]
-    h = F.layer_norm(ref[0].permute(0, 2, 1), (C,), ref[2], ref[3], 1e-6)
-    h = F.gelu(h @ ref[4].T + ref[5]) @ ref[6].T + ref[7]
-    yr = h.permute(0, 2, 1) + ref[1]
-    (yr * g).sum().backward()
+
+    def torch_ref(dt):
+        ref = [t.to(dt).clone().requires_grad_(True) for t in args]
+        h = F.layer_norm(ref[0].permute(0, 2, 1), (C,), ref[2], ref[3], 1e-6)
+        h = F.gelu(h @ ref[4].T + ref[5]) @ ref[6].T + ref[7]
+        yr = h.permute(0, 2, 1) + ref[1]
+        (yr * g.to(dt)).sum().backward()
+        return yr.detach().double(), [r.grad.double() for r in ref]
+
+    yr, gr = torch_ref(d)
+    _, g32 = torch_ref(torch.float32)          # conditioning: fp32 torch on the same inputs
     dev = [_leaf(t) for t in args]
     y = CnxPwFn.apply(dev[0].view(N, C, 1, HW), dev[1].view(N, C, 1, HW), *dev[2:])
     (y.view(N, C, HW) * g.cuda().float()).sum().backward()
-    assert rel_l2(y.detach().cpu().view(N, C, HW), yr.detach()) <= 1e-5
-    for i, (a, r) in enumerate(zip(_grads(dev), ref)):
-        if C == 1 and i in (0, 2, 4):
-            # LayerNorm over one channel: its output is beta, so dxd, dgamma and dW1 (it
-            # multiplies beta only through the bias... dW1 = dh ln with ln = beta) -- compare
-            # with an absolute bar scaled by the shortcut's gradient
-            assert float((a - r.grad).norm()) <= 1e-5 * float(g.norm()) + 1e-5 * float(r.grad.norm()), i
-            continue
-        assert rel_l2(a, r.grad) <= 1e-5, (i, rel_l2(a, r.grad))
+    assert rel_l2(y.detach().cpu().view(N, C, HW), yr) <= 1e-5
+    for i, (a, r, r32) in enumerate(zip(_grads(dev), gr, g32)):
+        # LayerNorm over 1-2 channels makes dxd / dgamma cancellation-dominated: the bar is
+        # max(1e-5, 3 x fp32 torch's own distance from fp64)
+        bar = max(1e-5, 3 * rel_l2(r32, r))
+        assert rel_l2(a, r) <= bar, (i, rel_l2(a, r), bar)
 
 
 @pytest.mark.parametrize("N,C,H,W,k", [(3, 4, 61, 61, (2, 2)), (5, 2, 7, 6, (2, 2)), (7, 3, 1, 41, (1, 2))])
@@ -178,7 +182,7 @@ def _model(case):
     ("nc_unet2d_train", 2, "nc", True), ("unet1d_bag_train", 1, "fpe", True),
     ("unet1d_all", 1, "fpe", True)])
 def test_perminv_unet_attn_vs_oracle(case, dim, variant, train):
-    from test_oracle_golden import unet_grad_bar, unet_oracle_run
+    from test_oracle_golden import unet_fp32_envelope, unet_grad_bar, unet_oracle_run
     m, g = _model(case)
     if "run_mean" in g:
         depth = int(g["depth"])
@@ -194,9 +198,9 @@ def test_perminv_unet_attn_vs_oracle(case, dim, variant, train):
     (y * torch.from_numpy(g["cot"]).cuda()).sum().backward()
     torch.cuda.synchronize()
     o64, g64, x64 = unet_oracle_run(g, dim, variant, train)
-    o32, g32, x32 = unet_oracle_run(g, dim, variant, train, "fp32")
+    env_o, env_g, env_x = unet_fp32_envelope(g, dim, variant, train, o64, g64, x64)
     yo = y.detach().double().cpu().numpy()
-    assert rel_l2(yo, o64) <= max(1e-5, 3 * rel_l2(o32, o64)), rel_l2(yo, o64)
+    assert rel_l2(yo, o64) <= max(1e-5, 3 * env_o), rel_l2(yo, o64)
     assert rel_l2(yo, g["out"]) <= 2e-5                      # the reference itself (fp32)
     scale = max(float(np.linalg.norm(v)) for v in g64.values())
     worst = (0.0, None)
@@ -204,16 +208,17 @@ def test_perminv_unet_attn_vs_oracle(case, dim, variant, train):
         if k not in g64:
             assert p.grad is None or float(p.grad.abs().max()) == 0.0, k    # unused heads
             continue
-        a = p.grad.detach().double().cpu().numpy()
-        if np.iscomplexobj(g64[k]):
+        if p.grad.is_complex():
             a = p.grad.detach().cpu().numpy().astype(np.complex128)
+        else:
+            a = p.grad.detach().double().cpu().numpy()
         if np.linalg.norm(g64[k]) <= 1e-10 * scale:
             assert np.linalg.norm(a) <= 1e-5 * scale, k       # conv bias before a train-mode BN
             continue
-        e, e32 = rel_l2(a, g64[k]), rel_l2(g32[k], g64[k])
+        e, e32 = rel_l2(a, g64[k]), env_g[k]
         assert e <= unet_grad_bar(e32), (k, e, e32)
         worst = max(worst, (e / unet_grad_bar(e32), k))
-    assert rel_l2(x.grad.double().cpu().numpy(), x64) <= unet_grad_bar(rel_l2(x32, x64))
+    assert rel_l2(x.grad.double().cpu().numpy(), x64) <= unet_grad_bar(env_x)
     # running statistics of the skip BatchNorms after a train-mode forward (momentum 0.1)
     if train and case in ("unet2d_train",):
         ev = load_golden("unet2d_eval")
@@ -238,7 +243,7 @@ def test_unet_graph_replay_matches_eager():
     for graphed in (False, True):
         torch.manual_seed(1)
         m = unet.PermInvUNet_attn(1, 2, 1, 4, (N, N)).cuda().train()
-        opt = FlatAdam(trained_parameters(m, exclude_prefixes=()), lr=5e-4)
+        opt = FlatAdam(trained_parameters(m), lr=5e-4)
         if graphed:
             dp = DataParallel(opt)
             step = GraphedBagStep(m, blindno.mse_loss, opt, dp, x, y, None)

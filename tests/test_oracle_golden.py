@@ -286,8 +286,10 @@ def unet_recipe_params(g):
     return make_state(shapes, seed=int(g["recipe_seed"]), complex_names=cplx)
 
 
-def unet_oracle_run(g, dim, variant, train, prec="fp64"):
-    """(out, {name: grad}, dx) of the oracle on a UNet golden's inputs and cotangent."""
+def unet_oracle_run(g, dim, variant, train, prec="fp64", perturb=None):
+    """(out, {name: grad}, dx) of the oracle on a UNet golden's inputs and cotangent.
+    ``perturb`` (a seed): inputs and parameters multiplied by 1 + 2^-24 N(0, 1) first, i.e.
+    an fp32-rounding-sized input perturbation (the conditioning envelope below)."""
     st = unet_recipe_params(g)
     if "run_mean" in g:                      # eval: running stats after the train forward
         depth = int(g["depth"])
@@ -301,7 +303,21 @@ def unet_oracle_run(g, dim, variant, train, prec="fp64"):
     try:
         p = {k: torch.from_numpy(np.asarray(v)).to(cdt if np.iscomplexobj(v) else rdt)
              .requires_grad_(np.asarray(v).dtype.kind in "fc") for k, v in st.items()}
-        x = torch.from_numpy(g["in.x"]).to(rdt).requires_grad_(True)
+        x = torch.from_numpy(g["in.x"]).to(rdt)
+        if perturb is not None:
+            gen = torch.Generator().manual_seed(perturb)
+
+            def jit(t):
+                if not t.is_floating_point():
+                    return t
+                return (t.double() * (1 + 2.0 ** -24 * torch.randn(t.shape, generator=gen,
+                                                                   dtype=torch.float64))).to(t.dtype)
+            x = jit(x)
+            with torch.no_grad():
+                for k in p:
+                    if p[k].is_floating_point() and k.split(".")[-1] in ("weight", "bias", "weights1", "weights2"):
+                        p[k].copy_(jit(p[k]))
+        x.requires_grad_(True)
         idx = g["idx"].tolist() if "idx" in g else None
         y = oracle.unet_ref.perminv_unet_attn(p, x, int(g["depth"]), dim, idx=idx, bn_train=train,
                                               variant=variant)
@@ -311,6 +327,24 @@ def unet_oracle_run(g, dim, variant, train, prec="fp64"):
     grads = {k: v.grad.detach().to(torch.complex128 if v.is_complex() else torch.float64).numpy()
              for k, v in p.items() if v.grad is not None}
     return y.detach().double().numpy(), grads, x.grad.double().numpy()
+
+
+def unet_fp32_envelope(g, dim, variant, train, o64, g64, x64, n=3, include_ref=True):
+    """Largest distance from fp64 over fp32 evaluations of the same model: the oracle in fp32
+    unperturbed and with n fp32-sized input perturbations, and the reference's own fp32
+    gradients.  The UNet's ConvNeXt LayerNorms over 1-2 channels make some gradients hinge on a
+    few near-degenerate pixels, so one fp32 run is a noisy yardstick; the envelope is not."""
+    env_o, env_g, env_x = 0.0, {}, 0.0
+    for seed in [None] + list(range(1, n + 1)):
+        o32, g32, x32 = unet_oracle_run(g, dim, variant, train, "fp32", perturb=seed)
+        env_o = max(env_o, rel_l2(o32, o64))
+        env_x = max(env_x, rel_l2(x32, x64))
+        for k in g64:
+            env_g[k] = max(env_g.get(k, 0.0), rel_l2(g32[k], g64[k]))
+    for k in g64:
+        if include_ref and "g." + k in g:
+            env_g[k] = max(env_g[k], rel_l2(g["g." + k], g64[k]))
+    return env_o, env_g, env_x
 
 
 def unet_grad_bar(e32):
@@ -331,7 +365,7 @@ def test_perminv_unet_attn(case, dim, variant, train):
     gradients; gradient bars per unet_grad_bar (the fp32 oracle run gives the conditioning)."""
     g = load_golden(case)
     o64, g64, x64 = unet_oracle_run(g, dim, variant, train)
-    o32, g32, x32 = unet_oracle_run(g, dim, variant, train, "fp32")
+    _, env_g, env_x = unet_fp32_envelope(g, dim, variant, train, o64, g64, x64, n=2, include_ref=False)
     assert rel_l2(g["out"], o64) <= FWD_TOL
     n = 0
     scale = max(float(np.linalg.norm(v)) for v in g64.values())
@@ -342,12 +376,13 @@ def test_perminv_unet_attn(case, dim, variant, train):
                 # structurally zero (a conv bias in front of a train-mode BatchNorm): fp32 noise
                 assert np.linalg.norm(v) <= 1e-5 * scale, name
             else:
-                e, e32 = rel_l2(v, g64[name]), rel_l2(g32[name], g64[name])
+                # the reference against the envelope of the oracle's own fp32 runs
+                e, e32 = rel_l2(v, g64[name]), env_g[name]
                 assert e <= unet_grad_bar(e32), (name, e, e32)
             n += 1
         elif k.startswith("gnorm."):
             name = k[6:]
             assert abs(np.linalg.norm(g64[name]) - float(v)) <= GRAD_TOL * float(v), name
             n += 1
-    assert rel_l2(g["gin.x"], x64) <= unet_grad_bar(rel_l2(x32, x64))
+    assert rel_l2(g["gin.x"], x64) <= unet_grad_bar(env_x)
     assert n > 20
