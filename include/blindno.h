@@ -416,11 +416,11 @@ int blindno_spectral_conv1d_bwd(const float* dy, const float* saved, const float
                                 int Co, int P2, int m, blindno_stream_t stream);
 
 /* ---- permutation-invariant attention UNet, PermInvUNet_attn ("BlinDNO")
- * 2d_FPE/NIOModules.py:1014-1181 (2D), 1d_FPE/NIOModules.py:163-443 (1D: height-1 fields,
+ * 2d_FPE/NIOModules.py:1044-1181 (2D), 1d_FPE/NIOModules.py:165-443 (1D: height-1 fields,
  * KH = 1).  The 3x3 convolutions and the 1x1 final_conv use blindno_conv2d_*, the skip
  * BatchNorms (and the NC copy's ConvBlock BN + ReLU) blindno_bn_act_* (slope 1 / 0).
  *
- * Depthwise convolution of ConvNeXtBlock (nn.Conv2d(C, C, 7, padding=3, groups=C), :1016;
+ * Depthwise convolution of ConvNeXtBlock (nn.Conv2d(C, C, 7, padding=3, groups=C), :1047;
  * Conv1d(C, C, 7, padding=3, groups=C), 1d_FPE/NIOModules.py:167): x, y (N, C, H, W), w (C, KH, KW),
  * padding (KH/2, KW/2), KH KW <= 49.  bwd_weight: dwb (C, KH KW + 1), last column = db; partial:
  * nsplit x C x (KH KW + 1) floats (nsplit = blindno_dwconv_wgrad_nsplit; NULL when 1). */
@@ -432,7 +432,7 @@ int blindno_dwconv_wgrad_nsplit(int N, int C, int H, int W);
 int blindno_dwconv_bwd_weight(const float* dy, const float* x, float* dwb, float* partial,
                               int nsplit, int N, int C, int H, int W, int KH, int KW,
                               blindno_stream_t stream);
-/* Rest of ConvNeXtBlock.forward (2d_FPE/NIOModules.py:1023-1032): per pixel of xd (the depthwise
+/* Rest of ConvNeXtBlock.forward (2d_FPE/NIOModules.py:1053-1062): per pixel of xd (the depthwise
  * output, (N, C, HW)) LayerNorm over C (eps 1e-6, gamma lw / beta lb) -> Linear(C, 4C) (w1, b1)
  * -> exact GELU -> Linear(4C, C) (w2, b2) -> + sc (the shortcut).  C in {1,2,4,...,64}.
  * bwd: dxd = gradient at xd (the shortcut's is dy itself); dparams = [dw1 (4C x C) | db1 (4C) |
@@ -446,13 +446,13 @@ int blindno_cnx_pw_bwd(const float* dy, const float* xd, const float* lw, const 
                        const float* w1, const float* b1, const float* w2, float* dxd,
                        float* dparams, float* partial, int nblk, int N, int C, int HW,
                        blindno_stream_t stream);
-/* MaxPool2d(2) / MaxPool1d(2) (:1092, 1d :239): window = stride = KH x KW, floor; arg (NC, Ho, Wo)
+/* MaxPool2d(2) / MaxPool1d(2) (:1115, 1d :239): window = stride = KH x KW, floor; arg (NC, Ho, Wo)
  * uint8 index of the window's maximum (first in scan order; a NaN wins). */
 int blindno_maxpool_fwd(const float* x, float* y, uint8_t* arg, int NC, int H, int W, int KH,
                         int KW, blindno_stream_t stream);
 int blindno_maxpool_bwd(const float* dy, const uint8_t* arg, float* dx, int NC, int H, int W,
                         int KH, int KW, blindno_stream_t stream);
-/* ConvTranspose2d(Ci, Co, kernel = stride = 2, output_padding) of the up path (:1106-1110;
+/* ConvTranspose2d(Ci, Co, kernel = stride = 2, output_padding) of the up path (:1130-1134;
  * 1d :258-261 with KH = 1): x (N, Ci, Hi, Wi), w (Ci, Co, KH, KW), y (N, Co, Ho, Wo) with
  * KH Hi <= Ho < KH (Hi + 1) (the extra rows / columns are output_padding).  bwd_weight:
  * dwb = [dW (Ci Co KH KW) | db (Co)], partial N x (Ci Co KH KW + Co) floats (NULL when N = 1). */
@@ -464,7 +464,7 @@ int blindno_convt_bwd_data(const float* dy, const float* w, float* dx, int N, in
 int blindno_convt_bwd_weight(const float* dy, const float* x, float* dwb, float* partial, int N,
                              int Ci, int Hi, int Wi, int Co, int KH, int KW, int Ho, int Wo,
                              blindno_stream_t stream);
-/* TemporalSelfAttention + the bag mean that follows it (:1035-1054 and :1152-1153 / :1160-1162):
+/* TemporalSelfAttention + the bag mean that follows it (:1065-1083 and :1163-1164 / :1171-1172):
  * Y (B, D) = mean_l LayerNorm_D(A X + X)_l, A = softmax(X X^T / sqrt D), X (B, L, D) the bag's L
  * snapshot features flattened to D = C H W, LayerNorm eps `eps` with gamma lw / beta lb (D).
  * Collapsed to a centred Gram matrix per bag (see csrc/unet.hip).  L <= 480.

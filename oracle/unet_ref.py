@@ -2,14 +2,14 @@
 PermInvUNet_attn) -- TEST INFRASTRUCTURE only (tests/, smoke(), bench.py's cpu_baseline).
 
 Restated from the reference's behaviour:
-  * 2D: ConvNeXtBlock, TemporalSelfAttention, PermInvUNet_attn (2d_FPE/NIOModules.py:1014-1181).
+  * 2D: ConvNeXtBlock, TemporalSelfAttention, PermInvUNet_attn (2d_FPE/NIOModules.py:1044-1181).
   * 2D NC: the 2d_Non_conservative_FPE copy of PermInvUNet_attn (2d_Non_conservative_FPE/
     NIOModules.py:897-1053) is a different network: its down/up blocks are Conv2d +
     BatchNorm2d (batch statistics over the B*L snapshots in train mode) + ReLU instead of
     ConvNeXt blocks, and its forward uses the heads fno_Fx / fno_Fy (fno_drift /
     fno_diffusion are registered but unused).
   * 1D: ConvNeXtBlock1D, TemporalSelfAttention1D, PermInvUNet_attn1D (all T snapshots) and
-    PermInvUNet_attn1D_bag (train-mode bag draw) (1d_FPE/NIOModules.py:163-443).
+    PermInvUNet_attn1D_bag (train-mode bag draw) (1d_FPE/NIOModules.py:165-443; the 1d_GPE copies with one head fno_V, 1d_GPE/NIOModules.py:342-560).
 
 The per-snapshot layers are written with torch's functional convolutions (the reference's own
 building blocks, evaluated here in float64); the temporal attention is written out as the
@@ -40,7 +40,7 @@ def _gelu(x):
 
 
 def convnext(p: Dict[str, torch.Tensor], x: torch.Tensor, dim: int) -> torch.Tensor:
-    """ConvNeXtBlock(1D) (2d_FPE/NIOModules.py:1014-1032, 1d_FPE/NIOModules.py:163-182):
+    """ConvNeXtBlock(1D) (2d_FPE/NIOModules.py:1044-1062, 1d_FPE/NIOModules.py:165-184):
     7(x7) depthwise conv, LayerNorm over channels (eps 1e-6), Linear(C,4C), exact GELU,
     Linear(4C,C), residual."""
     C = x.shape[1]
@@ -60,7 +60,7 @@ def convnext(p: Dict[str, torch.Tensor], x: torch.Tensor, dim: int) -> torch.Ten
 
 
 def temporal_attention(p: Dict[str, torch.Tensor], x: torch.Tensor) -> torch.Tensor:
-    """TemporalSelfAttention(1D) (2d_FPE/NIOModules.py:1035-1054, 1d_FPE/NIOModules.py:184-207):
+    """TemporalSelfAttention(1D) (2d_FPE/NIOModules.py:1065-1083, 1d_FPE/NIOModules.py:186-209):
     tokens = the L snapshots of a bag flattened to D = C*H*W; A = softmax(X X^T / sqrt(D)),
     LayerNorm_D(A X + X) (eps 1e-5, elementwise affine of size D).  x: (B, L, C, *S)."""
     B, L = x.shape[:2]
@@ -96,7 +96,7 @@ def skip_sizes(n: int, depth: int):
 
 
 def output_paddings(sizes):
-    """ConvTranspose output_padding of each up step (2d_FPE/NIOModules.py:1064-1072)."""
+    """ConvTranspose output_padding of each up step (2d_FPE/NIOModules.py:1094-1107)."""
     pads, cur = [], sizes[-1]
     for sz in reversed(sizes[:-1]):
         pads.append(sz - ((cur - 1) * 2 + 2))
@@ -115,7 +115,7 @@ def _bn(p, prefix, x, bn_train):
 def perminv_unet_attn(p: Dict[str, torch.Tensor], x: torch.Tensor, depth: int, dim: int,
                       idx: Optional[Sequence[int]] = None, bn_train: bool = True,
                       variant: str = "fpe", taps: Optional[list] = None) -> torch.Tensor:
-    """PermInvUNet_attn.forward (2d_FPE/NIOModules.py:1129-1181) for dim 2, x (B, T, H, W);
+    """PermInvUNet_attn.forward (2d_FPE/NIOModules.py:1144-1181) for dim 2, x (B, T, H, W);
     PermInvUNet_attn1D(_bag).forward (1d_FPE/NIOModules.py:283-322, 398-443) for dim 1,
     x (B, T, L); ``variant="nc"``: the 2d_Non_conservative_FPE model (ConvBlocks, heads
     fno_Fx/fno_Fy; 2d_Non_conservative_FPE/NIOModules.py:1009-1053).  ``idx`` is the
@@ -176,5 +176,6 @@ def perminv_unet_attn(p: Dict[str, torch.Tensor], x: torch.Tensor, depth: int, d
         heads = [fno_ref.fno2d(sub_params(p, hd), fused) for hd in names]
     else:
         fused = fused.permute(0, 2, 1)
-        heads = [fno_ref.fno1d(sub_params(p, hd), fused) for hd in ("fno_drift", "fno_diffusion")]
+        names = ("fno_V",) if "fno_V.fc0.weight" in p else ("fno_drift", "fno_diffusion")
+        heads = [fno_ref.fno1d(sub_params(p, hd), fused) for hd in names]
     return torch.cat(heads, dim=-1)

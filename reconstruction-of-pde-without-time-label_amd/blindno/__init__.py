@@ -13,6 +13,8 @@ from .nio import (NIOFP, NIOFP2D, NIOFP2D_FNO, NIOFP2D_FNO_attn, NIOFP_FNO,  # n
                   NIOFP_schrodinger, draw_bag)
 from .deeponet import FFN, DeepOnetNoBiasOrg, FeedForwardNN  # noqa: F401
 from .encoders import ConvBlock, Encoder, Encoder2D  # noqa: F401
+from .unet import (PermInvUNet_attn, PermInvUNet_attn1D, PermInvUNet_attn1D_bag,  # noqa: F401
+                   PermInvUNet_attn1D_bag_GPE, PermInvUNet_attn1D_bag_V, PermInvUNet_attn_NC)
 from .ops import mse_loss, pad_amount  # noqa: F401
 from . import torch_ops  # noqa: F401  (registers torch.ops.blindno.*)
 

@@ -14,9 +14,12 @@ encoder kernels and the 1D GPE head layout:
   1d_GPE                    NIOFP_schrodinger / NIOFP_FNO head fno_V; Encoder (5,7,4) + conv4
                             (1d_GPE/NIOModules.py:160-289; 1d_GPE/Baselines.py:254-290)
 
-Classes outside the hot-path scope (attention / Transolver / UNet / 3D variants, SURVEY.md
-section 2 rows C14, C15, C18) are importable -- the reference scripts import them next to the
-in-scope ones -- but raise NotImplementedError when constructed.
+The attention UNet ("BlinDNO") maps to blindno.unet: PermInvUNet_attn (2d_FPE),
+its ConvBlock copy PermInvUNet_attn_NC (2d_Non_conservative_FPE), PermInvUNet_attn1D(_bag)
+(1d_FPE) and the one-head 1d_GPE copies.  Classes outside the hot-path scope (Transolver /
+plain-UNet / 3D / ODE variants) are importable -- the
+reference scripts import them next to the in-scope ones -- but raise NotImplementedError when
+constructed.
 """
 from __future__ import annotations
 
@@ -26,6 +29,7 @@ from . import deeponet as _don
 from . import encoders as _enc
 from . import fno as _fno
 from . import nio as _nio
+from . import unet as _unet
 
 
 def _out_of_scope(name: str, where: str):
@@ -118,32 +122,39 @@ def _oos(where, *names):
 
 
 _2D_OOS = ("NIOFP2D_Trans", "NIOFP2D_Trans_attn", "NIOFP2D_attn",
-           "NIOFP_ode", "NIOFP3D", "PermInvUNet", "PermInvUNet_attn", "ConvNeXtBlock",
-           "TemporalSelfAttention")
+           "NIOFP_ode", "NIOFP3D", "PermInvUNet")
 
 EXPERIMENTS = {
     "2d_FPE": dict(
         NIOModules=dict(NIOFP2D=_NIOFP2D_2d, NIOFP2D_FNO=_NIOFP2D_FNO_2d, NIOFP=_NIOFP_1d,
                         NIOFP2D_FNO_attn=_NIOFP2D_FNO_attn_2d,
+                        PermInvUNet_attn=_unet.PermInvUNet_attn, ConvNeXtBlock=_unet.ConvNeXtBlock,
+                        TemporalSelfAttention=_unet.TemporalSelfAttention,
                         draw_bag=_nio.draw_bag, **_oos("2d_FPE/NIOModules.py", *_2D_OOS)),
     ),
     "2d_Non_conservative_FPE": dict(
         NIOModules=dict(NIOFP2D=_NIOFP2D_nc, NIOFP2D_FNO=_NIOFP2D_FNO_nc, NIOFP=_NIOFP_1d,
                         NIOFP2D_FNO_attn=_NIOFP2D_FNO_attn_nc,
+                        PermInvUNet_attn=_unet.PermInvUNet_attn_NC,
+                        TemporalSelfAttention=_unet.TemporalSelfAttention,
                         draw_bag=_nio.draw_bag,
                         **_oos("2d_Non_conservative_FPE/NIOModules.py", *_2D_OOS)),
     ),
     "1d_FPE": dict(
         NIOModules=dict(NIOFP=_NIOFP_1d, NIOFP_FNO=_NIOFP_FNO_1d, draw_bag=_nio.draw_bag,
-                        **_oos("1d_FPE/NIOModules.py", "ConvNeXtBlock1D", "TemporalSelfAttention1D",
-                               "PermInvUNet_attn1D", "PermInvUNet_attn1D_bag")),
+                        ConvNeXtBlock1D=_unet.ConvNeXtBlock1D,
+                        TemporalSelfAttention1D=_unet.TemporalSelfAttention1D,
+                        PermInvUNet_attn1D=_unet.PermInvUNet_attn1D,
+                        PermInvUNet_attn1D_bag=_unet.PermInvUNet_attn1D_bag),
     ),
     "1d_GPE": dict(
         NIOModules=dict(NIOFP_schrodinger=_nio.NIOFP_schrodinger, NIOFP_FNO=_NIOFP_FNO_gpe,
                         draw_bag=_nio.draw_bag,
-                        **_oos("1d_GPE/NIOModules.py", "NIOFP2D", "NIOFP", "ConvNeXtBlock1D",
-                               "TemporalSelfAttention1D", "PermInvUNet_attn1D_bag",
-                               "PermInvUNet_attn1D_bag_GPE")),
+                        ConvNeXtBlock1D=_unet.ConvNeXtBlock1D,
+                        TemporalSelfAttention1D=_unet.TemporalSelfAttention1D,
+                        PermInvUNet_attn1D_bag=_unet.PermInvUNet_attn1D_bag_V,
+                        PermInvUNet_attn1D_bag_GPE=_unet.PermInvUNet_attn1D_bag_GPE,
+                        **_oos("1d_GPE/NIOModules.py", "NIOFP2D", "NIOFP")),
     ),
 }
 for _exp in EXPERIMENTS.values():

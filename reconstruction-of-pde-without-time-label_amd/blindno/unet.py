@@ -4,13 +4,15 @@ call "BlinDNO"  -- on the HIP kernels.
 Drop-in for (same class names, constructor signatures, attribute names, parameter shapes and
 creation order, so reference checkpoints load and a seeded construction gives identical
 weights):
-  * ``PermInvUNet_attn``      2d_FPE/NIOModules.py:1062-1181 (ConvNeXt down/up blocks)
+  * ``PermInvUNet_attn``      2d_FPE/NIOModules.py:1086-1181 (ConvNeXt down/up blocks)
   * ``PermInvUNet_attn_NC``   the 2d_Non_conservative_FPE copy of PermInvUNet_attn
                               (2d_Non_conservative_FPE/NIOModules.py:932-1053: Conv2d +
                               BatchNorm2d + ReLU blocks, heads fno_Fx / fno_Fy; the dropin shim of
                               that experiment exports it under the reference's name)
-  * ``PermInvUNet_attn1D``    1d_FPE/NIOModules.py:209-322 (all T snapshots)
-  * ``PermInvUNet_attn1D_bag`` 1d_FPE/NIOModules.py:325-443 (train-mode bag draw)
+  * ``PermInvUNet_attn1D``    1d_FPE/NIOModules.py:212-322 (all T snapshots)
+  * ``PermInvUNet_attn1D_bag`` 1d_FPE/NIOModules.py:326-443 (train-mode bag draw); the 1d_GPE
+                              copies (one head fno_V): ``PermInvUNet_attn1D_bag_V`` and
+                              ``PermInvUNet_attn1D_bag_GPE`` (1d_GPE/NIOModules.py:342-560)
 
 Per-snapshot layers (3x3 conv, 7x7 depthwise conv, the ConvNeXt pointwise MLP with its
 LayerNorm, 2x2 max pool) run on the B*L snapshots of a bag; the temporal self-attention + bag
@@ -52,7 +54,7 @@ def _as4(x):
 
 class DWConvFn(torch.autograd.Function):
     """Depthwise KHxKW convolution, padding (KH/2, KW/2), with bias: ConvNeXtBlock.dwconv
-    (2d_FPE/NIOModules.py:1016; 1d_FPE/NIOModules.py:167).  x (N, C, H, W); w (C, 1, KH, KW)."""
+    (2d_FPE/NIOModules.py:1047; 1d_FPE/NIOModules.py:169).  x (N, C, H, W); w (C, 1, KH, KW)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -87,7 +89,7 @@ class DWConvFn(torch.autograd.Function):
 
 
 class CnxPwFn(torch.autograd.Function):
-    """ConvNeXtBlock after the depthwise conv (2d_FPE/NIOModules.py:1023-1032): per pixel
+    """ConvNeXtBlock after the depthwise conv (2d_FPE/NIOModules.py:1053-1062): per pixel
     LayerNorm(C, eps 1e-6) -> pwconv1 -> exact GELU -> pwconv2 -> + shortcut, one kernel
     each way.  xd, sc (N, C, H, W)."""
 
@@ -129,7 +131,7 @@ class CnxPwFn(torch.autograd.Function):
 
 
 class MaxPoolFn(torch.autograd.Function):
-    """MaxPool2d(2) / MaxPool1d(2) (2d_FPE/NIOModules.py:1092; 1d_FPE/NIOModules.py:239) on
+    """MaxPool2d(2) / MaxPool1d(2) (2d_FPE/NIOModules.py:1115; 1d_FPE/NIOModules.py:239) on
     (N, C, H, W) with window (KH, KW)."""
 
     @staticmethod
@@ -157,7 +159,7 @@ class MaxPoolFn(torch.autograd.Function):
 
 class ConvTFn(torch.autograd.Function):
     """ConvTranspose2d(Ci, Co, kernel = stride = 2, output_padding) (2d_FPE/NIOModules.py:
-    1106-1110; 1D: kernel (1, 2)).  x (N, Ci, Hi, Wi), w (Ci, Co, KH, KW) -> (N, Co, Ho, Wo)."""
+    1130-1134; 1D: kernel (1, 2)).  x (N, Ci, Hi, Wi), w (Ci, Co, KH, KW) -> (N, Co, Ho, Wo)."""
 
     @staticmethod
     def forward(ctx, x, w, b, Ho, Wo):
@@ -193,8 +195,8 @@ class ConvTFn(torch.autograd.Function):
 
 
 class TokAttnMeanFn(torch.autograd.Function):
-    """TemporalSelfAttention followed by the bag mean (2d_FPE/NIOModules.py:1035-1054 with
-    :1152-1153 / :1160-1162): X (B, L, D) -> mean_l LayerNorm_D(softmax(X X^T/sqrt D) X + X)_l,
+    """TemporalSelfAttention followed by the bag mean (2d_FPE/NIOModules.py:1065-1083 with
+    :1163-1164 / :1171-1172): X (B, L, D) -> mean_l LayerNorm_D(softmax(X X^T/sqrt D) X + X)_l,
     (B, D).  One collapsed HIP op each way (csrc/unet.hip)."""
 
     @staticmethod
@@ -249,7 +251,7 @@ def _bn(bn: nn.Module, x, slope):
 
 
 class ConvNeXtBlock(nn.Module):
-    """ConvNeXtBlock, 2d_FPE/NIOModules.py:1014-1032."""
+    """ConvNeXtBlock, 2d_FPE/NIOModules.py:1044-1062."""
 
     def __init__(self, dim):
         super().__init__()
@@ -269,7 +271,7 @@ class ConvNeXtBlock(nn.Module):
 
 
 class ConvNeXtBlock1D(ConvNeXtBlock):
-    """ConvNeXtBlock1D, 1d_FPE/NIOModules.py:163-182."""
+    """ConvNeXtBlock1D, 1d_FPE/NIOModules.py:165-184."""
 
     def __init__(self, dim):
         nn.Module.__init__(self)
@@ -281,7 +283,7 @@ class ConvNeXtBlock1D(ConvNeXtBlock):
 
 
 class TemporalSelfAttention(nn.Module):
-    """TemporalSelfAttention, 2d_FPE/NIOModules.py:1035-1054 (D = C H W, LayerNorm(D)).
+    """TemporalSelfAttention, 2d_FPE/NIOModules.py:1065-1083 (D = C H W, LayerNorm(D)).
     ``forward`` is the reference's (B, L, C, H, W) -> same; the UNet itself only ever uses the
     bag mean of it, ``bag_mean`` (the collapsed HIP op)."""
 
@@ -299,7 +301,7 @@ class TemporalSelfAttention(nn.Module):
 
 
 class TemporalSelfAttention1D(TemporalSelfAttention):
-    """TemporalSelfAttention1D, 1d_FPE/NIOModules.py:184-207 (D = C L)."""
+    """TemporalSelfAttention1D, 1d_FPE/NIOModules.py:186-209 (D = C L)."""
 
     def __init__(self, C, L):
         nn.Module.__init__(self)
@@ -309,7 +311,7 @@ class TemporalSelfAttention1D(TemporalSelfAttention):
 
 
 def _sizes_and_pads(n, depth):
-    """Skip sizes and ConvTranspose output_padding (2d_FPE/NIOModules.py:1064-1072)."""
+    """Skip sizes and ConvTranspose output_padding (2d_FPE/NIOModules.py:1094-1107)."""
     s = [n]
     for _ in range(depth):
         s.append(s[-1] // 2)
@@ -403,7 +405,7 @@ class _UNetBase(nn.Module):
 
 
 class PermInvUNet_attn(_UNetBase):
-    """PermInvUNet_attn, 2d_FPE/NIOModules.py:1062-1181."""
+    """PermInvUNet_attn, 2d_FPE/NIOModules.py:1086-1181."""
 
     def __init__(self, in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=(61, 61)):
         super().__init__()
@@ -467,17 +469,19 @@ class PermInvUNet_attn_NC(PermInvUNet_attn):
 
 
 class PermInvUNet_attn1D(_UNetBase):
-    """PermInvUNet_attn1D, 1d_FPE/NIOModules.py:209-322: every one of the T snapshots (no bag
+    """PermInvUNet_attn1D, 1d_FPE/NIOModules.py:212-322: every one of the T snapshots (no bag
     draw); heads FNO1d(modes 15, width 30, 3 layers)."""
 
     dim = 1
     _bag = False
 
+    _width = 30
+
     def __init__(self, in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=61, device=None):
         super().__init__()
         self.device = device
         self.depth = depth
-        self.width = 30
+        self.width = self._width
         self.chs = [base_ch * (2 ** i) for i in range(depth + 1)]
         sl, pads = _sizes_and_pads(input_size, depth)
         self.down_convs = nn.ModuleList()
@@ -498,6 +502,9 @@ class PermInvUNet_attn1D(_UNetBase):
             self.up_convs.append(nn.Sequential(nn.Conv1d(self.chs[i] * 2, self.chs[i], 3, padding=1),
                                                ConvNeXtBlock1D(self.chs[i])))
         self.final_conv = nn.Conv1d(self.chs[0], self.width, 1)
+        self._make_heads()
+
+    def _make_heads(self):
         self.fno_drift = FNO1d(modes=15, width=self.width, n_layers=3, input_dim=self.width, output_dim=1,
                                device=self.device)
         self.fno_diffusion = FNO1d(modes=15, width=self.width, n_layers=3, input_dim=self.width,
@@ -505,7 +512,38 @@ class PermInvUNet_attn1D(_UNetBase):
 
 
 class PermInvUNet_attn1D_bag(PermInvUNet_attn1D):
-    """PermInvUNet_attn1D_bag, 1d_FPE/NIOModules.py:325-443: as PermInvUNet_attn1D with the
+    """PermInvUNet_attn1D_bag, 1d_FPE/NIOModules.py:326-443: as PermInvUNet_attn1D with the
     train-mode bag draw L = randint(50, T), idx = choice(T, L) (with replacement)."""
 
     _bag = True
+
+
+class PermInvUNet_attn1D_bag_V(PermInvUNet_attn1D_bag):
+    """The 1d_GPE copy of PermInvUNet_attn1D_bag (1d_GPE/NIOModules.py:342-453): width 10 and one
+    head fno_V = FNO1d(modes 30) (the GPE potential); the dropin shim of 1d_GPE exports it under
+    the reference's name."""
+
+    _width = 10
+    _heads = ("fno_V",)
+
+    def _make_heads(self):
+        self.fno_V = FNO1d(modes=30, width=self.width, n_layers=3, input_dim=self.width, output_dim=1,
+                           device=self.device)
+
+
+class PermInvUNet_attn1D_bag_GPE(PermInvUNet_attn1D_bag):
+    """PermInvUNet_attn1D_bag_GPE, 1d_GPE/NIOModules.py:455-560: as the 1d_GPE bag UNet with the
+    head's ``width`` and ``modes`` as constructor arguments."""
+
+    _heads = ("fno_V",)
+
+    def __init__(self, in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=61, device=None, width=None,
+                 modes=None):
+        self._width = width
+        self.modes = modes
+        super().__init__(in_ch, out_ch, base_ch, depth, input_size, device)
+        self.modes = modes
+
+    def _make_heads(self):
+        self.fno_V = FNO1d(modes=self.modes, width=self.width, n_layers=3, input_dim=self.width,
+                           output_dim=1, device=self.device)

@@ -1,5 +1,5 @@
 // Kernels of the permutation-invariant attention UNet, PermInvUNet_attn ("BlinDNO";
-// 2d_FPE/NIOModules.py:1014-1181, 1D: 1d_FPE/NIOModules.py:163-443), that the generic
+// 2d_FPE/NIOModules.py:1044-1181, 1D: 1d_FPE/NIOModules.py:165-443), that the generic
 // convolution (conv.hip) and BatchNorm (batchnorm.hip) kernels do not cover:
 //
 //   dwconv    7x7 (1x7) depthwise convolution of ConvNeXtBlock (groups = C, padding 3)

@@ -74,7 +74,7 @@ def group(exp):
         x = torch.from_numpy(make_array((2, 60, n, n), seed, tag + ".x"))
         np.random.seed(23)
         L = np.random.randint(50, x.shape[1])
-        idx = np.random.choice(x.shape[1], L)             # 2d_FPE/NIOModules.py:1131-1133
+        idx = np.random.choice(x.shape[1], L)             # 2d_FPE/NIOModules.py:1145-1148
         np.random.seed(23)
         m.train()
         _capture(f"{tag}_train", m, {"x": x}, lambda: m(x), seed=seed, save_params=False,
@@ -96,13 +96,25 @@ def group(exp):
         np.savez(os.path.join(HERE, f"{tag}_init.npz"), **fp)
         key = f"{'2d' if exp == '2d_FPE' else '2d_NC'}.PermInvUNet_attn(1,2,1,4,(61,61))"
         out[key] = _layout(NM.PermInvUNet_attn(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=(61, 61)))
+    elif exp == "1d_GPE":
+        # the one-head copies: layouts and seeded-init fingerprints
+        fp = _init_fingerprint("unet1d_gpe_bag", lambda: NM.PermInvUNet_attn1D_bag(
+            in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=128, device="cpu"), 534)
+        fp.update(_init_fingerprint("unet1d_gpe", lambda: NM.PermInvUNet_attn1D_bag_GPE(
+            in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=128, device="cpu", width=20, modes=40), 535))
+        np.savez(os.path.join(HERE, "unet1d_gpe_init.npz"), **fp)
+        out["1d_GPE.PermInvUNet_attn1D_bag(1,2,1,4,128)"] = _layout(
+            NM.PermInvUNet_attn1D_bag(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=128, device="cpu"))
+        out["1d_GPE.PermInvUNet_attn1D_bag_GPE(1,2,1,4,128,20,40)"] = _layout(
+            NM.PermInvUNet_attn1D_bag_GPE(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=128, device="cpu",
+                                          width=20, modes=40))
     else:  # 1d_FPE
         m = NM.PermInvUNet_attn1D_bag(in_ch=1, out_ch=2, base_ch=1, depth=5, input_size=40, device="cpu")
         rec = _load_recipe(m, 511)
         x = torch.from_numpy(make_array((2, 60, 40), 511, "unet1d_bag.x"))
         np.random.seed(29)
         L = np.random.randint(50, x.shape[1])
-        idx = np.random.choice(x.shape[1], L)             # 1d_FPE/NIOModules.py:399-403
+        idx = np.random.choice(x.shape[1], L)             # 1d_FPE/NIOModules.py:398-402
         np.random.seed(29)
         m.train()
         _capture("unet1d_bag_train", m, {"x": x}, lambda: m(x), seed=511, save_params=False,
@@ -140,7 +152,7 @@ def main():
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
     path = os.path.join(HERE, "layouts.json")
     layouts = json.load(open(path))
-    for g in ("2d_FPE", "2d_Non_conservative_FPE", "1d_FPE"):
+    for g in ("2d_FPE", "2d_Non_conservative_FPE", "1d_FPE", "1d_GPE"):
         subprocess.run([sys.executable, __file__, "--ref", a.ref, "--group", g], check=True,
                        cwd="/tmp", env=env)
         p = os.path.join(HERE, f"_layouts_unet_{g}.json")

@@ -20,6 +20,19 @@ CASES = [
     ("2d_Non_conservative_FPE", "NIOFP2D(2,3,100,25,3,12,32,2)", "2d_NC.NIOFP2D(2,3,100,25,3,12,32,2)"),
     ("1d_FPE", "NIOFP_FNO(3,30,15,2,'cpu')", "1d_FPE.NIOFP_FNO(3,30,15,2)"),
     ("1d_GPE", "NIOFP_FNO(3,20,40,1,'cpu')", "1d_GPE.NIOFP_FNO(3,20,40,1)"),
+    # the attention UNet ("BlinDNO"): each experiment's own copy
+    ("2d_FPE", "PermInvUNet_attn(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=(61, 61))",
+     "2d.PermInvUNet_attn(1,2,1,4,(61,61))"),
+    ("2d_Non_conservative_FPE", "PermInvUNet_attn(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=(61, 61))",
+     "2d_NC.PermInvUNet_attn(1,2,1,4,(61,61))"),
+    ("1d_FPE", "PermInvUNet_attn1D_bag(in_ch=1, out_ch=2, base_ch=1, depth=5, input_size=80, device='cpu')",
+     "1d.PermInvUNet_attn1D_bag(1,2,1,5,80)"),
+    ("1d_FPE", "PermInvUNet_attn1D(in_ch=1, out_ch=2, base_ch=1, depth=6, input_size=80, device='cpu')",
+     "1d.PermInvUNet_attn1D(1,2,1,6,80)"),
+    ("1d_GPE", "PermInvUNet_attn1D_bag(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=128, device='cpu')",
+     "1d_GPE.PermInvUNet_attn1D_bag(1,2,1,4,128)"),
+    ("1d_GPE", "PermInvUNet_attn1D_bag_GPE(in_ch=1, out_ch=2, base_ch=1, depth=4, input_size=128, device='cpu', "
+     "width=20, modes=40)", "1d_GPE.PermInvUNet_attn1D_bag_GPE(1,2,1,4,128,20,40)"),
 ]
 
 IMPORTS = {

@@ -62,7 +62,7 @@ def test_dwconv(N, C, H, W, k):
                                     (32, 6, 5), (64, 40, 1)])
 def test_convnext_pointwise(C, N, HW):
     """LayerNorm(C, 1e-6) -> Linear(C,4C) -> GELU -> Linear(4C,C) -> + shortcut
-    (2d_FPE/NIOModules.py:1023-1032) vs fp64, forward and every gradient."""
+    (2d_FPE/NIOModules.py:1053-1062) vs fp64, forward and every gradient."""
     from blindno.unet import CnxPwFn
     torch.manual_seed(2)
     d = torch.float64
@@ -137,8 +137,8 @@ def test_conv_transpose(N, Ci, Co, Hi, Wi, k, op):
 @pytest.mark.parametrize("B,L,D,scale", [(2, 57, 3721, 1.0), (4, 99, 144, 1.0), (3, 1, 900, 1.0), (1, 7, 5000, 0.3),
                                          (2, 64, 80, 3.0), (2, 150, 2048, 0.5)])
 def test_temporal_attention_bag_mean(B, L, D, scale):
-    """mean_l LayerNorm_D(softmax(X X^T/sqrt D) X + X)_l (2d_FPE/NIOModules.py:1035-1054,
-    1152-1153) vs the oracle's literal form in fp64; X with a per-token offset (centring)."""
+    """mean_l LayerNorm_D(softmax(X X^T/sqrt D) X + X)_l (2d_FPE/NIOModules.py:1065-1083,
+    1163-1164) vs the oracle's literal form in fp64; X with a per-token offset (centring)."""
     from blindno.unet import TokAttnMeanFn
     torch.manual_seed(5)
     d = torch.float64
@@ -260,3 +260,51 @@ def test_unet_graph_replay_matches_eager():
         torch.cuda.synchronize()
         finals.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu())
     assert rel_l2(finals[1].numpy(), finals[0].numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("kind", ["bag_V", "bag_GPE"])
+def test_unet_1d_gpe_copies_vs_oracle(kind):
+    """The one-head 1d_GPE copies (1d_GPE/NIOModules.py:342-560) on seeded weights vs the fp64
+    oracle (train mode, recorded bag): forward 1e-5, every gradient 1e-4 (fp32 envelope bar)."""
+    from blindno import unet
+    from test_oracle_golden import unet_grad_bar
+    torch.manual_seed(11)
+    if kind == "bag_V":
+        m = unet.PermInvUNet_attn1D_bag_V(1, 2, 1, 4, 64, device="cpu")
+    else:
+        m = unet.PermInvUNet_attn1D_bag_GPE(1, 2, 2, 3, 48, device="cpu", width=12, modes=16)
+    m = m.cuda().train()
+    n = 64 if kind == "bag_V" else 48
+    x = torch.randn(3, 60, n)
+    rs = np.random.RandomState(3)
+    idx = rs.choice(60, rs.randint(50, 60))
+    cot = torch.randn(3, n, 1)
+    y = m(x.cuda(), bag_idx=idx)
+    (y * cot.cuda()).sum().backward()
+    res = {}
+    for prec, dt in (("fp64", torch.float64), ("fp32", torch.float32)):
+        oracle.set_precision(prec)
+        try:
+            p = {k: (v.detach().cpu().to(torch.complex128 if v.is_complex() else dt).requires_grad_(True)
+                     if v.is_floating_point() or v.is_complex() else v.cpu()) for k, v in m.state_dict().items()}
+            if prec == "fp32":
+                p = {k: (v.detach().to(torch.complex64).requires_grad_(True) if v.is_complex() else v)
+                     for k, v in p.items()}
+            yo = oracle.unet_ref.perminv_unet_attn(p, x.to(dt), m.depth, 1, idx=idx.tolist())
+            (yo * cot.to(dt)).sum().backward()
+        finally:
+            oracle.set_precision("fp64")
+        res[prec] = (yo.detach().double().numpy(), {k: v.grad for k, v in p.items()
+                                                    if torch.is_tensor(v) and v.grad is not None})
+    o64, g64 = res["fp64"]
+    assert rel_l2(y.detach().double().cpu().numpy(), o64) <= 1e-5
+    for k, prm in m.named_parameters():
+        if k not in g64:
+            continue
+        a = prm.grad.detach().cpu()
+        a = a.to(torch.complex128) if a.is_complex() else a.double()
+        r, r32 = g64[k], res["fp32"][1][k]
+        r32 = r32.to(torch.complex128) if r32.is_complex() else r32.double()
+        if float(r.norm()) == 0.0:
+            continue
+        assert rel_l2(a.numpy(), r.detach().numpy()) <= unet_grad_bar(rel_l2(r32.numpy(), r.detach().numpy())), k

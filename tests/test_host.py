@@ -197,6 +197,11 @@ def _unet_ctors():
                                                   lambda: unet.PermInvUNet_attn1D_bag(1, 2, 1, 5, 80, device="cpu")),
         "1d.PermInvUNet_attn1D(1,2,1,6,80)": ("unet1d", 533,
                                               lambda: unet.PermInvUNet_attn1D(1, 2, 1, 6, 80, device="cpu")),
+        "1d_GPE.PermInvUNet_attn1D_bag(1,2,1,4,128)": (
+            "unet1d_gpe_bag", 534, lambda: unet.PermInvUNet_attn1D_bag_V(1, 2, 1, 4, 128, device="cpu")),
+        "1d_GPE.PermInvUNet_attn1D_bag_GPE(1,2,1,4,128,20,40)": (
+            "unet1d_gpe", 535, lambda: unet.PermInvUNet_attn1D_bag_GPE(1, 2, 1, 4, 128, device="cpu", width=20,
+                                                                       modes=40)),
     }
 
 
@@ -210,7 +215,8 @@ def test_unet_layout_and_seeded_init_match_reference(key):
     m = ctor()
     got = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in m.state_dict().items()]
     assert got == lay[key]
-    fp = np.load(os.path.join(GOLDEN, ("unet1d" if tag.startswith("unet1d") else tag) + "_init.npz"))
+    fname = "unet1d_gpe" if tag.startswith("unet1d_gpe") else ("unet1d" if tag.startswith("unet1d") else tag)
+    fp = np.load(os.path.join(GOLDEN, fname + "_init.npz"))
     for k, v in m.state_dict().items():
         a = (torch.view_as_real(v) if v.is_complex() else v).double().reshape(-1).numpy()
         ref = fp[f"{tag}|{k}"]

@@ -359,9 +359,9 @@ def unet_grad_bar(e32):
     ("nc_unet2d_train", 2, "nc", True), ("unet1d_bag_train", 1, "fpe", True),
     ("unet1d_all", 1, "fpe", True)])
 def test_perminv_unet_attn(case, dim, variant, train):
-    """PermInvUNet_attn (2d_FPE/NIOModules.py:1062-1181), its NC copy with ConvBlocks
+    """PermInvUNet_attn (2d_FPE/NIOModules.py:1086-1181), its NC copy with ConvBlocks
     (2d_Non_conservative_FPE/NIOModules.py:932-1053) and the 1D models
-    (1d_FPE/NIOModules.py:209-443): the fp64 oracle against the reference's fp32 outputs and
+    (1d_FPE/NIOModules.py:212-443): the fp64 oracle against the reference's fp32 outputs and
     gradients; gradient bars per unet_grad_bar (the fp32 oracle run gives the conditioning)."""
     g = load_golden(case)
     o64, g64, x64 = unet_oracle_run(g, dim, variant, train)
