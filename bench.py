@@ -53,6 +53,13 @@ CONFIGS = {
     # replacement, 2d_FPE/NIOModules.py:344-345)
     "C_attn": dict(desc="2d_FPE NIOFP2D_FNO_attn(2,3,100,25,3,12,32,2,128,128)", dim=2, N=128, T=100,
                    B=4, lr=5e-4),
+    # the attention UNet ("BlinDNO") at the reference's own training configurations
+    "U": dict(desc="2d_FPE train_unet.py PermInvUNet_attn(1,2,1,4,(61,61))", dim=2, N=61, T=100, B=4,
+              lr=5e-4),
+    "U_NC": dict(desc="2d_Non_conservative_FPE train_unet.py PermInvUNet_attn(1,2,1,5,(80,80))", dim=2,
+                 N=80, T=100, B=4, lr=5e-4),
+    "U1": dict(desc="1d_FPE train_unet_bag.py PermInvUNet_attn1D_bag(1,2,1,5,80)", dim=1, N=80, T=256,
+               B=32, lr=1e-3),
 }
 
 
@@ -65,6 +72,16 @@ def build_model(cfg_name, N, dev):
     if cfg_name == "B":
         m = blindno.NIOFP_FNO(3, 20, 40, 1, dev, heads=("fno_V",))
         return m.to(dev), trained_parameters(m), 1
+    if cfg_name in ("U", "U_NC", "U1"):
+        from blindno import unet
+        if cfg_name == "U":
+            m = unet.PermInvUNet_attn(1, 2, 1, 4, (N, N))
+        elif cfg_name == "U_NC":
+            m = unet.PermInvUNet_attn_NC(1, 2, 1, 5, (N, N))
+        else:
+            m = unet.PermInvUNet_attn1D_bag(1, 2, 1, 5, N, device=dev)
+        m = m.to(dev)
+        return m, trained_parameters(m), 2
     if cfg_name == "C_attn":
         m = blindno.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 12, 32, 2, N, N)
         return m.to(dev), trained_parameters(m), 2
@@ -151,7 +168,7 @@ def main():
     graphed = None
     # one graph per bag size (device-resident bag indices); the NIO branch (D) stays eager: its
     # MIOpen convolutions allocate workspace per call
-    if not a.no_graph and a.config in ("A", "B", "C", "E", "C_attn"):
+    if not a.no_graph and a.config in ("A", "B", "C", "E", "C_attn", "U", "U_NC", "U1"):
         # one HIP graph per bag size L = randint(50, T) (captured here, before the warm-up; the
         # numpy draw below stays the reference's: L and idx are drawn on the host every step)
         graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc)

@@ -455,12 +455,14 @@ int blindno_maxpool_bwd(const float* dy, const uint8_t* arg, float* dx, int NC, 
 /* ConvTranspose2d(Ci, Co, kernel = stride = 2, output_padding) of the up path (:1130-1134;
  * 1d :258-261 with KH = 1): x (N, Ci, Hi, Wi), w (Ci, Co, KH, KW), y (N, Co, Ho, Wo) with
  * KH Hi <= Ho < KH (Hi + 1) (the extra rows / columns are output_padding).  bwd_weight:
- * dwb = [dW (Ci Co KH KW) | db (Co)], partial N x (Ci Co KH KW + Co) floats (NULL when N = 1). */
+ * dwb = [dW (Ci Co KH KW) | db (Co)], partial blindno_convt_wgrad_nparts(N, Hi, Wi) x
+ * (Ci Co KH KW + Co) floats. */
 int blindno_convt_fwd(const float* x, const float* w, const float* b, float* y, int N, int Ci,
                       int Hi, int Wi, int Co, int KH, int KW, int Ho, int Wo,
                       blindno_stream_t stream);
 int blindno_convt_bwd_data(const float* dy, const float* w, float* dx, int N, int Ci, int Hi,
                            int Wi, int Co, int KH, int KW, int Ho, int Wo, blindno_stream_t stream);
+int blindno_convt_wgrad_nparts(int N, int Hi, int Wi);
 int blindno_convt_bwd_weight(const float* dy, const float* x, float* dwb, float* partial, int N,
                              int Ci, int Hi, int Wi, int Co, int KH, int KW, int Ho, int Wo,
                              blindno_stream_t stream);

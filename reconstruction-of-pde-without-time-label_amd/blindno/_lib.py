@@ -100,6 +100,7 @@ SIGNATURES = {
     "blindno_maxpool_bwd": "ppp" + "iiiii" + "s",
     "blindno_convt_fwd": "pppp" + "iiiiiiiii" + "s",
     "blindno_convt_bwd_data": "ppp" + "iiiiiiiii" + "s",
+    "blindno_convt_wgrad_nparts": "iii",
     "blindno_convt_bwd_weight": "pppp" + "iiiiiiiii" + "s",
     "blindno_tok_gram_nchunk": "l",
     "blindno_tok_attn_save_floats": "iil",

@@ -1,6 +1,6 @@
 """CNN snapshot encoders of the NIO branch (OpenFWI-style ConvBlocks,
-2d_FPE/Baselines.py:40-52,186-249,254-287).  The convolutions are dense and run on
-MIOpen through torch; only the layer layout/initialisation order matters for drop-in.
+2d_FPE/Baselines.py:40-52,186-249,254-287).  The layer layout and initialisation order match
+the reference (drop-in checkpoints); execution is on libblindno (below).
 
 Divergence (documented in DESIGN.md): the reference's Encoder2D hard-codes its last
 kernel to the grid ((2,1) for 61^2 in 2d_FPE, (3,2) for 80^2 in the non-conservative

@@ -67,9 +67,30 @@ class Experiment:
     loss_files: Sequence[str] = field(default_factory=lambda: ("train_losses", "test_losses"))
 
 
-def _experiments():
-    from . import data, nio
+def _experiments(model: str = "fno"):
+    """The reference's train_*.py configurations.  ``model="unet"``: the attention-UNet scripts
+    (2d_FPE/train_unet.py:62-110, 2d_Non_conservative_FPE/train_unet.py:60-110,
+    1d_FPE/train_unet_bag.py:61-92, 1d_GPE/train_unet_GPE.py:80-110): same loop, metric quirk
+    and best-checkpoint rule as train_fno.py, their own model / lr / batch / result directory."""
+    from . import data, nio, unet
     from .encoders import Encoder2D
+    if model == "unet":
+        all4 = ("train_losses", "test_losses", "test_losses_drift", "test_losses_diffusion")
+        return {
+            "2d_FPE": Experiment("2d_FPE", 2, data.TrajectoryDataset2D,
+                                 lambda n, dev: unet.PermInvUNet_attn(1, 2, 1, 4, (n, n)), 5e-4, 4, 5,
+                                 "result_unet", True, all4),
+            "2d_Non_conservative_FPE": Experiment(
+                "2d_Non_conservative_FPE", 2, data.TrajectoryDataset2DForce,
+                lambda n, dev: unet.PermInvUNet_attn_NC(1, 2, 1, 5, (n, n)), 5e-4, 4, 5, "result_unet", True),
+            "1d_FPE": Experiment("1d_FPE", 1, data.TrajectoryDataset1D,
+                                 lambda n, dev: unet.PermInvUNet_attn1D_bag(1, 2, 1, 5, n, device=dev), 1e-3, 32,
+                                 10, "results_unet_bag", True, all4),
+            "1d_GPE": Experiment("1d_GPE", 1, data.ParameterDataset,
+                                 lambda n, dev: unet.PermInvUNet_attn1D_bag_GPE(1, 2, 1, 4, n, device=dev,
+                                                                                width=20, modes=40),
+                                 1e-3, 32, 10, "results_GPE_unet", False),
+        }
 
     def nio2d(heads):
         return lambda n, dev: nio.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2, heads=heads,
@@ -257,9 +278,10 @@ class Trainer:
 
 
 def main(argv=None):
-    exps = _experiments()
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    ap.add_argument("--experiment", choices=sorted(exps), default="2d_FPE")
+    ap.add_argument("--experiment", choices=sorted(_experiments()), default="2d_FPE")
+    ap.add_argument("--model", choices=["fno", "unet"], default="fno",
+                    help="fno: train_fno*.py (NIO-FNO); unet: train_unet*.py (attention UNet)")
     ap.add_argument("--data", required=True, help="the experiment's dataset file (npz, or the GPE .npy dict)")
     ap.add_argument("--outdir", default=None, help="result directory (default: the reference's)")
     ap.add_argument("--epochs", type=int, default=400)
@@ -276,7 +298,7 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
-    exp = exps[a.experiment]
+    exp = _experiments(a.model)[a.experiment]
     t = Trainer(exp, a.data, a.outdir or exp.result_dir, torch.device("cuda", local), epochs=a.epochs,
                 seed=a.seed, split_seed=a.split_seed, scheduler_mode=a.scheduler_mode,
                 eval_mode=a.eval_mode, save_interval=a.save_interval, batch=a.batch, lr=a.lr,

@@ -187,7 +187,7 @@ class ConvTFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             E = Ci * Co * KH * KW + Co
             dwb = _e(E, like=dy)
-            part = _e(N * E, like=dy) if N > 1 else None
+            part = _e(query("blindno_convt_wgrad_nparts", N, Hi, Wi) * E, like=dy)
             call("blindno_convt_bwd_weight", ptr(dy), ptr(x), ptr(dwb), ptr(part), *g, stream_ptr())
             dw = dwb[:E - Co].view(w.shape)
             db = dwb[E - Co:]

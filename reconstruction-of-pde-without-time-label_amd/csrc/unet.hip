@@ -490,30 +490,36 @@ __global__ __launch_bounds__(kBlock) void convt_bwd_data_kernel(
   dx[e] = acc;
 }
 
-// partial[n][Ci Co KH KW + Co]: sample n's share of dW (input pixels x tap outputs) and db
-// (every output pixel, output_padding included)
+// partial[n S + s][Ci Co KH KW + Co]: dW over input-pixel chunk s of sample n (flattened
+// input pixels [s Q, (s+1) Q), their KH x KW output taps) and db over output-pixel chunk s
+// (flattened output pixels, output_padding included); S chunks per sample.
+constexpr int kConvtChunk = 64;
 __global__ __launch_bounds__(kBlock) void convt_wgrad_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ partial,
-    int Ci, int Hi, int Wi, int Co, int KH, int KW, int Ho, int Wo) {
-  const int n = blockIdx.x;
+    int Ci, int Hi, int Wi, int Co, int KH, int KW, int Ho, int Wo, int S) {
+  const int s = blockIdx.x, n = blockIdx.y;
   const int T = KH * KW;
   const int EW = Ci * Co * T, E = EW + Co;
-  const float* xs = x + (int64_t)n * Ci * Hi * Wi;
-  const float* gs = dy + (int64_t)n * Co * Ho * Wo;
-  float* out = partial + (int64_t)n * E;
-  for (int e = blockIdx.y * blockDim.x + threadIdx.x; e < E; e += gridDim.y * blockDim.x) {
+  const int HWi = Hi * Wi, HWo = Ho * Wo;
+  const int q0 = s * kConvtChunk, q1 = min(HWi, q0 + kConvtChunk);
+  const int o0 = (int)((int64_t)s * HWo / S), o1 = (int)((int64_t)(s + 1) * HWo / S);
+  const float* xs = x + (int64_t)n * Ci * HWi;
+  const float* gs = dy + (int64_t)n * Co * HWo;
+  float* out = partial + ((int64_t)n * S + s) * E;
+  for (int e = blockIdx.z * blockDim.x + threadIdx.x; e < E; e += gridDim.z * blockDim.x) {
     float acc = 0.f;
     if (e < EW) {
       const int t = e % T, co = (e / T) % Co, ci = e / (T * Co);
       const int a = t / KW, bb = t - (t / KW) * KW;
-      const float* xp = xs + (int64_t)ci * Hi * Wi;
-      const float* gp = gs + (int64_t)co * Ho * Wo;
-      for (int hi = 0; hi < Hi; ++hi)
-        for (int wi = 0; wi < Wi; ++wi)
-          acc = fmaf(xp[hi * Wi + wi], gp[(int64_t)(hi * KH + a) * Wo + wi * KW + bb], acc);
+      const float* xp = xs + (int64_t)ci * HWi;
+      const float* gp = gs + (int64_t)co * HWo + (int64_t)a * Wo + bb;
+      for (int q = q0; q < q1; ++q) {
+        const int hi = q / Wi, wi = q - hi * Wi;
+        acc = fmaf(xp[q], gp[(int64_t)hi * KH * Wo + wi * KW], acc);
+      }
     } else {
-      const float* gp = gs + (int64_t)(e - EW) * Ho * Wo;
-      for (int q = 0; q < Ho * Wo; ++q) acc += gp[q];
+      const float* gp = gs + (int64_t)(e - EW) * HWo;
+      for (int o = o0; o < o1; ++o) acc += gp[o];
     }
     out[e] = acc;
   }
@@ -533,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void tok_mean_kernel(const float* __restric
 
 constexpr int kGramPts = 32;     // points per LDS sub-tile
 constexpr int kMaxTok = 480;     // tokens per bag: the Gram kernel's LDS tile (L x 33 floats) <= 64 KiB
-constexpr int kGramChunk = 512;  // points per workgroup (one partial)
+constexpr int kGramChunk = 128;  // points per workgroup (one partial): D = 3721 -> 30 chunks
 
 // partial[chunk][b][L][L]: the chunk's share of the centred Gram matrix; each thread owns 4 x 4
 // blocks of the upper block triangle (blockIdx.y = round of 256 blocks) and mirrors them.
@@ -595,72 +601,80 @@ __global__ __launch_bounds__(kBlock) void tok_gram_kernel(const float* __restric
     }
 }
 
-// Forward bag algebra, one workgroup per bag.  In: Gc[b] (L x L), xbar[b] (L).  Out: A[b]
-// (softmax, L x L), P[b] = M Gc (L x L), st[b][l] = (mu_l, r_l, c_l, 0), kap[b].
-__global__ __launch_bounds__(kBlock) void tok_stats_kernel(const float* __restrict__ Gc,
-                                                           const float* __restrict__ xbar,
-                                                           float* __restrict__ A,
-                                                           float* __restrict__ Pm,
-                                                           float4* __restrict__ st,
-                                                           float* __restrict__ kap, int L,
-                                                           int64_t D, float eps) {
-  __shared__ float red[8];
-  const int b = blockIdx.x;
+// Forward bag algebra, one workgroup per (token row l, bag b) -- B L workgroups, every row's
+// L^2 work spread over the workgroup's threads.  In: Gc[b] (L x L), xbar[b] (L).  Out: row l of
+// A[b] = softmax((Gc + D xbar xbar^T) / sqrt D), row l of P[b] = M Gc (M = A + I), and
+// st[b][l] = (mu_l, r_l, ., .) with mu_l = sum_s M_ls xbar_s, var_l = (1/D) sum_s P_ls M_ls.
+constexpr int kRowThreads = 128;
+__global__ __launch_bounds__(kRowThreads) void tok_rows_kernel(const float* __restrict__ Gc,
+                                                               const float* __restrict__ xbar,
+                                                               float* __restrict__ A,
+                                                               float* __restrict__ Pm,
+                                                               float4* __restrict__ st, int L,
+                                                               int64_t D, float eps) {
+  __shared__ float red[4];
+  __shared__ float arow[kMaxTok];
+  const int l = blockIdx.x, b = blockIdx.y;
   const float* G = Gc + (int64_t)b * L * L;
   const float* xb = xbar + (int64_t)b * L;
-  float* Ab = A + (int64_t)b * L * L;
-  float* Pb = Pm + (int64_t)b * L * L;
   const float Df = (float)D, isd = 1.0f / sqrtf(Df);
-  // softmax rows of S = (Gc + D xbar xbar^T) / sqrt D
-  for (int l = 0; l < L; ++l) {
-    float mx = -INFINITY;
-    for (int t = threadIdx.x; t < L; t += blockDim.x) {
-      const float s = (G[(int64_t)l * L + t] + Df * xb[l] * xb[t]) * isd;
-      Ab[(int64_t)l * L + t] = s;
-      mx = fmaxf(mx, s);
-    }
-    const float m = block_max(mx, red);
-    float sum = 0.f;
-    for (int t = threadIdx.x; t < L; t += blockDim.x) {
-      const float e = __expf(Ab[(int64_t)l * L + t] - m);
-      Ab[(int64_t)l * L + t] = e;
-      sum += e;
-    }
-    sum = block_sum(sum, red);
-    const float inv = 1.0f / sum;
-    for (int t = threadIdx.x; t < L; t += blockDim.x) Ab[(int64_t)l * L + t] *= inv;
-    __syncthreads();
+  const float xl = xb[l];
+  float mx = -INFINITY;
+  for (int t = threadIdx.x; t < L; t += blockDim.x) {
+    const float sc = (G[(int64_t)l * L + t] + Df * xl * xb[t]) * isd;
+    arow[t] = sc;
+    mx = fmaxf(mx, sc);
   }
-  // P = M Gc (M = A + I), mu_l, var_l = (1/D) sum_s P_ls M_ls
-  __shared__ float sr[kMaxTok], smu[kMaxTok];
-  for (int l = 0; l < L; ++l) {
-    float q = 0.f, mu = 0.f;
-    for (int s = threadIdx.x; s < L; s += blockDim.x) {
-      float p = G[(int64_t)l * L + s];
-      for (int t = 0; t < L; ++t) p = fmaf(Ab[(int64_t)l * L + t], G[(int64_t)t * L + s], p);
-      Pb[(int64_t)l * L + s] = p;
-      const float m = Ab[(int64_t)l * L + s] + (s == l ? 1.f : 0.f);
-      q = fmaf(p, m, q);
-      mu = fmaf(m, xb[s], mu);
-    }
-    q = block_sum(q, red);
-    mu = block_sum(mu, red);
-    if (threadIdx.x == 0) {
-      const float var = fmaxf(q / Df, 0.f);
-      sr[l] = 1.0f / sqrtf(var + eps);
-      smu[l] = mu;
-    }
-    __syncthreads();
+  const float m = block_max(mx, red);
+  float sum = 0.f;
+  for (int t = threadIdx.x; t < L; t += blockDim.x) {
+    const float e = __expf(arow[t] - m);
+    arow[t] = e;
+    sum += e;
   }
-  // c_t = (1/L) sum_l r_l M_lt,  kappa = (1/L) sum_l r_l mu_l
+  const float inv = 1.0f / block_sum(sum, red);
+  for (int t = threadIdx.x; t < L; t += blockDim.x) {
+    arow[t] *= inv;
+    A[((int64_t)b * L + l) * L + t] = arow[t];
+  }
+  __syncthreads();
+  // P_ls = Gc_ls + sum_t A_lt Gc_ts (Gc rows coalesced over s), q = sum_s P_ls M_ls, mu
+  float q = 0.f, mu = 0.f;
+  for (int s2 = threadIdx.x; s2 < L; s2 += blockDim.x) {
+    float p = G[(int64_t)l * L + s2];
+    for (int t = 0; t < L; ++t) p = fmaf(arow[t], G[(int64_t)t * L + s2], p);
+    Pm[((int64_t)b * L + l) * L + s2] = p;
+    const float mls = arow[s2] + (s2 == l ? 1.f : 0.f);
+    q = fmaf(p, mls, q);
+    mu = fmaf(mls, xb[s2], mu);
+  }
+  q = block_sum(q, red);
+  mu = block_sum(mu, red);
+  if (threadIdx.x == 0) {
+    const float var = fmaxf(q / Df, 0.f);
+    st[(int64_t)b * L + l] = make_float4(mu, 1.0f / sqrtf(var + eps), 0.f, 0.f);
+  }
+}
+
+// c_t = (1/L) sum_l r_l M_lt (into st[b][t].z) and kappa_b = (1/L) sum_l r_l mu_l; one
+// workgroup per bag, thread = token t (A rows coalesced over t)
+__global__ __launch_bounds__(kBlock) void tok_coef_kernel(const float* __restrict__ A,
+                                                          float4* __restrict__ st,
+                                                          float* __restrict__ kap, int L) {
+  __shared__ float red[8];
+  __shared__ float sr[kMaxTok];
+  const int b = blockIdx.x;
+  for (int l = threadIdx.x; l < L; l += blockDim.x) sr[l] = st[(int64_t)b * L + l].y;
+  __syncthreads();
   const float iL = 1.0f / (float)L;
+  const float* Ab = A + (int64_t)b * L * L;
   for (int t = threadIdx.x; t < L; t += blockDim.x) {
     float c = sr[t];
     for (int l = 0; l < L; ++l) c = fmaf(sr[l], Ab[(int64_t)l * L + t], c);
-    st[(int64_t)b * L + t] = make_float4(smu[t], sr[t], c * iL, 0.f);
+    st[(int64_t)b * L + t].z = c * iL;
   }
   float k = 0.f;
-  for (int l = threadIdx.x; l < L; l += blockDim.x) k = fmaf(sr[l], smu[l], k);
+  for (int l = threadIdx.x; l < L; l += blockDim.x) k = fmaf(sr[l], st[(int64_t)b * L + l].x, k);
   k = block_sum(k, red);
   if (threadIdx.x == 0) kap[b] = k * iL;
 }
@@ -732,75 +746,66 @@ __global__ __launch_bounds__(kBlock) void tok_ln_wgrad_kernel(const float* __res
   if (dlb) dlb[d] = c;
 }
 
-// Backward bag algebra, one workgroup per bag: R[b] (L x L) and coef[b][t] = (a_t, k_t) with
-// dX_t = a_t g + sum_s R_ts X_s + k_t.  Scratch W[b] (L x L) holds dS, then N.
-__global__ __launch_bounds__(kBlock) void tok_bwd_stats_kernel(
+// Backward bag algebra, two row-parallel passes (B L workgroups each).
+// Pass 1, workgroup (l, b): a_l = r_l / L, b_l = a_l r_l^2 (sum_t M_lt h_t) / D, the row
+// dA_l. = a_l h - b_l P_l. and the softmax backward dS_l. = A_l. o (dA_l. - A_l..dA_l.), written
+// to W[b]; ab[b][l] = (a_l, b_l).
+__global__ __launch_bounds__(kRowThreads) void tok_bwd_rows_kernel(
     const float* __restrict__ A, const float* __restrict__ Pm, const float4* __restrict__ st,
-    const float* __restrict__ xbar, const float* __restrict__ h, const float* __restrict__ gbar,
-    float* __restrict__ R, float* __restrict__ Wk, float2* __restrict__ coef, int L, int64_t D) {
-  __shared__ float red[8];
-  __shared__ float sa[kMaxTok], sbt[kMaxTok], sh[kMaxTok], sx[kMaxTok];
-  const int b = blockIdx.x;
+    const float* __restrict__ h, float* __restrict__ Wk, float2* __restrict__ ab, int L,
+    int64_t D) {
+  __shared__ float red[4];
+  const int l = blockIdx.x, b = blockIdx.y;
+  const float* Arow = A + ((int64_t)b * L + l) * L;
+  const float* Prow = Pm + ((int64_t)b * L + l) * L;
+  const float* hb = h + (int64_t)b * L;
+  const float Df = (float)D;
+  const float r = st[(int64_t)b * L + l].y;
+  float go = 0.f;
+  for (int t = threadIdx.x; t < L; t += blockDim.x) go = fmaf(Arow[t] + (t == l ? 1.f : 0.f), hb[t], go);
+  go = block_sum(go, red);
+  const float al = r / (float)L;
+  const float bl = al * r * r * go / Df;
+  float dot = 0.f;
+  for (int t = threadIdx.x; t < L; t += blockDim.x)
+    dot = fmaf(Arow[t], al * hb[t] - bl * Prow[t], dot);
+  dot = block_sum(dot, red);
+  float* Wrow = Wk + ((int64_t)b * L + l) * L;
+  for (int t = threadIdx.x; t < L; t += blockDim.x)
+    Wrow[t] = Arow[t] * (al * hb[t] - bl * Prow[t] - dot);
+  if (threadIdx.x == 0) ab[(int64_t)b * L + l] = make_float2(al, bl);
+}
+
+// Pass 2, workgroup (t, b): row t of R = (dS + dS^T)/sqrt D - N, N_ts = sum_l M_lt b_l M_ls, and
+// coef[b][t] = (a_t, k_t): a_t = sum_l M_lt alpha_l, k_t = sum_s Q_ts xbar_s - a_t gb.
+__global__ __launch_bounds__(kRowThreads) void tok_bwd_rrow_kernel(
+    const float* __restrict__ A, const float* __restrict__ Wk, const float2* __restrict__ ab,
+    const float* __restrict__ xbar, const float* __restrict__ gbar, float* __restrict__ R,
+    float2* __restrict__ coef, int L, int64_t D) {
+  __shared__ float red[4];
+  __shared__ float mcol[kMaxTok];
+  const int t = blockIdx.x, b = blockIdx.y;
   const float* Ab = A + (int64_t)b * L * L;
-  const float* Pb = Pm + (int64_t)b * L * L;
-  float* Rb = R + (int64_t)b * L * L;
-  float* Wb = Wk + (int64_t)b * L * L;
-  const float Df = (float)D, isd = 1.0f / sqrtf(Df), iL = 1.0f / (float)L;
-  const float gb = gbar[b];
-  for (int t = threadIdx.x; t < L; t += blockDim.x) {
-    sh[t] = h[(int64_t)b * L + t];
-    sx[t] = xbar[(int64_t)b * L + t];
-  }
-  __syncthreads();
-  // alpha_l = r_l / L, beta_l = alpha_l r_l^2 (sum_t M_lt h_t) / D  (h centred)
+  const float* Wb = Wk + (int64_t)b * L * L;
+  const float isd = 1.0f / sqrtf((float)D);
+  float a = 0.f;
   for (int l = threadIdx.x; l < L; l += blockDim.x) {
-    const float4 s4 = st[(int64_t)b * L + l];
-    float go = sh[l];
-    for (int t = 0; t < L; ++t) go = fmaf(Ab[(int64_t)l * L + t], sh[t], go);
-    const float al = s4.y * iL;
-    sa[l] = al;
-    sbt[l] = al * s4.y * s4.y * go / Df;
+    const float2 abl = ab[(int64_t)b * L + l];
+    const float mlt = Ab[(int64_t)l * L + t] + (l == t ? 1.f : 0.f);
+    mcol[l] = mlt * abl.y;                       // M_lt b_l
+    a = fmaf(mlt, abl.x, a);
   }
-  __syncthreads();
-  // dA_lt and softmax backward: dS_lt = A_lt (dA_lt - sum_s A_ls dA_ls)
-  for (int l = 0; l < L; ++l) {
-    float dot = 0.f;
-    for (int t = threadIdx.x; t < L; t += blockDim.x) {
-      const float da = sa[l] * sh[t] - sbt[l] * Pb[(int64_t)l * L + t];
-      Wb[(int64_t)l * L + t] = da;
-      dot = fmaf(Ab[(int64_t)l * L + t], da, dot);
-    }
-    dot = block_sum(dot, red);
-    for (int t = threadIdx.x; t < L; t += blockDim.x) {
-      const float a = Ab[(int64_t)l * L + t];
-      Wb[(int64_t)l * L + t] = a * (Wb[(int64_t)l * L + t] - dot);
-    }
-    __syncthreads();
-  }
-  // R = (dS + dS^T) / sqrt D - N,  N_ts = sum_l M_lt b_l M_ls
-  for (int e = threadIdx.x; e < L * L; e += blockDim.x) {
-    const int t = e / L, s = e % L;
+  a = block_sum(a, red);                          // (the reduction's barriers publish mcol)
+  float k = 0.f;
+  for (int s2 = threadIdx.x; s2 < L; s2 += blockDim.x) {
     float n = 0.f;
-    for (int l = 0; l < L; ++l) {
-      const float mlt = Ab[(int64_t)l * L + t] + (l == t ? 1.f : 0.f);
-      const float mls = Ab[(int64_t)l * L + s] + (l == s ? 1.f : 0.f);
-      n = fmaf(mlt * sbt[l], mls, n);
-    }
-    Rb[e] = (Wb[(int64_t)t * L + s] + Wb[(int64_t)s * L + t]) * isd - n;
+    for (int l = 0; l < L; ++l) n = fmaf(mcol[l], Ab[(int64_t)l * L + s2] + (l == s2 ? 1.f : 0.f), n);
+    const float qv = (Wb[(int64_t)t * L + s2] + Wb[(int64_t)s2 * L + t]) * isd;
+    R[((int64_t)b * L + t) * L + s2] = qv - n;
+    k = fmaf(qv, xbar[(int64_t)b * L + s2], k);
   }
-  __syncthreads();
-  // a_t = sum_l M_lt alpha_l,  k_t = sum_s Q_ts xbar_s - a_t gb  (dX is formed from centred
-  // tokens: sum_s R_ts X_s + sum_s N_ts xbar_s = sum_s R_ts (X_s - xbar_s) + sum_s Q_ts xbar_s)
-  for (int t = threadIdx.x; t < L; t += blockDim.x) {
-    float a = sa[t];
-    for (int l = 0; l < L; ++l) a = fmaf(Ab[(int64_t)l * L + t], sa[l], a);
-    float k = 0.f;
-    for (int s = 0; s < L; ++s) {
-      const float q = (Wb[(int64_t)t * L + s] + Wb[(int64_t)s * L + t]) * isd;
-      k = fmaf(q, sx[s], k);
-    }
-    coef[(int64_t)b * L + t] = make_float2(a, k - a * gb);
-  }
+  k = block_sum(k, red);
+  if (threadIdx.x == 0) coef[(int64_t)b * L + t] = make_float2(a, k - a * gbar[b]);
 }
 
 // dX[b][t][d] = a_t gamma[d] dY[b][d] + sum_s R_ts (X_s[d] - xbar_s) + k_t; a thread owns kTT
@@ -864,9 +869,10 @@ BLINDNO_API int blindno_dwconv_bwd_data(const float* dy, const float* w, float* 
 }
 
 BLINDNO_API int blindno_dwconv_wgrad_nsplit(int N, int C, int H, int W) {
+  // ~1024 output pixels per workgroup (4 per thread), so even a 1-channel level fills the chip
   const int64_t P = (int64_t)N * H * W;
-  int64_t s = (P + 8191) / 8192;
-  return (int)(s < 1 ? 1 : (s > 256 ? 256 : s));
+  int64_t s = (P + 1023) / 1024;
+  return (int)(s < 1 ? 1 : (s > 2048 ? 2048 : s));
 }
 
 BLINDNO_API int blindno_dwconv_bwd_weight(const float* dy, const float* x, float* dwb,
@@ -969,19 +975,25 @@ BLINDNO_API int blindno_convt_bwd_data(const float* dy, const float* w, float* d
   return (int)hipGetLastError();
 }
 
-// dwb = [dW (Ci Co KH KW) | db (Co)]; partial: N x (Ci Co KH KW + Co) floats (N > 1)
+// dwb = [dW (Ci Co KH KW) | db (Co)]; partial: blindno_convt_wgrad_nparts(N, Hi, Wi) x
+// (Ci Co KH KW + Co) floats
+BLINDNO_API int blindno_convt_wgrad_nparts(int N, int Hi, int Wi) {
+  return N * ((Hi * Wi + kConvtChunk - 1) / kConvtChunk);
+}
+
 BLINDNO_API int blindno_convt_bwd_weight(const float* dy, const float* x, float* dwb,
                                          float* partial, int N, int Ci, int Hi, int Wi, int Co,
                                          int KH, int KW, int Ho, int Wo, void* stream) {
-  if (N < 1 || Ci < 1 || Co < 1 || (N > 1 && !partial)) return (int)hipErrorInvalidValue;
+  if (N < 1 || Ci < 1 || Co < 1 || !partial) return (int)hipErrorInvalidValue;
   const int E = Ci * Co * KH * KW + Co;
-  int gy = (E + kBlock - 1) / kBlock;
-  if (gy > 64) gy = 64;
+  const int S = (Hi * Wi + kConvtChunk - 1) / kConvtChunk;
+  int gz = (E + kBlock - 1) / kBlock;
+  if (gz > 16) gz = 16;
   hipStream_t st = (hipStream_t)stream;
-  convt_wgrad_kernel<<<dim3(N, gy), kBlock, 0, st>>>(dy, x, N > 1 ? partial : dwb, Ci, Hi, Wi, Co, KH,
-                                                     KW, Ho, Wo);
-  if (N > 1) return blindno_reduce_partials(partial, dwb, N, E, stream);
-  return (int)hipGetLastError();
+  convt_wgrad_kernel<<<dim3(S, N, gz), kBlock, 0, st>>>(dy, x, partial, Ci, Hi, Wi, Co, KH, KW, Ho, Wo, S);
+  const int err = (int)hipGetLastError();
+  if (err) return err;
+  return blindno_reduce_partials(partial, dwb, N * S, E, stream);
 }
 
 BLINDNO_API int blindno_tok_gram_nchunk(int64_t D) {
@@ -1021,16 +1033,18 @@ BLINDNO_API int blindno_tok_attn_fwd(const float* X, const float* lw, const floa
     err = blindno_reduce_partials(gram_partial, gram, nch, (int)BLL, stream);
     if (err) return err;
   }
-  tok_stats_kernel<<<B, kBlock, 0, st>>>(gram, xbar, A, Pm, stt, kap, L, D, eps);
+  tok_rows_kernel<<<dim3(L, B), kRowThreads, 0, st>>>(gram, xbar, A, Pm, stt, L, D, eps);
+  tok_coef_kernel<<<B, kBlock, 0, st>>>(A, stt, kap, L);
   tok_out_kernel<<<dim3((unsigned)((D + kBlock - 1) / kBlock), B), kBlock, 0, st>>>(X, stt, xbar, lw, lb,
                                                                                    Y, U, L, D);
   return (int)hipGetLastError();
 }
 
 // Backward scratch (floats; 8-B aligned base): coef (2 B L) | h (B L) | gbar (B) | R (B L L) |
-// W (B L L)
+// W (B L L) | [pad to 8 B] | ab (2 B L)
 BLINDNO_API int64_t blindno_tok_attn_bwd_scratch_floats(int B, int L) {
-  return 2 * (int64_t)B * L + (int64_t)B * L + B + 2 * (int64_t)B * L * L;
+  const int64_t BL = (int64_t)B * L;
+  return 2 * BL + BL + B + 2 * BL * L + 1 + 2 * BL;
 }
 
 BLINDNO_API int blindno_tok_attn_bwd(const float* dY, const float* X, const float* lw,
@@ -1055,7 +1069,9 @@ BLINDNO_API int blindno_tok_attn_bwd(const float* dY, const float* X, const floa
     tok_ln_wgrad_kernel<<<(unsigned)((D + kBlock - 1) / kBlock), kBlock, 0, st>>>(dY, U, dlw, dlb, B, D);
   if (dX) {
     tok_bwd_dot_kernel<<<(unsigned)BL, kBlock, 0, st>>>(X, xbar, dY, lw, h, gb, L, D);
-    tok_bwd_stats_kernel<<<B, kBlock, 0, st>>>(A, Pm, stt, xbar, h, gb, R, Wk, coef, L, D);
+    float2* abv = reinterpret_cast<float2*>(h + BL + B + 2 * BLL + ((BL + B) & 1));
+    tok_bwd_rows_kernel<<<dim3(L, B), kRowThreads, 0, st>>>(A, Pm, stt, h, Wk, abv, L, D);
+    tok_bwd_rrow_kernel<<<dim3(L, B), kRowThreads, 0, st>>>(A, Wk, abv, xbar, gb, R, coef, L, D);
     tok_bwd_dx_kernel<<<dim3((unsigned)((D + kBlock - 1) / kBlock), (L + kTT - 1) / kTT, B), kBlock, 0,
                         st>>>(X, xbar, R, coef, lw, dY, dX, L, D);
   }

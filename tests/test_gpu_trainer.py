@@ -73,3 +73,21 @@ def test_trainer_1d_gpe(tmp_path):
     assert len(t.train_idx) == 9 and len(hist["train_losses"]) == 2 and len(hist["test_losses"]) == 1
     assert sorted(os.listdir(out)) == sorted([f"model_checkpoint_best_{hist['test_losses'][0]:.6f}.pt",
                                               "test_losses.npy", "train_losses.npy"])
+
+
+def test_trainer_unet_2d(tmp_path):
+    """train_unet.py's loop (2d_FPE/train_unet.py:124-200) on the attention UNet through the
+    native trainer: graphed epochs, the two-channel metric, best checkpoint in result_unet."""
+    from blindno import trainer
+    data = str(tmp_path / "ds.npz")
+    _npz_2d(data, M=10, T=60, N=52)
+    out = str(tmp_path / "result_unet")
+    exp = trainer._experiments("unet")["2d_FPE"]
+    t = trainer.Trainer(exp, data, out, torch.device("cuda"), epochs=2, save_interval=1, log=lambda s: None)
+    hist = t.fit()
+    assert len(hist["train_losses"]) == 2 and all(np.isfinite(hist["train_losses"]))
+    ckpts = [f for f in os.listdir(out) if f.startswith("model_checkpoint_best_")]
+    assert ckpts == [f"model_checkpoint_best_{min(hist['test_losses']):.6f}.pt"]
+    sd = torch.load(os.path.join(out, ckpts[0]), weights_only=True)
+    m = exp.model(52, "cuda")
+    m.load_state_dict(sd)
