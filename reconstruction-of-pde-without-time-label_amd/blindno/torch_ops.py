@@ -11,6 +11,12 @@ functions) and the dispatcher, with autograd formulas registered through torch.l
     conv2d(x, w, b, stride, padding)                  the NIO encoders' nn.Conv2d, Baselines.py:40-52
     mse_loss(pred, target)                            nn.MSELoss, 2d_FPE/train_fno.py:116,142
     time_averaged_relative_l2(pt_pred, pt_ref)        2d_Non_conservative_FPE/compute_time_error.py:321-333
+  attention UNet ("BlinDNO"; blindno.unet):
+    depthwise_conv(x, w, b)                           ConvNeXtBlock.dwconv, 2d_FPE/NIOModules.py:1047
+    convnext_pointwise(xd, sc, lw, lb, w1, b1, w2, b2)  LN -> Linear -> GELU -> Linear -> + x, :1053-1062
+    max_pool(x, kh, kw) -> (y, arg)                   MaxPool2d(2) / MaxPool1d(2), :1115
+    conv_transpose(x, w, b, Ho, Wo)                   ConvTranspose2d(k = s = 2, output_padding), :1130-1134
+    temporal_attention_mean(X, lw, lb, eps) -> (Y, state)  TemporalSelfAttention + bag mean, :1065-1083
 
 Every operator runs only libblindno kernels (the same launch sequences as blindno.ops' autograd
 Functions, which the models use on their fast path).  The spectral operators also return the
@@ -454,5 +460,189 @@ def _(pt_pred, pt_ref):
     return pt_pred.new_empty((), dtype=torch.float64)
 
 
+# ---------------------------------------------------------------------------- attention UNet
+def _unet():
+    from . import unet
+    return unet
+
+
+@custom_op("blindno::depthwise_conv", mutates_args=())
+def depthwise_conv(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return _unet().dwconv_fwd(x, w, b)
+
+
+@depthwise_conv.register_fake
+def _(x, w, b):
+    return torch.empty_like(x)
+
+
+@custom_op("blindno::depthwise_conv_backward", mutates_args=())
+def depthwise_conv_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> List[torch.Tensor]:
+    return list(_unet().dwconv_bwd(dy, x, w))
+
+
+@depthwise_conv_backward.register_fake
+def _(dy, x, w):
+    return [torch.empty_like(x), torch.empty_like(w), w.new_empty(w.shape[0])]
+
+
+def _dw_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[0], inputs[1])
+
+
+def _dw_grad(ctx, gy):
+    x, w = ctx.saved_tensors
+    dx, dw, db = torch.ops.blindno.depthwise_conv_backward(gy, x, w)
+    return dx, dw, db
+
+
+depthwise_conv.register_autograd(_dw_grad, setup_context=_dw_setup)
+
+
+@custom_op("blindno::convnext_pointwise", mutates_args=())
+def convnext_pointwise(xd: torch.Tensor, sc: torch.Tensor, lw: torch.Tensor, lb: torch.Tensor, w1: torch.Tensor,
+                       b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor) -> torch.Tensor:
+    return _unet().cnx_pw_fwd(xd, sc, lw, lb, w1, b1, w2, b2)
+
+
+@convnext_pointwise.register_fake
+def _(xd, sc, lw, lb, w1, b1, w2, b2):
+    return torch.empty_like(xd)
+
+
+@custom_op("blindno::convnext_pointwise_backward", mutates_args=())
+def convnext_pointwise_backward(dy: torch.Tensor, xd: torch.Tensor, lw: torch.Tensor, lb: torch.Tensor,
+                                w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor) -> List[torch.Tensor]:
+    return [t.clone() if t.storage_offset() else t for t in _unet().cnx_pw_bwd(dy, xd, lw, lb, w1, b1, w2)]
+
+
+@convnext_pointwise_backward.register_fake
+def _(dy, xd, lw, lb, w1, b1, w2):
+    C = xd.shape[1]
+    return [torch.empty_like(xd), lw.new_empty(C), lw.new_empty(C), torch.empty_like(w1), b1.new_empty(4 * C),
+            torch.empty_like(w2), lw.new_empty(C)]
+
+
+def _cnx_setup(ctx, inputs, output):
+    xd, sc, lw, lb, w1, b1, w2, b2 = inputs
+    ctx.save_for_backward(xd, lw, lb, w1, b1, w2)
+
+
+def _cnx_grad(ctx, gy):
+    xd, lw, lb, w1, b1, w2 = ctx.saved_tensors
+    dxd, dlw, dlb, dw1, db1, dw2, db2 = torch.ops.blindno.convnext_pointwise_backward(gy, xd, lw, lb, w1, b1, w2)
+    return dxd, gy, dlw, dlb, dw1, db1, dw2, db2
+
+
+convnext_pointwise.register_autograd(_cnx_grad, setup_context=_cnx_setup)
+
+
+@custom_op("blindno::max_pool", mutates_args=())
+def max_pool(x: torch.Tensor, kh: int, kw: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    return _unet().maxpool_fwd(x, kh, kw)
+
+
+@max_pool.register_fake
+def _(x, kh, kw):
+    N, C, H, W = x.shape
+    return x.new_empty(N, C, H // kh, W // kw), x.new_empty(N, C, H // kh, W // kw, dtype=torch.uint8)
+
+
+@custom_op("blindno::max_pool_backward", mutates_args=())
+def max_pool_backward(dy: torch.Tensor, arg: torch.Tensor, H: int, W: int, kh: int, kw: int) -> torch.Tensor:
+    return _unet().maxpool_bwd(dy, arg, H, W, kh, kw)
+
+
+@max_pool_backward.register_fake
+def _(dy, arg, H, W, kh, kw):
+    return dy.new_empty(dy.shape[0], dy.shape[1], H, W)
+
+
+def _mp_setup(ctx, inputs, output):
+    x, kh, kw = inputs
+    ctx.save_for_backward(output[1])
+    ctx.geom = (x.shape[2], x.shape[3], kh, kw)
+
+
+def _mp_grad(ctx, gy, garg):
+    (arg,) = ctx.saved_tensors
+    return torch.ops.blindno.max_pool_backward(gy, arg, *ctx.geom), None, None
+
+
+max_pool.register_autograd(_mp_grad, setup_context=_mp_setup)
+
+
+@custom_op("blindno::conv_transpose", mutates_args=())
+def conv_transpose(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, Ho: int, Wo: int) -> torch.Tensor:
+    return _unet().convt_fwd(x, w, b, Ho, Wo)
+
+
+@conv_transpose.register_fake
+def _(x, w, b, Ho, Wo):
+    return x.new_empty(x.shape[0], w.shape[1], Ho, Wo)
+
+
+@custom_op("blindno::conv_transpose_backward", mutates_args=())
+def conv_transpose_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> List[torch.Tensor]:
+    return [t.clone() if t.storage_offset() else t for t in _unet().convt_bwd(dy, x, w)]
+
+
+@conv_transpose_backward.register_fake
+def _(dy, x, w):
+    return [torch.empty_like(x), torch.empty_like(w), w.new_empty(w.shape[1])]
+
+
+def _ct_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[0], inputs[1])
+
+
+def _ct_grad(ctx, gy):
+    x, w = ctx.saved_tensors
+    dx, dw, db = torch.ops.blindno.conv_transpose_backward(gy, x, w)
+    return dx, dw, db, None, None
+
+
+conv_transpose.register_autograd(_ct_grad, setup_context=_ct_setup)
+
+
+@custom_op("blindno::temporal_attention_mean", mutates_args=())
+def temporal_attention_mean(X: torch.Tensor, lw: torch.Tensor, lb: torch.Tensor,
+                            eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    return _unet().tok_attn_fwd(X, lw, lb, eps)
+
+
+@temporal_attention_mean.register_fake
+def _(X, lw, lb, eps):
+    B, L, D = X.shape
+    n = 4 * B * L + B * L + 2 * B * L * L + B + B * D
+    return X.new_empty(B, D), X.new_empty(n)
+
+
+@custom_op("blindno::temporal_attention_mean_backward", mutates_args=())
+def temporal_attention_mean_backward(dY: torch.Tensor, X: torch.Tensor, lw: torch.Tensor,
+                                     state: torch.Tensor) -> List[torch.Tensor]:
+    return list(_unet().tok_attn_bwd(dY, X, lw, state))
+
+
+@temporal_attention_mean_backward.register_fake
+def _(dY, X, lw, state):
+    return [torch.empty_like(X), torch.empty_like(lw), torch.empty_like(lw)]
+
+
+def _ta_setup(ctx, inputs, output):
+    X, lw, lb, eps = inputs
+    ctx.save_for_backward(X, lw, output[1])
+
+
+def _ta_grad(ctx, gY, gstate):
+    X, lw, state = ctx.saved_tensors
+    dX, dlw, dlb = torch.ops.blindno.temporal_attention_mean_backward(gY, X, lw, state)
+    return dX, dlw, dlb, None
+
+
+temporal_attention_mean.register_autograd(_ta_grad, setup_context=_ta_setup)
+
+
 REGISTERED = ("spectral_conv2d", "spectral_conv1d", "fno2d", "fno1d", "project_mlp", "bag_mean", "conv2d",
-              "mse_loss", "time_averaged_relative_l2")
+              "mse_loss", "time_averaged_relative_l2", "depthwise_conv", "convnext_pointwise", "max_pool",
+              "conv_transpose", "temporal_attention_mean")

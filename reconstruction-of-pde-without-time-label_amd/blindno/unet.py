@@ -50,182 +50,239 @@ def _as4(x):
     return x if x.dim() == 4 else x.unsqueeze(2)
 
 
+# ---------------------------------------------------------------------------- kernel launchers
+# (shared by the autograd Functions below and the torch.ops.blindno.* operators of torch_ops.py)
+
+def dwconv_fwd(x, w, b):
+    """Depthwise KHxKW convolution, padding (KH/2, KW/2), with bias: ConvNeXtBlock.dwconv
+    (2d_FPE/NIOModules.py:1047; 1d_FPE/NIOModules.py:169).  x (N, C, H, W); w (C, 1, KH, KW)."""
+    ops.require_device(x, w)
+    x, w, b = _c(x), _c(w), _c(b)
+    N, C, H, W = x.shape
+    y = torch.empty_like(x)
+    call("blindno_dwconv_fwd", ptr(x), ptr(w), ptr(b), ptr(y), N, C, H, W, w.shape[-2], w.shape[-1], stream_ptr())
+    return y
+
+
+def dwconv_bwd(dy, x, w, need_dx=True, need_w=True):
+    N, C, H, W = x.shape
+    KH, KW = w.shape[-2], w.shape[-1]
+    dy = _c(dy)
+    dx = dw = db = None
+    if need_dx:
+        dx = torch.empty_like(x)
+        call("blindno_dwconv_bwd_data", ptr(dy), ptr(w), ptr(dx), N, C, H, W, KH, KW, stream_ptr())
+    if need_w:
+        ns = query("blindno_dwconv_wgrad_nsplit", N, C, H, W)
+        dwb = _e(C, KH * KW + 1, like=dy)
+        part = _e(ns * C * (KH * KW + 1), like=dy) if ns > 1 else None
+        call("blindno_dwconv_bwd_weight", ptr(dy), ptr(x), ptr(dwb), ptr(part), ns, N, C, H, W, KH, KW,
+             stream_ptr())
+        dw = dwb[:, :-1].reshape(w.shape)
+        db = dwb[:, -1].contiguous()
+    return dx, dw, db
+
+
+def cnx_pw_fwd(xd, sc, lw, lb, w1, b1, w2, b2):
+    """ConvNeXtBlock after the depthwise conv (2d_FPE/NIOModules.py:1053-1062): per pixel
+    LayerNorm(C, eps 1e-6) -> pwconv1 -> exact GELU -> pwconv2 -> + shortcut.  xd, sc (N, C, *S)."""
+    ops.require_device(xd, sc)
+    xd, sc = _c(xd), _c(sc)
+    lw, lb, w1, b1, w2, b2 = (_c(t) for t in (lw, lb, w1, b1, w2, b2))
+    N, C = xd.shape[0], xd.shape[1]
+    HW = xd[0, 0].numel()
+    y = torch.empty_like(xd)
+    call("blindno_cnx_pw_fwd", ptr(xd), ptr(sc), ptr(lw), ptr(lb), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(y),
+         N, C, HW, stream_ptr())
+    return y
+
+
+def cnx_pw_bwd(dy, xd, lw, lb, w1, b1, w2):
+    """-> (dxd, dlw, dlb, dw1, db1, dw2, db2); the shortcut's gradient is dy itself."""
+    N, C = xd.shape[0], xd.shape[1]
+    HW = xd[0, 0].numel()
+    dy = _c(dy)
+    nblk = query("blindno_cnx_pw_bwd_nblk", N, C, HW)
+    E = 8 * C * C + 7 * C
+    dxd = torch.empty_like(xd)
+    dp = _e(E, like=dy)
+    part = _e(nblk * E, like=dy)
+    call("blindno_cnx_pw_bwd", ptr(dy), ptr(_c(xd)), ptr(_c(lw)), ptr(_c(lb)), ptr(_c(w1)), ptr(_c(b1)),
+         ptr(_c(w2)), ptr(dxd), ptr(dp), ptr(part), nblk, N, C, HW, stream_ptr())
+    H4 = 4 * C
+    o = 0
+    dw1 = dp[o:o + H4 * C].view(H4, C); o += H4 * C
+    db1 = dp[o:o + H4]; o += H4
+    dw2 = dp[o:o + C * H4].view(C, H4); o += C * H4
+    db2 = dp[o:o + C]; o += C
+    dlw = dp[o:o + C]; o += C
+    dlb = dp[o:o + C]
+    return dxd, dlw, dlb, dw1, db1, dw2, db2
+
+
+def maxpool_fwd(x, KH, KW):
+    """MaxPool2d(2) / MaxPool1d(2) (2d_FPE/NIOModules.py:1115; 1d_FPE/NIOModules.py:239) on
+    (N, C, H, W) with window (KH, KW) -> (y, arg uint8)."""
+    ops.require_device(x)
+    x = _c(x)
+    N, C, H, W = x.shape
+    Ho, Wo = H // KH, W // KW
+    y = _e(N, C, Ho, Wo, like=x)
+    arg = torch.empty(N, C, Ho, Wo, device=x.device, dtype=torch.uint8)
+    call("blindno_maxpool_fwd", ptr(x), ptr(y), ptr(arg), N * C, H, W, KH, KW, stream_ptr())
+    return y, arg
+
+
+def maxpool_bwd(dy, arg, H, W, KH, KW):
+    N, C = dy.shape[0], dy.shape[1]
+    dy = _c(dy)
+    dx = _e(N, C, H, W, like=dy)
+    call("blindno_maxpool_bwd", ptr(dy), ptr(_c(arg)), ptr(dx), N * C, H, W, KH, KW, stream_ptr())
+    return dx
+
+
+def convt_fwd(x, w, b, Ho, Wo):
+    """ConvTranspose2d(Ci, Co, kernel = stride = 2, output_padding) (2d_FPE/NIOModules.py:
+    1130-1134; 1D: kernel (1, 2)).  x (N, Ci, Hi, Wi), w (Ci, Co, KH, KW) -> (N, Co, Ho, Wo)."""
+    ops.require_device(x, w)
+    x, w, b = _c(x), _c(w), _c(b)
+    N, Ci, Hi, Wi = x.shape
+    Co, KH, KW = w.shape[1], w.shape[2], w.shape[3]
+    y = _e(N, Co, Ho, Wo, like=x)
+    call("blindno_convt_fwd", ptr(x), ptr(w), ptr(b), ptr(y), N, Ci, Hi, Wi, Co, KH, KW, Ho, Wo, stream_ptr())
+    return y
+
+
+def convt_bwd(dy, x, w, need_dx=True, need_w=True):
+    N, Ci, Hi, Wi = x.shape
+    Co, KH, KW = w.shape[1], w.shape[2], w.shape[3]
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    g = (N, Ci, Hi, Wi, Co, KH, KW, Ho, Wo)
+    dy = _c(dy)
+    dx = dw = db = None
+    if need_dx:
+        dx = torch.empty_like(x)
+        call("blindno_convt_bwd_data", ptr(dy), ptr(_c(w)), ptr(dx), *g, stream_ptr())
+    if need_w:
+        E = Ci * Co * KH * KW + Co
+        dwb = _e(E, like=dy)
+        part = _e(query("blindno_convt_wgrad_nparts", N, Hi, Wi) * E, like=dy)
+        call("blindno_convt_bwd_weight", ptr(dy), ptr(_c(x)), ptr(dwb), ptr(part), *g, stream_ptr())
+        dw = dwb[:E - Co].view(w.shape)
+        db = dwb[E - Co:]
+    return dx, dw, db
+
+
+def tok_attn_fwd(X, lw, lb, eps):
+    """TemporalSelfAttention followed by the bag mean (2d_FPE/NIOModules.py:1065-1083 with
+    :1163-1164 / :1171-1172): X (B, L, D) -> (mean_l LayerNorm_D(softmax(X X^T/sqrt D) X + X)_l
+    (B, D), the saved state of the backward)."""
+    ops.require_device(X, lw)
+    X, lw, lb = _c(X), _c(lw), _c(lb)
+    B, L, D = X.shape
+    save = _e(query("blindno_tok_attn_save_floats", B, L, D), like=X)
+    nch = query("blindno_tok_gram_nchunk", D)
+    gram = _e(B * L * L, like=X)
+    gp = _e(nch * B * L * L, like=X) if nch > 1 else None
+    Y = _e(B, D, like=X)
+    call("blindno_tok_attn_fwd", ptr(X), ptr(lw), ptr(lb), ptr(Y), ptr(save), ptr(gp), ptr(gram), B, L, D,
+         float(eps), stream_ptr())
+    return Y, save
+
+
+def tok_attn_bwd(dY, X, lw, save, need_dx=True, need_lw=True, need_lb=True):
+    B, L, D = X.shape
+    dY = _c(dY)
+    dX = torch.empty_like(X) if need_dx else None
+    dlw = _e(D, like=dY) if need_lw else None
+    dlb = _e(D, like=dY) if need_lb else None
+    scratch = _e(query("blindno_tok_attn_bwd_scratch_floats", B, L), like=dY)
+    call("blindno_tok_attn_bwd", ptr(dY), ptr(_c(X)), ptr(_c(lw)), ptr(save), ptr(dX), ptr(dlw), ptr(dlb),
+         ptr(scratch), B, L, D, stream_ptr())
+    return dX, dlw, dlb
+
+
 # ---------------------------------------------------------------------------- autograd ops
 
 class DWConvFn(torch.autograd.Function):
-    """Depthwise KHxKW convolution, padding (KH/2, KW/2), with bias: ConvNeXtBlock.dwconv
-    (2d_FPE/NIOModules.py:1047; 1d_FPE/NIOModules.py:169).  x (N, C, H, W); w (C, 1, KH, KW)."""
+    """``dwconv_fwd`` with its adjoint."""
 
     @staticmethod
     def forward(ctx, x, w, b):
-        ops.require_device(x, w)
-        x, w, b = _c(x), _c(w), _c(b)
-        N, C, H, W = x.shape
-        KH, KW = w.shape[-2], w.shape[-1]
-        y = torch.empty_like(x)
-        call("blindno_dwconv_fwd", ptr(x), ptr(w), ptr(b), ptr(y), N, C, H, W, KH, KW, stream_ptr())
-        ctx.save_for_backward(x, w)
+        y = dwconv_fwd(x, w, b)
+        ctx.save_for_backward(_c(x), _c(w))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        N, C, H, W = x.shape
-        KH, KW = w.shape[-2], w.shape[-1]
-        dy = _c(dy)
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            call("blindno_dwconv_bwd_data", ptr(dy), ptr(w), ptr(dx), N, C, H, W, KH, KW, stream_ptr())
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            ns = query("blindno_dwconv_wgrad_nsplit", N, C, H, W)
-            dwb = _e(C, KH * KW + 1, like=dy)
-            part = _e(ns * C * (KH * KW + 1), like=dy) if ns > 1 else None
-            call("blindno_dwconv_bwd_weight", ptr(dy), ptr(x), ptr(dwb), ptr(part), ns, N, C, H, W,
-                 KH, KW, stream_ptr())
-            dw = dwb[:, :-1].reshape(w.shape) if ctx.needs_input_grad[1] else None
-            db = dwb[:, -1].contiguous() if ctx.needs_input_grad[2] else None
-        return dx, dw, db
+        return dwconv_bwd(dy, x, w, ctx.needs_input_grad[0],
+                          ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
 
 
 class CnxPwFn(torch.autograd.Function):
-    """ConvNeXtBlock after the depthwise conv (2d_FPE/NIOModules.py:1053-1062): per pixel
-    LayerNorm(C, eps 1e-6) -> pwconv1 -> exact GELU -> pwconv2 -> + shortcut, one kernel
-    each way.  xd, sc (N, C, H, W)."""
+    """``cnx_pw_fwd`` with its adjoint (one kernel each way)."""
 
     @staticmethod
     def forward(ctx, xd, sc, lw, lb, w1, b1, w2, b2):
-        ops.require_device(xd, sc)
-        xd, sc = _c(xd), _c(sc)
-        lw, lb, w1, b1, w2, b2 = (_c(t) for t in (lw, lb, w1, b1, w2, b2))
-        N, C = xd.shape[0], xd.shape[1]
-        HW = xd[0, 0].numel()
-        y = torch.empty_like(xd)
-        call("blindno_cnx_pw_fwd", ptr(xd), ptr(sc), ptr(lw), ptr(lb), ptr(w1), ptr(b1), ptr(w2),
-             ptr(b2), ptr(y), N, C, HW, stream_ptr())
-        ctx.save_for_backward(xd, lw, lb, w1, b1, w2)
+        y = cnx_pw_fwd(xd, sc, lw, lb, w1, b1, w2, b2)
+        ctx.save_for_backward(*(_c(t) for t in (xd, lw, lb, w1, b1, w2)))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xd, lw, lb, w1, b1, w2 = ctx.saved_tensors
-        N, C = xd.shape[0], xd.shape[1]
-        HW = xd[0, 0].numel()
-        dy = _c(dy)
-        nblk = query("blindno_cnx_pw_bwd_nblk", N, C, HW)
-        E = 8 * C * C + 7 * C
-        dxd = torch.empty_like(xd)
-        dp = _e(E, like=dy)
-        part = _e(nblk * E, like=dy)
-        call("blindno_cnx_pw_bwd", ptr(dy), ptr(xd), ptr(lw), ptr(lb), ptr(w1), ptr(b1), ptr(w2),
-             ptr(dxd), ptr(dp), ptr(part), nblk, N, C, HW, stream_ptr())
-        H4 = 4 * C
-        o = 0
-        dw1 = dp[o:o + H4 * C].view(H4, C); o += H4 * C
-        db1 = dp[o:o + H4]; o += H4
-        dw2 = dp[o:o + C * H4].view(C, H4); o += C * H4
-        db2 = dp[o:o + C]; o += C
-        dlw = dp[o:o + C]; o += C
-        dlb = dp[o:o + C]
+        dxd, dlw, dlb, dw1, db1, dw2, db2 = cnx_pw_bwd(dy, xd, lw, lb, w1, b1, w2)
         return dxd, dy, dlw, dlb, dw1, db1, dw2, db2
 
 
 class MaxPoolFn(torch.autograd.Function):
-    """MaxPool2d(2) / MaxPool1d(2) (2d_FPE/NIOModules.py:1115; 1d_FPE/NIOModules.py:239) on
-    (N, C, H, W) with window (KH, KW)."""
+    """``maxpool_fwd`` with its adjoint."""
 
     @staticmethod
     def forward(ctx, x, KH, KW):
-        ops.require_device(x)
-        x = _c(x)
-        N, C, H, W = x.shape
-        Ho, Wo = H // KH, W // KW
-        y = _e(N, C, Ho, Wo, like=x)
-        arg = torch.empty(N, C, Ho, Wo, device=x.device, dtype=torch.uint8)
-        call("blindno_maxpool_fwd", ptr(x), ptr(y), ptr(arg), N * C, H, W, KH, KW, stream_ptr())
+        y, arg = maxpool_fwd(x, KH, KW)
         ctx.save_for_backward(arg)
-        ctx.geom = (N, C, H, W, KH, KW)
+        ctx.geom = (x.shape[2], x.shape[3], KH, KW)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (arg,) = ctx.saved_tensors
-        N, C, H, W, KH, KW = ctx.geom
-        dy = _c(dy)
-        dx = _e(N, C, H, W, like=dy)
-        call("blindno_maxpool_bwd", ptr(dy), ptr(arg), ptr(dx), N * C, H, W, KH, KW, stream_ptr())
-        return dx, None, None
+        return maxpool_bwd(dy, arg, *ctx.geom), None, None
 
 
 class ConvTFn(torch.autograd.Function):
-    """ConvTranspose2d(Ci, Co, kernel = stride = 2, output_padding) (2d_FPE/NIOModules.py:
-    1130-1134; 1D: kernel (1, 2)).  x (N, Ci, Hi, Wi), w (Ci, Co, KH, KW) -> (N, Co, Ho, Wo)."""
+    """``convt_fwd`` with its adjoint."""
 
     @staticmethod
     def forward(ctx, x, w, b, Ho, Wo):
-        ops.require_device(x, w)
-        x, w, b = _c(x), _c(w), _c(b)
-        N, Ci, Hi, Wi = x.shape
-        Co, KH, KW = w.shape[1], w.shape[2], w.shape[3]
-        y = _e(N, Co, Ho, Wo, like=x)
-        call("blindno_convt_fwd", ptr(x), ptr(w), ptr(b), ptr(y), N, Ci, Hi, Wi, Co, KH, KW, Ho, Wo,
-             stream_ptr())
-        ctx.save_for_backward(x, w)
-        ctx.geom = (N, Ci, Hi, Wi, Co, KH, KW, Ho, Wo)
+        y = convt_fwd(x, w, b, Ho, Wo)
+        ctx.save_for_backward(_c(x), _c(w))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        g = ctx.geom
-        N, Ci, Hi, Wi, Co, KH, KW, Ho, Wo = g
-        dy = _c(dy)
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            call("blindno_convt_bwd_data", ptr(dy), ptr(w), ptr(dx), *g, stream_ptr())
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            E = Ci * Co * KH * KW + Co
-            dwb = _e(E, like=dy)
-            part = _e(query("blindno_convt_wgrad_nparts", N, Hi, Wi) * E, like=dy)
-            call("blindno_convt_bwd_weight", ptr(dy), ptr(x), ptr(dwb), ptr(part), *g, stream_ptr())
-            dw = dwb[:E - Co].view(w.shape)
-            db = dwb[E - Co:]
+        dx, dw, db = convt_bwd(dy, x, w, ctx.needs_input_grad[0],
+                               ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         return dx, dw, db, None, None
 
 
 class TokAttnMeanFn(torch.autograd.Function):
-    """TemporalSelfAttention followed by the bag mean (2d_FPE/NIOModules.py:1065-1083 with
-    :1163-1164 / :1171-1172): X (B, L, D) -> mean_l LayerNorm_D(softmax(X X^T/sqrt D) X + X)_l,
-    (B, D).  One collapsed HIP op each way (csrc/unet.hip)."""
+    """``tok_attn_fwd`` with its adjoint: one collapsed HIP op each way (csrc/unet.hip)."""
 
     @staticmethod
     def forward(ctx, X, lw, lb, eps):
-        ops.require_device(X, lw)
-        X, lw, lb = _c(X), _c(lw), _c(lb)
-        B, L, D = X.shape
-        nsave = query("blindno_tok_attn_save_floats", B, L, D)
-        save = _e(nsave, like=X)
-        nch = query("blindno_tok_gram_nchunk", D)
-        gram = _e(B * L * L, like=X)
-        gp = _e(nch * B * L * L, like=X) if nch > 1 else None
-        Y = _e(B, D, like=X)
-        call("blindno_tok_attn_fwd", ptr(X), ptr(lw), ptr(lb), ptr(Y), ptr(save), ptr(gp), ptr(gram),
-             B, L, D, float(eps), stream_ptr())
-        ctx.save_for_backward(X, lw, save)
+        Y, save = tok_attn_fwd(X, lw, lb, eps)
+        ctx.save_for_backward(_c(X), _c(lw), save)
         return Y
 
     @staticmethod
     def backward(ctx, dY):
         X, lw, save = ctx.saved_tensors
-        B, L, D = X.shape
-        dY = _c(dY)
-        dX = torch.empty_like(X) if ctx.needs_input_grad[0] else None
-        dlw = _e(D, like=dY) if ctx.needs_input_grad[1] else None
-        dlb = _e(D, like=dY) if ctx.needs_input_grad[2] else None
-        scratch = _e(query("blindno_tok_attn_bwd_scratch_floats", B, L), like=dY)
-        call("blindno_tok_attn_bwd", ptr(dY), ptr(X), ptr(lw), ptr(save), ptr(dX), ptr(dlw), ptr(dlb),
-             ptr(scratch), B, L, D, stream_ptr())
+        n = ctx.needs_input_grad
+        dX, dlw, dlb = tok_attn_bwd(dY, X, lw, save, n[0], n[1], n[2])
         return dX, dlw, dlb, None
 
 

@@ -187,3 +187,41 @@ def test_opcheck():
     torch.library.opcheck(torch.ops.blindno.conv2d, (xc, wc, bc, [2, 2], [1, 1]), test_utils=utils)
     pred = torch.randn(5, 7, device="cuda", requires_grad=True)
     torch.library.opcheck(torch.ops.blindno.mse_loss, (pred, torch.randn(5, 7, device="cuda")), test_utils=utils)
+
+
+def test_unet_ops_match_functions_and_opcheck():
+    """torch.ops.blindno.{depthwise_conv, convnext_pointwise, max_pool, conv_transpose,
+    temporal_attention_mean} give the blindno.unet autograd Functions' values and gradients
+    (the same kernels), and pass torch.library.opcheck (schema, autograd registration, fake)."""
+    from blindno import torch_ops  # noqa: F401
+    from blindno import unet
+    torch.manual_seed(3)
+    utils = ("test_schema", "test_autograd_registration", "test_faketensor")
+
+    def leaf(*shape):
+        return torch.randn(*shape, device="cuda", requires_grad=True)
+
+    cases = [
+        (torch.ops.blindno.depthwise_conv, unet.DWConvFn.apply, (leaf(3, 4, 9, 8), leaf(4, 1, 7, 7), leaf(4))),
+        (torch.ops.blindno.convnext_pointwise, unet.CnxPwFn.apply,
+         (leaf(3, 4, 5, 6), leaf(3, 4, 5, 6), leaf(4), leaf(4), leaf(16, 4), leaf(16), leaf(4, 16), leaf(4))),
+        (torch.ops.blindno.conv_transpose, unet.ConvTFn.apply, (leaf(2, 4, 5, 5), leaf(4, 3, 2, 2), leaf(3), 11, 10)),
+        (torch.ops.blindno.temporal_attention_mean, unet.TokAttnMeanFn.apply,
+         (leaf(2, 9, 40), leaf(40), leaf(40), 1e-5)),
+    ]
+    for op, fn, args in cases:
+        y_op = op(*args)
+        y_op = y_op[0] if isinstance(y_op, tuple) else y_op
+        g = torch.randn_like(y_op)
+        ts = [a for a in args if torch.is_tensor(a)]
+        gr_op = torch.autograd.grad(y_op, ts, g)
+        y_fn = fn(*args)
+        gr_fn = torch.autograd.grad(y_fn, ts, g)
+        assert torch.equal(y_op, y_fn)
+        for a, b in zip(gr_op, gr_fn):
+            assert torch.equal(a, b)
+        torch.library.opcheck(op, args, test_utils=utils)
+    x = leaf(2, 3, 7, 6)
+    y, arg = torch.ops.blindno.max_pool(x, 2, 2)
+    assert torch.equal(y, unet.MaxPoolFn.apply(x, 2, 2))
+    torch.library.opcheck(torch.ops.blindno.max_pool, (x, 2, 2), test_utils=utils)
