@@ -113,6 +113,9 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the GPU-vs-CPU-reference parity leg")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graphs")
+    ap.add_argument("--overlap", default="auto", choices=("auto", "on", "off"),
+                    help="two-graph step with the heads' gradient all-reduce beside the encoder's "
+                         "backward (auto: at N > 1)")
     ap.add_argument("--timer-steps", type=int, default=4,
                     help="eager steps after the timed region that time the dominant kernel (graph mode)")
     return ap.parse_args()
@@ -171,7 +174,8 @@ def main():
     if not a.no_graph and a.config in ("A", "B", "C", "E", "C_attn", "U", "U_NC", "U1"):
         # one HIP graph per bag size L = randint(50, T) (captured here, before the warm-up; the
         # numpy draw below stays the reference's: L and idx are drawn on the host every step)
-        graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc)
+        graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc,
+                                 overlap=None if a.overlap == "auto" else a.overlap == "on")
         torch.index_select(X, 0, order[:B], out=xb)
         torch.index_select(Y, 0, order[:B], out=yb)
         # keys: the bag size L, or with deduplicated bags the number of distinct snapshots
@@ -252,7 +256,10 @@ def main():
                                    + " replacement", "dataset_bags": a.bags,
                        "sharding": "bag i on rank i mod world (bag-keyed synthetic set, same data at any N)",
                        "parallelism": f"dp{world}", "optimizer": f"Adam lr {cfg['lr']} (fused flat)",
-                       "launch": "hip-graph per bag size L (all kernels replayed each step)" if graphed else "eager"},
+                       "launch": ("eager" if not graphed else
+                                  "hip-graph per bag size L (all kernels replayed each step)" +
+                                  ("; two graphs per step, heads' gradient all-reduce overlapped "
+                                   "with the encoder backward" if graphed.overlap else ""))},
         }
         if timer:
             res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS,

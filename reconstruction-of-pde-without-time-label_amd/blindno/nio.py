@@ -138,6 +138,16 @@ class NIOFP2D_FNO(nn.Module):
         Without input gradients the snapshot encoder + bag mean run as the fused HIP path
         (ops.BagEncoderFn: snapshots read from x through the bag's indices); otherwise as the
         generic composition below (same numerics, gradients for x and grid)."""
+        return self.forward_heads(self.forward_encoder(x, grid, bag_idx))
+
+    def forward_heads(self, h):
+        """The two FNO heads on the bag-mean field h (B, Nx, Ny, width) (:577-581)."""
+        return _run_heads(self, h)
+
+    def forward_encoder(self, x, grid, bag_idx=None):
+        """FNO_input on the bag + the fixed-weight bag mean (:548-575) -> h (B, Nx, Ny, width).
+        Split from the heads so a training step can be replayed as two graphs and the heads'
+        gradient all-reduce overlap the encoder's backward (train.GraphedBagStep, overlap)."""
         if self._fused_ok(x, grid):
             fno = self.FNO_input
             lw = None
@@ -158,17 +168,15 @@ class NIOFP2D_FNO(nn.Module):
                 idx_t = torch.as_tensor(idx, device=x.device)
                 if w is not None:
                     lw = torch.as_tensor(w, device=x.device)
-            h = ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, lw, grid, self.fc0.weight.data,
-                                       self.fc0.bias.data, *fno_params(fno, 2))
-            return _run_heads(self, h)
+            return ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, lw, grid, self.fc0.weight.data,
+                                          self.fc0.bias.data, *fno_params(fno, 2))
         x, L, lw = _select(self, x, bag_idx, dedup=True)
         B, _, nx, ny = x.shape
         x_in = x.reshape(B * L, 1, nx, ny)
         grid_r = grid.permute(2, 0, 1).unsqueeze(0).expand(B * L, 2, nx, ny)
         inp = torch.cat((x_in, grid_r), dim=1).permute(0, 2, 3, 1).contiguous()
         u = self.FNO_input(inp)                       # (B*L, nx, ny, 1)
-        h = _bag_mean_2d(self, u, grid, B, L, nx, ny, lw)
-        return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
+        return _bag_mean_2d(self, u, grid, B, L, nx, ny, lw)
 
 
 def draw_bag_distinct(T: int):

@@ -72,23 +72,36 @@ class FlatAdam:
         for p in self.params:
             p.grad = None
 
-    def gather_grads(self):
-        """Copy every parameter's .grad into the flat grad buffer (one multi-tensor copy;
-        alignment pads stay zero)."""
+    def gather_grads(self, subset=None):
+        """Copy every parameter's .grad (or only those of ``subset``, a list of the trained
+        parameters) into the flat grad buffer (one multi-tensor copy; alignment pads stay
+        zero)."""
+        sel = range(len(self.params)) if subset is None else \
+            [i for i, p in enumerate(self.params) if any(p is q for q in subset)]
         gs = []
-        for p in self.params:
+        for i in sel:
+            p = self.params[i]
             if p.grad is None:
                 raise RuntimeError("FlatAdam: a trained parameter received no gradient")
             gs.append(_real(p.grad).reshape(-1))
         if self.grad.is_cuda and all(g.is_contiguous() for g in gs):
             # one blindno_gather_flat launch (segments as kernel arguments; graph-capturable)
             srcs = (ctypes.c_void_p * len(gs))(*[g.data_ptr() for g in gs])
-            offs = (ctypes.c_int64 * len(gs))(*self.offsets)
+            offs = (ctypes.c_int64 * len(gs))(*[self.offsets[i] for i in sel])
             ns = (ctypes.c_int64 * len(gs))(*[g.numel() for g in gs])
             call("blindno_gather_flat", srcs, offs, ns, len(gs), ptr(self.grad), stream_ptr())
         else:
-            torch._foreach_copy_(self._gviews, gs)
+            torch._foreach_copy_([self._gviews[i] for i in sel], gs)
         return self.grad
+
+    def span(self, subset):
+        """[lo, hi) of the flat buffer holding ``subset`` (must be contiguous in it)."""
+        idx = sorted(i for i, p in enumerate(self.params) if any(p is q for q in subset))
+        if not idx or idx != list(range(idx[0], idx[-1] + 1)):
+            raise ValueError("FlatAdam.span: the parameters are not one contiguous run")
+        lo = self.offsets[idx[0]]
+        hi = self.offsets[idx[-1]] + self.sizes[idx[-1]]
+        return lo, hi
 
     def step(self, grad_scale: float = 1.0, gather: bool = True):
         if gather:
@@ -163,6 +176,13 @@ class DataParallel:
                 dist.all_reduce(g[off:off + self.bucket], group=self.group)
         self.opt.step(grad_scale=1.0 / self.world, gather=False)
 
+    def reduce_range(self, lo: int, hi: int):
+        """All-reduce the flat gradient's [lo, hi) (buckets) on the current stream."""
+        if self.world > 1:
+            g = self.opt.grad
+            for off in range(lo, hi, self.bucket):
+                dist.all_reduce(g[off:min(hi, off + self.bucket)], group=self.group)
+
 
 class GraphedBagStep:
     """One training step of a snapshot-bag model (forward, loss, backward, gradient gather)
@@ -173,13 +193,28 @@ class GraphedBagStep:
     nothing alive between replays).  The bag indices reach the graph through a static device
     buffer per L, filled from a small ring of pinned host buffers; the inputs x / y are static
     buffers the caller fills (e.g. index_select(..., out=)).  After the replay the gradient
-    all-reduce (RCCL, N > 1) and the fused Adam update run eagerly.  Every kernel of the step
+    all-reduce (RCCL, N > 1) and the fused Adam update run eagerly.  With ``overlap`` the step
+    is two graphs per key and the heads' all-reduce runs beside the encoder's backward (step()).  Every kernel of the step
     still runs on every replay: the graph removes the host launch overhead, not work."""
 
     def __init__(self, model, loss_fn, opt: "FlatAdam", dp: "DataParallel", x, y, grid,
-                 loss_acc: Optional[torch.Tensor] = None):
+                 loss_acc: Optional[torch.Tensor] = None, overlap: Optional[bool] = None):
         from . import nio
         self.model, self.loss_fn, self.opt, self.dp = model, loss_fn, opt, dp
+        # overlap (default: with more than one rank, for models split into encoder + heads):
+        # the step is replayed as two graphs -- A: forward, loss and the heads' backward; B: the
+        # encoder's backward -- and the heads' gradient all-reduce (the bulk of the flat
+        # gradient: 3.54 of 3.56 M parameters at config C) runs on a side stream beside B
+        split_ok = hasattr(model, "forward_encoder") and hasattr(model, "forward_heads")
+        self.overlap = (dp.world > 1) if overlap is None else bool(overlap)
+        self.overlap = self.overlap and split_ok
+        if self.overlap:
+            heads = [p for n in model._heads for p in getattr(model, n).parameters()]
+            enc = [p for p in opt.params if not any(p is q for q in heads)]
+            self.head_params, self.enc_params = [p for p in opt.params if any(p is q for q in heads)], enc
+            self.head_span = opt.span(self.head_params)
+            self.enc_span = opt.span(self.enc_params)
+            self.side = torch.cuda.Stream(x.device)
         self.x, self.y, self.grid = x, y, grid
         self.loss_acc = loss_acc
         self.pool = torch.cuda.graph_pool_handle()
@@ -207,9 +242,30 @@ class GraphedBagStep:
             self.loss_acc.add_(loss.detach())
         return out.detach(), loss.detach()
 
+    def _body_a(self, L, accumulate=True):
+        """Graph A: forward, loss, the heads' backward (to the bag-mean field and the head
+        parameters) and their gradient gather."""
+        bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
+        h = self.model.forward_encoder(self.x, self.grid, bag_idx=bag)
+        hd = h.detach().requires_grad_(True)
+        out = self.model.forward_heads(hd)
+        loss = self.loss_fn(out, self.y)
+        loss.backward()
+        self.opt.gather_grads(self.head_params)
+        if accumulate and self.loss_acc is not None:
+            self.loss_acc.add_(loss.detach())
+        return h, hd, out.detach(), loss.detach()
+
+    def _body_b(self, h, hd):
+        """Graph B: the encoder's backward from the heads' input gradient, and its gather."""
+        h.backward(hd.grad)
+        self.opt.gather_grads(self.enc_params)
+
     def capture(self, L: int):
         if L in self.graphs:
             return
+        if self.overlap:
+            return self._capture_split(L)
         blob = torch.zeros(2 * L, dtype=torch.int32, device=self.x.device)
         self.blob = getattr(self, "blob", {})
         self.blob[L] = blob
@@ -228,6 +284,33 @@ class GraphedBagStep:
         self.opt.zero_grad()
         self.graphs[L] = g
 
+    def _capture_split(self, L: int):
+        blob = torch.zeros(2 * L, dtype=torch.int32, device=self.x.device)
+        self.blob = getattr(self, "blob", {})
+        self.blob[L] = blob
+        self.idx[L] = blob[:L]
+        self.lw[L] = blob[L:].view(torch.float32)
+        side = torch.cuda.Stream(self.x.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):                 # eager warm-up of both halves
+            h, hd, _, _ = self._body_a(L, accumulate=False)
+            self._body_b(h, hd)
+            self.opt.zero_grad()
+        del h, hd
+        torch.cuda.current_stream().wait_stream(side)
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga, pool=self.pool):
+            h, hd, self.out[L], self.loss[L] = self._body_a(L)
+        with torch.cuda.graph(gb, pool=self.pool):
+            self._body_b(h, hd)
+        # what A writes and B reads (h's saved activations, hd.grad) lives in the shared pool;
+        # it is only live between A(L) and B(L), which always replay back to back, so later
+        # captures may reuse it (keeping h would also pin the parameters' AccumulateGrad nodes
+        # to this capture's stream)
+        del h, hd
+        self.opt.zero_grad()
+        self.graphs[L] = (ga, gb)
+
     def release(self):
         """Drop every captured graph and its static buffers (frees the shared graph pool)."""
         self.graphs.clear()
@@ -241,14 +324,42 @@ class GraphedBagStep:
 
     def step(self, idx) -> int:
         """One training step on the drawn bag ``idx``: replay, all-reduce, Adam.  Returns the
-        graph key (``self.out[key]`` / ``self.loss[key]`` hold this step's output and loss)."""
-        key = self.replay(idx)
-        self.dp.reduce_and_step()
+        graph key (``self.out[key]`` / ``self.loss[key]`` hold this step's output and loss).
+        With ``overlap``: replay A, the heads' all-reduce on the side stream while B (the
+        encoder's backward) replays on the main stream, then the encoder's (small) all-reduce,
+        the join, and Adam."""
+        if not self.overlap:
+            key = self.replay(idx)
+            self.dp.reduce_and_step()
+            return key
+        key = self.stage(idx)
+        ga, gb = self.graphs[key]
+        main = torch.cuda.current_stream()
+        ga.replay()
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.dp.reduce_range(*self.head_span)
+        gb.replay()
+        self.dp.reduce_range(*self.enc_span)
+        main.wait_stream(self.side)
+        self.opt.step(grad_scale=1.0 / self.dp.world, gather=False)
         return key
 
     def replay(self, idx) -> int:
         """Stage the bag and replay its graph (forward, loss, backward, gradient gather into
         ``opt.grad``) without the optimizer step.  Returns the graph key."""
+        L = self.stage(idx)
+        g = self.graphs[L]
+        if isinstance(g, tuple):
+            for gg in g:
+                gg.replay()
+        else:
+            g.replay()
+        return L
+
+    def stage(self, idx) -> int:
+        """Capture the bag's graph(s) if needed and copy its indices (and multiplicity weights)
+        into the graph's static buffer through the pinned ring.  Returns the graph key."""
         idx = np.asarray(idx, dtype=np.int32)
         w = None
         if self.dedup:
@@ -274,7 +385,6 @@ class GraphedBagStep:
         ev = torch.cuda.Event()
         ev.record()
         self._ev[k] = ev
-        self.graphs[L].replay()
         return L
 
 

@@ -6,6 +6,9 @@ kernel -- is the same code the RCCL run executes).  Each rank draws its bags fro
 seeded 1234 + rank (the reference's seed + process_index, 2d_FPE/train_fno.py:78-81) and
 trains 3 steps.  A single-process emulation then replays both ranks' draws, sums their
 gradients and applies Adam with grad_scale 1/2; parameters must agree to rel-L2 <= 1e-5.
+The "graphed" mode runs the ranks through train.GraphedBagStep, which at world size > 1 replays
+each step as two graphs and all-reduces the heads' gradient on a side stream while the
+encoder's backward replays (the overlapped path bench.py takes at N > 1).
 """
 import os
 import socket
@@ -46,24 +49,35 @@ def _data(rank):
     return x.cuda(), y.cuda()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="eager"):
     import torch.distributed as dist
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         blindno, m, grid = _setup()
-        from blindno.train import DataParallel, FlatAdam, trained_parameters
+        from blindno.train import DataParallel, FlatAdam, GraphedBagStep, trained_parameters
+        from blindno.nio import draw_bag
         opt = FlatAdam(trained_parameters(m), lr=5e-4)
         dp = DataParallel(opt)
         dp.broadcast_parameters(0)
         x, y = _data(rank)
         np.random.seed(1234 + rank)
-        for s in range(STEPS):
-            loss = blindno.mse_loss(m(x[s], grid), y[s])
-            loss.backward()
-            dp.step()
-            opt.zero_grad()
+        if mode == "graphed":
+            xs, ys = x[0].clone(), y[0].clone()
+            gstep = GraphedBagStep(m, blindno.mse_loss, opt, dp, xs, ys, grid)
+            assert gstep.overlap
+            for s in range(STEPS):
+                _, idx = draw_bag(T)
+                xs.copy_(x[s])
+                ys.copy_(y[s])
+                gstep.step(idx)
+        else:
+            for s in range(STEPS):
+                loss = blindno.mse_loss(m(x[s], grid), y[s])
+                loss.backward()
+                dp.step()
+                opt.zero_grad()
         torch.cuda.synchronize()
         q.put((rank, opt.flat.cpu().numpy().copy()))
         dist.destroy_process_group()
@@ -72,14 +86,15 @@ def _worker(rank, world, port, q):
         raise
 
 
-def test_two_ranks_match_single_process_emulation():
+@pytest.mark.parametrize("mode", ["eager", "graphed"])
+def test_two_ranks_match_single_process_emulation(mode):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(2))

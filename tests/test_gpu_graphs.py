@@ -33,8 +33,10 @@ def _models():
     yield "1d_gpe", blindno.NIOFP_FNO(3, 20, 40, 1, "cuda", heads=("fno_V",)), (4, 70, 64), 1
 
 
-@pytest.mark.parametrize("case", ["2d", "1d", "1d_gpe"])
-def test_graphed_steps_match_eager(case):
+@pytest.mark.parametrize("case,overlap", [("2d", False), ("2d", True), ("1d", False), ("1d_gpe", False)])
+def test_graphed_steps_match_eager(case, overlap):
+    """overlap=True forces the two-graph step (encoder / heads split, the heads' gradient
+    reduced on a side stream) at world size 1."""
     import blindno
     from blindno.train import DataParallel, FlatAdam, GraphedBagStep, grid1d, grid2d, trained_parameters
     name, model, xshape, cout = next((m for m in _models() if m[0] == case))
@@ -49,7 +51,8 @@ def test_graphed_steps_match_eager(case):
     draws = [rs.choice(T, rs.randint(50, T)) for _ in range(3)]
 
     opt = FlatAdam(trained_parameters(model), lr=1e-3)
-    gstep = GraphedBagStep(model, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+    gstep = GraphedBagStep(model, blindno.mse_loss, opt, DataParallel(opt), x, y, grid, overlap=overlap)
+    assert gstep.overlap == overlap
     for idx in draws:
         gstep.step(idx)
     torch.cuda.synchronize()
