@@ -148,6 +148,14 @@ int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc, const 
                         int P2, int m2, int act, blindno_stream_t stream);
 int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2);
 
+/* 1 when the spectrum Z that blindno_colpass(_g) writes and blindno_rowidft_epi/bwd(_g) read
+ * is in A-tile order instead of Z[n][h][k][c]: C in {8, 12, 16} (the FNO heads, width 12), m2
+ * even (m2/2 <= 16, <= 24 for C = 8), P1 % 4 == 0, P1 >= 16, field < 2^31 elements.  Layout:
+ * Zt[((q C/4 + g) m2/2 + s) 64 + l] = Re (kk even) / Im (kk odd) of Z[row 4q + (l&15)/4][kk/2]
+ * [4g + (l&3)] with kk = 4s + l/16, rows n P1 + h.  Both sides agree by construction; a caller
+ * that builds Z itself for such a shape must use this order. */
+int blindno_spectrum_tile_layout(int Bn, int C, int P1, int P2, int m2);
+
 /* --- snapshot-encoder first layer with the lift folded in (NIOFP2D_FNO.FNO_input) ----------
  * The encoder input is cat(u_l, gx, gy) for snapshots u_l = X[b][idx[l]] of the bag tensor X
  * (B, T, N1, N2) (2d_FPE/NIOModules.py:548-560), lifted by fc0 (C x 3) and zero-padded to

@@ -34,6 +34,7 @@ SIGNATURES = {
     "blindno_rowidft_bwd": "pppppppiiiiiis",
     "blindno_conv_wgrad": "pppiiiiiis",
     "blindno_reduce_partials": "ppiis",
+    "blindno_spectrum_tile_layout": "iiiii",
     "blindno_pack_w2d": "pppiiiiis",
     "blindno_unpack_w2d": "pppiiiiis",
     "blindno_pack_w1d": "ppiiiis",

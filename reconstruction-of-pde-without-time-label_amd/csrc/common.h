@@ -57,6 +57,15 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// XCD-major workgroup order.  Workgroups are dispatched round-robin over the 8 XCDs (block b on
+// XCD b % 8), each XCD with its own L2; renumbering so that consecutive virtual blocks share an
+// XCD keeps the neighbouring work items that reuse one input (e.g. the column tiles of one
+// spectrum row quad) on one L2.  A bijection on [0, nb): the last nb % 8 blocks keep their id.
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int per = nb >> 3;
+  return b >= per * 8 ? b : (b & 7) * per + (b >> 3);
+}
+
 // Hermitian weight of a complex-to-real inverse of length n at bin k (< n/2+1):
 // bin 0 and the Nyquist bin (even n) count once, every other bin twice.
 __device__ __forceinline__ float c2r_weight(int k, int n) {

@@ -19,4 +19,7 @@ int project_bwd_mfma(const float* z, const float* w1, const float* b1, const flo
                      int dout_div, int G, int64_t wgs, hipStream_t st,
                      const float* lscale = nullptr);
 
+// rowinv.hip: shapes whose spectrum (colidft output / rowidft input) is in A-tile order
+bool rowinv_tile_layout(int Bn, int C, int P1, int P2, int m2);
+
 }  // namespace blindno

@@ -294,6 +294,156 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
   }
 }
 
+// Wide fields (C = 8, 12, 16: the FNO heads, C = 12).  One work item = 4 grid rows x TPW
+// column tiles x ALL channel groups (the kernel above takes one group per item): the layer
+// input (MODE 0) or dz (MODE 1) of a point is loaded and GELU'd once instead of once per group,
+// the twiddle operand is loaded once per tile for every group, and the groups' MFMA chains
+// share it.  The spectrum arrives in A-tile order (rowinv_tile_layout: colidft writes it so),
+// so each A operand is one coalesced 256-B load; gathered from the [row][k][c] order instead,
+// those loads were half of the kernel's time (measured).  Items run XCD-major (xcd_block) so
+// the column tiles of one row quad read its spectrum through one L2.  The 1x1 conv weights (C x
+// C + C per weight group, transposed for MODE 1) sit in LDS: as scalar operands they would not
+// fit the SGPR file.  No weight-gradient or LIFT variants (C > 4 uses conv_wgrad).
+constexpr int kWideMaxG = 4;
+#ifndef ROWINV_WIDE_WAVES
+#define ROWINV_WIDE_WAVES 2
+#endif
+// EX: m2 == 2 KSM (the heads: m2 = 32), every mode bound a compile-time constant
+template <int CM, int KSM, int MODE, int ACT, bool EX>
+__global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
+    const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
+    const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
+    const float* __restrict__ TB, int Bn, int P1, int P2, int m2_, int TPW, int Bg,
+    int64_t wgs) {
+  constexpr int NGM = CM / 4;
+  constexpr int C = CM;
+  const int m2 = EX ? 2 * KSM : m2_;
+  const int KS = m2 >> 1;                           // m2 even (rowinv_tile_layout)
+  const int NT = (P2 + 15) >> 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const int nrows = Bn * P1;                        // a multiple of 4
+  const int nquads = nrows >> 2;
+  const int NC = (NT + TPW - 1) / TPW;
+  const int nitems = nquads * NC;
+  const int HW = P1 * P2;                           // field < 2^31 elements (launcher)
+  const bool has_wc = wc != nullptr;
+  // conv weights of every weight group: [g][c][i] = wc[c][i] (MODE 0) or wc[i][c] (MODE 1),
+  // then the bias
+  constexpr int per = CM * CM + CM;
+  __shared__ float swc[kWideMaxG][per];
+  const int ngw = wgs ? Bn / Bg : 1;
+  if (has_wc) {
+    for (int e = threadIdx.x; e < ngw * per; e += blockDim.x) {
+      const int g = e / per, q = e - g * per;
+      float v = 0.f;
+      if (q < CM * CM) {
+        const int a = q / CM, b = q - (q / CM) * CM;
+        v = MODE == 0 ? wc[g * wgs + a * C + b] : wc[g * wgs + b * C + a];
+      } else if (MODE == 0) {
+        v = bc[g * wgs + q - CM * CM];
+      }
+      swc[g][q] = v;
+    }
+    __syncthreads();
+  }
+  const int vb = xcd_block(blockIdx.x, gridDim.x);
+  for (int item = vb * kW + wave; item < nitems; item += gridDim.x * kW) {
+    const int chunk = item % NC, quad = item / NC;
+    // A operands of every group: one coalesced load per (group, K step), tile order
+    float av[NGM][KSM];
+#pragma unroll
+    for (int g = 0; g < NGM; ++g)
+#pragma unroll
+      for (int s = 0; s < KSM; ++s)
+        av[g][s] = s < KS ? Z[(unsigned)(((quad * NGM + g) * KS + s) * 64 + lane)] : 0.f;
+    // this lane's output point: row 4 quad + g4, column 16 tile + c16, channels 4 g + r.
+    // 32-bit element offsets from the uniform bases: one VGPR per address
+    const int ro = 4 * quad + g4;
+    const int n = ro / P1, h = ro - (ro / P1) * P1;
+    const unsigned rbase = (unsigned)(n * C * HW + h * P2);
+    const float* sw = swc[wgs ? uniform_int((4 * quad) / P1 / Bg) : 0];
+    const int t0 = chunk * TPW, t1 = min(NT, t0 + TPW);
+    for (int tile = t0; tile < t1; ++tile) {
+      const int w = 16 * tile + c16;
+      const bool pok = w < P2;
+      float fv[CM], sv[CM], bv[KSM];
+#pragma unroll
+      for (int s = 0; s < KSM; ++s) bv[s] = s < KS ? TB[(unsigned)((s * NT + tile) * 64 + lane)] : 0.f;
+#pragma unroll
+      for (int i = 0; i < CM; ++i) {
+        // unconditional loads from clamped offsets, then a select: a guarded load per value
+        // would be a branch with its own saved exec mask (SGPR pressure -> spills)
+        const unsigned off = pok ? rbase + (unsigned)(i * HW + w) : 0u;
+        fv[i] = 0.f;
+        sv[i] = 0.f;
+        if (has_wc) {
+          const float v = (MODE == 0 ? xs : dz)[off];
+          fv[i] = pok ? v : 0.f;
+          if (MODE == 1 && ACT) {
+            const float u = xs[off];
+            sv[i] = pok ? u : 0.f;
+          }
+        }
+      }
+      if (MODE == 0 && ACT) {
+#pragma unroll
+        for (int i = 0; i < CM; ++i) fv[i] = gelu_f(fv[i]);
+      }
+      if (MODE == 1 && ACT) {
+#pragma unroll
+        for (int i = 0; i < CM; ++i) sv[i] = gelu_grad_f(sv[i]);
+      }
+#pragma unroll
+      for (int g = 0; g < NGM; ++g) {
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KSM; ++s)
+          if (s < KS) d = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bv[s], d, 0, 0, 0);
+        if (!pok) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 4 * g + r;
+          float v = d[r];
+          if (has_wc) {
+            // row c of the staged (MODE 0) or transposed (MODE 1) conv weights
+            if (MODE == 0) v += sw[CM * CM + c];
+#pragma unroll
+            for (int i = 0; i < CM; i += 4) {
+              const float4 wv = *reinterpret_cast<const float4*>(sw + c * CM + i);
+              v = fmaf(wv.x, fv[i], v);
+              v = fmaf(wv.y, fv[i + 1], v);
+              v = fmaf(wv.z, fv[i + 2], v);
+              v = fmaf(wv.w, fv[i + 3], v);
+            }
+            if (MODE == 1 && ACT) v *= sv[c];
+          }
+          out[rbase + (unsigned)(c * HW + w)] = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+namespace blindno {
+// The spectrum of a 2D layer whose inverse runs in rowinv_wide_kernel is written by colidft in
+// A-tile order: for row quad q (grid rows 4q..4q+3 of the Bn P1 rows), channel group g, K step s
+// and lane l, Zt[((q NG + g) KS + s) 64 + l] = Re / Im Z[row 4q + (l&15)/4][k][4g + (l&3)] with
+// kk = 4s + l/16, k = kk/2, Re for even kk.  Shapes: C in {8, 12, 16}, m2 even with m2/2 <= 16
+// (<= 24 for C = 8), P1 % 4 == 0 and P1 >= 16 (2D), field < 2^31 elements.
+bool rowinv_tile_layout(int Bn, int C, int P1, int P2, int m2) {
+  if (!(C == 8 || C == 12 || C == 16) || m2 <= 0 || (m2 & 1) || P1 < 16 || (P1 & 3) || Bn <= 0)
+    return false;
+  if (m2 / 2 > (C == 8 ? 24 : 16)) return false;
+  return (int64_t)Bn * C * P1 * P2 < INT32_MAX && (int64_t)Bn * P1 * m2 * C * 2 < INT32_MAX;
+}
+}  // namespace blindno
+
+namespace {
+
 struct RowinvGeom {
   int nitems, TPW, blocks;
   bool ldsb;
@@ -302,6 +452,10 @@ struct RowinvGeom {
 
 #ifndef ROWINV_MIN_ITEMS
 #define ROWINV_MIN_ITEMS 4096
+#endif
+// work items the wide kernel aims at when splitting rows into column chunks
+#ifndef ROWINV_WIDE_ITEMS
+#define ROWINV_WIDE_ITEMS 2048
 #endif
 
 RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
@@ -351,6 +505,36 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   const int cm = C <= 4 ? 4 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
   const int ks = (m2 + 1) / 2;
   if (ks > 24) return (int)hipErrorInvalidValue;               // m2 <= 48
+  if constexpr (!WG && !LIFT) {
+    // wide fields with the spectrum in A-tile order (rowinv_tile_layout)
+    if (rowinv_tile_layout(Bn, C, P1, P2, m2)) {
+      if (G > kWideMaxG) return (int)hipErrorInvalidValue;
+      const int NT = (P2 + 15) / 16, nquads = Bn * P1 / 4;
+      int tpw = NT;
+      while (tpw > 1 && (int64_t)nquads * ((NT + tpw - 1) / tpw) < ROWINV_WIDE_ITEMS) tpw = (tpw + 1) / 2;
+      const int nitems = nquads * ((NT + tpw - 1) / tpw);
+      int nbw = (nitems + kW - 1) / kW;
+      if (nbw > 2048) nbw = 2048;
+#define RW(CM_, KS_)                                                                          \
+  do {                                                                                        \
+    if (m2 == 2 * KS_)                                                                        \
+      rowinv_wide_kernel<CM_, KS_, MODE, ACT, true><<<nbw, 256, 0, st>>>(                     \
+          Z, xs, dz, wc, bc, out, TB, Bn, P1, P2, m2, tpw, Bg, wgs);                          \
+    else                                                                                      \
+      rowinv_wide_kernel<CM_, KS_, MODE, ACT, false><<<nbw, 256, 0, st>>>(                    \
+          Z, xs, dz, wc, bc, out, TB, Bn, P1, P2, m2, tpw, Bg, wgs);                          \
+  } while (0)
+      if (C == 8) {
+        if (ks <= 8) RW(8, 8); else if (ks <= 16) RW(8, 16); else RW(8, 24);
+      } else if (C == 12) {
+        if (ks <= 8) RW(12, 8); else RW(12, 16);
+      } else {
+        if (ks <= 8) RW(16, 8); else RW(16, 16);
+      }
+#undef RW
+      return (int)hipGetLastError();
+    }
+  }
 #define RI(CM_, KS_)                                                                         \
   do {                                                                                       \
     if (g.ldsb)                                                                              \
@@ -393,6 +577,10 @@ BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float*
                                     const float* bc, float* z, const float* tb, int Bn, int C,
                                     int P1, int P2, int m2, int act, void* stream) {
   return blindno_rowidft_epi_g(Z, x, wc, bc, z, tb, 1, 0, Bn, C, P1, P2, m2, act, stream);
+}
+
+BLINDNO_API int blindno_spectrum_tile_layout(int Bn, int C, int P1, int P2, int m2) {
+  return rowinv_tile_layout(Bn, C, P1, P2, m2) ? 1 : 0;
 }
 
 BLINDNO_API int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2) {

@@ -10,6 +10,7 @@
 // m2/P2-sized row spectra and run one workgroup per (sample, column mode).
 #include "common.h"
 #include "blindno.h"
+#include "kernels.h"
 
 using namespace blindno;
 
@@ -328,11 +329,12 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
 
 // Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
 // tile, 64 spectrum rows (k, o)); one 16-row MFMA tile per wave; the result is transposed
-// through LDS so that each h row of Z is written as one contiguous run.
+// through LDS so that each h row of Z is written as one contiguous run.  tiled: Z in the
+// A-tile order of the wide row inverse instead (rowinv_tile_layout, rowinv.hip).
 __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__ Y,
                                                       const f32x4* __restrict__ GB,
                                                       float2* __restrict__ Z, int Cout, int P1,
-                                                      int m1, int m2) {
+                                                      int m1, int m2, int tiled) {
   __shared__ float2 sZ[16][65];
   const int K1 = kept_rows_count(m1, P1);
   const int Jt = (K1 + 15) >> 4, K1p = Jt * 16;
@@ -363,7 +365,22 @@ __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__
   for (int e = threadIdx.x; e < 16 * 64; e += blockDim.x) {
     const int hl = e >> 6, rl = e & 63;
     const int h = ht * 16 + hl, row = row0 + rl;
-    if (h < P1 && row < R) Z[((int64_t)n * P1 + h) * R + row] = sZ[hl][rl];
+    if (h < P1 && row < R) {
+      if (!tiled) {
+        Z[((int64_t)n * P1 + h) * R + row] = sZ[hl][rl];
+      } else {
+        // grid row gr = n P1 + h -> quad gr / 4, A row (gr & 3); channel o -> group o / 4,
+        // column o & 3; mode k -> K step k / 2, lanes 32 (k & 1) + (0: Re | 16: Im) + c16
+        const float2 v = sZ[hl][rl];
+        const int k = row / Cout, o = row - (row / Cout) * Cout;
+        const int gr = n * P1 + h;
+        const int c16 = 4 * (gr & 3) + (o & 3);
+        float* zt = reinterpret_cast<float*>(Z) +
+                    ((int64_t)((gr >> 2) * (Cout >> 2) + (o >> 2)) * (m2 >> 1) + (k >> 1)) * 64;
+        zt[32 * (k & 1) + c16] = v.x;
+        zt[32 * (k & 1) + 16 + c16] = v.y;
+      }
+    }
   }
 }
 
@@ -656,8 +673,9 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const int Ht = (P1 + 15) / 16;
   const int Mt = (m2 * cout + 15) / 16;
   const dim3 g2((unsigned)(Bn * Ht), (unsigned)((Mt + 3) / 4));
+  const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
   colidft_kernel<<<g2, 256, 0, st>>>((const float2*)Y, (const f32x4*)GB, (float2*)Z, cout, P1, m1,
-                                     m2);
+                                     m2, tiled);
   return (int)hipGetLastError();
 }
 
