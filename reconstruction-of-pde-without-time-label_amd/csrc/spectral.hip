@@ -228,7 +228,11 @@ __device__ __forceinline__ void load4c(const float2* src, int len, bool vec, flo
   }
 }
 
-template <int DIR>
+// FULL: every h block's operands are loaded before the first MFMA (HB <= kFullHB): the head
+// layers launch one workgroup per (sample, mode) pair -- one wave per SIMD -- so a one-block
+// lookahead leaves each step waiting a full memory latency (measured ~16 us for 10 steps)
+constexpr int kFullHB = 10;
+template <int DIR, bool FULL>
 __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restrict__ At,
                                                          const float2* __restrict__ Wt,
                                                          const f32x4* __restrict__ FB,
@@ -260,22 +264,39 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
     const float2* ar = At + ((int64_t)q0 * Cin + (rok ? row : 0)) * P1;
     const f32x4* fb = FB + ((int64_t)jt * HB * 64 + lane) * 2;
     f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
-    // operands of the next 16-row block are loaded before this block's MFMAs
-    float nre[4], nim[4];
-    load4c(ar + kq * 4, rok ? P1 - kq * 4 : 0, vec, nre, nim);
-    f32x4 nf0 = fb[0], nf1 = fb[1];
-    for (int hb = 0; hb < HB; ++hb) {
-      float re[4], im[4];
+    if constexpr (FULL) {
+      float are[kFullHB][4], aim[kFullHB][4];
+      f32x4 af0[kFullHB], af1[kFullHB];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) { re[s] = nre[s]; im[s] = nim[s]; }
-      const f32x4 f0 = nf0, f1 = nf1;
-      if (hb + 1 < HB) {
-        const int h1 = (hb + 1) * 16 + kq * 4;
-        load4c(ar + h1, rok ? P1 - h1 : 0, vec, nre, nim);
-        nf0 = fb[(hb + 1) * 128];
-        nf1 = fb[(hb + 1) * 128 + 1];
+      for (int hb = 0; hb < kFullHB; ++hb) {
+        if (hb < HB) {
+          const int h1 = hb * 16 + kq * 4;
+          load4c(ar + h1, rok ? P1 - h1 : 0, vec, are[hb], aim[hb]);
+          af0[hb] = fb[hb * 128];
+          af1[hb] = fb[hb * 128 + 1];
+        }
       }
-      cmfma4(re, im, f0, f1, dr, di);
+#pragma unroll
+      for (int hb = 0; hb < kFullHB; ++hb)
+        if (hb < HB) cmfma4(are[hb], aim[hb], af0[hb], af1[hb], dr, di);
+    } else {
+      // operands of the next 16-row block are loaded before this block's MFMAs
+      float nre[4], nim[4];
+      load4c(ar + kq * 4, rok ? P1 - kq * 4 : 0, vec, nre, nim);
+      f32x4 nf0 = fb[0], nf1 = fb[1];
+      for (int hb = 0; hb < HB; ++hb) {
+        float re[4], im[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) { re[s] = nre[s]; im[s] = nim[s]; }
+        const f32x4 f0 = nf0, f1 = nf1;
+        if (hb + 1 < HB) {
+          const int h1 = (hb + 1) * 16 + kq * 4;
+          load4c(ar + h1, rok ? P1 - h1 : 0, vec, nre, nim);
+          nf0 = fb[(hb + 1) * 128];
+          nf1 = fb[(hb + 1) * 128 + 1];
+        }
+        cmfma4(re, im, f0, f1, dr, di);
+      }
     }
     const int j = jt * 16 + r16;
 #pragma unroll
@@ -291,11 +312,13 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
   }
   __syncthreads();
 
+  // the mix: output channel o fastest across threads, so the weight loads W[k][j][c][o] of
+  // neighbouring threads are contiguous (j fastest put every lane on its own cache line)
   const int nout = np * Cout * K1p;
   for (int e = threadIdx.x; e < nout; e += blockDim.x) {
-    const int j = e % K1p;
-    const int t = e / K1p;
-    const int o = t % Cout, p = t / Cout;
+    const int o = e % Cout;
+    const int t = e / Cout;
+    const int j = t % K1p, p = t / K1p;
     const int k = (q0 + p) % m2;
     float re = 0.f, im = 0.f;
     if (j < K1) {
@@ -658,16 +681,19 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
   hipStream_t st = (hipStream_t)stream;
   const dim3 g1((unsigned)cdiv(npairs, G));
-  if (dir == 0)
-    coldft_mix_kernel<0><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,
-                                              (const f32x4*)FB, (float2*)Xs, (float2*)Y,
-                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg,
-                                              wtgs);
-  else
-    coldft_mix_kernel<1><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,
-                                              (const f32x4*)FB, (float2*)Xs, (float2*)Y,
-                                              (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg,
-                                              wtgs);
+  // full operand prefetch when the launch is too small to hide latency with waves
+  const bool full = (P1 + 15) / 16 <= kFullHB && (int64_t)g1.x * 4 < 4096;
+#define CM_(D_, F_)                                                                         \
+  coldft_mix_kernel<D_, F_><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,      \
+                                                 (const f32x4*)FB, (float2*)Xs, (float2*)Y, \
+                                                 (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, \
+                                                 Bg, wtgs)
+  if (dir == 0) {
+    if (full) CM_(0, true); else CM_(0, false);
+  } else {
+    if (full) CM_(1, true); else CM_(1, false);
+  }
+#undef CM_
   int e = (int)hipGetLastError();
   if (e) return e;
   const int Ht = (P1 + 15) / 16;
