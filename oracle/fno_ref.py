@@ -31,7 +31,7 @@ def set_precision(name: str = "fp64") -> None:
 __all__ = ["set_precision", 
     "pad_amount", "gelu", "c2r_weights", "spectral_conv2d", "spectral_conv1d",
     "fno2d", "fno1d", "bag_mean", "bag_attention", "niofp2d_fno", "niofp2d_fno_attn", "niofp_fno", "encoder2d",
-    "ffn", "deeponet_nobias", "niofp2d", "mse", "train_rel_l2_2ch", "rel_l2",
+    "ffn", "deeponet_nobias", "niofp2d", "encoder1d", "niofp", "mse", "train_rel_l2_2ch", "rel_l2",
     "time_averaged_relative_l2", "time_averaged_L2_error", "adam_step",
     "sub_params", "n_layers_of",
 ]
@@ -350,6 +350,49 @@ def encoder2d(p: Dict[str, torch.Tensor], x: torch.Tensor,
         h = F.leaky_relu(h, 0.2) if masks is None else torch.where(masks[k], h, 0.2 * h)
     h = h.flatten(1).view(B, L, -1)
     return _linear(h, p, "linear")
+
+
+def encoder1d(p: Dict[str, torch.Tensor], x: torch.Tensor, kernels=(5, 4, 15), conv4: bool = False,
+              masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+    """1D snapshot Encoder.forward (train-mode BatchNorm), 1d_FPE/Baselines.py:254-287 (final
+    kernels 5, 4, 15; final_conv1..3 applied) and 1d_GPE/Baselines.py:254-287 (5, 7, 4;
+    final_conv1..4 applied).  Each (1, k) ConvBlock is a Conv2d over a (B L, C, 1, N) image.
+    x (B, L, N) -> (B, L, n_out).  ``masks``: see encoder2d."""
+    B, L, N = x.shape
+    h = x.reshape(B * L, 1, 1, N).to(DT)
+    blocks = [("conv1", (1, 2), (0, 1)), ("conv2", (1, 2), (0, 1)), ("conv3", (1, 2), (0, 1)),
+              ("final_conv1", (1, 1), (0, 1)), ("final_conv2", (1, 1), (0, 0)),
+              ("final_conv3", (1, 1), (0, 0))]
+    if conv4:
+        blocks.append(("final_conv4", (1, 1), (0, 0)))
+    for k, (name, stride, pad) in enumerate(blocks):
+        h = F.conv2d(h, p[f"{name}.layers.0.weight"].to(DT), p[f"{name}.layers.0.bias"].to(DT),
+                     stride=stride, padding=pad)
+        h = F.batch_norm(h, None, None, p[f"{name}.layers.1.weight"].to(DT),
+                         p[f"{name}.layers.1.bias"].to(DT), training=True, eps=1e-5)
+        h = F.leaky_relu(h, 0.2) if masks is None else torch.where(masks[k], h, 0.2 * h)
+    return _linear(h.reshape(B, L, -1), p, "linear")
+
+
+def niofp(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
+          idx: Optional[Sequence[int]] = None, n_hidden_layers: int = 3,
+          heads: Sequence[str] = ("fno_drift", "fno_diffusion"), kernels=(5, 4, 15),
+          conv4: bool = False, branch_masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+    """1D NIO: NIOFP.forward 1d_FPE/NIOModules.py:55-84; NIOFP_schrodinger.forward
+    1d_GPE/NIOModules.py:194-223 (heads ("fno_V",), kernels (5, 7, 4), conv4=True).
+    x (B, T, N), grid (N, 1)."""
+    x = x.to(DT)
+    if idx is not None:
+        x = x[:, list(idx)]
+    B, L, nx = x.shape
+    g = grid.to(DT)
+    w = encoder1d(sub_params(p, "branch"), x, kernels, conv4, branch_masks)
+    basis = ffn(sub_params(p, "trunk"), g.reshape(-1, 1), n_hidden_layers)
+    u = deeponet_nobias(w, basis, p["deeponet.b0"]).view(B, L, nx)
+    gcf = g.unsqueeze(0).repeat(B, 1, 1).permute(0, 2, 1)
+    h = bag_mean(u, gcf, p["fc0.weight"], p["fc0.bias"])
+    outs = [fno1d(sub_params(p, hd), h) for hd in heads]
+    return torch.cat(outs, dim=-1) if len(outs) > 1 else outs[0]
 
 
 def ffn(p: Dict[str, torch.Tensor], x: torch.Tensor, n_hidden_layers: int) -> torch.Tensor:

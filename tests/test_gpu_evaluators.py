@@ -136,6 +136,63 @@ def test_niofp2d_nio_branch_trunk():
     assert eg <= max(1e-4, 2 * er), (eg, er)
 
 
+@pytest.mark.parametrize("case", ["nio1d_train", "gpe_nio1d_train"])
+def test_niofp_nio_1d(case):
+    """1D NIO models (NIOFP, 1d_FPE/NIOModules.py:15-84; NIOFP_schrodinger,
+    1d_GPE/NIOModules.py:160-223) in train mode: the 1D Encoder branch (HIP implicit-GEMM (1, k)
+    convolutions + fused BatchNorm/LeakyReLU), FFN trunk, DeepONet, bag mean and FNO1d heads,
+    recipe parameters and the recorded bag draw, against the float64 oracle (itself pinned to
+    the reference fixture on CPU).  Bars as test_niofp2d_nio_branch_trunk: within SURVEY 8c's
+    1e-5 / 1e-4 or 2x the reference fp32 run's own distance from fp64."""
+    import oracle
+    from blindno import NIOFP, NIOFP_schrodinger
+    from test_oracle_golden import NIO1D_CASES, nio1d_params
+    heads, kernels, conv4 = NIO1D_CASES[case]
+    g = load_golden(case)
+    st, p64 = nio1d_params(g)
+    if case == "nio1d_train":
+        m = NIOFP(1, 3, 100, 25, 2, 6, 8, 2, "cuda")
+    else:
+        m = NIOFP_schrodinger(1, 3, 100, 25, 2, 6, 8, 1, "cuda")
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()}, strict=True)
+    m = m.cuda().train()
+    x = torch.from_numpy(g["in.x"]).cuda().requires_grad_(True)
+    grid = torch.from_numpy(g["in.grid"]).cuda()
+    out = m(x, grid, bag_idx=g["idx"])
+    cot = torch.from_numpy(g["cot"]).cuda()
+    (out * cot).sum().backward()
+    torch.cuda.synchronize()
+    x64 = x.detach().cpu().double().requires_grad_(True)
+    ref = oracle.niofp(p64, x64, grid.cpu().double(), idx=g["idx"].tolist(), heads=heads,
+                       kernels=kernels, conv4=conv4)
+    (ref * cot.cpu().double()).sum().backward()
+    refn = ref.detach().numpy()
+    e, e_ref = rel_l2(out.detach().cpu().numpy(), refn), rel_l2(g["out"], refn)
+    assert e <= max(1e-5, 2 * e_ref), (e, e_ref)
+    named = dict(m.named_parameters())
+    rows = []
+    gmax = max(float(p64[k[6:]].grad.norm()) for k in g if k.startswith("gnorm."))
+    for k, v in g.items():
+        if k.startswith("g."):
+            ref_g = p64[k[2:]].grad.numpy()
+            rows.append((k, rel_l2(named[k[2:]].grad.cpu().numpy(), ref_g), rel_l2(v, ref_g)))
+        elif k.startswith("gpre."):
+            ref_g = p64[k[5:]].grad.reshape(-1)[:v.size].numpy()
+            got = named[k[5:]].grad.reshape(-1)[:v.size].cpu().numpy()
+            rows.append((k, rel_l2(got, ref_g), rel_l2(v, ref_g)))
+        elif k.startswith("gnorm."):
+            want = float(p64[k[6:]].grad.norm())
+            got = float(named[k[6:]].grad.double().norm())
+            assert abs(got - want) <= max(2 * abs(float(v) - want), 1e-4 * want) + 1e-5 * gmax, k
+    med = float(np.median([r[2] for r in rows]))
+    for k, eg, er in rows:
+        assert eg <= max(1e-4, 2 * er, 2 * med), (k, eg, er, med)
+    assert len(rows) > 20
+    eg = rel_l2(x.grad.cpu().numpy(), x64.grad.numpy())
+    er = rel_l2(g["gin.x"], x64.grad.numpy())
+    assert eg <= max(1e-4, 2 * er), (eg, er)
+
+
 def test_flat_adam_matches_reference_two_steps():
     from blindno.train import FlatAdam
     g = load_golden("adam_fno2d")

@@ -153,6 +153,53 @@ def test_niofp2d_nio_branch_trunk():
             assert abs(got - float(v)) <= 1e-3 * abs(float(v)) + 1e-5 * gmax, k
 
 
+NIO1D_CASES = {
+    # fixture: (heads, final kernels, conv4) -- 1d_FPE/NIOModules.py:15-84, 1d_GPE/NIOModules.py:160-223
+    "nio1d_train": (("fno_drift", "fno_diffusion"), (5, 4, 15), False),
+    "gpe_nio1d_train": (("fno_V",), (5, 7, 4), True),
+}
+
+
+def nio1d_params(g):
+    """Recipe parameters of a 1D NIO fixture (float64 leaves)."""
+    import json
+    shapes = [(k, tuple(s)) for k, s in json.loads(str(g["layout_json"]))]
+    st = make_state(shapes, seed=int(g["recipe_seed"]), complex_names=json.loads(str(g["complex_json"])))
+    return st, {k: torch.from_numpy(v).to(torch.complex128 if v.dtype.kind == "c" else torch.float64)
+                .requires_grad_(v.dtype.kind in "fc") for k, v in st.items()}
+
+
+@pytest.mark.parametrize("case", sorted(NIO1D_CASES))
+def test_niofp_nio_1d(case):
+    """1D NIO (Encoder branch + FFN trunk + DeepONet + FNO1d heads) in train mode, recipe
+    parameters, recorded bag draw.  The fixture is the reference's fp32 run; ten train-mode
+    BatchNorms make the encoder gradients fp32-sensitive (as nio2d_nc_train): fwd 1e-5,
+    gradients 1e-3, prefix/norm entries of the big convolutions 1e-3."""
+    heads, kernels, conv4 = NIO1D_CASES[case]
+    g = load_golden(case)
+    _, p = nio1d_params(g)
+    x = torch.from_numpy(g["in.x"]).double().requires_grad_(True)
+    grid = torch.from_numpy(g["in.grid"]).double()
+    y = oracle.niofp(p, x, grid, idx=g["idx"].tolist(), heads=heads, kernels=kernels, conv4=conv4)
+    assert rel_l2(y.detach().numpy(), g["out"]) <= FWD_TOL
+    (y * torch.from_numpy(g["cot"]).double()).sum().backward()
+    gmax = max(float(v) for k, v in g.items() if k.startswith("gnorm."))
+    n = 0
+    for k, v in g.items():
+        if k.startswith("g."):
+            assert rel_l2(p[k[2:]].grad.numpy(), v) <= 1e-3, (k, rel_l2(p[k[2:]].grad.numpy(), v))
+            n += 1
+        elif k.startswith("gpre."):
+            got = p[k[5:]].grad.reshape(-1)[:v.size].numpy()
+            assert rel_l2(got, v) <= 1e-3, k
+            n += 1
+        elif k.startswith("gnorm."):
+            got = float(p[k[6:]].grad.norm())
+            assert abs(got - float(v)) <= 1e-3 * abs(float(v)) + 1e-5 * gmax, k
+    assert n > 20
+    assert rel_l2(x.grad.numpy(), g["gin.x"]) <= 1e-3
+
+
 def test_adam_two_steps():
     g = load_golden("adam_fno2d")
     names = [k[3:] for k in g if k.startswith("p0.")]
