@@ -195,6 +195,13 @@ int blindno_conv_wgrad_nchunk(int Bn, int P1, int P2);
 int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np,
                             blindno_stream_t stream);
 
+/* Several reductions in one launch: segment i is blindno_reduce_partials(partials[i], outs[i],
+ * nchunks[i], nps[i]) (bit-identical results); the deferred weight-gradient reductions of one
+ * backward pass (blindno.ops.deferred_reductions). */
+int blindno_reduce_partials_multi(const void* const* partials, void* const* outs,
+                                  const int* nchunks, const int* nps, int nseg,
+                                  blindno_stream_t stream);
+
 /* Pack reference-layout 2D weights (Ci,Co,m1,m2,2) x2 into Wt (m2,K1,Ci,Co) complex. */
 int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, int Ci, int Co, int m1,
                      int m2, int P1, blindno_stream_t stream);
@@ -207,6 +214,14 @@ int blindno_pack_w2d_2(const float* w1a, const float* w2a, const float* w1b, con
                        float* Wt, int Ci, int Co, int m1, int m2, int P1, blindno_stream_t stream);
 int blindno_unpack_w2d_2(const float* dWt, float* dw1a, float* dw2a, float* dw1b, float* dw2b,
                          int Ci, int Co, int m1, int m2, int P1, blindno_stream_t stream);
+/* Several blindno_unpack_w2d in one launch: segment i unpacks dWts[i] into dw1s[i], dw2s[i]
+ * with shape shapes[5 i .. 5 i + 4] = (Ci, Co, m1, m2, P1). */
+int blindno_unpack_w2d_multi(const void* const* dWts, void* const* dw1s, void* const* dw2s,
+                             const int* shapes, int nseg, blindno_stream_t stream);
+/* Several blindno_pack_w2d in one launch: segment i packs (w1s[i], w2s[i]) into Wts[i] with
+ * shape shapes[5 i .. 5 i + 4] = (Ci, Co, m1, m2, P1). */
+int blindno_pack_w2d_multi(const void* const* w1s, const void* const* w2s, void* const* Wts,
+                           const int* shapes, int nseg, blindno_stream_t stream);
 /* 1D: (Ci,Co,m) complex <-> Wt (m,Ci,Co) complex; dir 0 pack, 1 unpack. */
 int blindno_pack_w1d(const float* w, float* Wt, int Ci, int Co, int m, int dir,
                      blindno_stream_t stream);

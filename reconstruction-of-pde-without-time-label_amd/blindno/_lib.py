@@ -68,6 +68,9 @@ SIGNATURES = {
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",
     "blindno_gather_flat": "pppips",
+    "blindno_reduce_partials_multi": "ppppis",
+    "blindno_unpack_w2d_multi": "ppppis",
+    "blindno_pack_w2d_multi": "ppppis",
     "blindno_fp_propagate": "pppiiiiiids",
     "blindno_bagattn_nchunk": "i",
     "blindno_bagattn_fwd": "pppppppp" + "iiii" + "s",

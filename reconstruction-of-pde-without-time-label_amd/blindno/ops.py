@@ -11,6 +11,8 @@ There is no CPU path: CPU tensors raise.
 """
 from __future__ import annotations
 
+import contextlib
+import ctypes
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -155,10 +157,67 @@ def _empty(*shape, like):
     return torch.empty(*shape, dtype=F32, device=like.device)
 
 
+# Deferred weight-gradient finalisation.  Inside ``deferred_reductions()`` the partial-sum
+# reductions and the spectral-weight unpacks of a backward pass are only recorded; the returned
+# gradient tensors are filled by two batched launches (blindno_reduce_partials_multi,
+# blindno_unpack_w2d_multi) when the context exits -- 10 + 5 small latency-bound launches per
+# config-C step become 2, with bit-identical results.  The recorded sources stay referenced
+# until the flush is enqueued, so the allocator cannot hand their memory to later kernels.
+# Only for callers that read no returned gradient before the exit (GraphedBagStep: the
+# gradients are consumed by the flat gather after backward, and are None before it).
+_DEFER = None
+
+
+class _Deferred:
+    def __init__(self):
+        self.red = []      # (partial, out, nchunk, np)
+        self.unp = []      # (dWt slice, dw1, dw2, (Ci, Co, m1, m2, P1))
+
+    def flush(self):
+        if self.red:
+            n = len(self.red)
+            srcs = (ctypes.c_void_p * n)(*[r[0].data_ptr() for r in self.red])
+            outs = (ctypes.c_void_p * n)(*[r[1].data_ptr() for r in self.red])
+            ncs = (ctypes.c_int * n)(*[r[2] for r in self.red])
+            nps = (ctypes.c_int * n)(*[r[3] for r in self.red])
+            call("blindno_reduce_partials_multi", srcs, outs, ncs, nps, n, stream_ptr())
+        if self.unp:
+            n = len(self.unp)
+            srcs = (ctypes.c_void_p * n)(*[u[0].data_ptr() for u in self.unp])
+            d1 = (ctypes.c_void_p * n)(*[u[1].data_ptr() for u in self.unp])
+            d2 = (ctypes.c_void_p * n)(*[u[2].data_ptr() for u in self.unp])
+            shp = (ctypes.c_int * (5 * n))(*[v for u in self.unp for v in u[3]])
+            call("blindno_unpack_w2d_multi", srcs, d1, d2, shp, n, stream_ptr())
+        self.red, self.unp = [], []
+
+
+@contextlib.contextmanager
+def deferred_reductions():
+    global _DEFER
+    prev, _DEFER = _DEFER, _Deferred()
+    try:
+        yield
+        _DEFER.flush()
+    finally:
+        _DEFER = prev
+
+
 def reduce_partials(partial: torch.Tensor, nchunk: int, np_: int) -> torch.Tensor:
     out = _empty(np_, like=partial)
+    if _DEFER is not None:
+        _DEFER.red.append((partial, out, int(nchunk), int(np_)))
+        return out
     call("blindno_reduce_partials", ptr(partial), ptr(out), nchunk, np_, stream_ptr())
     return out
+
+
+def unpack_w2d_into(dWt: torch.Tensor, dw1: torch.Tensor, dw2: torch.Tensor, P1: int):
+    """dWt (m2, K1, Ci, Co, 2) -> dw1, dw2 in the reference layout (Ci, Co, m1, m2, 2)."""
+    Ci, Co, m1, m2 = dw1.shape[:4]
+    if _DEFER is not None:
+        _DEFER.unp.append((dWt, dw1, dw2, (Ci, Co, m1, m2, P1)))
+        return
+    call("blindno_unpack_w2d", ptr(dWt), ptr(dw1), ptr(dw2), Ci, Co, m1, m2, P1, stream_ptr())
 
 
 # ---------------------------------------------------------------------------- kernel wrappers
@@ -203,11 +262,36 @@ def k_pack_w2d(w1, w2, P1):
     return Wt
 
 
+def _pack_into(pairs, Wts, P1):
+    """Pack the spectral weights (w1, w2) of several 2D layers into the contiguous Wts[i]
+    (m2, K1, Ci, Co, 2) with ONE launch (blindno_pack_w2d_multi)."""
+    w1s, w2s, shp = [], [], []
+    for (w1, w2), W in zip(pairs, Wts):
+        w1, w2 = _c(w1), _c(w2)
+        Ci, Co, m1, m2 = w1.shape[:4]
+        if W.shape != (m2, kept_rows_count(m1, P1), Ci, Co, 2) or not W.is_contiguous():
+            raise BlindnoError("pack: bad Wt buffer")
+        w1s.append(w1.data_ptr())
+        w2s.append(w2.data_ptr())
+        shp += [Ci, Co, m1, m2, P1]
+    n = len(Wts)
+    call("blindno_pack_w2d_multi", (ctypes.c_void_p * n)(*w1s), (ctypes.c_void_p * n)(*w2s),
+         (ctypes.c_void_p * n)(*[W.data_ptr() for W in Wts]), (ctypes.c_int * (5 * n))(*shp), n,
+         stream_ptr())
+
+
+def pack_w2d_many(pairs, P1):
+    """One packed Wt (m2, K1, Ci, Co, 2) per (w1, w2) pair, all in one launch."""
+    Wts = [_empty(w1.shape[3], kept_rows_count(w1.shape[2], P1), w1.shape[0], w1.shape[1], 2, like=w1)
+           for w1, _ in pairs]
+    _pack_into(pairs, Wts, P1)
+    return Wts
+
+
 def k_unpack_w2d(dWt, w1, P1):
-    Ci, Co, m1, m2 = w1.shape[:4]
     dw1 = torch.empty_like(w1)
     dw2 = torch.empty_like(w1)
-    call("blindno_unpack_w2d", ptr(dWt), ptr(dw1), ptr(dw2), Ci, Co, m1, m2, P1, stream_ptr())
+    unpack_w2d_into(dWt, dw1, dw2, P1)
     return dw1, dw2
 
 
@@ -558,11 +642,12 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
     FB, GB = twiddle_cols(P1, meta.m1, inp.device)
     src, act = x0, 0
     Xs, Wts, zs = [], [], []
+    # every layer's spectral weights of both heads in one launch: Wt_all[k] = (G, m2, K1, C, C, 2)
+    Wt_all = _empty(n, G, meta.m2, K1, C, C, 2, like=inp)
+    segs = [(prms[g][2 + 4 * k], prms[g][3 + 4 * k]) for k in range(n) for g in range(G)]
+    _pack_into(segs, [Wt_all[k, g] for k in range(n) for g in range(G)], P1)
     for k in range(n):
-        off = 2 + 4 * k
-        Wt = _empty(G, meta.m2, K1, C, C, 2, like=inp)
-        call("blindno_pack_w2d_2", ptr(_c(prms[0][off])), ptr(_c(prms[0][off + 1])), ptr(_c(prms[1][off])),
-             ptr(_c(prms[1][off + 1])), ptr(Wt), C, C, meta.m1, meta.m2, P1, stream_ptr())
+        Wt = Wt_all[k]
         At = k_rowdft(src, Bn, C, P1, P2, meta.m2, act)
         X = _empty(Bn, meta.m2, C, K1, 2, like=inp)
         Y = _empty(Bn, meta.m2, C, K1p, 2, like=inp)
@@ -636,8 +721,12 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         call("blindno_mix_wgrad_g", ptr(Xs[k]), ptr(Gs), ptr(dWt), ptr(part) if part is not None else None,
              ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
         dws = [torch.empty_like(prms[g][off]) for g in range(G) for _ in range(2)]
-        call("blindno_unpack_w2d_2", ptr(dWt), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), C, C,
-             meta.m1, meta.m2, P1, stream_ptr())
+        if _DEFER is not None:
+            for g in range(G):
+                unpack_w2d_into(dWt[g], dws[2 * g], dws[2 * g + 1], P1)
+        else:
+            call("blindno_unpack_w2d_2", ptr(dWt), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), C,
+                 C, meta.m1, meta.m2, P1, stream_ptr())
         for g in range(G):
             grads[g][off], grads[g][off + 1] = dws[2 * g], dws[2 * g + 1]
         nch = query("blindno_conv_wgrad_nchunk", Bg, P1, P2)
@@ -817,10 +906,11 @@ class BagEncoderFn(torch.autograd.Function):
         Gt = _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, meta.m2, cacheable=frozen)
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         Xs, Wts, zs = [], [], []
+        Wts_all = pack_w2d_many([(prm[2 + 4 * k], prm[3 + 4 * k]) for k in range(n)], P1)
         for k in range(n):
             off = 2 + k * 4
             w1, w2, cw, cb = prm[off:off + 4]
-            Wt = pack_weights((w1, w2), P1, 2)
+            Wt = Wts_all[k]
             if k == 0:
                 At = k_rowdft_bag_lift(X, idx_t, fc0w, Gt, B, T, L, N1, N2, C, P1, P2, meta.m2)
                 Xk, Z = k_colpass(At, Wt, Bn, C, C, P1, meta.m1, meta.m2, P2, 0)

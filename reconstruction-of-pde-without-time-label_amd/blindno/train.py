@@ -22,6 +22,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import ops
 from ._lib import call, ptr, stream_ptr
 
 
@@ -236,7 +237,8 @@ class GraphedBagStep:
         bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
         out = self.model(self.x, self.grid, bag_idx=bag)
         loss = self.loss_fn(out, self.y)
-        loss.backward()
+        with ops.deferred_reductions():               # one batched gradient finalisation
+            loss.backward()
         self.opt.gather_grads()
         if accumulate and self.loss_acc is not None:
             self.loss_acc.add_(loss.detach())
@@ -250,7 +252,8 @@ class GraphedBagStep:
         hd = h.detach().requires_grad_(True)
         out = self.model.forward_heads(hd)
         loss = self.loss_fn(out, self.y)
-        loss.backward()
+        with ops.deferred_reductions():
+            loss.backward()
         self.opt.gather_grads(self.head_params)
         if accumulate and self.loss_acc is not None:
             self.loss_acc.add_(loss.detach())
@@ -258,7 +261,8 @@ class GraphedBagStep:
 
     def _body_b(self, h, hd):
         """Graph B: the encoder's backward from the heads' input gradient, and its gather."""
-        h.backward(hd.grad)
+        with ops.deferred_reductions():
+            h.backward(hd.grad)
         self.opt.gather_grads(self.enc_params)
 
     def capture(self, L: int):

@@ -254,14 +254,13 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restr
 // slice t / PB); every slice sums its chunks with four independent accumulators in a fixed
 // order, then the slices are added in slice order.  Small parameter counts (the lift's 16,
 // a conv's 20) therefore still use all 1024 threads instead of 16 lanes.
-__global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __restrict__ partial,
-                                                               float* __restrict__ out,
-                                                               int nchunk, int np, int PB) {
-  __shared__ float red[1024];
+__device__ __forceinline__ void reduce_partials_block(const float* __restrict__ partial,
+                                                      float* __restrict__ out, int nchunk, int np,
+                                                      int PB, int blk, float* red) {
   const int S = 1024 / PB;
   const int t = threadIdx.x;
   const int pl = t % PB, sl = t / PB;
-  const int p = blockIdx.x * PB + pl;
+  const int p = blk * PB + pl;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (sl < S && p < np) {
     int c = sl;
@@ -280,6 +279,35 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __re
     for (int k = 1; k < S; ++k) v += red[k * PB + pl];
     out[p] = v;
   }
+}
+
+__global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __restrict__ partial,
+                                                               float* __restrict__ out,
+                                                               int nchunk, int np, int PB) {
+  __shared__ float red[1024];
+  reduce_partials_block(partial, out, nchunk, np, PB, blockIdx.x, red);
+}
+
+// Several reductions in one launch (the deferred weight-gradient reductions of one backward
+// pass, blindno.ops.deferred_reductions): segment i owns workgroups [cum[i], cum[i+1]), each
+// reduced exactly as by reduce_partials_kernel, so the results are bit-identical to separate
+// launches.  Segments are passed by value (a graph capture bakes them in).
+constexpr int kRedSegs = 32;
+struct ReduceSegs {
+  const float* src[kRedSegs];
+  float* out[kRedSegs];
+  int nchunk[kRedSegs], np[kRedSegs], pb[kRedSegs];
+  int cum[kRedSegs + 1];
+  int nseg;
+};
+
+__global__ __launch_bounds__(1024) void reduce_partials_multi_kernel(ReduceSegs segs) {
+  __shared__ float red[1024];
+  const int b = blockIdx.x;
+  int sg = 0;
+  while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;    // uniform scan
+  reduce_partials_block(segs.src[sg], segs.out[sg], segs.nchunk[sg], segs.np[sg], segs.pb[sg],
+                        b - segs.cum[sg], red);
 }
 
 // ---------------------------------------------------------------- projection MLP
@@ -701,6 +729,33 @@ BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nc
   const int PB = np < 64 ? np : 64;
   reduce_partials_kernel<<<cdiv(np, PB), 1024, 0, (hipStream_t)stream>>>(partial, out, nchunk, np,
                                                                            PB);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_reduce_partials_multi(const void* const* partials, void* const* outs,
+                                              const int* nchunks, const int* nps, int nseg,
+                                              void* stream) {
+  if (nseg < 0) return (int)hipErrorInvalidValue;
+  for (int s0 = 0; s0 < nseg; s0 += kRedSegs) {
+    ReduceSegs segs{};
+    const int k = nseg - s0 < kRedSegs ? nseg - s0 : kRedSegs;
+    segs.nseg = k;
+    int blocks = 0;
+    for (int i = 0; i < k; ++i) {
+      const int nc = nchunks[s0 + i], np = nps[s0 + i];
+      if (nc < 1 || np < 1) return (int)hipErrorInvalidValue;
+      segs.src[i] = (const float*)partials[s0 + i];
+      segs.out[i] = (float*)outs[s0 + i];
+      segs.nchunk[i] = nc;
+      segs.np[i] = np;
+      segs.pb[i] = np < 64 ? np : 64;
+      segs.cum[i] = blocks;
+      blocks += cdiv(np, segs.pb[i]);
+    }
+    segs.cum[k] = blocks;
+    if (blocks == 0) continue;
+    reduce_partials_multi_kernel<<<blocks, 1024, 0, (hipStream_t)stream>>>(segs);
+  }
   return (int)hipGetLastError();
 }
 

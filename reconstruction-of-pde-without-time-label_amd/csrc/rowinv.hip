@@ -453,6 +453,12 @@ struct RowinvGeom {
 #ifndef ROWINV_MIN_ITEMS
 #define ROWINV_MIN_ITEMS 4096
 #endif
+// fewest work items for which the twiddle image is staged in LDS (with the 1024-block cap,
+// >= 4 items per workgroup); 8192 left the FNO_input layers of bags with U < 52 distinct
+// snapshots (Bn < 205 at 160^2) on the L2-read path, ~20% slower per launch (r02e profile)
+#ifndef ROWINV_LDSB_ITEMS
+#define ROWINV_LDSB_ITEMS 4096
+#endif
 // work items the wide kernel aims at when splitting rows into column chunks
 #ifndef ROWINV_WIDE_ITEMS
 #define ROWINV_WIDE_ITEMS 2048
@@ -476,7 +482,7 @@ RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   // staging pays when a workgroup's items read the table at least twice over (each item reads
   // TPW of its NT column tiles)
   const int64_t items_per_block = (g.nitems + 1023) / 1024;
-  g.ldsb = tbytes <= 48 * 1024 && g.nitems >= 8192 && items_per_block * tpw >= 2 * NT;
+  g.ldsb = tbytes <= 48 * 1024 && g.nitems >= ROWINV_LDSB_ITEMS && items_per_block * tpw >= 2 * NT;
   const int cap = g.ldsb ? 1024 : 2048;
   g.blocks = b < cap ? b : cap;
   g.lds = g.ldsb ? tbytes : 0;

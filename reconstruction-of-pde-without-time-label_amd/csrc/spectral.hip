@@ -800,6 +800,147 @@ BLINDNO_API int blindno_unpack_w2d_2(const float* dWt, float* dw1a, float* dw2a,
   return (int)hipGetLastError();
 }
 
+// Several blindno_pack_w2d in one launch: segment i packs (w1s[i], w2s[i]) of shape
+// (Ci, Co, m1, m2) at row count P1 into Wts[i] (m2, K1, Ci, Co) complex -- the spectral weights
+// of every layer of one FNO body (or of both grouped heads) before its forward chain.
+constexpr int kPackSegs = 16;
+struct PackSegs {
+  const float* w1[kPackSegs];
+  const float* w2[kPackSegs];
+  float2* Wt[kPackSegs];
+  int Ci[kPackSegs], Co[kPackSegs], m1[kPackSegs], m2[kPackSegs], P1[kPackSegs];
+  int cum[kPackSegs + 1];
+  int nseg;
+};
+
+__global__ __launch_bounds__(kBlock) void pack_w2d_multi_kernel(PackSegs segs) {
+  const int b = blockIdx.x;
+  int sg = 0;
+  while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;    // uniform scan
+  const int Ci = segs.Ci[sg], Co = segs.Co[sg], m1 = segs.m1[sg], m2 = segs.m2[sg];
+  const int P1 = segs.P1[sg];
+  const int K1 = kept_rows_count(m1, P1);
+  const int idx = (b - segs.cum[sg]) * kBlock + threadIdx.x;
+  if (idx >= m2 * K1 * Ci * Co) return;
+  const int o = idx % Co;
+  int t = idx / Co;
+  const int i = t % Ci;
+  t /= Ci;
+  const int j = t % K1;
+  const int k = t / K1;
+  const int r = kept_row(j, K1, m1, P1);
+  const bool second = r >= P1 - m1;
+  const float* src = second ? segs.w2[sg] : segs.w1[sg];
+  const int jj = second ? r - (P1 - m1) : r;
+  const float* p = src + ((((int64_t)i * Co + o) * m1 + jj) * m2 + k) * 2;
+  segs.Wt[sg][idx] = make_float2(p[0], p[1]);
+}
+
+BLINDNO_API int blindno_pack_w2d_multi(const void* const* w1s, const void* const* w2s,
+                                       void* const* Wts, const int* shapes, int nseg,
+                                       void* stream) {
+  // shapes: 5 ints per segment (Ci, Co, m1, m2, P1)
+  if (nseg < 0) return (int)hipErrorInvalidValue;
+  for (int s0 = 0; s0 < nseg; s0 += kPackSegs) {
+    PackSegs segs{};
+    const int k = nseg - s0 < kPackSegs ? nseg - s0 : kPackSegs;
+    segs.nseg = k;
+    int64_t blocks = 0;
+    for (int i = 0; i < k; ++i) {
+      const int* sh = shapes + 5 * (s0 + i);
+      if (sh[2] > sh[4] || sh[0] < 1 || sh[1] < 1 || sh[2] < 1 || sh[3] < 1) return (int)hipErrorInvalidValue;
+      const int64_t total = (int64_t)sh[3] * kept_rows_count(sh[2], sh[4]) * sh[0] * sh[1];
+      if (total >= INT32_MAX) return (int)hipErrorInvalidValue;
+      segs.w1[i] = (const float*)w1s[s0 + i];
+      segs.w2[i] = (const float*)w2s[s0 + i];
+      segs.Wt[i] = (float2*)Wts[s0 + i];
+      segs.Ci[i] = sh[0]; segs.Co[i] = sh[1]; segs.m1[i] = sh[2]; segs.m2[i] = sh[3]; segs.P1[i] = sh[4];
+      segs.cum[i] = (int)blocks;
+      blocks += (total + kBlock - 1) / kBlock;
+    }
+    segs.cum[k] = (int)blocks;
+    if (blocks == 0) continue;
+    if (blocks >= INT32_MAX) return (int)hipErrorInvalidValue;
+    pack_w2d_multi_kernel<<<(unsigned)blocks, kBlock, 0, (hipStream_t)stream>>>(segs);
+  }
+  return (int)hipGetLastError();
+}
+
+// Several unpacks in one launch (blindno.ops.deferred_reductions): segment i = one weight set
+// (dWt slice -> dw1, dw2) of shape (Ci, Co, m1, m2) at row count P1; workgroups
+// [cum[i], cum[i+1]) cover its 2 Ci Co m1 m2 complex entries, kBlock per workgroup.
+constexpr int kUnpackSegs = 16;
+struct UnpackSegs {
+  const float2* dWt[kUnpackSegs];
+  float* dw1[kUnpackSegs];
+  float* dw2[kUnpackSegs];
+  int Ci[kUnpackSegs], Co[kUnpackSegs], m1[kUnpackSegs], m2[kUnpackSegs], P1[kUnpackSegs];
+  int cum[kUnpackSegs + 1];
+  int nseg;
+};
+
+__global__ __launch_bounds__(kBlock) void unpack_w2d_multi_kernel(UnpackSegs segs) {
+  const int b = blockIdx.x;
+  int sg = 0;
+  while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;    // uniform scan
+  const int Ci = segs.Ci[sg], Co = segs.Co[sg], m1 = segs.m1[sg], m2 = segs.m2[sg];
+  const int P1 = segs.P1[sg];
+  const int K1 = kept_rows_count(m1, P1);
+  const int per = Ci * Co * m1 * m2;
+  const int idx = (b - segs.cum[sg]) * kBlock + threadIdx.x;
+  if (idx >= 2 * per) return;
+  const int which = idx >= per;
+  const int e = which ? idx - per : idx;
+  const int k = e % m2;
+  int t = e / m2;
+  const int jj = t % m1;
+  t /= m1;
+  const int o = t % Co;
+  const int i = t / Co;
+  int j = -1;
+  if (which) {
+    const int r = P1 - m1 + jj;
+    j = (K1 == P1) ? r : m1 + jj;
+  } else if (jj < P1 - m1) {
+    j = jj;                       // otherwise shadowed by weights2 (overlapping rows)
+  }
+  float2 v = make_float2(0.f, 0.f);
+  if (j >= 0) v = segs.dWt[sg][(((int64_t)k * K1 + j) * Ci + i) * Co + o];
+  float* dst = (which ? segs.dw2[sg] : segs.dw1[sg]) + (int64_t)e * 2;
+  dst[0] = v.x;
+  dst[1] = v.y;
+}
+
+BLINDNO_API int blindno_unpack_w2d_multi(const void* const* dWts, void* const* dw1s,
+                                         void* const* dw2s, const int* shapes, int nseg,
+                                         void* stream) {
+  // shapes: 5 ints per segment (Ci, Co, m1, m2, P1)
+  if (nseg < 0) return (int)hipErrorInvalidValue;
+  for (int s0 = 0; s0 < nseg; s0 += kUnpackSegs) {
+    UnpackSegs segs{};
+    const int k = nseg - s0 < kUnpackSegs ? nseg - s0 : kUnpackSegs;
+    segs.nseg = k;
+    int64_t blocks = 0;
+    for (int i = 0; i < k; ++i) {
+      const int* sh = shapes + 5 * (s0 + i);
+      if (sh[2] > sh[4] || sh[0] < 1 || sh[1] < 1 || sh[2] < 1 || sh[3] < 1) return (int)hipErrorInvalidValue;
+      const int64_t total = 2 * (int64_t)sh[0] * sh[1] * sh[2] * sh[3];
+      if (total >= INT32_MAX) return (int)hipErrorInvalidValue;
+      segs.dWt[i] = (const float2*)dWts[s0 + i];
+      segs.dw1[i] = (float*)dw1s[s0 + i];
+      segs.dw2[i] = (float*)dw2s[s0 + i];
+      segs.Ci[i] = sh[0]; segs.Co[i] = sh[1]; segs.m1[i] = sh[2]; segs.m2[i] = sh[3]; segs.P1[i] = sh[4];
+      segs.cum[i] = (int)blocks;
+      blocks += (total + kBlock - 1) / kBlock;
+    }
+    segs.cum[k] = (int)blocks;
+    if (blocks == 0) continue;
+    if (blocks >= INT32_MAX) return (int)hipErrorInvalidValue;
+    unpack_w2d_multi_kernel<<<(unsigned)blocks, kBlock, 0, (hipStream_t)stream>>>(segs);
+  }
+  return (int)hipGetLastError();
+}
+
 BLINDNO_API int blindno_pack_w1d(const float* w, float* Wt, int Ci, int Co, int m, int dir,
                                  void* stream) {
   const int64_t total = (int64_t)Ci * Co * m;
