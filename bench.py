@@ -116,6 +116,9 @@ def parse():
     ap.add_argument("--overlap", default="auto", choices=("auto", "on", "off"),
                     help="two-graph step with the heads' gradient all-reduce beside the encoder's "
                          "backward (auto: at N > 1)")
+    ap.add_argument("--mix", default=None, choices=("fp32", "fp16"),
+                    help="channel-mix operand precision of the 2D spectral layers (default: fp16 "
+                         "for config E as BASELINE.json names it, fp32 otherwise)")
     ap.add_argument("--timer-steps", type=int, default=4,
                     help="eager steps after the timed region that time the dominant kernel (graph mode)")
     return ap.parse_args()
@@ -151,6 +154,8 @@ def main():
     N = a.grid or cfg["N"]
     T = a.T or cfg["T"]
     B = a.batch or cfg["B"]
+    mix = a.mix or ("fp16" if a.config == "E" else "fp32")
+    blindno.set_mix_precision(mix)
     model, params, out_ch = build_model(a.config, N, dev)
     model.train()
     opt = FlatAdam(params, lr=cfg["lr"])
@@ -248,7 +253,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if mix == "fp32" else "f32 (fp16 channel-mix operands, fp32 accumulate)",
             "data": "synthetic (standardised N(0,1) bags resident in HBM; reference datasets not shipped)",
             "config": {"workload": f"{cfg['desc']} ({a.config}), grid {'x'.join([str(N)] * cfg['dim'])}",
                        "per_gpu_batch": B, "global_batch": B * world, "T": T,
@@ -271,7 +276,7 @@ def main():
             # the reference's CPU path on the same weights / inputs: accuracy parity of the
             # benched step (the "rel-L2 drift error" half of BASELINE's metric), then its timing
             if not a.no_parity:
-                res["parity"] = parity_check(a.config, model, graphed, opt, xb, yb, grid, T)
+                res["parity"] = parity_check(a.config, model, graphed, opt, xb, yb, grid, T, mix=mix)
             if a.config == "C" and not a.no_cpu:
                 res["cpu_baseline"] = cpu_baseline(a.config, model, xb, yb, grid, T, budget=a.cpu_seconds)
         res["loss_mean"] = float(loss_acc) / (a.warmup + a.steps)
@@ -344,7 +349,12 @@ def _cpu_step(cfg_name, p, x, y, grid, idx):
     return out.detach(), loss.detach()
 
 
-def parity_check(cfg_name, model, graphed, opt, xb, yb, grid, T, seed=4321):
+# separately stated tolerance of the fp16 channel mix (config E): fp16 operands carry a unit
+# roundoff of 2^-11 = 4.9e-4, so the spectral branch of every layer is ~1e-3 off fp32
+MIX16_TOL = {"fields": 5e-3, "grads": 2e-2}
+
+
+def parity_check(cfg_name, model, graphed, opt, xb, yb, grid, T, seed=4321, mix="fp32"):
     """Accuracy of the benched GPU step (graph replay: deduplicated bag, grouped heads) on one
     recorded bag draw, against (1) the reference's fp32 CPU step (oracle.cpu_ref: pocketfft,
     F.gelu, F.linear -- how the reference computes) and (2) the same step in float64 (same
@@ -414,8 +424,9 @@ def parity_check(cfg_name, model, graphed, opt, xb, yb, grid, T, seed=4321):
            "gpu_vs_fp64": dict(fmt(gpu64), grad_max=float(f"{gw:.3e}"), grad_worst=gk,
                                loss=float(f"{abs(float(loss_gpu) - float(loss64)) / abs(float(loss64)):.3e}")),
            "ref_fp32_vs_fp64": dict(fmt(ref64), grad_max=float(f"{rw:.3e}"), grad_worst=rk),
-           "tolerance": {"fields": 1e-5, "grads": 1e-4}}
-    res["pass"] = bool(gpu64["fwd"] <= 1e-5 and gw <= 1e-4 and gpu32["fwd"] <= 1e-5)
+           "tolerance": {"fields": 1e-5, "grads": 1e-4} if mix == "fp32" else dict(MIX16_TOL, mix="fp16")}
+    tf, tg = (1e-5, 1e-4) if mix == "fp32" else (MIX16_TOL["fields"], MIX16_TOL["grads"])
+    res["pass"] = bool(gpu64["fwd"] <= tf and gw <= tg and gpu32["fwd"] <= tf)
     return res
 
 

@@ -15,7 +15,7 @@ from .deeponet import FFN, DeepOnetNoBiasOrg, FeedForwardNN  # noqa: F401
 from .encoders import ConvBlock, Encoder, Encoder2D  # noqa: F401
 from .unet import (PermInvUNet_attn, PermInvUNet_attn1D, PermInvUNet_attn1D_bag,  # noqa: F401
                    PermInvUNet_attn1D_bag_GPE, PermInvUNet_attn1D_bag_V, PermInvUNet_attn_NC)
-from .ops import mse_loss, pad_amount  # noqa: F401
+from .ops import mse_loss, pad_amount, set_mix_precision  # noqa: F401
 from . import torch_ops  # noqa: F401  (registers torch.ops.blindno.*)
 
 __version__ = "0.1.0"

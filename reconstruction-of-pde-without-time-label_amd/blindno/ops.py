@@ -21,6 +21,24 @@ from ._lib import BlindnoError, call, ptr, query, stream_ptr
 
 F32 = torch.float32
 
+# Channel-mix precision of the 2D spectral layers (BASELINE config E: "fp16 channel-mix + fp32
+# spectral accumulate"): "fp32" (default, the reference's arithmetic) or "fp16" (fp16 operands,
+# fp32 accumulation, block-scaled spectra; csrc/spectral.hip coldft_mix_kernel H16).  The DFT
+# stages and the weight gradient stay fp32.  Read when a layer is launched (a captured graph
+# keeps the mode it was captured with).
+MIX_F16 = False
+
+
+def set_mix_precision(name: str) -> None:
+    global MIX_F16
+    if name not in ("fp32", "fp16"):
+        raise BlindnoError(f"mix precision must be 'fp32' or 'fp16', got {name!r}")
+    MIX_F16 = name == "fp16"
+
+
+def _mixdir(direction: int) -> int:
+    return direction | (2 if MIX_F16 else 0)
+
 # ---------------------------------------------------------------------------- helpers
 
 
@@ -171,7 +189,7 @@ _DEFER = None
 class _Deferred:
     def __init__(self):
         self.red = []      # (partial, out, nchunk, np)
-        self.unp = []      # (dWt slice, dw1, dw2, (Ci, Co, m1, m2, P1))
+        self.unp = []      # (dWt slice, dw1, dw2, (Ci, Co, m1, m2, P1), base of dw1 / dw2)
 
     def flush(self):
         if self.red:
@@ -211,13 +229,20 @@ def reduce_partials(partial: torch.Tensor, nchunk: int, np_: int) -> torch.Tenso
     return out
 
 
-def unpack_w2d_into(dWt: torch.Tensor, dw1: torch.Tensor, dw2: torch.Tensor, P1: int):
-    """dWt (m2, K1, Ci, Co, 2) -> dw1, dw2 in the reference layout (Ci, Co, m1, m2, 2)."""
-    Ci, Co, m1, m2 = dw1.shape[:4]
+def unpack_w2d(dWt: torch.Tensor, like: torch.Tensor, P1: int):
+    """dWt (m2, K1, Ci, Co, 2) -> (dw1, dw2) in the reference layout of ``like`` (Ci, Co, m1,
+    m2, 2).  Both are views of one fresh (2, ...) buffer: deferred, the list keeps the BASE
+    alive, not the returned views, so autograd's AccumulateGrad still adopts the views as the
+    parameters' .grad instead of cloning them (a clone before the flush would copy unwritten
+    memory -- as with reduce_partials, whose returned gradients are slices of ``out``)."""
+    Ci, Co, m1, m2 = like.shape[:4]
+    base = torch.empty((2,) + tuple(like.shape), dtype=like.dtype, device=like.device)
     if _DEFER is not None:
-        _DEFER.unp.append((dWt, dw1, dw2, (Ci, Co, m1, m2, P1)))
-        return
-    call("blindno_unpack_w2d", ptr(dWt), ptr(dw1), ptr(dw2), Ci, Co, m1, m2, P1, stream_ptr())
+        _DEFER.unp.append((dWt, base[0], base[1], (Ci, Co, m1, m2, P1), base))
+    else:
+        call("blindno_unpack_w2d", ptr(dWt), ptr(base[0]), ptr(base[1]), Ci, Co, m1, m2, P1,
+             stream_ptr())
+    return base[0], base[1]
 
 
 # ---------------------------------------------------------------------------- kernel wrappers
@@ -241,7 +266,7 @@ def k_colpass(At, Wt, Bn, Ci, Co, P1, m1, m2, P2, direction):
     Z = _empty(Bn, P1, m2, cout, 2, like=At)
     FB, GB = twiddle_cols(P1, m1, At.device)
     call("blindno_colpass", ptr(At), ptr(Wt), ptr(Xs), ptr(Y), ptr(Z), ptr(FB), ptr(GB), Bn,
-         Ci, Co, P1, m1, m2, P2, direction, stream_ptr())
+         Ci, Co, P1, m1, m2, P2, _mixdir(direction), stream_ptr())
     return Xs, Z
 
 
@@ -289,10 +314,7 @@ def pack_w2d_many(pairs, P1):
 
 
 def k_unpack_w2d(dWt, w1, P1):
-    dw1 = torch.empty_like(w1)
-    dw2 = torch.empty_like(w1)
-    unpack_w2d_into(dWt, dw1, dw2, P1)
-    return dw1, dw2
+    return unpack_w2d(dWt, w1, P1)
 
 
 def k_pack_w1d(w):
@@ -653,7 +675,7 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
         Y = _empty(Bn, meta.m2, C, K1p, 2, like=inp)
         Z = _empty(Bn, P1, meta.m2, C, 2, like=inp)
         call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(X), ptr(Y), ptr(Z), ptr(FB), ptr(GB), G,
-             Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, 0, stream_ptr())
+             Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, _mixdir(0), stream_ptr())
         z = _empty(Bn, C, P1, P2, like=inp)
         call("blindno_rowidft_epi_g", ptr(Z), ptr(src), ptr(_sub(small, offs[2 + 2 * k])),
              ptr(_sub(small, offs[3 + 2 * k])), ptr(z), ptr(twiddle_rowinv(P2, meta.m2, inp.device)),
@@ -714,17 +736,16 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         Y = _empty(Bn, meta.m2, C, K1p, 2, like=inp)
         GZ = _empty(Bn, P1, meta.m2, C, 2, like=inp)
         call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(Gs), ptr(Y), ptr(GZ), ptr(FB), ptr(GB), G,
-             Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, 1, stream_ptr())
+             Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, _mixdir(1), stream_ptr())
         dWt = _empty(G, meta.m2, K1, C, C, 2, like=inp)
         ns = query("blindno_mix_wgrad_nsplit", Bg, C, C, K1, meta.m2)
         part = _empty(ns, G, meta.m2 * K1 * C * C * 2, like=inp) if ns > 1 else None
         call("blindno_mix_wgrad_g", ptr(Xs[k]), ptr(Gs), ptr(dWt), ptr(part) if part is not None else None,
              ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
-        dws = [torch.empty_like(prms[g][off]) for g in range(G) for _ in range(2)]
         if _DEFER is not None:
-            for g in range(G):
-                unpack_w2d_into(dWt[g], dws[2 * g], dws[2 * g + 1], P1)
+            dws = [d for g in range(G) for d in unpack_w2d(dWt[g], prms[g][off], P1)]
         else:
+            dws = [torch.empty_like(prms[g][off]) for g in range(G) for _ in range(2)]
             call("blindno_unpack_w2d_2", ptr(dWt), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), C,
                  C, meta.m1, meta.m2, P1, stream_ptr())
         for g in range(G):

@@ -232,7 +232,17 @@ __device__ __forceinline__ void load4c(const float2* src, int len, bool vec, flo
 // layers launch one workgroup per (sample, mode) pair -- one wave per SIMD -- so a one-block
 // lookahead leaves each step waiting a full memory latency (measured ~16 us for 10 steps)
 constexpr int kFullHB = 10;
-template <int DIR, bool FULL>
+// H16 (config E, blindno.ops.set_mix_precision("fp16")): the channel mix takes fp16 operands
+// with fp32 accumulation -- each complex multiply-add is two v_dot2c_f32_f16 (packed fp16
+// pairs, exact products, fp32 sum).  The column spectra are block-scaled first: the workgroup's
+// largest |Re|, |Im| is brought to [2^14, 2^15) by an exact power of two, undone after the sum,
+// so neither the unnormalised forward spectra (up to P1 P2 |x|) overflow fp16 nor the small
+// gradient spectra of the adjoint flush to zero.  The weights are converted unscaled (their
+// magnitudes sit far inside fp16's normal range).  Not on the matrix cores: the mix is a
+// batch of complex GEMVs (one Ci x Co matrix per kept mode, one row per sample), which would
+// fill a quarter of an MFMA tile at best.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+template <int DIR, bool FULL, bool H16>
 __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restrict__ At,
                                                          const float2* __restrict__ Wt,
                                                          const f32x4* __restrict__ FB,
@@ -312,6 +322,28 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
   }
   __syncthreads();
 
+  // H16: block scale 2^e with max |component| * 2^e in [2^14, 2^15)
+  float hs = 1.0f, hinv = 1.0f;
+  if constexpr (H16) {
+    __shared__ float smax[4];
+    float mx = 0.f;
+    for (int e = threadIdx.x; e < rows * K1p; e += blockDim.x) {
+      const float2 v = sX[(e / K1p) * LDX + e % K1p];
+      mx = fmaxf(mx, fmaxf(fabsf(v.x), fabsf(v.y)));
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    if (lane == 0) smax[wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    if (mx > 0.f && mx < 3.0e38f) {
+      int ex;
+      frexpf(mx, &ex);                            // mx in [2^(ex-1), 2^ex)
+      hs = ldexpf(1.0f, 15 - ex);
+      hinv = ldexpf(1.0f, ex - 15);
+    }
+  }
+
   // the mix: output channel o fastest across threads, so the weight loads W[k][j][c][o] of
   // neighbouring threads are contiguous (j fastest put every lane on its own cache line)
   const int nout = np * Cout * K1p;
@@ -327,17 +359,36 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
                               : Wt;
       const float2* wj = wg + ((int64_t)k * K1 + j) * Ci * Co;
       const float2* xp = sX + p * Cin * LDX + j;
+      if constexpr (H16) {
 #pragma unroll 4
-      for (int c = 0; c < Cin; ++c) {
-        const float2 a = xp[c * LDX];
-        if (DIR == 0) {
-          const float2 w = wj[c * Co + o];
-          re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
-          im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
-        } else {
-          const float2 w = wj[o * Co + c];            // conj(w) * a
-          re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
-          im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+        for (int c = 0; c < Cin; ++c) {
+          const float2 a = xp[c * LDX];
+          const f16x2 ah = {(_Float16)(a.x * hs), (_Float16)(a.y * hs)};
+          const float2 w = DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
+          const _Float16 wr = (_Float16)w.x, wi = (_Float16)w.y;
+          if (DIR == 0) {                             // a w
+            re = __builtin_amdgcn_fdot2(ah, (f16x2){wr, (_Float16)(-wi)}, re, false);
+            im = __builtin_amdgcn_fdot2(ah, (f16x2){wi, wr}, im, false);
+          } else {                                    // conj(w) a
+            re = __builtin_amdgcn_fdot2(ah, (f16x2){wr, wi}, re, false);
+            im = __builtin_amdgcn_fdot2(ah, (f16x2){(_Float16)(-wi), wr}, im, false);
+          }
+        }
+        re *= hinv;
+        im *= hinv;
+      } else {
+#pragma unroll 4
+        for (int c = 0; c < Cin; ++c) {
+          const float2 a = xp[c * LDX];
+          if (DIR == 0) {
+            const float2 w = wj[c * Co + o];
+            re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
+            im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
+          } else {
+            const float2 w = wj[o * Co + c];            // conj(w) * a
+            re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
+            im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+          }
         }
       }
       if (DIR == 0) {
@@ -660,9 +711,12 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
                                   const float* FB, const float* GB, int Gw, int64_t wtgs, int Bn,
                                   int Ci, int Co, int P1, int m1, int m2, int P2, int dir,
                                   void* stream) {
-  if (Bn <= 0 || m1 <= 0 || m1 > P1 || m2 <= 0 || m2 > P2 / 2 + 1 || (dir != 0 && dir != 1) ||
-      Gw < 1 || Bn % Gw)
+  // dir bit 0: 0 forward / 1 adjoint; bit 1: fp16-operand mix (H16 above)
+  if (Bn <= 0 || m1 <= 0 || m1 > P1 || m2 <= 0 || m2 > P2 / 2 + 1 || (dir & ~3) || Gw < 1 ||
+      Bn % Gw)
     return (int)hipErrorInvalidValue;
+  const bool h16 = (dir & 2) != 0;
+  dir &= 1;
   const int Bg = Bn / Gw;
   if (Gw == 1) wtgs = 0;
   const int K1 = kept_rows_count(m1, P1);
@@ -683,17 +737,19 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const dim3 g1((unsigned)cdiv(npairs, G));
   // full operand prefetch when the launch is too small to hide latency with waves
   const bool full = (P1 + 15) / 16 <= kFullHB && (int64_t)g1.x * 4 < 4096;
-#define CM_(D_, F_)                                                                         \
-  coldft_mix_kernel<D_, F_><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,      \
-                                                 (const f32x4*)FB, (float2*)Xs, (float2*)Y, \
-                                                 (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, \
-                                                 Bg, wtgs)
+#define CM3_(D_, F_, H_)                                                                    \
+  coldft_mix_kernel<D_, F_, H_><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,  \
+                                                     (const f32x4*)FB, (float2*)Xs, (float2*)Y, \
+                                                     (int)npairs, Ci, Co, P1, m1, m2, P2, G, \
+                                                     vec, Bg, wtgs)
+#define CM_(D_, F_) do { if (h16) CM3_(D_, F_, true); else CM3_(D_, F_, false); } while (0)
   if (dir == 0) {
     if (full) CM_(0, true); else CM_(0, false);
   } else {
     if (full) CM_(1, true); else CM_(1, false);
   }
 #undef CM_
+#undef CM3_
   int e = (int)hipGetLastError();
   if (e) return e;
   const int Ht = (P1 + 15) / 16;
