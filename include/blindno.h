@@ -266,6 +266,10 @@ int blindno_bagattn_bwd(const float* grid, const float* u, const float* dy, cons
  * partial[nblk] and grad = gscale * 2 (p - t) / n (grad may be NULL). */
 int blindno_mse(const float* p, const float* t, float* partial, float* grad, int64_t n,
                 int nblk, const float* gscale, blindno_stream_t stream);
+/* loss[0] = (sum_{b < nblk} partial[b]) / n, fixed order (the forward scalar of MSELoss from
+ * blindno_mse's per-block partials). */
+int blindno_mse_finish(const float* partial, int nblk, int64_t n, float* loss,
+                       blindno_stream_t stream);
 
 /* Per-row sums of squares in fp64 for relative-L2 metrics (2d_FPE/train_fno.py:160-163,
  * eval_fno.py:124-128, 2d_Non_conservative_FPE/compute_time_error.py:321-333).

@@ -1116,6 +1116,12 @@ class BagAttnFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------- loss
 
 
+def _mse_blocks(n):
+    # ~1024 elements per workgroup (4 per thread): a config-C output (4 x 128^2 x 2) gets 128
+    # workgroups instead of 32
+    return max(1, min(1024, (n + 1023) // 1024))
+
+
 class MSEFn(torch.autograd.Function):
     """nn.MSELoss() (mean reduction) with a fused gradient kernel."""
 
@@ -1124,18 +1130,20 @@ class MSEFn(torch.autograd.Function):
         require_device(pred, target)
         pred, target = _c(pred), _c(target)
         n = pred.numel()
-        nblk = max(1, min(1024, (n + 4095) // 4096))
+        nblk = _mse_blocks(n)
         partial = _empty(nblk, like=pred)
         call("blindno_mse", ptr(pred), ptr(target), ptr(partial), None, n, nblk, None,
              stream_ptr())
+        loss = _empty((), like=pred)
+        call("blindno_mse_finish", ptr(partial), nblk, n, ptr(loss), stream_ptr())
         ctx.save_for_backward(pred, target)
-        return partial.sum() / n
+        return loss
 
     @staticmethod
     def backward(ctx, g):
         pred, target = ctx.saved_tensors
         n = pred.numel()
-        nblk = max(1, min(1024, (n + 4095) // 4096))
+        nblk = _mse_blocks(n)
         partial = _empty(nblk, like=pred)
         grad = torch.empty_like(pred)
         g = _c(g.reshape(1))

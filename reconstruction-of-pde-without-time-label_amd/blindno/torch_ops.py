@@ -424,7 +424,7 @@ def _(pred, target):
 def mse_loss_backward(g: torch.Tensor, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     pred, target = ops._c(pred), ops._c(target)
     n = pred.numel()
-    nblk = max(1, min(1024, (n + 4095) // 4096))
+    nblk = ops._mse_blocks(n)
     partial = ops._empty(nblk, like=pred)
     grad = torch.empty_like(pred)
     call("blindno_mse", ptr(pred), ptr(target), ptr(partial), ptr(grad), n, nblk, ptr(ops._c(g.reshape(1))),

@@ -569,6 +569,23 @@ __global__ __launch_bounds__(kBlock) void mse_kernel(const float* __restrict__ p
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
+// loss = (sum of the nblk partials, fixed order) / n: the scalar of nn.MSELoss's forward in one
+// single-workgroup launch (instead of a torch sum and a torch division)
+__global__ __launch_bounds__(kBlock) void mse_finish_kernel(const float* __restrict__ partial,
+                                                            int nblk, int64_t n,
+                                                            float* __restrict__ loss) {
+  __shared__ float red[kBlock];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += kBlock) acc += partial[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kBlock / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] / (float)n;
+}
+
 // Row r holds n points of `stride` floats: out[2r] = sum (a[.+off_a] - b[.+off_b])^2,
 // out[2r+1] = sum b[.+off_b]^2 or, with den_all, over all `stride` channels of b (the train
 // loop's denominator quirk, 2d_FPE/train_fno.py:161,163).  fp64 accumulation.
@@ -880,6 +897,13 @@ BLINDNO_API int blindno_bagmean_bwd(const float* dy, const float* w, float* s, i
                                     int d, int width, int L, void* stream) {
   bagmean_bwd_kernel<<<grid_for((int64_t)B * S), kBlock, 0, (hipStream_t)stream>>>(
       dy, w, s, B, S, d, width, L);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_mse_finish(const float* partial, int nblk, int64_t n, float* loss,
+                                   void* stream) {
+  if (nblk < 1 || n < 1) return (int)hipErrorInvalidValue;
+  mse_finish_kernel<<<1, kBlock, 0, (hipStream_t)stream>>>(partial, nblk, n, loss);
   return (int)hipGetLastError();
 }
 
