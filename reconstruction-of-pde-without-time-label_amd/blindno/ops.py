@@ -231,18 +231,19 @@ def reduce_partials(partial: torch.Tensor, nchunk: int, np_: int) -> torch.Tenso
 
 def unpack_w2d(dWt: torch.Tensor, like: torch.Tensor, P1: int):
     """dWt (m2, K1, Ci, Co, 2) -> (dw1, dw2) in the reference layout of ``like`` (Ci, Co, m1,
-    m2, 2).  Both are views of one fresh (2, ...) buffer: deferred, the list keeps the BASE
+    m2, 2).  Deferred, both are views of one fresh (2, ...) buffer and the list keeps the BASE
     alive, not the returned views, so autograd's AccumulateGrad still adopts the views as the
     parameters' .grad instead of cloning them (a clone before the flush would copy unwritten
     memory -- as with reduce_partials, whose returned gradients are slices of ``out``)."""
     Ci, Co, m1, m2 = like.shape[:4]
-    base = torch.empty((2,) + tuple(like.shape), dtype=like.dtype, device=like.device)
     if _DEFER is not None:
+        base = torch.empty((2,) + tuple(like.shape), dtype=like.dtype, device=like.device)
         _DEFER.unp.append((dWt, base[0], base[1], (Ci, Co, m1, m2, P1), base))
-    else:
-        call("blindno_unpack_w2d", ptr(dWt), ptr(base[0]), ptr(base[1]), Ci, Co, m1, m2, P1,
-             stream_ptr())
-    return base[0], base[1]
+        return base[0], base[1]
+    # two separate tensors (torch custom ops may not return aliasing outputs)
+    dw1, dw2 = torch.empty_like(like), torch.empty_like(like)
+    call("blindno_unpack_w2d", ptr(dWt), ptr(dw1), ptr(dw2), Ci, Co, m1, m2, P1, stream_ptr())
+    return dw1, dw2
 
 
 # ---------------------------------------------------------------------------- kernel wrappers
