@@ -242,7 +242,11 @@ constexpr int kFullHB = 10;
 // batch of complex GEMVs (one Ci x Co matrix per kept mode, one row per sample), which would
 // fill a quarter of an MFMA tile at best.
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-template <int DIR, bool FULL, bool H16>
+// WPF: the mix weights of this thread's (up to kWpfE) outputs are loaded into registers at
+// kernel entry, so their latency hides behind the column DFT (in the loop they were kWpfC
+// dependent-latency rounds per output, the bulk of the head layers' column pass)
+constexpr int kWpfE = 4, kWpfC = 16;
+template <int DIR, bool FULL, bool H16, bool WPF>
 __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restrict__ At,
                                                          const float2* __restrict__ Wt,
                                                          const f32x4* __restrict__ FB,
@@ -266,6 +270,37 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
   const int wave = uniform_int(threadIdx.x >> 6);
   const int r16 = lane & 15, kq = lane >> 4;
   const float inv = 1.0f / ((float)P1 * (float)P2);
+  const int nout = np * Cout * K1p;
+
+  // weights of output e = (p, j, o), o fastest: W[k][j][c][o] (DIR 0) / W[k][j][o][c] (DIR 1)
+  auto wrow = [&](int e, int& o, int& j, int& p, int& k) -> const float2* {
+    o = e % Cout;
+    const int t = e / Cout;
+    j = t % K1p;
+    p = t / K1p;
+    k = (q0 + p) % m2;
+    const float2* wg = wtgs ? reinterpret_cast<const float2*>(
+                                  reinterpret_cast<const float*>(Wt) + ((q0 + p) / m2 / Bg) * wtgs)
+                            : Wt;
+    return wg + ((int64_t)k * K1 + (j < K1 ? j : 0)) * Ci * Co;
+  };
+  float2 wpre[WPF ? kWpfE : 1][WPF ? kWpfC : 1];
+  if constexpr (WPF) {
+#pragma unroll
+    for (int i = 0; i < kWpfE; ++i) {
+      const int e = threadIdx.x + i * 256;
+      int o = 0, j = 0, p = 0, k = 0;
+      const float2* wj = wrow(e < nout ? e : 0, o, j, p, k);
+      // unconditional loads from clamped (always valid) offsets and no select: entries of
+      // c >= Cin, e >= nout or j >= K1 are never used by the mix (a guarded load per value
+      // compiled to one branch and one wait per load)
+#pragma unroll
+      for (int c = 0; c < kWpfC; ++c) {
+        const int cc = c < Cin ? c : 0;
+        wpre[i][c] = DIR == 0 ? wj[cc * Co + o] : wj[o * Co + cc];
+      }
+    }
+  }
 
   for (int item = wave; item < Mt * Jt; item += 4) {
     const int mt = item / Jt, jt = item % Jt;
@@ -346,25 +381,23 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
 
   // the mix: output channel o fastest across threads, so the weight loads W[k][j][c][o] of
   // neighbouring threads are contiguous (j fastest put every lane on its own cache line)
-  const int nout = np * Cout * K1p;
-  for (int e = threadIdx.x; e < nout; e += blockDim.x) {
-    const int o = e % Cout;
-    const int t = e / Cout;
-    const int j = t % K1p, p = t / K1p;
-    const int k = (q0 + p) % m2;
+  auto mix_one = [&](int e, const float2* wreg) {
+    int o, j, p, k;
+    const float2* wj = wrow(e, o, j, p, k);
     float re = 0.f, im = 0.f;
     if (j < K1) {
-      const float2* wg = wtgs ? reinterpret_cast<const float2*>(
-                                    reinterpret_cast<const float*>(Wt) + ((q0 + p) / m2 / Bg) * wtgs)
-                              : Wt;
-      const float2* wj = wg + ((int64_t)k * K1 + j) * Ci * Co;
       const float2* xp = sX + p * Cin * LDX + j;
+      auto wload = [&](int c) -> float2 {
+        if constexpr (WPF) return wreg[c];
+        return DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
+      };
       if constexpr (H16) {
-#pragma unroll 4
-        for (int c = 0; c < Cin; ++c) {
+#pragma unroll (WPF ? kWpfC : 4)
+        for (int c = 0; c < (WPF ? kWpfC : Cin); ++c) {
+          if (WPF && c >= Cin) break;
           const float2 a = xp[c * LDX];
           const f16x2 ah = {(_Float16)(a.x * hs), (_Float16)(a.y * hs)};
-          const float2 w = DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
+          const float2 w = wload(c);
           const _Float16 wr = (_Float16)w.x, wi = (_Float16)w.y;
           if (DIR == 0) {                             // a w
             re = __builtin_amdgcn_fdot2(ah, (f16x2){wr, (_Float16)(-wi)}, re, false);
@@ -377,15 +410,15 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
         re *= hinv;
         im *= hinv;
       } else {
-#pragma unroll 4
-        for (int c = 0; c < Cin; ++c) {
+#pragma unroll (WPF ? kWpfC : 4)
+        for (int c = 0; c < (WPF ? kWpfC : Cin); ++c) {
+          if (WPF && c >= Cin) break;
           const float2 a = xp[c * LDX];
+          const float2 w = wload(c);
           if (DIR == 0) {
-            const float2 w = wj[c * Co + o];
             re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
             im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
-          } else {
-            const float2 w = wj[o * Co + c];            // conj(w) * a
+          } else {                                    // conj(w) * a
             re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
             im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
           }
@@ -398,6 +431,15 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
       }
     }
     Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
+  };
+  if constexpr (WPF) {
+#pragma unroll
+    for (int i = 0; i < kWpfE; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < nout) mix_one(e, wpre[i]);
+    }
+  } else {
+    for (int e = threadIdx.x; e < nout; e += blockDim.x) mix_one(e, nullptr);
   }
 }
 
@@ -405,6 +447,7 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
 // tile, 64 spectrum rows (k, o)); one 16-row MFMA tile per wave; the result is transposed
 // through LDS so that each h row of Z is written as one contiguous run.  tiled: Z in the
 // A-tile order of the wide row inverse instead (rowinv_tile_layout, rowinv.hip).
+constexpr int kColJt = 4;        // K1 <= 64 kept rows: full operand prefetch
 __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__ Y,
                                                       const f32x4* __restrict__ GB,
                                                       float2* __restrict__ Z, int Cout, int P1,
@@ -426,10 +469,27 @@ __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__
     const float2* yr = Y + ((int64_t)n * R + (rok ? row : 0)) * K1p;
     const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
     f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
-    for (int jb = 0; jb < Jt; ++jb) {
-      float re[4], im[4];
-      load4c(yr + jb * 16 + kq * 4, rok ? 4 : 0, true, re, im);
-      cmfma4(re, im, gb[jb * 128], gb[jb * 128 + 1], dr, di);
+    if (Jt <= kColJt) {
+      // every K block's operands in flight before the first MFMA (one memory latency)
+      float re[kColJt][4], im[kColJt][4];
+      f32x4 g0[kColJt], g1[kColJt];
+#pragma unroll
+      for (int jb = 0; jb < kColJt; ++jb) {
+        if (jb < Jt) {
+          load4c(yr + jb * 16 + kq * 4, rok ? 4 : 0, true, re[jb], im[jb]);
+          g0[jb] = gb[jb * 128];
+          g1[jb] = gb[jb * 128 + 1];
+        }
+      }
+#pragma unroll
+      for (int jb = 0; jb < kColJt; ++jb)
+        if (jb < Jt) cmfma4(re[jb], im[jb], g0[jb], g1[jb], dr, di);
+    } else {
+      for (int jb = 0; jb < Jt; ++jb) {
+        float re[4], im[4];
+        load4c(yr + jb * 16 + kq * 4, rok ? 4 : 0, true, re, im);
+        cmfma4(re, im, gb[jb * 128], gb[jb * 128 + 1], dr, di);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) sZ[r16][wave * 16 + kq * 4 + r] = make_float2(dr[r], di[r]);
@@ -737,11 +797,14 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const dim3 g1((unsigned)cdiv(npairs, G));
   // full operand prefetch when the launch is too small to hide latency with waves
   const bool full = (P1 + 15) / 16 <= kFullHB && (int64_t)g1.x * 4 < 4096;
-#define CM3_(D_, F_, H_)                                                                    \
-  coldft_mix_kernel<D_, F_, H_><<<g1, 256, sh, st>>>((const float2*)At, (const float2*)Wt,  \
-                                                     (const f32x4*)FB, (float2*)Xs, (float2*)Y, \
-                                                     (int)npairs, Ci, Co, P1, m1, m2, P2, G, \
-                                                     vec, Bg, wtgs)
+  // register prefetch of the mix weights when every thread has <= kWpfE outputs of <= kWpfC
+  // input channels
+  const bool wpf = (int64_t)G * cout * K1p <= 256 * kWpfE && cin <= kWpfC;
+#define CM4_(D_, F_, H_, W_)                                                                \
+  coldft_mix_kernel<D_, F_, H_, W_><<<g1, 256, sh, st>>>(                                  \
+      (const float2*)At, (const float2*)Wt, (const f32x4*)FB, (float2*)Xs, (float2*)Y,     \
+      (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg, wtgs)
+#define CM3_(D_, F_, H_) do { if (wpf) CM4_(D_, F_, H_, true); else CM4_(D_, F_, H_, false); } while (0)
 #define CM_(D_, F_) do { if (h16) CM3_(D_, F_, true); else CM3_(D_, F_, false); } while (0)
   if (dir == 0) {
     if (full) CM_(0, true); else CM_(0, false);
@@ -750,6 +813,7 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   }
 #undef CM_
 #undef CM3_
+#undef CM4_
   int e = (int)hipGetLastError();
   if (e) return e;
   const int Ht = (P1 + 15) / 16;

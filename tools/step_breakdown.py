@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Per-step kernel breakdown of the LAST k training steps in a rocprofv3 kernel trace.
 
-    python tools/step_breakdown.py gpurun_out/prof_TAG/run_kernel_trace.csv [k] [top]
+    python tools/step_breakdown.py gpurun_out/prof_TAG/run_kernel_trace.csv [k] [top] [skip]
+
+skip: trailing Adam windows to drop first (bench.py's eager kernel-timer steps after the timed
+region, 4 by default there).
 
 A step ends with the fused Adam launch (adam_kernel); the k windows between the last k+1 Adam
 launches are the timed steps.  Prints each kernel's time per step, its share of the summed
@@ -17,10 +20,13 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     for r in rows:
         r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     rows.sort(key=lambda r: r["s"])
     ad = [i for i, r in enumerate(rows) if re.search(r"adam", r["Kernel_Name"])]
+    if skip:
+        ad = ad[:-skip]
     ad = ad[-(k + 1):]
     per = defaultdict(float)
     cnt = defaultdict(int)
