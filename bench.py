@@ -189,13 +189,24 @@ def main():
             graphed.capture(L)
         torch.cuda.synchronize()
 
+    hostp = {"batch_select": 0.0, "draw": 0.0, "step": 0.0, "n": 0}
+
     def step(i, eager=False):
+        t0_ = time.perf_counter()
         j = (i * B) % (n_local - B + 1)
         ids = order[j:j + B]
         torch.index_select(X, 0, ids, out=xb)
         torch.index_select(Y, 0, ids, out=yb)
         if graphed is not None and not eager:
-            graphed.step((draw_distinct if a.config == "C_attn" else blindno.draw_bag)(T)[1])
+            t1_ = time.perf_counter()
+            idx = (draw_distinct if a.config == "C_attn" else blindno.draw_bag)(T)[1]
+            t2_ = time.perf_counter()
+            graphed.step(idx)
+            t3_ = time.perf_counter()
+            hostp["batch_select"] += t1_ - t0_
+            hostp["draw"] += t2_ - t1_
+            hostp["step"] += t3_ - t2_
+            hostp["n"] += 1
             return
         out = model(xb, grid)
         loss = blindno.mse_loss(out, yb)
@@ -219,6 +230,9 @@ def main():
     t0 = time.perf_counter()
     if timer and graphed is None:
         timer.start()
+    hostp.update(batch_select=0.0, draw=0.0, step=0.0, n=0)
+    if graphed is not None:
+        graphed.host_times = {}
     for i in range(a.steps):
         step(a.warmup + i)
     t_enq = time.perf_counter() - t0          # host time to enqueue the K steps
@@ -270,6 +284,13 @@ def main():
             res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS,
                                              traffic_per_point=timing.pmc_traffic(ROOT, timing.DOMINANT)
                                              if a.config == "C" else None)
+            rec = timing.pmc_record(ROOT, timing.DOMINANT) if a.config == "C" else None
+            if res["roofline"] and rec and "valu_issue_util" in rec:
+                # the limiter of this kernel (profiles/pmc_traffic.json, tools/pmc_traffic.py)
+                res["roofline"]["valu_issue_util"] = rec["valu_issue_util"]
+                res["roofline"]["valu_issue_util_source"] = (
+                    "PMC SQ_INSTS_VALU / _TRANS_F32 / _MFMA, GRBM_GUI_ACTIVE clock, kbench Bn=300: " +
+                    rec["source"])
             if a.config in ("C", "E"):
                 res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
         if world == 1 and a.config in ("A", "B", "C", "E"):
@@ -281,6 +302,11 @@ def main():
                 res["cpu_baseline"] = cpu_baseline(a.config, model, xb, yb, grid, T, budget=a.cpu_seconds)
         res["loss_mean"] = float(loss_acc) / (a.warmup + a.steps)
         res["host_enqueue_ms_per_step"] = round(1000.0 * t_enq / a.steps, 4)
+        if hostp["n"]:
+            hb = {k: round(1e6 * hostp[k] / hostp["n"], 1) for k in ("batch_select", "draw", "step")}
+            for k, v in (getattr(graphed, "host_times", None) or {}).items():
+                hb["step." + k] = round(1e6 * v / hostp["n"], 1)
+            res["host_us_per_step"] = hb
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
@@ -319,10 +345,19 @@ def spectral_roofline(model, grid, B, T, N, dev):
     ms = ev0.elapsed_time(ev1) / reps
     nbytes = 4 * Bn * C * P * P * 2 + 16 * C * C * m * m
     gbs = nbytes / (ms * 1e-3) / 1e9
-    return {"kernels": "blindno_rowdft + blindno_colpass + blindno_rowidft_epi (one FNO_input layer)",
-            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_per_layer": round(ms, 4),
-            "algorithmic_bytes": int(nbytes), "snapshots": Bn}
+    res = {"kernels": "blindno_rowdft + blindno_colpass + blindno_rowidft_epi (one FNO_input layer)",
+           "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_per_layer": round(ms, 4),
+           "algorithmic_bytes": int(nbytes), "snapshots": Bn, "traffic": None}
+    # measured HBM bytes of the same layer shape (Bn = 300: tools/kbench.py "[input]" under
+    # tools/pmc_kbench.sh -> profiles/pmc_traffic.json)
+    from blindno import timing
+    parts = {k: timing.pmc_record(ROOT, k) for k in ("blindno_rowdft", "coldft_mix (blindno_colpass)",
+                                                      "colidft (blindno_colpass)", "blindno_rowidft_epi")}
+    if Bn == 300 and all(v is not None for v in parts.values()):
+        res["traffic"] = int(sum(v["hbm_bytes_per_dispatch"] for v in parts.values()))
+        res["traffic_by_kernel"] = {k: v["hbm_bytes_per_dispatch"] for k, v in parts.items()}
+    return res
 
 
 def _cpu_params(model):

@@ -93,6 +93,11 @@ int blindno_project_bwd_w(const float* z, const float* w1, const float* b1, cons
  * ceil(P2/16), n < Npad = 16*ceil(2*m2/16), zero padded. */
 int blindno_rowdft(const float* x, float* At, const float* Tp, int Bn, int C, int P1,
                    int P2, int m2, int act, blindno_stream_t stream);
+/* blindno_rowdft reading only the valid region h < N1v, w < N2v of every P1 x P2 plane (the rest
+ * counts as zero and is never read): the gradient of a cropped FNO output, left unfilled on the
+ * padding by blindno_project_bwd. */
+int blindno_rowdft_crop(const float* x, float* At, const float* Tp, int Bn, int C, int P1,
+                        int P2, int m2, int act, int N1v, int N2v, blindno_stream_t stream);
 
 /* Column pass of SpectralConv2d: column DFT at the K1 kept rows, per-mode complex channel
  * mix (compl_mul2d, 2d_FPE/FNOModules.py:141-154, 170-173), column inverse -- two complex
@@ -146,6 +151,10 @@ int blindno_rowidft_epi(const float* Z, const float* x, const float* wc, const f
 int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc, const float* xsrc,
                         float* dx, const float* tb, float* partial, int Bn, int C, int P1,
                         int P2, int m2, int act, blindno_stream_t stream);
+/* blindno_rowidft_bwd with dz read only on h < dN1, w < dN2 (zero elsewhere, never read). */
+int blindno_rowidft_bwd_crop(const float* G, const float* dz, const float* wc, const float* xsrc,
+                             float* dx, const float* tb, float* partial, int Bn, int C, int P1,
+                             int P2, int m2, int act, int dN1, int dN2, blindno_stream_t stream);
 int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2);
 
 /* 1 when the spectrum Z that blindno_colpass(_g) writes and blindno_rowidft_epi/bwd(_g) read

@@ -24,6 +24,7 @@ SIGNATURES = {
     "blindno_project_fwd": "ppppppiiiiiiiiiis",
     "blindno_project_bwd": "pppppppiiiiiiiiiiiis",
     "blindno_rowdft": "pppiiiiiis",
+    "blindno_rowdft_crop": "pppiiiiiiiis",
     "blindno_rowdft_bag_lift": "ppppppiiiiiiiiis",
     "blindno_rowidft_epi_lift": "ppppppppppiiiiiiiiis",
     "blindno_rowidft_bwd_lift": "ppppppppppiiiiiiiiis",
@@ -32,6 +33,7 @@ SIGNATURES = {
     "blindno_mix1d": "ppppiiiiiis",
     "blindno_rowidft_epi": "ppppppiiiiiis",
     "blindno_rowidft_bwd": "pppppppiiiiiis",
+    "blindno_rowidft_bwd_crop": "pppppppiiiiiiiis",
     "blindno_conv_wgrad": "pppiiiiiis",
     "blindno_reduce_partials": "ppiis",
     "blindno_spectrum_tile_layout": "iiiii",

@@ -249,10 +249,15 @@ def unpack_w2d(dWt: torch.Tensor, like: torch.Tensor, P1: int):
 # ---------------------------------------------------------------------------- kernel wrappers
 
 
-def k_rowdft(x, Bn, C, P1, P2, m2, act):
+def k_rowdft(x, Bn, C, P1, P2, m2, act, valid=None):
+    """Row DFT; ``valid`` = (N1v, N2v): read only that region of each plane (zero elsewhere)."""
     At = _empty(Bn, m2, C, P1, 2, like=x)
-    call("blindno_rowdft", ptr(x), ptr(At), ptr(twiddle_mfma(P2, m2, x.device)), Bn, C, P1, P2,
-         m2, act, stream_ptr())
+    if valid is None:
+        call("blindno_rowdft", ptr(x), ptr(At), ptr(twiddle_mfma(P2, m2, x.device)), Bn, C, P1, P2,
+             m2, act, stream_ptr())
+    else:
+        call("blindno_rowdft_crop", ptr(x), ptr(At), ptr(twiddle_mfma(P2, m2, x.device)), Bn, C, P1,
+             P2, m2, act, valid[0], valid[1], stream_ptr())
     return At
 
 
@@ -349,16 +354,19 @@ def k_rowidft_epi(Z, x, wc, bc, Bn, C, P1, P2, m2, act):
     return z
 
 
-def k_rowidft_bwd(G, dz, wc, xsrc, Bn, C, P1, P2, m2, act, want_wgrad=False):
+def k_rowidft_bwd(G, dz, wc, xsrc, Bn, C, P1, P2, m2, act, want_wgrad=False, valid=None):
     """dx = irow^H(G) + Wc^T dz, times GELU'(xsrc) if act.  With want_wgrad (C <= 8) the
-    1x1-conv weight/bias gradients are reduced in the same pass (C <= 4): returns (dx, gw, gb)."""
+    1x1-conv weight/bias gradients are reduced in the same pass (C <= 4): returns (dx, gw, gb).
+    ``valid`` = (N1v, N2v): dz is read only on that region (zero elsewhere)."""
     dx = _empty(Bn, C, P1, P2, like=G)
     partial, nchunk = None, 0
     if want_wgrad:
         nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, m2)
         partial = _empty(nchunk, C * C + C, like=G)
-    call("blindno_rowidft_bwd", ptr(G), ptr(dz), ptr(wc), ptr(xsrc), ptr(dx),
-         ptr(twiddle_rowinv(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, stream_ptr())
+    dN1, dN2 = valid if valid is not None else (P1, P2)
+    call("blindno_rowidft_bwd_crop", ptr(G), ptr(dz), ptr(wc), ptr(xsrc), ptr(dx),
+         ptr(twiddle_rowinv(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, dN1, dN2,
+         stream_ptr())
     if not want_wgrad:
         return dx, None, None
     g = reduce_partials(partial, nchunk, C * C + C)
@@ -399,9 +407,10 @@ def spec_forward(x, act, Wt, sh: SpecShape):
     return k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 0)
 
 
-def spec_backward(dz, X, Wt, sh: SpecShape):
-    """Adjoint of spec_forward: returns (dWt, GZ) for the layer's output gradient dz."""
-    At = k_rowdft(dz, sh.Bn, sh.Co, sh.P1, sh.P2, sh.m2, 0)
+def spec_backward(dz, X, Wt, sh: SpecShape, valid=None):
+    """Adjoint of spec_forward: returns (dWt, GZ) for the layer's output gradient dz (read only
+    on ``valid`` = (N1v, N2v) when given, 2D)."""
+    At = k_rowdft(dz, sh.Bn, sh.Co, sh.P1, sh.P2, sh.m2, 0, valid)
     if sh.dim == 2:
         G, GZ = k_colpass(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
     else:
@@ -980,7 +989,11 @@ class BagEncoderFn(torch.autograd.Function):
         # projection (dout read per bag: dout_div = L)
         off_fc1 = 2 + 4 * n
         fc1w, fc1b, fc2w = prm[off_fc1:off_fc1 + 3]
-        dz = torch.zeros(Bn, C, P1, P2, dtype=F32, device=gh.device)
+        # the projection backward writes dz on the Ho x Wo crop only; with >= 2 layers its two
+        # consumers (the last layer's row DFT and row-inverse adjoint) read just that region, so
+        # the padding (36% of the field at 128^2) is never zero-filled (88 MB at config C)
+        crop = (Ho, Wo) if n >= 2 else None
+        dz = _empty(Bn, C, P1, P2, like=gh) if crop else torch.zeros(Bn, C, P1, P2, dtype=F32, device=gh.device)
         np_p = Hd * C + Hd + Cout * Hd + Cout
         nchunk = query("blindno_project_bwd_nchunk", Bn, Ho, Wo)
         partial = _empty(nchunk, np_p, like=gh)
@@ -1001,10 +1014,12 @@ class BagEncoderFn(torch.autograd.Function):
         for k in reversed(range(n)):
             off = 2 + 4 * k
             w1, w2, cw, cb = prm[off:off + 4]
-            dWt, GZ = spec_backward(dz, Xs[k], Wts[k], sh)
+            valid = crop if k == n - 1 else None
+            dWt, GZ = spec_backward(dz, Xs[k], Wts[k], sh, valid)
             grads[off], grads[off + 1] = unpack_weights(dWt, (w1, w2), P1, 2)
             if k > 0:
-                dz, gw, gb = k_rowidft_bwd(GZ, dz, cw, zs[k - 1], Bn, C, P1, P2, meta.m2, 1, True)
+                dz, gw, gb = k_rowidft_bwd(GZ, dz, cw, zs[k - 1], Bn, C, P1, P2, meta.m2, 1, True,
+                                           valid)
                 grads[off + 2], grads[off + 3] = gw.view_as(cw), gb
             else:
                 nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, meta.m2)

@@ -70,6 +70,15 @@ def cost(name, args):
     return 0, 0
 
 
+def pmc_record(root: str, name: str):
+    """The profiles/pmc_traffic.json record of ``name`` (tools/pmc_traffic.py), or None."""
+    import json
+    p = os.path.join(root, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    return json.load(open(p)).get(name)
+
+
 def pmc_traffic(root: str, name: str):
     """HBM bytes per crop point of ``name`` measured with rocprofv3 PMC counters
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from FETCH_SIZE x 2 + WRITE_SIZE,

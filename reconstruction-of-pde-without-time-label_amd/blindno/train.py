@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import time
 from typing import Iterable, List, Optional
 
 import numpy as np
@@ -332,9 +333,18 @@ class GraphedBagStep:
         With ``overlap``: replay A, the heads' all-reduce on the side stream while B (the
         encoder's backward) replays on the main stream, then the encoder's (small) all-reduce,
         the join, and Adam."""
+        ht = getattr(self, "host_times", None)
         if not self.overlap:
-            key = self.replay(idx)
+            t0 = time.perf_counter()
+            key = self.stage(idx)
+            t1 = time.perf_counter()
+            self.graphs[key].replay()
+            t2 = time.perf_counter()
             self.dp.reduce_and_step()
+            if ht is not None:     # host-side breakdown (bench.py host_us_per_step)
+                t3 = time.perf_counter()
+                for k, v in (("stage", t1 - t0), ("replay", t2 - t1), ("reduce_adam", t3 - t2)):
+                    ht[k] = ht.get(k, 0.0) + v
             return key
         key = self.stage(idx)
         ga, gb = self.graphs[key]

@@ -50,7 +50,9 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int C, int P1, int P2,
-    int m2, int TPW, BagLift bl, int Bg, int64_t wgs) {
+    int m2, int TPW, BagLift bl, int Bg, int64_t wgs, int dN1, int dN2) {
+  // MODE 1: dz is read only on its valid region h < dN1, w < dN2 (zero elsewhere: the gradient
+  // of a cropped FNO output; see rowdft_mfma_kernel)
   extern __shared__ float sTB[];                    // [KS][NT][64] when LDSB
   const int KS = (m2 + 1) >> 1;
   const int NT = (P2 + 15) >> 4;
@@ -121,6 +123,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     auto load_ops = [&](int tile, Ops& o) {
       const int w = 16 * tile + c16;
       const bool pok = rok && w < P2;
+      const bool dok = pok && (MODE == 0 || (h < dN1 && w < dN2));
       o.lok = false;
       o.lin[0] = o.lin[1] = o.lin[2] = 0.f;
       if (LIFT) {
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
       }
 #pragma unroll
       for (int i = 0; i < CM; ++i)
-        o.fv[i] = (!(LIFT && MODE == 0) && pok && has_wc && i < C)
+        o.fv[i] = (!(LIFT && MODE == 0) && dok && has_wc && i < C)
                       ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -170,9 +173,10 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
             lin[2] = grow[2 * w + 1];
           }
         }
+        const bool dok = pok && (MODE == 0 || (h < dN1 && w < dN2));
 #pragma unroll
         for (int i = 0; i < CM; ++i)
-          fv[i] = (!(LIFT && MODE == 0) && pok && has_wc && i < C)
+          fv[i] = (!(LIFT && MODE == 0) && dok && has_wc && i < C)
                       ? (MODE == 0 ? xs[rbase + i * HW + w] : dz[rbase + i * HW + w]) : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -493,7 +497,10 @@ template <int MODE, int ACT, int WG, int LIFT = 0>
 int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
                   const float* bc, float* out, const float* TB, float* partial, int nblocks,
                   int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{},
-                  int G = 1, int64_t wgs = 0) {
+                  int G = 1, int64_t wgs = 0, int dN1 = 0, int dN2 = 0) {
+  if (dN1 <= 0) dN1 = P1;
+  if (dN2 <= 0) dN2 = P2;
+  if (dN1 > P1 || dN2 > P2) return (int)hipErrorInvalidValue;
   if (G < 1 || Bn % G || (G > 1 && (WG || LIFT || P1 % 4))) return (int)hipErrorInvalidValue;
   const int Bg = Bn / G;
   if (G == 1) wgs = 0;
@@ -512,8 +519,8 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   const int ks = (m2 + 1) / 2;
   if (ks > 24) return (int)hipErrorInvalidValue;               // m2 <= 48
   if constexpr (!WG && !LIFT) {
-    // wide fields with the spectrum in A-tile order (rowinv_tile_layout)
-    if (rowinv_tile_layout(Bn, C, P1, P2, m2)) {
+    // wide fields with the spectrum in A-tile order (rowinv_tile_layout; full-field dz only)
+    if (rowinv_tile_layout(Bn, C, P1, P2, m2) && dN1 == P1 && dN2 == P2) {
       if (G > kWideMaxG) return (int)hipErrorInvalidValue;
       const int NT = (P2 + 15) / 16, nquads = Bn * P1 / 4;
       int tpw = NT;
@@ -545,10 +552,12 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   do {                                                                                       \
     if (g.ldsb)                                                                              \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 1, LIFT><<<nblocks, 256, sh, st>>>(        \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs);       \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
+          dN2);                                                                              \
     else                                                                                     \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 0, LIFT><<<nblocks, 256, sh, st>>>(        \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs);       \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
+          dN2);                                                                              \
   } while (0)
 #define RI_K(CM_) \
   if (ks <= 8) RI(CM_, 8); else if (ks <= 16) RI(CM_, 16); else RI(CM_, 24);
@@ -606,21 +615,35 @@ BLINDNO_API int blindno_rowidft_bwd_g(const float* Gs, const float* dz, const fl
                                 st, BagLift{}, G, wgs);
 }
 
+BLINDNO_API int blindno_rowidft_bwd_crop(const float* G, const float* dz, const float* wc,
+                                         const float* xsrc, float* dx, const float* tb,
+                                         float* partial, int Bn, int C, int P1, int P2, int m2,
+                                         int act, int dN1, int dN2, void* stream) {
+  if (dN1 < 1 || dN1 > P1 || dN2 < 1 || dN2 > P2) return (int)hipErrorInvalidValue;
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  hipStream_t st = (hipStream_t)stream;
+  const BagLift nb0{};
+  if (partial) {
+    if (C > 4 || !wc) return (int)hipErrorInvalidValue;
+    if (act)
+      return rowinv_launch<1, 1, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st,
+                                    nb0, 1, 0, dN1, dN2);
+    return rowinv_launch<1, 0, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st,
+                                  nb0, 1, 0, dN1, dN2);
+  }
+  if (act)
+    return rowinv_launch<1, 1, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                  nb0, 1, 0, dN1, dN2);
+  return rowinv_launch<1, 0, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                nb0, 1, 0, dN1, dN2);
+}
+
 BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc,
                                     const float* xsrc, float* dx, const float* tb,
                                     float* partial, int Bn, int C, int P1, int P2, int m2,
                                     int act, void* stream) {
-  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
-  hipStream_t st = (hipStream_t)stream;
-  if (partial) {
-    if (C > 4 || !wc) return (int)hipErrorInvalidValue;
-    if (act)
-      return rowinv_launch<1, 1, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st);
-    return rowinv_launch<1, 0, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st);
-  }
-  if (act)
-    return rowinv_launch<1, 1, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
-  return rowinv_launch<1, 0, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st);
+  return blindno_rowidft_bwd_crop(G, dz, wc, xsrc, dx, tb, partial, Bn, C, P1, P2, m2, act, P1, P2,
+                                  stream);
 }
 
 // Snapshot-encoder first layer (LIFT): the layer input is fc0([u, gx, gy]) recomputed from

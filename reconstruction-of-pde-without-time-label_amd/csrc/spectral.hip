@@ -29,13 +29,22 @@ namespace {
 // f = GELU (act) is applied once per loaded element (VALU, beside the matrix pipe).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Valid region (N1v, N2v): only rows h < N1v and columns w < N2v of each P1 x P2 plane are
+// read, the rest counts as zero -- for the gradient of a cropped FNO output (2d_FPE/
+// FNOModules.py:234), which is zero on the padding by construction, so the producer
+// (project_bwd) need not zero-fill it; KB then covers only the ceil(N2v / 16) live K blocks.
+// workgroup cap of the row DFT grid (each workgroup stages the twiddle image once; beyond the
+// cap waves loop over several 16-row tiles)
+#ifndef ROWDFT_MAX_BLOCKS
+#define ROWDFT_MAX_BLOCKS 4096
+#endif
 template <int NT, int ALIGNED>
 __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
                                                           float* __restrict__ At,
                                                           const float* __restrict__ Tp,
                                                           int nrows, int C, int P1, int P2,
                                                           int m2, int KB, int Npad, int ntile_groups,
-                                                          int act) {
+                                                          int act, int N1v, int N2v) {
   extern __shared__ float smT[];                 // [KB][4][Npad][4]
   const int nT = KB * 16 * Npad;
   stage_to_lds(smT, Tp, nT);
@@ -50,7 +59,7 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
     const int tg = (int)(wk % ntile_groups);
     const int t0 = tg * NT;                       // first 16-column tile of this wave
     const int row = rt * 16 + r16;
-    const bool rok = row < nrows;
+    const bool rok = row < nrows && (N1v >= P1 || row % P1 < N1v);
     const float* xr = x + (int64_t)(rok ? row : 0) * P2;
     f32x4 acc[NT];
 #pragma unroll
@@ -58,12 +67,12 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
     // x loads run two K blocks ahead of the MFMAs (small fields are latency-bound)
     auto load_a = [&](int kb, float (&a)[4]) {
       const int w0 = kb * 16 + kq * 4;
-      if (ALIGNED && w0 + 3 < P2) {
+      if (ALIGNED && w0 + 3 < N2v) {
         const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
         a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
       } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < P2) ? xr[w0 + s] : 0.f;
+        for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
       }
     };
     float a1[4], a2[4] = {0.f, 0.f, 0.f, 0.f};
@@ -687,14 +696,16 @@ __global__ void pack_w1d_kernel(const float2* __restrict__ src, float2* __restri
 
 }  // namespace
 
-BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int Bn, int C,
-                               int P1, int P2, int m2, int act, void* stream) {
-  if (Bn <= 0 || C <= 0 || P1 <= 0 || P2 <= 0 || m2 <= 0 || m2 > P2 / 2 + 1)
+BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, int Bn, int C,
+                                    int P1, int P2, int m2, int act, int N1v, int N2v,
+                                    void* stream) {
+  if (Bn <= 0 || C <= 0 || P1 <= 0 || P2 <= 0 || m2 <= 0 || m2 > P2 / 2 + 1 || N1v < 1 ||
+      N1v > P1 || N2v < 1 || N2v > P2)
     return (int)hipErrorInvalidValue;
   const int64_t nrows64 = (int64_t)Bn * C * P1;
   if (nrows64 > INT32_MAX) return (int)hipErrorInvalidValue;
   const int nrows = (int)nrows64;
-  const int KB = (P2 + 15) / 16;
+  const int KB = (N2v + 15) / 16;                 // K blocks past the valid columns are zero
   const int Npad = ((2 * m2 + 15) / 16) * 16;
   const int ntiles = Npad / 16;
   const size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
@@ -707,12 +718,12 @@ BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int B
   while (ntiles % nt) --nt;
   const int groups = ntiles / nt;
   const int64_t nwork = (int64_t)nrt * groups;
-  const int blocks = (int)((nwork + 3) / 4 < 4096 ? (nwork + 3) / 4 : 4096);
+  const int blocks = (int)((nwork + 3) / 4 < ROWDFT_MAX_BLOCKS ? (nwork + 3) / 4 : ROWDFT_MAX_BLOCKS);
   const bool aligned = (P2 % 4) == 0 && (((uintptr_t)x) & 15) == 0;
   hipStream_t st = (hipStream_t)stream;
 #define RD(NT_, AL_)                                                                       \
   rowdft_mfma_kernel<NT_, AL_><<<blocks, 256, sh, st>>>(x, At, Tp, nrows, C, P1, P2, m2, KB, \
-                                                        Npad, groups, act)
+                                                        Npad, groups, act, N1v, N2v)
 #define RD_AL(NT_) \
   if (aligned) RD(NT_, 1); else RD(NT_, 0);
   switch (nt) {
@@ -724,6 +735,11 @@ BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int B
 #undef RD_AL
 #undef RD
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int Bn, int C,
+                               int P1, int P2, int m2, int act, void* stream) {
+  return blindno_rowdft_crop(x, At, Tp, Bn, C, P1, P2, m2, act, P1, P2, stream);
 }
 
 BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const float* w0,
