@@ -26,6 +26,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW = 4;      // waves per workgroup
 
+// lookahead of the adjoint's epilogue operands for the narrow (C <= 4) fields
+#ifndef ROWINV_PRE_BWD
+#define ROWINV_PRE_BWD 0
+#endif
+
 // Snapshot-encoder lift source (LIFT kernels): the layer input is x0 = fc0([u, gx, gy]),
 // zero outside the N1 x N2 crop, recomputed from the bag tensor instead of being stored.
 struct BagLift {
@@ -144,7 +149,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     };
     // (forward epilogue of narrow fields only: the adjoint's and the 12-channel heads' larger
     // operand sets cost more occupancy than the lookahead gains -- measured)
-    constexpr bool kPre = MODE == 0 && CM <= 8;
+    constexpr bool kPre = (MODE == 0 && CM <= 8) || (ROWINV_PRE_BWD && MODE == 1 && CM <= 4);
     Ops nx;
     if (kPre) load_ops(t0, nx);
     for (int tile = t0; tile < t1; ++tile) {

@@ -29,15 +29,15 @@ namespace {
 // f = GELU (act) is applied once per loaded element (VALU, beside the matrix pipe).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Valid region (N1v, N2v): only rows h < N1v and columns w < N2v of each P1 x P2 plane are
-// read, the rest counts as zero -- for the gradient of a cropped FNO output (2d_FPE/
-// FNOModules.py:234), which is zero on the padding by construction, so the producer
-// (project_bwd) need not zero-fill it; KB then covers only the ceil(N2v / 16) live K blocks.
 // workgroup cap of the row DFT grid (each workgroup stages the twiddle image once; beyond the
 // cap waves loop over several 16-row tiles)
 #ifndef ROWDFT_MAX_BLOCKS
 #define ROWDFT_MAX_BLOCKS 4096
 #endif
+// Valid region (N1v, N2v): only rows h < N1v and columns w < N2v of each P1 x P2 plane are
+// read, the rest counts as zero -- for the gradient of a cropped FNO output (2d_FPE/
+// FNOModules.py:234), which is zero on the padding by construction, so the producer
+// (project_bwd) need not zero-fill it; KB then covers only the ceil(N2v / 16) live K blocks.
 template <int NT, int ALIGNED>
 __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
                                                           float* __restrict__ At,
@@ -251,11 +251,7 @@ constexpr int kFullHB = 10;
 // batch of complex GEMVs (one Ci x Co matrix per kept mode, one row per sample), which would
 // fill a quarter of an MFMA tile at best.
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-// WPF: the mix weights of this thread's (up to kWpfE) outputs are loaded into registers at
-// kernel entry, so their latency hides behind the column DFT (in the loop they were kWpfC
-// dependent-latency rounds per output, the bulk of the head layers' column pass)
-constexpr int kWpfE = 4, kWpfC = 16;
-template <int DIR, bool FULL, bool H16, bool WPF>
+template <int DIR, bool FULL, bool H16>
 __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restrict__ At,
                                                          const float2* __restrict__ Wt,
                                                          const f32x4* __restrict__ FB,
@@ -293,24 +289,6 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
                             : Wt;
     return wg + ((int64_t)k * K1 + (j < K1 ? j : 0)) * Ci * Co;
   };
-  float2 wpre[WPF ? kWpfE : 1][WPF ? kWpfC : 1];
-  if constexpr (WPF) {
-#pragma unroll
-    for (int i = 0; i < kWpfE; ++i) {
-      const int e = threadIdx.x + i * 256;
-      int o = 0, j = 0, p = 0, k = 0;
-      const float2* wj = wrow(e < nout ? e : 0, o, j, p, k);
-      // unconditional loads from clamped (always valid) offsets and no select: entries of
-      // c >= Cin, e >= nout or j >= K1 are never used by the mix (a guarded load per value
-      // compiled to one branch and one wait per load)
-#pragma unroll
-      for (int c = 0; c < kWpfC; ++c) {
-        const int cc = c < Cin ? c : 0;
-        wpre[i][c] = DIR == 0 ? wj[cc * Co + o] : wj[o * Co + cc];
-      }
-    }
-  }
-
   for (int item = wave; item < Mt * Jt; item += 4) {
     const int mt = item / Jt, jt = item % Jt;
     const int row = mt * 16 + r16;
@@ -390,20 +368,16 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
 
   // the mix: output channel o fastest across threads, so the weight loads W[k][j][c][o] of
   // neighbouring threads are contiguous (j fastest put every lane on its own cache line)
-  auto mix_one = [&](int e, const float2* wreg) {
+  auto mix_one = [&](int e) {
     int o, j, p, k;
     const float2* wj = wrow(e, o, j, p, k);
     float re = 0.f, im = 0.f;
     if (j < K1) {
       const float2* xp = sX + p * Cin * LDX + j;
-      auto wload = [&](int c) -> float2 {
-        if constexpr (WPF) return wreg[c];
-        return DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
-      };
+      auto wload = [&](int c) -> float2 { return DIR == 0 ? wj[c * Co + o] : wj[o * Co + c]; };
       if constexpr (H16) {
-#pragma unroll (WPF ? kWpfC : 4)
-        for (int c = 0; c < (WPF ? kWpfC : Cin); ++c) {
-          if (WPF && c >= Cin) break;
+#pragma unroll 4
+        for (int c = 0; c < Cin; ++c) {
           const float2 a = xp[c * LDX];
           const f16x2 ah = {(_Float16)(a.x * hs), (_Float16)(a.y * hs)};
           const float2 w = wload(c);
@@ -419,9 +393,8 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
         re *= hinv;
         im *= hinv;
       } else {
-#pragma unroll (WPF ? kWpfC : 4)
-        for (int c = 0; c < (WPF ? kWpfC : Cin); ++c) {
-          if (WPF && c >= Cin) break;
+#pragma unroll 4
+        for (int c = 0; c < Cin; ++c) {
           const float2 a = xp[c * LDX];
           const float2 w = wload(c);
           if (DIR == 0) {
@@ -441,22 +414,13 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
     }
     Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
   };
-  if constexpr (WPF) {
-#pragma unroll
-    for (int i = 0; i < kWpfE; ++i) {
-      const int e = threadIdx.x + i * 256;
-      if (e < nout) mix_one(e, wpre[i]);
-    }
-  } else {
-    for (int e = threadIdx.x; e < nout; e += blockDim.x) mix_one(e, nullptr);
-  }
+  for (int e = threadIdx.x; e < nout; e += blockDim.x) mix_one(e);
 }
 
 // Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
 // tile, 64 spectrum rows (k, o)); one 16-row MFMA tile per wave; the result is transposed
 // through LDS so that each h row of Z is written as one contiguous run.  tiled: Z in the
 // A-tile order of the wide row inverse instead (rowinv_tile_layout, rowinv.hip).
-constexpr int kColJt = 4;        // K1 <= 64 kept rows: full operand prefetch
 __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__ Y,
                                                       const f32x4* __restrict__ GB,
                                                       float2* __restrict__ Z, int Cout, int P1,
@@ -478,27 +442,10 @@ __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__
     const float2* yr = Y + ((int64_t)n * R + (rok ? row : 0)) * K1p;
     const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
     f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
-    if (Jt <= kColJt) {
-      // every K block's operands in flight before the first MFMA (one memory latency)
-      float re[kColJt][4], im[kColJt][4];
-      f32x4 g0[kColJt], g1[kColJt];
-#pragma unroll
-      for (int jb = 0; jb < kColJt; ++jb) {
-        if (jb < Jt) {
-          load4c(yr + jb * 16 + kq * 4, rok ? 4 : 0, true, re[jb], im[jb]);
-          g0[jb] = gb[jb * 128];
-          g1[jb] = gb[jb * 128 + 1];
-        }
-      }
-#pragma unroll
-      for (int jb = 0; jb < kColJt; ++jb)
-        if (jb < Jt) cmfma4(re[jb], im[jb], g0[jb], g1[jb], dr, di);
-    } else {
-      for (int jb = 0; jb < Jt; ++jb) {
-        float re[4], im[4];
-        load4c(yr + jb * 16 + kq * 4, rok ? 4 : 0, true, re, im);
-        cmfma4(re, im, gb[jb * 128], gb[jb * 128 + 1], dr, di);
-      }
+    for (int jb = 0; jb < Jt; ++jb) {
+      float re[4], im[4];
+      load4c(yr + jb * 16 + kq * 4, rok ? 4 : 0, true, re, im);
+      cmfma4(re, im, gb[jb * 128], gb[jb * 128 + 1], dr, di);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) sZ[r16][wave * 16 + kq * 4 + r] = make_float2(dr[r], di[r]);
@@ -813,14 +760,10 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const dim3 g1((unsigned)cdiv(npairs, G));
   // full operand prefetch when the launch is too small to hide latency with waves
   const bool full = (P1 + 15) / 16 <= kFullHB && (int64_t)g1.x * 4 < 4096;
-  // register prefetch of the mix weights when every thread has <= kWpfE outputs of <= kWpfC
-  // input channels
-  const bool wpf = (int64_t)G * cout * K1p <= 256 * kWpfE && cin <= kWpfC;
-#define CM4_(D_, F_, H_, W_)                                                                \
-  coldft_mix_kernel<D_, F_, H_, W_><<<g1, 256, sh, st>>>(                                  \
+#define CM3_(D_, F_, H_)                                                                    \
+  coldft_mix_kernel<D_, F_, H_><<<g1, 256, sh, st>>>(                                       \
       (const float2*)At, (const float2*)Wt, (const f32x4*)FB, (float2*)Xs, (float2*)Y,     \
       (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg, wtgs)
-#define CM3_(D_, F_, H_) do { if (wpf) CM4_(D_, F_, H_, true); else CM4_(D_, F_, H_, false); } while (0)
 #define CM_(D_, F_) do { if (h16) CM3_(D_, F_, true); else CM3_(D_, F_, false); } while (0)
   if (dir == 0) {
     if (full) CM_(0, true); else CM_(0, false);
@@ -829,7 +772,6 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   }
 #undef CM_
 #undef CM3_
-#undef CM4_
   int e = (int)hipGetLastError();
   if (e) return e;
   const int Ht = (P1 + 15) / 16;

@@ -7,3 +7,8 @@ bash tools/gpu_kbench_variants.sh $TAG "input" > gpurun_out/kbv_$TAG.log 2>&1 ||
 echo "kbench variants ok"
 bash tools/pmc_kbench.sh $TAG "input" || exit $?
 echo "pmc ok"
+for lib in variants/*/libblindno.so; do
+  v=$(basename $(dirname $lib))
+  BLINDNO_LIB=$lib timeout -k 10 200 python -u bench.py --steps 30 --warmup 10 --no-cpu --no-parity --no-kernel-timer > gpurun_out/benchv_${TAG}_$v.json 2>/dev/null || { echo "bench variant $v failed"; exit 1; }
+  echo "== bench $v"; cut -c1-200 gpurun_out/benchv_${TAG}_$v.json
+done
