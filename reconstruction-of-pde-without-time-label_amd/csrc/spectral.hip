@@ -34,11 +34,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef ROWDFT_MAX_BLOCKS
 #define ROWDFT_MAX_BLOCKS 4096
 #endif
+#ifndef ROWDFT_STAGE_ITEMS
+#define ROWDFT_STAGE_ITEMS 1
+#endif
 // Valid region (N1v, N2v): only rows h < N1v and columns w < N2v of each P1 x P2 plane are
 // read, the rest counts as zero -- for the gradient of a cropped FNO output (2d_FPE/
 // FNOModules.py:234), which is zero on the padding by construction, so the producer
 // (project_bwd) need not zero-fill it; KB then covers only the ceil(N2v / 16) live K blocks.
-template <int NT, int ALIGNED>
+// STAGE: the twiddle image is staged in LDS by every workgroup; otherwise the B operands are
+// read from the global image (L1/L2-resident) -- when each wave runs about one work item the
+// staging is as many bytes as the wave's own x rows and costs a full latency up front.
+template <int NT, int ALIGNED, bool STAGE>
 __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
                                                           float* __restrict__ At,
                                                           const float* __restrict__ Tp,
@@ -46,9 +52,12 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
                                                           int m2, int KB, int Npad, int ntile_groups,
                                                           int act, int N1v, int N2v) {
   extern __shared__ float smT[];                 // [KB][4][Npad][4]
-  const int nT = KB * 16 * Npad;
-  stage_to_lds(smT, Tp, nT);
-  __syncthreads();
+  if constexpr (STAGE) {
+    const int nT = KB * 16 * Npad;
+    stage_to_lds(smT, Tp, nT);
+    __syncthreads();
+  }
+  const float* __restrict__ tsrc = STAGE ? smT : Tp;
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
   const int r16 = lane & 15, kq = lane >> 4;
@@ -90,7 +99,7 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(
-            smT + (((kb * 4 + kq) * Npad) + (t0 + t) * 16 + r16) * 4);
+            tsrc + (((kb * 4 + kq) * Npad) + (t0 + t) * 16 + r16) * 4);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc[t], 0, 0, 0);
@@ -668,9 +677,18 @@ BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, 
   const int blocks = (int)((nwork + 3) / 4 < ROWDFT_MAX_BLOCKS ? (nwork + 3) / 4 : ROWDFT_MAX_BLOCKS);
   const bool aligned = (P2 % 4) == 0 && (((uintptr_t)x) & 15) == 0;
   hipStream_t st = (hipStream_t)stream;
-#define RD(NT_, AL_)                                                                       \
-  rowdft_mfma_kernel<NT_, AL_><<<blocks, 256, sh, st>>>(x, At, Tp, nrows, C, P1, P2, m2, KB, \
-                                                        Npad, groups, act, N1v, N2v)
+  // stage the twiddle image only when the waves reuse it (>= ROWDFT_STAGE_ITEMS work items
+  // per wave)
+  const bool stage = nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * blocks;
+#define RD(NT_, AL_)                                                                        \
+  do {                                                                                      \
+    if (stage)                                                                              \
+      rowdft_mfma_kernel<NT_, AL_, true><<<blocks, 256, sh, st>>>(                          \
+          x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
+    else                                                                                    \
+      rowdft_mfma_kernel<NT_, AL_, false><<<blocks, 256, 0, st>>>(                          \
+          x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
+  } while (0)
 #define RD_AL(NT_) \
   if (aligned) RD(NT_, 1); else RD(NT_, 0);
   switch (nt) {

@@ -304,3 +304,35 @@ def test_dedup_bag_matches_full_bag(dim):
     assert rel_l2(res[0][0], res[1][0]) <= 1e-6
     for a, b in zip(res[0][1], res[1][1]):
         assert rel_l2(a, b) <= 1e-5
+
+
+@pytest.mark.parametrize("C,m,N,Bn", [(4, 12, 128, 12), (4, 12, 61, 3), (3, 5, 30, 5)])
+def test_crop_valid_region_kernels(C, m, N, Bn):
+    """blindno_rowdft_crop / blindno_rowidft_bwd_crop (the encoder adjoint's dz read only on the
+    N x N crop of the P x P field): garbage on the padding is never read, and the results are
+    BIT-identical to the full-field kernels on the same field with a zeroed padding (the skipped
+    K blocks contribute exact zeros)."""
+    from blindno import ops
+    P = N + ops.pad_amount(N)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    dz = torch.randn(Bn, C, P, P, device="cuda", generator=g)
+    dz_zero = dz.clone()
+    dz_zero[:, :, N:, :] = 0
+    dz_zero[:, :, :, N:] = 0
+    dz[:, :, N:, :] = float("nan")                   # never read by the crop kernels
+    dz[:, :, :, N:] = float("nan")
+    a_crop = ops.k_rowdft(dz, Bn, C, P, P, m, 0, valid=(N, N))
+    a_full = ops.k_rowdft(dz_zero, Bn, C, P, P, m, 0)
+    assert torch.equal(a_crop, a_full)
+    K1 = ops.kept_rows_count(m, P)
+    G = torch.randn(Bn, P, m, C, 2, device="cuda", generator=g)
+    cw = torch.randn(C, C, 1, 1, device="cuda", generator=g) * 0.3
+    xs = torch.randn(Bn, C, P, P, device="cuda", generator=g)
+    wg = C <= 4
+    r_crop = ops.k_rowidft_bwd(G, dz, cw, xs, Bn, C, P, P, m, 1, wg, valid=(N, N))
+    r_full = ops.k_rowidft_bwd(G, dz_zero, cw, xs, Bn, C, P, P, m, 1, wg)
+    torch.cuda.synchronize()
+    for a, b in zip(r_crop, r_full):
+        if a is not None:
+            assert torch.equal(a, b)
+    assert K1 > 0
