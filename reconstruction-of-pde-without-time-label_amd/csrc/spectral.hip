@@ -250,10 +250,6 @@ __device__ __forceinline__ void load4c(const float2* src, int len, bool vec, flo
 // layers launch one workgroup per (sample, mode) pair -- one wave per SIMD -- so a one-block
 // lookahead leaves each step waiting a full memory latency (measured ~16 us for 10 steps)
 constexpr int kFullHB = 10;
-// launches of fewer workgroups than this take the split column DFT (coldft_mix_split_kernel)
-#ifndef COLPASS_SPLIT_BELOW
-#define COLPASS_SPLIT_BELOW 0
-#endif
 // H16 (config E, blindno.ops.set_mix_precision("fp16")): the channel mix takes fp16 operands
 // with fp32 accumulation -- each complex multiply-add is two v_dot2c_f32_f16 (packed fp16
 // pairs, exact products, fp32 sum).  The column spectra are block-scaled first: the workgroup's
@@ -428,158 +424,6 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
     Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
   };
   for (int e = threadIdx.x; e < nout; e += blockDim.x) mix_one(e);
-}
-
-// Split form of coldft_mix for small launches (the head layers: 8 samples x 32 modes = 256
-// pairs, one wave per SIMD and a 160-MFMA chain per wave): workgroup = (pair group,
-// 16-column block jt of the kept rows) and its four waves split the P1 column-DFT reduction
-// (h blocks hb = wave, wave + 4, ...) over every row tile; the partial spectra are added in
-// wave order through LDS (deterministic), then the mix covers this workgroup's 16 kept rows.
-// Same arithmetic per output as coldft_mix_kernel up to the order of the h-block sum.
-template <int DIR, bool H16>
-__global__ __launch_bounds__(256) void coldft_mix_split_kernel(
-    const float2* __restrict__ At, const float2* __restrict__ Wt, const f32x4* __restrict__ FB,
-    float2* __restrict__ Xs, float2* __restrict__ Y, int npairs, int Ci, int Co, int P1, int m1,
-    int m2, int P2, int G, int vec, int Bg, int64_t wtgs) {
-  constexpr int kMtMax = 4;                        // G Cin <= 64 rows (the launcher's G)
-  extern __shared__ float2 sP[];                   // [4 waves][Mt 16][16] partials, then sX
-  const int K1 = kept_rows_count(m1, P1);
-  const int Jt = (K1 + 15) >> 4, K1p = Jt * 16;
-  const int Cin = DIR == 0 ? Ci : Co;
-  const int Cout = DIR == 0 ? Co : Ci;
-  const int HB = (P1 + 15) >> 4;
-  const int q0 = blockIdx.x * G;
-  const int jt = blockIdx.y;
-  const int np = min(G, npairs - q0);
-  const int rows = np * Cin;
-  const int Mt = (rows + 15) >> 4;
-  const int lane = threadIdx.x & 63;
-  const int wave = uniform_int(threadIdx.x >> 6);
-  const int r16 = lane & 15, kq = lane >> 4;
-  const float inv = 1.0f / ((float)P1 * (float)P2);
-  const f32x4* fb = FB + ((int64_t)jt * HB * 64 + lane) * 2;
-  f32x4 dr[kMtMax], di[kMtMax];
-#pragma unroll
-  for (int mt = 0; mt < kMtMax; ++mt) dr[mt] = di[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int hb = wave; hb < HB; hb += 4) {
-    const int h1 = hb * 16 + kq * 4;
-    const f32x4 f0 = fb[hb * 128], f1 = fb[hb * 128 + 1];
-    float re[kMtMax][4], im[kMtMax][4];
-#pragma unroll
-    for (int mt = 0; mt < kMtMax; ++mt) {
-      if (mt < Mt) {
-        const int row = mt * 16 + r16;
-        const bool rok = row < rows;
-        const float2* ar = At + ((int64_t)q0 * Cin + (rok ? row : 0)) * P1;
-        load4c(ar + h1, rok ? P1 - h1 : 0, vec, re[mt], im[mt]);
-      }
-    }
-#pragma unroll
-    for (int mt = 0; mt < kMtMax; ++mt)
-      if (mt < Mt) cmfma4(re[mt], im[mt], f0, f1, dr[mt], di[mt]);
-  }
-  // partials -> LDS [wave][row][jl], summed in wave order
-  const int LDP = 17;
-  float2* sX = sP + 4 * 64 * LDP;                  // [rows][17]
-#pragma unroll
-  for (int mt = 0; mt < kMtMax; ++mt) {
-    if (mt < Mt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int orow = mt * 16 + kq * 4 + r;
-        sP[(wave * 64 + orow) * LDP + r16] = make_float2(dr[mt][r], di[mt][r]);
-      }
-    }
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < rows * 16; e += blockDim.x) {
-    const int orow = e >> 4, jl = e & 15;
-    float2 v = sP[orow * LDP + jl];
-    const int nw = HB < 4 ? HB : 4;
-    for (int w = 1; w < nw; ++w) {
-      const float2 u = sP[(w * 64 + orow) * LDP + jl];
-      v.x += u.x;
-      v.y += u.y;
-    }
-    float sc = 1.0f;
-    if (DIR == 1) sc = c2r_weight((q0 + orow / Cin) % m2, P2) * inv;
-    v = make_float2(v.x * sc, v.y * sc);
-    sX[orow * LDP + jl] = v;
-    const int j = jt * 16 + jl;
-    if (j < K1) Xs[((int64_t)q0 * Cin + orow) * K1 + j] = v;
-  }
-  __syncthreads();
-
-  float hs = 1.0f, hinv = 1.0f;
-  if constexpr (H16) {
-    __shared__ float smax[4];
-    float mx = 0.f;
-    for (int e = threadIdx.x; e < rows * 16; e += blockDim.x) {
-      const float2 v = sX[(e >> 4) * LDP + (e & 15)];
-      mx = fmaxf(mx, fmaxf(fabsf(v.x), fabsf(v.y)));
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
-    if (lane == 0) smax[wave] = mx;
-    __syncthreads();
-    mx = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
-    if (mx > 0.f && mx < 3.0e38f) {
-      int ex;
-      frexpf(mx, &ex);
-      hs = ldexpf(1.0f, 15 - ex);
-      hinv = ldexpf(1.0f, ex - 15);
-    }
-  }
-
-  // the mix of this workgroup's 16 kept rows (output channel fastest across threads)
-  const int nout = np * Cout * 16;
-  for (int e = threadIdx.x; e < nout; e += blockDim.x) {
-    const int o = e % Cout;
-    const int t = e / Cout;
-    const int jl = t & 15, p = t >> 4;
-    const int j = jt * 16 + jl;
-    const int k = (q0 + p) % m2;
-    float re = 0.f, im = 0.f;
-    if (j < K1) {
-      const float2* wg = wtgs ? reinterpret_cast<const float2*>(
-                                    reinterpret_cast<const float*>(Wt) + ((q0 + p) / m2 / Bg) * wtgs)
-                              : Wt;
-      const float2* wj = wg + ((int64_t)k * K1 + j) * Ci * Co;
-      const float2* xp = sX + p * Cin * LDP + jl;
-#pragma unroll 4
-      for (int c = 0; c < Cin; ++c) {
-        const float2 a = xp[c * LDP];
-        const float2 w = DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
-        if constexpr (H16) {
-          const f16x2 ah = {(_Float16)(a.x * hs), (_Float16)(a.y * hs)};
-          const _Float16 wr = (_Float16)w.x, wi = (_Float16)w.y;
-          if (DIR == 0) {
-            re = __builtin_amdgcn_fdot2(ah, (f16x2){wr, (_Float16)(-wi)}, re, false);
-            im = __builtin_amdgcn_fdot2(ah, (f16x2){wi, wr}, im, false);
-          } else {
-            re = __builtin_amdgcn_fdot2(ah, (f16x2){wr, wi}, re, false);
-            im = __builtin_amdgcn_fdot2(ah, (f16x2){(_Float16)(-wi), wr}, im, false);
-          }
-        } else if (DIR == 0) {
-          re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
-          im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
-        } else {
-          re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
-          im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
-        }
-      }
-      if constexpr (H16) {
-        re *= hinv;
-        im *= hinv;
-      }
-      if (DIR == 0) {
-        const float sc = c2r_weight(k, P2) * inv;
-        re *= sc;
-        im *= sc;
-      }
-    }
-    Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
-  }
 }
 
 // Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
@@ -932,18 +776,6 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
   hipStream_t st = (hipStream_t)stream;
   const dim3 g1((unsigned)cdiv(npairs, G));
-  // small launches: one workgroup per (pair group, kept-row block), waves splitting the h sum
-  if ((int64_t)g1.x < COLPASS_SPLIT_BELOW && G * cin <= 64 && Jt > 1) {
-    const dim3 gs((unsigned)cdiv(npairs, G), (unsigned)Jt);
-    const size_t shs = sizeof(float2) * (size_t)(4 * 64 + 64) * 17;
-#define CS_(D_, H_)                                                                          \
-  coldft_mix_split_kernel<D_, H_><<<gs, 256, shs, st>>>(                                    \
-      (const float2*)At, (const float2*)Wt, (const f32x4*)FB, (float2*)Xs, (float2*)Y,      \
-      (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg, wtgs)
-    if (dir == 0) { if (h16) CS_(0, true); else CS_(0, false); }
-    else { if (h16) CS_(1, true); else CS_(1, false); }
-#undef CS_
-  } else {
   // full operand prefetch when the launch is too small to hide latency with waves
   const bool full = (P1 + 15) / 16 <= kFullHB && (int64_t)g1.x * 4 < 4096;
 #define CM3_(D_, F_, H_)                                                                    \
@@ -958,7 +790,6 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   }
 #undef CM_
 #undef CM3_
-  }
   int e = (int)hipGetLastError();
   if (e) return e;
   const int Ht = (P1 + 15) / 16;

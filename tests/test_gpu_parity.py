@@ -336,3 +336,31 @@ def test_crop_valid_region_kernels(C, m, N, Bn):
         if a is not None:
             assert torch.equal(a, b)
     assert K1 > 0
+
+
+@pytest.mark.parametrize("C,act,G", [(12, 1, 2), (12, 0, 1), (8, 1, 1), (3, 1, 1)])
+def test_conv_wgrad_vs_fp64(C, act, G):
+    """1x1-conv weight / bias gradient of an FNO layer (blindno_conv_wgrad_g: the heads' C = 12
+    layers, grouped over two weight groups) vs the float64 sums:
+    dW[o][i] = sum_p dz[o][p] f(x)[i][p], db[o] = sum_p dz[o][p], f = GELU if act."""
+    import oracle
+    from blindno import ops
+    from blindno._lib import call, ptr, query, stream_ptr
+    Bn, P = 4 * G, 160
+    g = torch.Generator(device="cuda").manual_seed(C + 10 * act)
+    dz = torch.randn(Bn, C, P, P, device="cuda", generator=g)
+    x = torch.randn(Bn, C, P, P, device="cuda", generator=g)
+    nch = query("blindno_conv_wgrad_nchunk", Bn // G, P, P)
+    part = torch.empty(nch, G, C * C + C, device="cuda")
+    call("blindno_conv_wgrad_g", ptr(dz), ptr(x), ptr(part), nch, G, Bn, C, P, P, act, stream_ptr())
+    got = ops.reduce_partials(part, nch, G * (C * C + C)).view(G, C * C + C).double().cpu()
+    d64, x64 = dz.double().cpu(), x.double().cpu()
+    f = oracle.gelu(x64) if act else x64
+    for gi in range(G):
+        sl = slice(gi * Bn // G, (gi + 1) * Bn // G)
+        w = torch.einsum("nohw,nihw->oi", d64[sl], f[sl])
+        b = d64[sl].sum(dim=(0, 2, 3))
+        # fp32 sums over 1e5 points of O(1) terms with O(sqrt n) results: a few 1e-6 (the
+        # 8c gradient bar is 1e-4)
+        assert rel_l2(got[gi, :C * C].numpy(), w.reshape(-1).numpy()) <= 5e-5
+        assert rel_l2(got[gi, C * C:].numpy(), b.numpy()) <= 5e-5
