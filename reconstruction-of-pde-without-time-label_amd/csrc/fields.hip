@@ -22,8 +22,8 @@ namespace {
 // ---------------------------------------------------------------- lift
 // Grouped launches (G > 1): samples n = g Bg + n' of group g use that group's weights at
 // w + g wgs and read the shared input sample n' (two FNO heads on one field).
-// One thread per point computing every output channel (the input vector is read once):
-// Bn x P1 x P2 threads; channels-last input, NCHW output (coalesced across w).
+// lift_fwd_pt_kernel: a lane quad per point (channels-last input, NCHW output coalesced
+// across w).
 template <int CM>
 __global__ __launch_bounds__(kBlock) void lift_fwd_pt_kernel(const float* __restrict__ in,
                                                              const float* __restrict__ w0,
@@ -32,16 +32,21 @@ __global__ __launch_bounds__(kBlock) void lift_fwd_pt_kernel(const float* __rest
                                                              int N1, int N2, int Cin, int C,
                                                              int P1, int P2, int Bg,
                                                              int64_t wgs) {
+  // four threads per point (a lane quad): lane q computes channels q, q + 4, ... (CM / 4 of
+  // them) from the point's Cin inputs, so each lane runs a quarter of the C x Cin products
+  // and four times as many waves hide the input reads' latency
+  constexpr int CQ = CM / 4;
+  const int q = threadIdx.x & 3;
   const int64_t HW = (int64_t)P1 * P2;
   const int64_t total = (int64_t)Bn * HW;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t idx = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; idx < total;
+       idx += ((int64_t)gridDim.x * blockDim.x) >> 2) {
     const int64_t n = idx / HW;
     const int64_t s = idx - n * HW;
     const int h = (int)(s / P2), w = (int)(s - (s / P2) * P2);
     float* xp = x0 + n * C * HW + s;
     if (h >= N1 || w >= N2) {
-      for (int c = 0; c < C; ++c) xp[c * HW] = 0.f;
+      for (int c = q; c < C; c += 4) xp[c * HW] = 0.f;
       continue;
     }
     const int g = (int)(n / Bg);
@@ -49,18 +54,18 @@ __global__ __launch_bounds__(kBlock) void lift_fwd_pt_kernel(const float* __rest
     const float* wg = w0 + g * wgs;
     const float* bg = b0 + g * wgs;
     const float* ip = in + ((ni * N1 + h) * N2 + w) * Cin;
-    float acc[CM];
+    float acc[CQ];
 #pragma unroll
-    for (int c = 0; c < CM; ++c) acc[c] = c < C ? bg[c] : 0.f;
+    for (int k = 0; k < CQ; ++k) acc[k] = q + 4 * k < C ? bg[q + 4 * k] : 0.f;
     for (int j = 0; j < Cin; ++j) {
       const float v = ip[j];
 #pragma unroll
-      for (int c = 0; c < CM; ++c)
-        if (c < C) acc[c] = fmaf(wg[c * Cin + j], v, acc[c]);
+      for (int k = 0; k < CQ; ++k)
+        if (q + 4 * k < C) acc[k] = fmaf(wg[(q + 4 * k) * Cin + j], v, acc[k]);
     }
 #pragma unroll
-    for (int c = 0; c < CM; ++c)
-      if (c < C) xp[c * HW] = acc[c];
+    for (int k = 0; k < CQ; ++k)
+      if (q + 4 * k < C) xp[(q + 4 * k) * HW] = acc[k];
   }
 }
 
@@ -567,6 +572,10 @@ __global__ __launch_bounds__(1024) void project_bwd_wsum_kernel(
 }
 
 // ---------------------------------------------------------------- snapshot-bag mean
+// Four threads per grid point (a quad of lanes): quad lane q sums snapshots l = q, q + 4, ...,
+// the quad adds its partials in a fixed order ((q0 + q1) + (q2 + q3), deterministic), and the
+// quad's lanes write channels c = q, q + 4, ... -- one thread per point left a 54-long
+// dependent sum per lane on one wave per SIMD (config C: 4 x 128^2 points).
 __global__ __launch_bounds__(kBlock) void bagmean_fwd_kernel(const float* __restrict__ u,
                                                              const float* __restrict__ grid,
                                                              const float* __restrict__ w,
@@ -578,17 +587,24 @@ __global__ __launch_bounds__(kBlock) void bagmean_fwd_kernel(const float* __rest
   // multiplicities: lw[l] = count_l / L_drawn)
   const int64_t total = (int64_t)B * S;
   const float invL = lw ? 1.0f : 1.0f / (float)L;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  const int q = threadIdx.x & 3;
+  for (int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; base < total;
+       base += ((int64_t)gridDim.x * blockDim.x) >> 2) {
+    const int64_t idx = base;
     const int s = (int)(idx % S);
     const int b = (int)(idx / S);
+    const float* ub = u + (int64_t)b * L * S + s;
     float sum = 0.f;
     if (lw) {
-      for (int l = 0; l < L; ++l) sum = fmaf(lw[l], u[((int64_t)b * L + l) * S + s], sum);
+#pragma unroll 4
+      for (int l = q; l < L; l += 4) sum = fmaf(lw[l], ub[(int64_t)l * S], sum);
     } else {
-      for (int l = 0; l < L; ++l) sum += u[((int64_t)b * L + l) * S + s];
+#pragma unroll 4
+      for (int l = q; l < L; l += 4) sum += ub[(int64_t)l * S];
     }
-    for (int c = 0; c < width; ++c) {
+    const float s1 = sum + __shfl_xor(sum, 1, 64);        // (q0 + q1), (q2 + q3)
+    sum = s1 + __shfl_xor(s1, 2, 64);                      // same order in every lane
+    for (int c = q; c < width; c += 4) {
       float v = bias[c];
       for (int e = 0; e < d; ++e) v = fmaf(w[c * (d + 1) + e], grid[(int64_t)s * d + e], v);
       v = fmaf(w[c * (d + 1) + d] * invL, sum, v);
@@ -728,7 +744,7 @@ BLINDNO_API int blindno_lift_fwd_g(const float* in, const float* w0, const float
   if (G == 1) wgs = 0;
   if (C > 4 && C <= 16) {         // wide lifts (the heads): one thread per point, all channels
     const int64_t pts = (int64_t)Bn * P1 * P2;
-    lift_fwd_pt_kernel<16><<<grid_for(pts, kBlock, 65536), kBlock, 0, st>>>(
+    lift_fwd_pt_kernel<16><<<grid_for(4 * pts, kBlock, 65536), kBlock, 0, st>>>(
         in, w0, b0, x0, Bn, N1, N2, Cin, C, P1, P2, Bg, wgs);
     return (int)hipGetLastError();
   }
@@ -779,7 +795,7 @@ BLINDNO_API int blindno_lift_bwd(const float* dx0, const float* in, const float*
 }
 
 #ifndef CONV_WGRAD_MFMA
-#define CONV_WGRAD_MFMA 0
+#define CONV_WGRAD_MFMA 1
 #endif
 BLINDNO_API int blindno_conv_wgrad_nchunk(int Bn, int P1, int P2) {
   const int64_t nt = (int64_t)Bn * cdiv((int64_t)P1 * P2, TP);
@@ -958,7 +974,7 @@ BLINDNO_API int blindno_project_bwd(const float* z, const float* w1, const float
 BLINDNO_API int blindno_bagmean_fwd_w(const float* u, const float* grid, const float* w,
                                       const float* bias, const float* lw, float* y, int B, int L,
                                       int S, int d, int width, void* stream) {
-  bagmean_fwd_kernel<<<grid_for((int64_t)B * S), kBlock, 0, (hipStream_t)stream>>>(
+  bagmean_fwd_kernel<<<grid_for(4 * (int64_t)B * S), kBlock, 0, (hipStream_t)stream>>>(
       u, grid, w, bias, lw, y, B, L, S, d, width);
   return (int)hipGetLastError();
 }
