@@ -2,7 +2,10 @@
 """Write profiles/pmc_traffic.json from a tools/pmc_kbench.sh run over kbench's "[input]" cases
 (config C's snapshot encoder at the mean bag size: Bn = 4 * 75 snapshots, P = 160, 128^2 crop).
 
-    python tools/pmc_traffic.py gpurun_out/pmck_TAG
+    python tools/pmc_traffic.py gpurun_out/pmck_TAG [profiles/rNN/TAG_pmc_summary.json]
+
+The optional second argument names the committed per-kernel summary of the same passes
+(tools/pmc_summary.py --json), recorded as each entry's "source".
 
 Per kernel: measured HBM bytes per dispatch (FETCH_SIZE doubled -- the gfx950 correction for
 16-B streaming reads, MI355X_MICROARCH.md "HBM" -- plus WRITE_SIZE, both KiB per dispatch) and,
@@ -39,6 +42,7 @@ KERNELS = {
 
 def main():
     root = sys.argv[1]
+    src = sys.argv[2] if len(sys.argv) > 2 else os.path.relpath(root, ROOT)
     acc = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
     for f in glob.glob(os.path.join(root, "p*", "run_counter_collection.csv")):
@@ -62,7 +66,7 @@ def main():
         write = 1024 * a.get("WRITE_SIZE", 0.0)
         rec = {"fetch_bytes_x2": int(fetch), "write_bytes": int(write),
                "hbm_bytes_per_dispatch": int(fetch + write), "us_per_dispatch_profiled": round(t * 1e6, 2),
-               "grid": key[1], "source": os.path.relpath(root, ROOT)}
+               "grid": key[1], "source": src}
         if abi.startswith("blindno_project"):
             rec["bytes_per_point"] = round((fetch + write) / NPTS, 3)
             rec["points"] = NPTS
