@@ -63,35 +63,49 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
   const int r16 = lane & 15, kq = lane >> 4;
   const int nrt = (nrows + 15) >> 4;
   const int64_t nwork = (int64_t)nrt * ntile_groups;
-  for (int64_t wk = (int64_t)blockIdx.x * 4 + wave; wk < nwork; wk += (int64_t)gridDim.x * 4) {
+  const int64_t wstep = (int64_t)gridDim.x * 4;
+  // row pointer of this lane in work item w (rok: row inside the valid region)
+  auto row_of = [&](int64_t w, bool& rok) -> const float* {
+    const int row = (int)(w / ntile_groups) * 16 + r16;
+    rok = w < nwork && row < nrows && (N1v >= P1 || row % P1 < N1v);
+    return x + (int64_t)(rok ? row : 0) * P2;
+  };
+  // x loads run two K blocks ahead of the MFMAs, across work items: the last two K blocks of
+  // an item prefetch the first two of the wave's next item (persistent grids)
+  auto load_a = [&](const float* xr, bool rok, int kb, float (&a)[4]) {
+    const int w0 = kb * 16 + kq * 4;
+    if (ALIGNED && w0 + 3 < N2v) {
+      const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
+    }
+  };
+  float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (KB >= 2) {                                  // (KB == 1: loaded at each item's start)
+    bool rok0;
+    const float* xr0 = row_of((int64_t)blockIdx.x * 4 + wave, rok0);
+    load_a(xr0, rok0, 0, a1);
+    load_a(xr0, rok0, 1, a2);
+  }
+  for (int64_t wk = (int64_t)blockIdx.x * 4 + wave; wk < nwork; wk += wstep) {
     const int rt = (int)(wk / ntile_groups);
     const int tg = (int)(wk % ntile_groups);
     const int t0 = tg * NT;                       // first 16-column tile of this wave
-    const int row = rt * 16 + r16;
-    const bool rok = row < nrows && (N1v >= P1 || row % P1 < N1v);
-    const float* xr = x + (int64_t)(rok ? row : 0) * P2;
+    bool rok, rokn;
+    const float* xr = row_of(wk, rok);
+    const float* xrn = row_of(wk + wstep, rokn);  // the wave's next item (rokn false if none)
+    if (KB < 2) load_a(xr, rok, 0, a1);
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // x loads run two K blocks ahead of the MFMAs (small fields are latency-bound)
-    auto load_a = [&](int kb, float (&a)[4]) {
-      const int w0 = kb * 16 + kq * 4;
-      if (ALIGNED && w0 + 3 < N2v) {
-        const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-      } else {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
-      }
-    };
-    float a1[4], a2[4] = {0.f, 0.f, 0.f, 0.f};
-    load_a(0, a1);
-    if (KB > 1) load_a(1, a2);
     for (int kb = 0; kb < KB; ++kb) {
       float a[4] = {a1[0], a1[1], a1[2], a1[3]};
 #pragma unroll
       for (int s = 0; s < 4; ++s) a1[s] = a2[s];
-      if (kb + 2 < KB) load_a(kb + 2, a2);
+      if (kb + 2 < KB) load_a(xr, rok, kb + 2, a2);
+      else if (KB >= 2) load_a(xrn, rokn, kb + 2 - KB, a2);
       if (act) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = gelu_f(a[s]);
