@@ -121,6 +121,10 @@ int blindno_colpass(const float* At, const float* Wt, float* Xs, float* Y, float
 int blindno_mix_wgrad_nsplit(int Bn, int Ci, int Co, int K1, int m2);
 int blindno_mix_wgrad(const float* X, const float* G, float* dWt, float* partial, int nsplit,
                       int Bn, int Ci, int Co, int K1, int m2, blindno_stream_t stream);
+/* The sample-split partials of blindno_mix_wgrad only (nsplit >= 2): partial[y][Gw][...]
+ * (complex); the caller reduces them (blindno_reduce_partials(_multi), 2 m2 K1 Ci Co Gw floats). */
+int blindno_mix_wgrad_part(const float* X, const float* G, float* partial, int nsplit, int Gw,
+                           int Bn, int Ci, int Co, int K1, int m2, blindno_stream_t stream);
 
 /* 1D mode mix (compl_mul1d + DC halving, 1d_FPE/FNOModules.py:43-58).  At (Bn,m,C,1).
  * dir 0 (forward):  Xs = At with X[.,0] *= 0.5 (saved); Z[n][0][k][o] = c_k/P2 sum_i Xs W.
@@ -177,6 +181,13 @@ int blindno_spectrum_tile_layout(int Bn, int C, int P1, int P2, int m2);
 int blindno_rowdft_bag_lift(const float* X, const int* idx, const float* w0, const float* Gt,
                             float* At, const float* Tp, int B, int T, int L, int N1, int N2,
                             int C, int P1, int P2, int m2, blindno_stream_t stream);
+/* blindno_rowdft_bag_lift with the grid/bias spectrum formed in the kernel: Dg (m2, 3, P1)
+ * complex holds the row spectra of the gx, gy and all-ones planes (zero past the N1 x N2 crop);
+ * the grid/bias part is W0[c,1] Dg[.,0] + W0[c,2] Dg[.,1] + b0[c] Dg[.,2]. */
+int blindno_rowdft_bag_lift_dg(const float* X, const int* idx, const float* w0, const float* b0,
+                               const float* Dg, float* At, const float* Tp, int B, int T, int L,
+                               int N1, int N2, int C, int P1, int P2, int m2,
+                               blindno_stream_t stream);
 
 /* blindno_rowidft_epi (act 0) with x = x0 recomputed from (X, idx, grid, w0, b0); C <= 4. */
 int blindno_rowidft_epi_lift(const float* Z, const float* X, const int* idx, const float* grid,

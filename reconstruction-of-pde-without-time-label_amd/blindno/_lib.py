@@ -26,10 +26,12 @@ SIGNATURES = {
     "blindno_rowdft": "pppiiiiiis",
     "blindno_rowdft_crop": "pppiiiiiiiis",
     "blindno_rowdft_bag_lift": "ppppppiiiiiiiiis",
+    "blindno_rowdft_bag_lift_dg": "pppppppiiiiiiiiis",
     "blindno_rowidft_epi_lift": "ppppppppppiiiiiiiiis",
     "blindno_rowidft_bwd_lift": "ppppppppppiiiiiiiiis",
     "blindno_colpass": "pppppppiiiiiiiis",
     "blindno_mix_wgrad": "ppppiiiiiis",
+    "blindno_mix_wgrad_part": "pppiiiiiiis",
     "blindno_mix1d": "ppppiiiiiis",
     "blindno_rowidft_epi": "ppppppiiiiiis",
     "blindno_rowidft_bwd": "pppppppiiiiiis",

@@ -277,8 +277,14 @@ def k_colpass(At, Wt, Bn, Ci, Co, P1, m1, m2, P2, direction):
 
 
 def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2):
-    dWt = _empty(m2, K1, Ci, Co, 2, like=X)
     ns = query("blindno_mix_wgrad_nsplit", Bn, Ci, Co, K1, m2)
+    if _DEFER is not None and ns > 1:
+        # partials now, their reduction with the batched finalisation (before the unpack)
+        part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X)
+        call("blindno_mix_wgrad_part", ptr(X), ptr(G), ptr(part), ns, 1, Bn, Ci, Co, K1, m2,
+             stream_ptr())
+        return reduce_partials(part, ns, m2 * K1 * Ci * Co * 2).view(m2, K1, Ci, Co, 2)
+    dWt = _empty(m2, K1, Ci, Co, 2, like=X)
     part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X) if ns > 1 else None
     call("blindno_mix_wgrad", ptr(X), ptr(G), ptr(dWt), ptr(part) if part is not None else None, ns,
          Bn, Ci, Co, K1, m2, stream_ptr())
@@ -857,47 +863,43 @@ class HeadPairFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------- fused snapshot encoder
 
 
-def k_rowdft_bag_lift(X, idx_t, w0, Gt, B, T, L, N1, N2, C, P1, P2, m2):
+def k_rowdft_bag_lift(X, idx_t, w0, b0, Dg, B, T, L, N1, N2, C, P1, P2, m2):
+    """Row DFT of the encoder's lifted first-layer input for every snapshot of the bag; the
+    grid/bias part is formed in the kernel from the grid-plane spectra Dg (_grid_planes)."""
     At = _empty(B * L, m2, C, P1, 2, like=X)
-    call("blindno_rowdft_bag_lift", ptr(X), ptr(idx_t), ptr(w0), ptr(Gt), ptr(At),
+    call("blindno_rowdft_bag_lift_dg", ptr(X), ptr(idx_t), ptr(w0), ptr(b0), ptr(Dg), ptr(At),
          ptr(twiddle_mfma(P2, m2, X.device)), B, T, L, N1, N2, C, P1, P2, m2, stream_ptr())
     return At
 
 
-_GT_CACHE = {}
+_DG_CACHE = {}
 
 
-def _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, m2, cacheable=True):
-    """Row DFT of the grid / bias part of the encoder's lifted input (x0 of an all-zero
-    snapshot).  It depends only on the grid and on FNO_input.fc0.
-
-    With frozen weights (eval / inference: ``cacheable``) it is cached, keyed by the storage
-    and version counters of grid, fc0.weight and fc0.bias.  In training it is recomputed every
-    step (a lift and a one-sample row DFT, ~17 us): fc0 is a trained parameter, and a HIP graph
-    captured around a cached tensor would replay the capture-time spectrum after the optimizer
-    has moved fc0 (that was a bug: a stale spectrum, 4e-3 rel-L2 on the first layer's weight
-    gradients after 25 steps).  Writers of the weights outside torch ops (FlatAdam's fused
-    kernel) bump the version counters (torch.autograd.graph.increment_version), so a cached
-    entry never outlives the weights it was computed from."""
-    key = (grid.device, grid.data_ptr(), grid._version, fc0w.data_ptr(), fc0w._version,
-           fc0b.data_ptr(), fc0b._version, N1, N2, C, P1, P2, m2)
+def _grid_planes(grid, N1, N2, P1, P2, m2):
+    """Row spectra Dg (m2, 3, P1, 2) of the planes gx, gy and 1 on the N1 x N2 crop (zero on the
+    padding): the encoder's grid/bias part W0[:,1] gx + W0[:,2] gy + b0 is linear in them, so
+    its spectrum is formed per step inside the bag-lift row DFT from Dg and the CURRENT fc0
+    (which is trained) -- no per-step lift / row DFT / concat.  Dg depends on the grid only and
+    is cached, keyed by its storage and version; a miss during a graph capture computes it
+    inside the graph without caching (the capture does not execute it)."""
+    key = (grid.device, grid.data_ptr(), grid._version, N1, N2, P1, P2, m2)
     capturing = torch.cuda.is_current_stream_capturing()
-    cacheable = cacheable and not capturing
-    hit = _GT_CACHE.get(key) if cacheable else None
-    Gt = hit[-1] if hit is not None else None
-    if Gt is None:
-        inp0 = torch.cat([torch.zeros(1, N1, N2, 1, device=grid.device), grid.view(1, N1, N2, 2)], -1)
-        g0 = _empty(1, C, P1, P2, like=grid)
-        call("blindno_lift_fwd", ptr(inp0), ptr(fc0w), ptr(fc0b), ptr(g0), 1, N1, N2, 3, C, P1, P2,
-             stream_ptr())
-        Gt = k_rowdft(g0, 1, C, P1, P2, m2, 0)
-        if cacheable:
-            if len(_GT_CACHE) > 16:
-                _GT_CACHE.clear()
-            # the entry holds the inputs too, so their storage (part of the key) is never
-            # reused by another tensor while the entry lives
-            _GT_CACHE[key] = (grid, fc0w, fc0b, Gt)
-    return Gt
+    hit = _DG_CACHE.get(key)
+    if hit is not None:
+        return hit[-1]
+    # the planes through the lift kernel: weights [[1, 0], [0, 1], [0, 0]], bias [0, 0, 1]
+    w = torch.tensor([[1.0, 0.0], [0.0, 1.0], [0.0, 0.0]], dtype=F32, device=grid.device)
+    b = torch.tensor([0.0, 0.0, 1.0], dtype=F32, device=grid.device)
+    g0 = _empty(1, 3, P1, P2, like=grid)
+    call("blindno_lift_fwd", ptr(_c(grid)), ptr(w), ptr(b), ptr(g0), 1, N1, N2, 2, 3, P1, P2,
+         stream_ptr())
+    Dg = k_rowdft(g0, 1, 3, P1, P2, m2, 0)
+    if not capturing:
+        if len(_DG_CACHE) > 16:
+            _DG_CACHE.clear()
+        # the entry holds the grid too, so its storage (part of the key) is never reused
+        _DG_CACHE[key] = (grid, Dg)
+    return Dg
 
 
 class BagEncoderFn(torch.autograd.Function):
@@ -932,9 +934,7 @@ class BagEncoderFn(torch.autograd.Function):
         if C > 4 or meta.dim != 2 or n < 1:
             raise BlindnoError("BagEncoderFn: needs a 2D FNO of width <= 4")
         fc0w, fc0b = prm[0], prm[1]
-        # cached only when no parameter of the encoder is being trained (frozen weights)
-        frozen = not any(ctx.needs_input_grad[7:])
-        Gt = _grid_spectrum(grid, fc0w, fc0b, N1, N2, C, P1, P2, meta.m2, cacheable=frozen)
+        Dg = _grid_planes(grid, N1, N2, P1, P2, meta.m2)
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         Xs, Wts, zs = [], [], []
         Wts_all = pack_w2d_many([(prm[2 + 4 * k], prm[3 + 4 * k]) for k in range(n)], P1)
@@ -943,7 +943,7 @@ class BagEncoderFn(torch.autograd.Function):
             w1, w2, cw, cb = prm[off:off + 4]
             Wt = Wts_all[k]
             if k == 0:
-                At = k_rowdft_bag_lift(X, idx_t, fc0w, Gt, B, T, L, N1, N2, C, P1, P2, meta.m2)
+                At = k_rowdft_bag_lift(X, idx_t, fc0w, fc0b, Dg, B, T, L, N1, N2, C, P1, P2, meta.m2)
                 Xk, Z = k_colpass(At, Wt, Bn, C, C, P1, meta.m1, meta.m2, P2, 0)
                 z = _empty(Bn, C, P1, P2, like=X)
                 call("blindno_rowidft_epi_lift", ptr(Z), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),

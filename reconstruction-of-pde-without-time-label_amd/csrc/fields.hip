@@ -267,6 +267,65 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restr
   }
 }
 
+// Lift (fc0) weight / bias gradient of the wide heads on the matrix cores:
+// dW0[c][j] = sum_p dx0[c][p] in[p][j], db0[c] = sum_p dx0[c][p] over the N1 x N2 points --
+// a C x (Cin + 1) GEMM over the points.  16 points per chunk (one run along w; N2 % 16 == 0,
+// checked by the launcher), four v_mfma_f32_16x16x4f32 per 16-column tile of (j, 1): lane
+// (c16, g4) feeds float4 dx0[c = c16][h][w0 + 4 g4 ..] (A) and in[p][j = 16 jt + c16] at
+// the same four points (B; column Cin is 1.0).  Waves add their blocks in wave order; the
+// partial layout is lift_bwd_w_kernel's: partial[blockIdx.x][g][C Cin + C].
+template <int JT>
+__global__ __launch_bounds__(256) void lift_bwd_w_mfma_kernel(const float* __restrict__ dx0,
+                                                              const float* __restrict__ in,
+                                                              float* __restrict__ partial, int Bn,
+                                                              int N1, int N2, int Cin, int C,
+                                                              int P1, int P2) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  __shared__ f32x4 sacc[4][JT][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const int grp = blockIdx.y;
+  dx0 += (int64_t)grp * Bn * C * P1 * P2;
+  const int cpr = N2 >> 4;                         // 16-point chunks per grid row
+  const int64_t nch = (int64_t)Bn * N1 * cpr;
+  f32x4 acc[JT];
+#pragma unroll
+  for (int t = 0; t < JT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int64_t ch = (int64_t)blockIdx.x * 4 + wave; ch < nch; ch += (int64_t)gridDim.x * 4) {
+    const int64_t r = ch / cpr;                    // grid row (n, h)
+    const int w0 = (int)(ch - r * cpr) * 16 + 4 * g4;
+    const int n = (int)(r / N1), h = (int)(r - (r / N1) * N1);
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c16 < C) {
+      const float4 v = *reinterpret_cast<const float4*>(dx0 + (((int64_t)n * C + c16) * P1 + h) * P2 + w0);
+      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+    }
+    const float* ip = in + (r * N2 + w0) * Cin;    // point (n, h, w0), channels-last
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const int j = 16 * t + c16;
+      float b[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) b[s] = j < Cin ? ip[s * Cin + j] : (j == Cin ? 1.0f : 0.f);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < JT; ++t) sacc[wave][t][lane] = acc[t];
+  __syncthreads();
+  // D[c = 4 g4 + r][j = 16 t + c16]
+  const int np = C * Cin + C;
+  float* pp = partial + ((int64_t)blockIdx.x * gridDim.y + grp) * np;
+  for (int e = threadIdx.x; e < np; e += blockDim.x) {
+    const int c = e < C * Cin ? e / Cin : e - C * Cin;
+    const int j = e < C * Cin ? e - (e / Cin) * Cin : Cin;
+    const int t = j >> 4, ln = 16 * (c >> 2) + (j & 15), rr = c & 3;
+    pp[e] = ((sacc[0][t][ln][rr] + sacc[1][t][ln][rr]) + sacc[2][t][ln][rr]) + sacc[3][t][ln][rr];
+  }
+}
+
 // 1x1-conv weight / bias gradient of the wide fields (the C = 12 heads) on the matrix cores:
 // dWc[o][i] = sum_p dz[o][p] f(x)[i][p] is a C x C GEMM over the points (K), 16 points per
 // four v_mfma_f32_16x16x4f32: lane (c16, g4) loads float4 dz[o = c16][p0 + 4 g4 ..] (A) and
@@ -798,6 +857,17 @@ BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const floa
   if (partial) {
     if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)
       return (int)hipErrorInvalidValue;
+    const bool mf = C >= 5 && C <= 16 && Cin + 1 <= 32 && N2 % 16 == 0 && P2 % 4 == 0 &&
+                    (((uintptr_t)dx0) & 15) == 0;
+    if (mf) {
+      if (Cin + 1 <= 16)
+        lift_bwd_w_mfma_kernel<1><<<dim3(nchunk, G), 256, 0, st>>>(dx0, in, partial, Bg, N1, N2,
+                                                                  Cin, C, P1, P2);
+      else
+        lift_bwd_w_mfma_kernel<2><<<dim3(nchunk, G), 256, 0, st>>>(dx0, in, partial, Bg, N1, N2,
+                                                                  Cin, C, P1, P2);
+      return (int)hipGetLastError();
+    }
     const size_t sh = sizeof(float) * (size_t)(C + Cin) * (TP + 1);
     lift_bwd_w_kernel<<<dim3(nchunk, G), kBlock, sh, st>>>(dx0, in, partial, Bg, N1, N2, Cin, C,
                                                           P1, P2);

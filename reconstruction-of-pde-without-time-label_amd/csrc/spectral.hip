@@ -63,49 +63,35 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
   const int r16 = lane & 15, kq = lane >> 4;
   const int nrt = (nrows + 15) >> 4;
   const int64_t nwork = (int64_t)nrt * ntile_groups;
-  const int64_t wstep = (int64_t)gridDim.x * 4;
-  // row pointer of this lane in work item w (rok: row inside the valid region)
-  auto row_of = [&](int64_t w, bool& rok) -> const float* {
-    const int row = (int)(w / ntile_groups) * 16 + r16;
-    rok = w < nwork && row < nrows && (N1v >= P1 || row % P1 < N1v);
-    return x + (int64_t)(rok ? row : 0) * P2;
-  };
-  // x loads run two K blocks ahead of the MFMAs, across work items: the last two K blocks of
-  // an item prefetch the first two of the wave's next item (persistent grids)
-  auto load_a = [&](const float* xr, bool rok, int kb, float (&a)[4]) {
-    const int w0 = kb * 16 + kq * 4;
-    if (ALIGNED && w0 + 3 < N2v) {
-      const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
-      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-    } else {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
-    }
-  };
-  float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
-  if (KB >= 2) {                                  // (KB == 1: loaded at each item's start)
-    bool rok0;
-    const float* xr0 = row_of((int64_t)blockIdx.x * 4 + wave, rok0);
-    load_a(xr0, rok0, 0, a1);
-    load_a(xr0, rok0, 1, a2);
-  }
-  for (int64_t wk = (int64_t)blockIdx.x * 4 + wave; wk < nwork; wk += wstep) {
+  for (int64_t wk = (int64_t)blockIdx.x * 4 + wave; wk < nwork; wk += (int64_t)gridDim.x * 4) {
     const int rt = (int)(wk / ntile_groups);
     const int tg = (int)(wk % ntile_groups);
     const int t0 = tg * NT;                       // first 16-column tile of this wave
-    bool rok, rokn;
-    const float* xr = row_of(wk, rok);
-    const float* xrn = row_of(wk + wstep, rokn);  // the wave's next item (rokn false if none)
-    if (KB < 2) load_a(xr, rok, 0, a1);
+    const int row = rt * 16 + r16;
+    const bool rok = row < nrows && (N1v >= P1 || row % P1 < N1v);
+    const float* xr = x + (int64_t)(rok ? row : 0) * P2;
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // x loads run two K blocks ahead of the MFMAs (small fields are latency-bound)
+    auto load_a = [&](int kb, float (&a)[4]) {
+      const int w0 = kb * 16 + kq * 4;
+      if (ALIGNED && w0 + 3 < N2v) {
+        const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
+      }
+    };
+    float a1[4], a2[4] = {0.f, 0.f, 0.f, 0.f};
+    load_a(0, a1);
+    if (KB > 1) load_a(1, a2);
     for (int kb = 0; kb < KB; ++kb) {
       float a[4] = {a1[0], a1[1], a1[2], a1[3]};
 #pragma unroll
       for (int s = 0; s < 4; ++s) a1[s] = a2[s];
-      if (kb + 2 < KB) load_a(xr, rok, kb + 2, a2);
-      else if (KB >= 2) load_a(xrn, rokn, kb + 2 - KB, a2);
+      if (kb + 2 < KB) load_a(kb + 2, a2);
       if (act) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = gelu_f(a[s]);
@@ -149,10 +135,15 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
 // X (B, T, N1, N2) through the bag's index list (snapshot n = b L + l -> X[b][idx[l]]), so
 // neither the gathered bag, the concatenated input nor x0 is ever materialised.
 template <int NT, int ALIGNED>
+// b0 != nullptr: Gt holds the row spectra Dg[k][j][h] of the three grid/bias planes (gx, gy,
+// 1 on the crop) instead, and the grid/bias part is formed here as
+// W0[c,1] Dg[k][0] + W0[c,2] Dg[k][1] + b0[c] Dg[k][2] (Dg depends on the grid only, so it is
+// computed once; fc0 is trained, so a precomputed Gt would not be).
 __global__ __launch_bounds__(256) void rowdft_bag_lift_kernel(
     const float* __restrict__ X, const int* __restrict__ idx, const float* __restrict__ w0,
-    const float* __restrict__ Gt, float* __restrict__ At, const float* __restrict__ Tp, int nrows,
-    int T, int L, int N1, int N2, int C, int P1, int m2, int KB, int Npad, int ntile_groups) {
+    const float* __restrict__ b0, const float* __restrict__ Gt, float* __restrict__ At,
+    const float* __restrict__ Tp, int nrows, int T, int L, int N1, int N2, int C, int P1, int m2,
+    int KB, int Npad, int ntile_groups) {
   extern __shared__ float smT[];                 // [KB][4][Npad][4]
   const int nT = KB * 16 * Npad;
   stage_to_lds(smT, Tp, nT);
@@ -205,9 +196,21 @@ __global__ __launch_bounds__(256) void rowdft_bag_lift_kernel(
         if (orow >= nrows) continue;
         const int on = orow / P1, oh = orow - (orow / P1) * P1;
         const float u = acc[t][r];
+        float dg0 = 0.f, dg1 = 0.f, dg2 = 0.f;
+        if (b0) {
+          const int64_t di = (((int64_t)k * 3) * P1 + oh) * 2 + part;
+          dg0 = Gt[di];
+          dg1 = Gt[di + 2 * P1];
+          dg2 = Gt[di + 4 * P1];
+        }
         for (int c = 0; c < C; ++c) {
-          const int64_t gi = (((int64_t)k * C + c) * P1 + oh) * 2 + part;
-          At[((((int64_t)on * m2 + k) * C + c) * P1 + oh) * 2 + part] = fmaf(w0[c * 3], u, Gt[gi]);
+          float g;
+          if (b0) {
+            g = fmaf(w0[c * 3 + 1], dg0, fmaf(w0[c * 3 + 2], dg1, b0[c] * dg2));
+          } else {
+            g = Gt[(((int64_t)k * C + c) * P1 + oh) * 2 + part];
+          }
+          At[((((int64_t)on * m2 + k) * C + c) * P1 + oh) * 2 + part] = fmaf(w0[c * 3], u, g);
         }
       }
     }
@@ -721,10 +724,10 @@ BLINDNO_API int blindno_rowdft(const float* x, float* At, const float* Tp, int B
   return blindno_rowdft_crop(x, At, Tp, Bn, C, P1, P2, m2, act, P1, P2, stream);
 }
 
-BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const float* w0,
-                                        const float* Gt, float* At, const float* Tp, int B, int T,
-                                        int L, int N1, int N2, int C, int P1, int P2, int m2,
-                                        void* stream) {
+BLINDNO_API int blindno_rowdft_bag_lift_dg(const float* X, const int* idx, const float* w0,
+                                           const float* b0, const float* Gt, float* At,
+                                           const float* Tp, int B, int T, int L, int N1, int N2,
+                                           int C, int P1, int P2, int m2, void* stream) {
   if (B <= 0 || L <= 0 || T <= 0 || C <= 0 || N1 > P1 || N2 > P2 || m2 <= 0 || m2 > P2 / 2 + 1)
     return (int)hipErrorInvalidValue;
   const int64_t nrows64 = (int64_t)B * L * P1;
@@ -747,8 +750,8 @@ BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const fl
   const bool aligned = (N2 % 4) == 0 && (((uintptr_t)X) & 15) == 0;
   hipStream_t st = (hipStream_t)stream;
 #define RB(NT_, AL_)                                                                          \
-  rowdft_bag_lift_kernel<NT_, AL_><<<blocks, 256, sh, st>>>(X, idx, w0, Gt, At, Tp, nrows, T, L, \
-                                                            N1, N2, C, P1, m2, KB, Npad, groups)
+  rowdft_bag_lift_kernel<NT_, AL_><<<blocks, 256, sh, st>>>(X, idx, w0, b0, Gt, At, Tp, nrows, T, \
+                                                            L, N1, N2, C, P1, m2, KB, Npad, groups)
 #define RB_AL(NT_) \
   if (aligned) RB(NT_, 1); else RB(NT_, 0);
   switch (nt) {
@@ -760,6 +763,14 @@ BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const fl
 #undef RB_AL
 #undef RB
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const float* w0,
+                                        const float* Gt, float* At, const float* Tp, int B, int T,
+                                        int L, int N1, int N2, int C, int P1, int P2, int m2,
+                                        void* stream) {
+  return blindno_rowdft_bag_lift_dg(X, idx, w0, nullptr, Gt, At, Tp, B, T, L, N1, N2, C, P1, P2,
+                                    m2, stream);
 }
 
 BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
@@ -829,6 +840,20 @@ BLINDNO_API int blindno_mix_wgrad_nsplit(int Bn, int Ci, int Co, int K1, int m2)
   if (ns > per) ns = per;
   if (ns < 1) ns = 1;
   return (int)(ns > 1024 ? 1024 : ns);
+}
+
+// The split weight gradient's partials only (nsplit > 1): partial[y][Gw][m2 K1 Ci Co] complex,
+// reduced by the caller (blindno.ops' deferred finalisation batches that reduction).
+BLINDNO_API int blindno_mix_wgrad_part(const float* X, const float* G, float* partial, int nsplit,
+                                       int Gw, int Bn, int Ci, int Co, int K1, int m2,
+                                       void* stream) {
+  const int64_t total = (int64_t)m2 * K1 * Ci * Co;
+  if (total >= INT32_MAX / 2 || nsplit < 2 || !partial || Gw < 1 || Bn % Gw)
+    return (int)hipErrorInvalidValue;
+  const dim3 g((unsigned)cdiv(total, kBlock), nsplit, Gw);
+  mix_wgrad_kernel<<<g, kBlock, 0, (hipStream_t)stream>>>((const float2*)X, (const float2*)G,
+                                                          (float2*)partial, Bn, Ci, Co, K1, m2);
+  return (int)hipGetLastError();
 }
 
 BLINDNO_API int blindno_mix_wgrad_g(const float* X, const float* G, float* dWt, float* partial,

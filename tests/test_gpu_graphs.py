@@ -91,8 +91,9 @@ def test_gather_flat_segments():
 
 
 def test_grid_spectrum_cache_follows_fc0_and_grid():
-    """The encoder's grid/bias spectrum is cached across steps (ops._grid_spectrum); an in-place
-    change of FNO_input.fc0 or of the grid must invalidate it."""
+    """The encoder's grid-plane spectra are cached across steps (ops._grid_planes) and its
+    grid/bias part is formed from them with the current FNO_input.fc0 in the kernel: an in-place
+    change of fc0 must show at once, one of the grid must invalidate the cache."""
     import blindno
     torch.manual_seed(3)
     m = blindno.NIOFP2D_FNO(2, 3, 100, 25, 2, 6, 5, 2).cuda().eval()

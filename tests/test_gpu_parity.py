@@ -364,3 +364,30 @@ def test_conv_wgrad_vs_fp64(C, act, G):
         # 8c gradient bar is 1e-4)
         assert rel_l2(got[gi, :C * C].numpy(), w.reshape(-1).numpy()) <= 5e-5
         assert rel_l2(got[gi, C * C:].numpy(), b.numpy()) <= 5e-5
+
+
+@pytest.mark.parametrize("C,Cin,N,G", [(12, 25, 128, 2), (12, 12, 64, 1), (8, 30, 48, 1), (12, 25, 61, 1)])
+def test_lift_wgrad_vs_fp64(C, Cin, N, G):
+    """fc0 (lift) weight / bias gradient of an FNO head (blindno_lift_bwd_g: the matrix-core
+    kernel when N % 16 == 0, the LDS-staged one otherwise) vs the float64 sums over the crop:
+    dW0[c][j] = sum_p dx0[c][p] in[p][j], db0[c] = sum_p dx0[c][p]."""
+    from blindno import ops
+    from blindno._lib import call, ptr, query, stream_ptr
+    Bg, P = 4, N + ops.pad_amount(N)
+    g = torch.Generator(device="cuda").manual_seed(C + Cin + N)
+    dx0 = torch.randn(G * Bg, C, P, P, device="cuda", generator=g)
+    inp = torch.randn(Bg, N, N, Cin, device="cuda", generator=g)
+    w0 = torch.randn(G, C, Cin, device="cuda", generator=g)
+    nch = query("blindno_lift_bwd_nchunk", Bg, N, N)
+    part = torch.empty(nch, G, C * Cin + C, device="cuda")
+    call("blindno_lift_bwd_g", ptr(dx0), ptr(inp), ptr(w0), None, ptr(part), nch, G, C * Cin, G * Bg,
+         N, N, Cin, C, P, P, stream_ptr())
+    got = ops.reduce_partials(part, nch, G * (C * Cin + C)).view(G, C * Cin + C).double().cpu()
+    d64 = dx0.double().cpu()[:, :, :N, :N]
+    i64 = inp.double().cpu()
+    for gi in range(G):
+        d = d64[gi * Bg:(gi + 1) * Bg]
+        w = torch.einsum("nchw,nhwj->cj", d, i64)
+        b = d.sum(dim=(0, 2, 3))
+        assert rel_l2(got[gi, :C * Cin].numpy(), w.reshape(-1).numpy()) <= 5e-5
+        assert rel_l2(got[gi, C * Cin:].numpy(), b.numpy()) <= 5e-5
