@@ -276,9 +276,12 @@ def k_colpass(At, Wt, Bn, Ci, Co, P1, m1, m2, P2, direction):
     return Xs, Z
 
 
-def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2):
+def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2, deferrable=False):
+    """Spectral weight gradient dWt (m2, K1, Ci, Co, 2).  ``deferrable``: the caller's only
+    reader of dWt is itself deferred (the 2D unpack), so under deferred_reductions() the
+    sample-split reduction may join the batched finalisation."""
     ns = query("blindno_mix_wgrad_nsplit", Bn, Ci, Co, K1, m2)
-    if _DEFER is not None and ns > 1:
+    if _DEFER is not None and deferrable and ns > 1:
         # partials now, their reduction with the batched finalisation (before the unpack)
         part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X)
         call("blindno_mix_wgrad_part", ptr(X), ptr(G), ptr(part), ns, 1, Bn, Ci, Co, K1, m2,
@@ -421,7 +424,8 @@ def spec_backward(dz, X, Wt, sh: SpecShape, valid=None):
         G, GZ = k_colpass(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
     else:
         G, GZ = k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 1)
-    dWt = k_mix_wgrad(X, G, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2)
+    # 2D: the gradient's only reader is unpack_w2d, deferred alongside (1D unpacks at once)
+    dWt = k_mix_wgrad(X, G, sh.Bn, sh.Ci, sh.Co, sh.K1, sh.m2, deferrable=sh.dim == 2)
     return dWt, GZ
 
 
