@@ -136,7 +136,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL ("nccl") across the node's GPUs; BLINDNO_BENCH_BACKEND=gloo rehearses the N > 1
+        # path with several ranks on one GPU (RCCL refuses two ranks per device)
+        backend = os.environ.get("BLINDNO_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     blindno.load_library()
