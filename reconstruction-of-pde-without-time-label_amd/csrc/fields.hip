@@ -96,39 +96,26 @@ __global__ __launch_bounds__(kBlock) void lift_fwd_kernel(const float* __restric
   }
 }
 
-// d_in[n][h][w][j] = sum_g sum_c W0[g][c][j] dx0[g Bn + n][c][h][w]: one thread per point
-// (w fastest across lanes, so each dx0 load is one coalesced run), all Cin outputs in
-// registers (CJ >= Cin); a thread per (point, j) issued ~25x as many (mostly redundant) loads.
-template <int CJ>
 __global__ __launch_bounds__(kBlock) void lift_bwd_in_kernel(const float* __restrict__ dx0,
                                                              const float* __restrict__ w0,
                                                              float* __restrict__ d_in, int Bn,
                                                              int N1, int N2, int Cin, int C,
                                                              int P1, int P2, int G, int64_t wgs) {
   // d_in has Bn samples; with G groups the gradient sums over the groups' samples g Bn + n
-  const int64_t total = (int64_t)Bn * N1 * N2;
+  const int64_t total = (int64_t)Bn * N1 * N2 * Cin;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int w = (int)(idx % N2);
-    const int64_t t = idx / N2;
+    const int j = (int)(idx % Cin);
+    int64_t t = idx / Cin;
+    const int w = (int)(t % N2);
+    t /= N2;
     const int h = (int)(t % N1);
     const int n = (int)(t / N1);
-    float acc[CJ];
-#pragma unroll
-    for (int j = 0; j < CJ; ++j) acc[j] = 0.f;
-    for (int g = 0; g < G; ++g) {
-      const float* wg = w0 + g * wgs;
-      for (int c = 0; c < C; ++c) {
-        const float v = dx0[((((int64_t)g * Bn + n) * C + c) * P1 + h) * P2 + w];
-#pragma unroll
-        for (int j = 0; j < CJ; ++j)
-          if (j < Cin) acc[j] = fmaf(wg[c * Cin + j], v, acc[j]);
-      }
-    }
-    float* dp = d_in + idx * Cin;
-#pragma unroll
-    for (int j = 0; j < CJ; ++j)
-      if (j < Cin) dp[j] = acc[j];
+    float v = 0.f;
+    for (int g = 0; g < G; ++g)
+      for (int c = 0; c < C; ++c)
+        v = fmaf(w0[g * wgs + c * Cin + j], dx0[((((int64_t)g * Bn + n) * C + c) * P1 + h) * P2 + w], v);
+    d_in[idx] = v;
   }
 }
 
@@ -845,14 +832,9 @@ BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const floa
   const int Bg = Bn / G;
   hipStream_t st = (hipStream_t)stream;
   if (d_in) {
-    const int64_t total = (int64_t)Bg * N1 * N2;
-    if (Cin > 32) return (int)hipErrorInvalidValue;
-    if (Cin <= 4)
-      lift_bwd_in_kernel<4><<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(
-          dx0, w0, d_in, Bg, N1, N2, Cin, C, P1, P2, G, G > 1 ? wgs : 0);
-    else
-      lift_bwd_in_kernel<32><<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(
-          dx0, w0, d_in, Bg, N1, N2, Cin, C, P1, P2, G, G > 1 ? wgs : 0);
+    const int64_t total = (int64_t)Bg * N1 * N2 * Cin;
+    lift_bwd_in_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(
+        dx0, w0, d_in, Bg, N1, N2, Cin, C, P1, P2, G, G > 1 ? wgs : 0);
   }
   if (partial) {
     if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)
