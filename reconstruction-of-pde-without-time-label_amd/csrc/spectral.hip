@@ -971,6 +971,77 @@ __global__ __launch_bounds__(kBlock) void pack_w2d_multi_kernel(PackSegs segs) {
   segs.Wt[sg][idx] = make_float2(p[0], p[1]);
 }
 
+// LDS-tiled packing / unpacking when no kept row overlaps (2 m1 < P1: kept row j < m1 is
+// weights1 row j, j >= m1 is weights2 row j - m1).  For each (which, jj) the move is a
+// transpose of the [Ci Co] x [m2] complex block (reference layout: k fastest; packed: (i, o)
+// fastest); a workgroup moves one 32 x 32 tile through LDS so that both the reads and the
+// writes are 256-B runs (the element-wise kernels read or wrote with an m1 m2 or Ci Co stride).
+// Block b of segment s -> (which, jj, io tile, k tile); DIR 0 packs, DIR 1 unpacks.
+template <int DIR>
+__global__ __launch_bounds__(256) void w2d_transpose_kernel(PackSegs segs) {
+  __shared__ float2 tile[32][33];
+  const int b = blockIdx.x;
+  int sg = 0;
+  while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;    // uniform scan
+  const int Ci = segs.Ci[sg], Co = segs.Co[sg], m1 = segs.m1[sg], m2 = segs.m2[sg];
+  const int CC = Ci * Co, K1 = 2 * m1;
+  const int nio = (CC + 31) >> 5, nk = (m2 + 31) >> 5;
+  int q = b - segs.cum[sg];
+  const int kt = q % nk; q /= nk;
+  const int iot = q % nio; q /= nio;
+  const int jj = q % m1;
+  const int which = q / m1;
+  // reference-layout block: w[io][jj][k] (complex, k fastest), io = i Co + o
+  const float2* wsrc = reinterpret_cast<const float2*>(which ? segs.w2[sg] : segs.w1[sg]);
+  float2* wdst = reinterpret_cast<float2*>(const_cast<float*>(which ? segs.w2[sg] : segs.w1[sg]));
+  float2* W = segs.Wt[sg];                       // packed: W[k][j][io], j = which m1 + jj
+  const int j = which * m1 + jj;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;      // 32 x 8 threads
+  if (DIR == 0) {
+#pragma unroll
+    for (int r = 0; r < 32; r += 8) {
+      const int io = iot * 32 + ty + r, k = kt * 32 + tx;
+      if (io < CC && k < m2) tile[ty + r][tx] = wsrc[((int64_t)io * m1 + jj) * m2 + k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 32; r += 8) {
+      const int k = kt * 32 + ty + r, io = iot * 32 + tx;
+      if (io < CC && k < m2) W[((int64_t)k * K1 + j) * CC + io] = tile[tx][ty + r];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 32; r += 8) {
+      const int k = kt * 32 + ty + r, io = iot * 32 + tx;
+      if (io < CC && k < m2) tile[tx][ty + r] = W[((int64_t)k * K1 + j) * CC + io];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 32; r += 8) {
+      const int io = iot * 32 + ty + r, k = kt * 32 + tx;
+      if (io < CC && k < m2) wdst[((int64_t)io * m1 + jj) * m2 + k] = tile[ty + r][tx];
+    }
+  }
+}
+
+// segments -> block table for w2d_transpose_kernel; false if a segment has overlapping kept
+// rows (the element-wise kernels handle those)
+static bool w2d_tiled_segs(PackSegs& segs, int64_t& blocks) {
+  blocks = 0;
+  for (int i = 0; i < segs.nseg; ++i) {
+    if (2 * segs.m1[i] >= segs.P1[i]) return false;
+    segs.cum[i] = (int)blocks;
+    const int64_t nio = (segs.Ci[i] * segs.Co[i] + 31) / 32, nk = (segs.m2[i] + 31) / 32;
+    blocks += 2 * (int64_t)segs.m1[i] * nio * nk;
+  }
+  segs.cum[segs.nseg] = (int)blocks;
+  return blocks < INT32_MAX;
+}
+
+#ifndef W2D_TILED
+#define W2D_TILED 1
+#endif
+
 BLINDNO_API int blindno_pack_w2d_multi(const void* const* w1s, const void* const* w2s,
                                        void* const* Wts, const int* shapes, int nseg,
                                        void* stream) {
@@ -996,6 +1067,11 @@ BLINDNO_API int blindno_pack_w2d_multi(const void* const* w1s, const void* const
     segs.cum[k] = (int)blocks;
     if (blocks == 0) continue;
     if (blocks >= INT32_MAX) return (int)hipErrorInvalidValue;
+    int64_t tb = 0;
+    if (W2D_TILED && w2d_tiled_segs(segs, tb)) {
+      w2d_transpose_kernel<0><<<(unsigned)tb, 256, 0, (hipStream_t)stream>>>(segs);
+      continue;
+    }
     pack_w2d_multi_kernel<<<(unsigned)blocks, kBlock, 0, (hipStream_t)stream>>>(segs);
   }
   return (int)hipGetLastError();
@@ -1071,6 +1147,22 @@ BLINDNO_API int blindno_unpack_w2d_multi(const void* const* dWts, void* const* d
     segs.cum[k] = (int)blocks;
     if (blocks == 0) continue;
     if (blocks >= INT32_MAX) return (int)hipErrorInvalidValue;
+    if (W2D_TILED) {
+      PackSegs ps{};
+      ps.nseg = k;
+      for (int i = 0; i < k; ++i) {
+        ps.w1[i] = segs.dw1[i];
+        ps.w2[i] = segs.dw2[i];
+        ps.Wt[i] = const_cast<float2*>(segs.dWt[i]);
+        ps.Ci[i] = segs.Ci[i]; ps.Co[i] = segs.Co[i]; ps.m1[i] = segs.m1[i];
+        ps.m2[i] = segs.m2[i]; ps.P1[i] = segs.P1[i];
+      }
+      int64_t tb = 0;
+      if (w2d_tiled_segs(ps, tb)) {
+        w2d_transpose_kernel<1><<<(unsigned)tb, 256, 0, (hipStream_t)stream>>>(ps);
+        continue;
+      }
+    }
     unpack_w2d_multi_kernel<<<(unsigned)blocks, kBlock, 0, (hipStream_t)stream>>>(segs);
   }
   return (int)hipGetLastError();
