@@ -26,16 +26,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW = 4;      // waves per workgroup
 
-// Field outputs of the row inverse (each element written once, read by a later kernel):
-// ROWINV_NT_STORE selects non-temporal (streaming) stores.
-#ifndef ROWINV_NT_STORE
-#define ROWINV_NT_STORE 0
-#endif
-__device__ __forceinline__ void st_field(float* p, float v) {
-  if constexpr (ROWINV_NT_STORE) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-
 // lookahead of the adjoint's epilogue operands for the narrow (C <= 4) fields
 #ifndef ROWINV_PRE_BWD
 #define ROWINV_PRE_BWD 0
@@ -228,12 +218,12 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
 #pragma unroll
             for (int i = 0; i < CM; ++i)
               if (i < C) v = fmaf(wcg[o * C + i], xv[i], v);
-            st_field(out + rbase + o * HW + w, v);
+            out[rbase + o * HW + w] = v;
           }
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (c0 + r < C) st_field(out + rbase + (c0 + r) * HW + w, d[r]);
+            if (c0 + r < C) out[rbase + (c0 + r) * HW + w] = d[r];
         }
       } else {
         if (has_wc) {
@@ -258,7 +248,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
                 wacc[NWC + 4 * r + 3] += gi;
               }
             } else if (i < C) {
-              st_field(out + rbase + i * HW + w, gi);
+              out[rbase + i * HW + w] = gi;
             }
           }
           if constexpr (WG != 0) {
@@ -273,7 +263,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (c0 + r < C) st_field(out + rbase + (c0 + r) * HW + w, d[r]);
+            if (c0 + r < C) out[rbase + (c0 + r) * HW + w] = d[r];
         }
       }
     }
@@ -438,7 +428,7 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
             }
             if (MODE == 1 && ACT) v *= sv[c];
           }
-          st_field(out + rbase + (unsigned)(c * HW + w), v);
+          out[rbase + (unsigned)(c * HW + w)] = v;
         }
       }
     }
