@@ -267,6 +267,10 @@ __device__ __forceinline__ void load4c(const float2* src, int len, bool vec, flo
 // layers launch one workgroup per (sample, mode) pair -- one wave per SIMD -- so a one-block
 // lookahead leaves each step waiting a full memory latency (measured ~16 us for 10 steps)
 constexpr int kFullHB = 10;
+// the column inverse fused into the column-DFT / mix workgroups (coldft_mix_kernel FUSE)
+#ifndef COLPASS_FUSE
+#define COLPASS_FUSE 0
+#endif
 // H16 (config E, blindno.ops.set_mix_precision("fp16")): the channel mix takes fp16 operands
 // with fp32 accumulation -- each complex multiply-add is two v_dot2c_f32_f16 (packed fp16
 // pairs, exact products, fp32 sum).  The column spectra are block-scaled first: the workgroup's
@@ -277,7 +281,10 @@ constexpr int kFullHB = 10;
 // batch of complex GEMVs (one Ci x Co matrix per kept mode, one row per sample), which would
 // fill a quarter of an MFMA tile at best.
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-template <int DIR, bool FULL, bool H16>
+// FUSE: the column inverse runs in the same workgroup on its own pairs (Y stays in LDS; the
+// colidft launch and the Y round trip disappear): Z[n][h][k][o] = sum_j Y[o][j] conj(F[h][j])
+// as a complex GEMM with M = the pairs' (p, o) rows, N = 16-row h tiles, K = the kept rows.
+template <int DIR, bool FULL, bool H16, bool FUSE>
 __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restrict__ At,
                                                          const float2* __restrict__ Wt,
                                                          const f32x4* __restrict__ FB,
@@ -285,9 +292,10 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
                                                          float2* __restrict__ Y, int npairs,
                                                          int Ci, int Co, int P1, int m1, int m2,
                                                          int P2, int G, int vec, int Bg,
-                                                         int64_t wtgs) {
+                                                         int64_t wtgs, const f32x4* __restrict__ GB,
+                                                         float2* __restrict__ Z, int tiled) {
   // grouped launches: samples n of weight group n / Bg use Wt + (n / Bg) wtgs (in floats)
-  extern __shared__ float2 sX[];                  // [G Cin][K1p + 1]
+  extern __shared__ float2 sX[];                  // [G Cin][K1p + 1] (+ FUSE: [G Cout][K1p + 1])
   const int K1 = kept_rows_count(m1, P1);
   const int Jt = (K1 + 15) >> 4, K1p = Jt * 16, LDX = K1p + 1;
   const int Cin = DIR == 0 ? Ci : Co;
@@ -438,9 +446,55 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
         im *= sc;
       }
     }
-    Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
+    if constexpr (FUSE) sX[(G * Cin + p * Cout + o) * LDX + j] = make_float2(re, im);
+    else Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
   };
   for (int e = threadIdx.x; e < nout; e += blockDim.x) mix_one(e);
+  if constexpr (FUSE) {
+    __syncthreads();
+    const float2* sY = sX + G * Cin * LDX;
+    const int rowsY = np * Cout;
+    const int MtY = (rowsY + 15) >> 4;
+    const int Ht = (P1 + 15) >> 4;
+    for (int item = wave; item < MtY * Ht; item += 4) {
+      const int mt = item / Ht, ht = item % Ht;
+      const int row = mt * 16 + r16;
+      const bool rok = row < rowsY;
+      const float2* yr = sY + (rok ? row : 0) * LDX;
+      const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
+      f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
+      for (int jb = 0; jb < Jt; ++jb) {
+        float re[4], im[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float2 v = rok ? yr[jb * 16 + kq * 4 + s] : make_float2(0.f, 0.f);
+          re[s] = v.x;
+          im[s] = v.y;
+        }
+        cmfma4(re, im, gb[jb * 128], gb[jb * 128 + 1], dr, di);
+      }
+      const int h = ht * 16 + r16;
+      if (h >= P1) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rowD = mt * 16 + kq * 4 + r;
+        if (rowD >= rowsY) continue;
+        const int p = rowD / Cout, o = rowD - p * Cout;
+        const int q = q0 + p, n = q / m2, k = q - n * m2;
+        if (!tiled) {
+          Z[(((int64_t)n * P1 + h) * m2 + k) * Cout + o] = make_float2(dr[r], di[r]);
+        } else {
+          // A-tile order of the wide row inverse (as colidft_kernel writes it)
+          const int gr = n * P1 + h;
+          const int c16 = 4 * (gr & 3) + (o & 3);
+          float* zt = reinterpret_cast<float*>(Z) +
+                      ((int64_t)((gr >> 2) * (Cout >> 2) + (o >> 2)) * (m2 >> 1) + (k >> 1)) * 64;
+          zt[32 * (k & 1) + c16] = dr[r];
+          zt[32 * (k & 1) + 16 + c16] = di[r];
+        }
+      }
+    }
+  }
 }
 
 // Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
@@ -796,17 +850,21 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   while (((G * cin + 15) / 16) * Jt < 4 && G * cin < 64) ++G;
   G = ((G * cin + 15) / 16) * 16 / cin;
   if (G < 1) G = 1;
-  const size_t sh = sizeof(float2) * (size_t)G * cin * (K1p + 1);
+  const bool fuse = COLPASS_FUSE != 0;
+  const size_t sh = sizeof(float2) * (size_t)G * (cin + (fuse ? cout : 0)) * (K1p + 1);
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
   const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
   hipStream_t st = (hipStream_t)stream;
   const dim3 g1((unsigned)cdiv(npairs, G));
+  const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
   // full operand prefetch when the launch is too small to hide latency with waves
   const bool full = (P1 + 15) / 16 <= kFullHB && (int64_t)g1.x * 4 < 4096;
-#define CM3_(D_, F_, H_)                                                                    \
-  coldft_mix_kernel<D_, F_, H_><<<g1, 256, sh, st>>>(                                       \
+#define CM4_(D_, F_, H_, U_)                                                                \
+  coldft_mix_kernel<D_, F_, H_, U_><<<g1, 256, sh, st>>>(                                   \
       (const float2*)At, (const float2*)Wt, (const f32x4*)FB, (float2*)Xs, (float2*)Y,     \
-      (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg, wtgs)
+      (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg, wtgs, (const f32x4*)GB, (float2*)Z, \
+      tiled)
+#define CM3_(D_, F_, H_) do { if (fuse) CM4_(D_, F_, H_, true); else CM4_(D_, F_, H_, false); } while (0)
 #define CM_(D_, F_) do { if (h16) CM3_(D_, F_, true); else CM3_(D_, F_, false); } while (0)
   if (dir == 0) {
     if (full) CM_(0, true); else CM_(0, false);
@@ -815,12 +873,12 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   }
 #undef CM_
 #undef CM3_
+#undef CM4_
   int e = (int)hipGetLastError();
-  if (e) return e;
+  if (e || fuse) return e;
   const int Ht = (P1 + 15) / 16;
   const int Mt = (m2 * cout + 15) / 16;
   const dim3 g2((unsigned)(Bn * Ht), (unsigned)((Mt + 3) / 4));
-  const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
   colidft_kernel<<<g2, 256, 0, st>>>((const float2*)Y, (const f32x4*)GB, (float2*)Z, cout, P1, m1,
                                      m2, tiled);
   return (int)hipGetLastError();
