@@ -160,6 +160,21 @@ int blindno_rowidft_bwd_crop(const float* G, const float* dz, const float* wc, c
                              float* dx, const float* tb, float* partial, int Bn, int C, int P1,
                              int P2, int m2, int act, int dN1, int dN2, blindno_stream_t stream);
 int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2);
+/* Layer chaining (the FNO layer loop, 2d_FPE/FNOModules.py:226-232): the next spectral layer's
+ * row DFT of the field a row inverse produces, taken in the same pass -- At / Tp exactly as
+ * blindno_rowdft(field, At, Tp, Bn, C, P1, P2, m2, act_next) would take them (m2 of the next
+ * layer equals this one's).  Fused for C <= 4, m2 <= 16 when a work item spans whole rows;
+ * otherwise the entry launches blindno_rowdft itself after the row inverse.  Same results. */
+/* blindno_rowidft_bwd_crop + At = rowDFT(dx) (act 0: the previous layer's adjoint input). */
+int blindno_rowidft_bwd_rd(const float* G, const float* dz, const float* wc, const float* xsrc,
+                           float* dx, const float* tb, float* partial, int Bn, int C, int P1,
+                           int P2, int m2, int act, int dN1, int dN2, float* At, const float* Tp,
+                           blindno_stream_t stream);
+/* blindno_rowidft_epi + At = rowDFT(f(z)), f = GELU when act_next. */
+int blindno_rowidft_epi_rd(const float* Z, const float* x, const float* wc, const float* bc,
+                           float* z, const float* tb, int Bn, int C, int P1, int P2, int m2,
+                           int act, float* At, const float* Tp, int act_next,
+                           blindno_stream_t stream);
 
 /* 1 when the spectrum Z that blindno_colpass(_g) writes and blindno_rowidft_epi/bwd(_g) read
  * is in A-tile order instead of Z[n][h][k][c]: C in {8, 12, 16} (the FNO heads, width 12), m2
@@ -194,6 +209,13 @@ int blindno_rowidft_epi_lift(const float* Z, const float* X, const int* idx, con
                              const float* w0, const float* b0, const float* wc, const float* bc,
                              float* z, const float* tb, int B, int T, int L, int N1, int N2,
                              int C, int P1, int P2, int m2, blindno_stream_t stream);
+/* blindno_rowidft_epi_lift + At = rowDFT(f(z)) for the second layer (f = GELU when act_next;
+ * see blindno_rowidft_epi_rd). */
+int blindno_rowidft_epi_lift_rd(const float* Z, const float* X, const int* idx, const float* grid,
+                                const float* w0, const float* b0, const float* wc,
+                                const float* bc, float* z, const float* tb, int B, int T, int L,
+                                int N1, int N2, int C, int P1, int P2, int m2, float* At,
+                                const float* Tp, int act_next, blindno_stream_t stream);
 
 /* Adjoint of blindno_rowidft_epi_lift: dx0 = irow^H(G) + Wc^T dz is NOT written; the pass
  * reduces partial[blindno_rowidft_bwd_nchunk(B L, C, P1, P2, m2)][C*C + C + 4 C] =

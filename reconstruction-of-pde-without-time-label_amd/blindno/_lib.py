@@ -36,6 +36,9 @@ SIGNATURES = {
     "blindno_rowidft_epi": "ppppppiiiiiis",
     "blindno_rowidft_bwd": "pppppppiiiiiis",
     "blindno_rowidft_bwd_crop": "pppppppiiiiiiiis",
+    "blindno_rowidft_bwd_rd": "pppppppiiiiiiiipps",
+    "blindno_rowidft_epi_rd": "ppppppiiiiiippis",
+    "blindno_rowidft_epi_lift_rd": "ppppppppppiiiiiiiiippis",
     "blindno_conv_wgrad": "pppiiiiiis",
     "blindno_reduce_partials": "ppiis",
     "blindno_spectrum_tile_layout": "iiiii",

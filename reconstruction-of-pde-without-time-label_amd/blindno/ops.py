@@ -363,23 +363,45 @@ def k_rowidft_epi(Z, x, wc, bc, Bn, C, P1, P2, m2, act):
     return z
 
 
-def k_rowidft_bwd(G, dz, wc, xsrc, Bn, C, P1, P2, m2, act, want_wgrad=False, valid=None):
+def k_rowidft_epi_rd(Z, x, wc, bc, Bn, C, P1, P2, m2, act, act_next):
+    """k_rowidft_epi plus the next layer's row DFT of f(z) (f = GELU if act_next) in the same
+    pass: returns (z, At) with At = k_rowdft(z, ..., act_next)."""
+    z = _empty(Bn, C, P1, P2, like=Z)
+    At = _empty(Bn, m2, C, P1, 2, like=Z)
+    call("blindno_rowidft_epi_rd", ptr(Z), ptr(x), ptr(wc), ptr(bc), ptr(z),
+         ptr(twiddle_rowinv(P2, m2, Z.device)), Bn, C, P1, P2, m2, act, ptr(At),
+         ptr(twiddle_mfma(P2, m2, Z.device)), act_next, stream_ptr())
+    return z, At
+
+
+def k_rowidft_bwd(G, dz, wc, xsrc, Bn, C, P1, P2, m2, act, want_wgrad=False, valid=None,
+                  rd=False):
     """dx = irow^H(G) + Wc^T dz, times GELU'(xsrc) if act.  With want_wgrad (C <= 8) the
     1x1-conv weight/bias gradients are reduced in the same pass (C <= 4): returns (dx, gw, gb).
-    ``valid`` = (N1v, N2v): dz is read only on that region (zero elsewhere)."""
+    ``valid`` = (N1v, N2v): dz is read only on that region (zero elsewhere).  ``rd``: also the
+    row DFT of dx for the previous layer's adjoint (k_rowdft(dx, ..., 0)) in the same pass,
+    appended to the result."""
     dx = _empty(Bn, C, P1, P2, like=G)
     partial, nchunk = None, 0
     if want_wgrad:
         nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, m2)
         partial = _empty(nchunk, C * C + C, like=G)
     dN1, dN2 = valid if valid is not None else (P1, P2)
-    call("blindno_rowidft_bwd_crop", ptr(G), ptr(dz), ptr(wc), ptr(xsrc), ptr(dx),
-         ptr(twiddle_rowinv(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, dN1, dN2,
-         stream_ptr())
-    if not want_wgrad:
-        return dx, None, None
-    g = reduce_partials(partial, nchunk, C * C + C)
-    return dx, g[: C * C], g[C * C:]
+    At = None
+    if rd:
+        At = _empty(Bn, m2, C, P1, 2, like=G)
+        call("blindno_rowidft_bwd_rd", ptr(G), ptr(dz), ptr(wc), ptr(xsrc), ptr(dx),
+             ptr(twiddle_rowinv(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, dN1,
+             dN2, ptr(At), ptr(twiddle_mfma(P2, m2, G.device)), stream_ptr())
+    else:
+        call("blindno_rowidft_bwd_crop", ptr(G), ptr(dz), ptr(wc), ptr(xsrc), ptr(dx),
+             ptr(twiddle_rowinv(P2, m2, G.device)), ptr(partial), Bn, C, P1, P2, m2, act, dN1,
+             dN2, stream_ptr())
+    out = (dx, None, None)
+    if want_wgrad:
+        g = reduce_partials(partial, nchunk, C * C + C)
+        out = (dx, g[: C * C], g[C * C:])
+    return out + (At,) if rd else out
 
 
 def k_conv_wgrad(dz, x, Bn, C, P1, P2, act):
@@ -408,18 +430,22 @@ class SpecShape:
             raise BlindnoError(f"modes1 {m1} exceed P1 = {P1}")
 
 
-def spec_forward(x, act, Wt, sh: SpecShape):
-    """Forward spectrum of layer input f(x) -> (saved spectrum X, row coefficients Z)."""
-    At = k_rowdft(x, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, act)
+def spec_forward(x, act, Wt, sh: SpecShape, At=None):
+    """Forward spectrum of layer input f(x) -> (saved spectrum X, row coefficients Z).  ``At``:
+    the row DFT of f(x), when the previous layer's row inverse already took it."""
+    if At is None:
+        At = k_rowdft(x, sh.Bn, sh.Ci, sh.P1, sh.P2, sh.m2, act)
     if sh.dim == 2:
         return k_colpass(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 0)
     return k_mix1d(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.m2, sh.P2, 0)
 
 
-def spec_backward(dz, X, Wt, sh: SpecShape, valid=None):
+def spec_backward(dz, X, Wt, sh: SpecShape, valid=None, At=None):
     """Adjoint of spec_forward: returns (dWt, GZ) for the layer's output gradient dz (read only
-    on ``valid`` = (N1v, N2v) when given, 2D)."""
-    At = k_rowdft(dz, sh.Bn, sh.Co, sh.P1, sh.P2, sh.m2, 0, valid)
+    on ``valid`` = (N1v, N2v) when given, 2D).  ``At``: the row DFT of dz, when the next layer's
+    row-inverse adjoint already took it."""
+    if At is None:
+        At = k_rowdft(dz, sh.Bn, sh.Co, sh.P1, sh.P2, sh.m2, 0, valid)
     if sh.dim == 2:
         G, GZ = k_colpass(At, Wt, sh.Bn, sh.Ci, sh.Co, sh.P1, sh.m1, sh.m2, sh.P2, 1)
     else:
@@ -942,20 +968,35 @@ class BagEncoderFn(torch.autograd.Function):
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         Xs, Wts, zs = [], [], []
         Wts_all = pack_w2d_many([(prm[2 + 4 * k], prm[3 + 4 * k]) for k in range(n)], P1)
+        # each row inverse but the last also takes the next layer's row DFT of GELU(z) in its
+        # pass (the field is not read back for it)
+        At_next = None
         for k in range(n):
             off = 2 + k * 4
             w1, w2, cw, cb = prm[off:off + 4]
             Wt = Wts_all[k]
+            last = k == n - 1
             if k == 0:
                 At = k_rowdft_bag_lift(X, idx_t, fc0w, fc0b, Dg, B, T, L, N1, N2, C, P1, P2, meta.m2)
                 Xk, Z = k_colpass(At, Wt, Bn, C, C, P1, meta.m1, meta.m2, P2, 0)
                 z = _empty(Bn, C, P1, P2, like=X)
-                call("blindno_rowidft_epi_lift", ptr(Z), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),
-                     ptr(fc0b), ptr(cw), ptr(cb), ptr(z), ptr(twiddle_rowinv(P2, meta.m2, X.device)),
-                     B, T, L, N1, N2, C, P1, P2, meta.m2, stream_ptr())
+                tb = ptr(twiddle_rowinv(P2, meta.m2, X.device))
+                if last:
+                    call("blindno_rowidft_epi_lift", ptr(Z), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),
+                         ptr(fc0b), ptr(cw), ptr(cb), ptr(z), tb, B, T, L, N1, N2, C, P1, P2,
+                         meta.m2, stream_ptr())
+                else:
+                    At_next = _empty(Bn, meta.m2, C, P1, 2, like=X)
+                    call("blindno_rowidft_epi_lift_rd", ptr(Z), ptr(X), ptr(idx_t), ptr(grid),
+                         ptr(fc0w), ptr(fc0b), ptr(cw), ptr(cb), ptr(z), tb, B, T, L, N1, N2, C, P1,
+                         P2, meta.m2, ptr(At_next), ptr(twiddle_mfma(P2, meta.m2, X.device)), 1,
+                         stream_ptr())
             else:
-                Xk, Z = spec_forward(zs[-1], 1, Wt, sh)
-                z = k_rowidft_epi(Z, zs[-1], cw, cb, Bn, C, P1, P2, meta.m2, 1)
+                Xk, Z = spec_forward(zs[-1], 1, Wt, sh, At=At_next)
+                if last:
+                    z = k_rowidft_epi(Z, zs[-1], cw, cb, Bn, C, P1, P2, meta.m2, 1)
+                else:
+                    z, At_next = k_rowidft_epi_rd(Z, zs[-1], cw, cb, Bn, C, P1, P2, meta.m2, 1, 1)
             Xs.append(Xk)
             Wts.append(Wt)
             zs.append(z)
@@ -1015,15 +1056,16 @@ class BagEncoderFn(torch.autograd.Function):
         grads[off_fc1 + 3] = gp[o:o + Cout]
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         fc0w, fc0b = prm[0], prm[1]
+        At_dz = None          # row DFT of dz taken by the later layer's adjoint pass
         for k in reversed(range(n)):
             off = 2 + 4 * k
             w1, w2, cw, cb = prm[off:off + 4]
             valid = crop if k == n - 1 else None
-            dWt, GZ = spec_backward(dz, Xs[k], Wts[k], sh, valid)
+            dWt, GZ = spec_backward(dz, Xs[k], Wts[k], sh, valid, At=At_dz)
             grads[off], grads[off + 1] = unpack_weights(dWt, (w1, w2), P1, 2)
             if k > 0:
-                dz, gw, gb = k_rowidft_bwd(GZ, dz, cw, zs[k - 1], Bn, C, P1, P2, meta.m2, 1, True,
-                                           valid)
+                dz, gw, gb, At_dz = k_rowidft_bwd(GZ, dz, cw, zs[k - 1], Bn, C, P1, P2, meta.m2, 1,
+                                                  True, valid, rd=True)
                 grads[off + 2], grads[off + 3] = gw.view_as(cw), gb
             else:
                 nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, meta.m2)

@@ -42,6 +42,18 @@ struct BagLift {
   int T, L, N1, N2;
 };
 
+// The next layer's row DFT taken in the row-inverse pass (RD kernels): At (Bn, m2, C, P1, 2) as
+// blindno_rowdft writes it, Tp its twiddle image (KB = ceil(P2 / 16), Npad = 16 ceil(2 m2 / 16)),
+// act: GELU of the field first (the next layer's input activation).
+struct RowDftNext {
+  float* At;
+  const float* Tp;
+  int Npad, act;
+};
+#ifndef ROWINV_FUSE_RD
+#define ROWINV_FUSE_RD 0
+#endif
+
 // MODE 0 (forward epilogue): z = acc + bc + Wc f(x)                (f = GELU if ACT)
 // MODE 1 (adjoint):          dx = (acc + Wc^T dz) * (ACT ? GELU'(xsrc) : 1)
 //                            + with WG (C <= 4, one group): per-lane dWc / dbc sums
@@ -50,20 +62,28 @@ struct BagLift {
 // x0 for the conv term, MODE 1 (with WG, ACT 0, C <= 4) recomputes it for dWc and, instead of
 // writing dx0, reduces fc0's gradient dW0[c][j] = sum dx0[c] [u, gx, gy]_j, db0[c] = sum dx0[c]
 // over the crop into partial[..][C*C + C + 4 C] (after the conv terms).
-template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB, int LIFT>
+// RD: the row DFT of the NEXT spectral layer (rowdft_mfma_kernel, spectral.hip) is taken in the
+// same pass from the field this kernel produces (MODE 0: f(z) with f = GELU when rd.act; MODE 1:
+// dx), so that field is not read back from HBM.  Needs whole rows per work item (TPW = NT), one
+// channel group (C <= 4) and 2 m2 <= 32: each column tile's 4 rows x 4 channels x 16 columns go
+// through a wave-private LDS tile into the A-operand order of the row DFT and are accumulated
+// into two 16-column MFMA tiles against rowdft's twiddle image rd.Tp ([KB][4][Npad][4]).
+template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB, int LIFT, int RD = 0>
 __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int C, int P1, int P2,
-    int m2, int TPW, BagLift bl, int Bg, int64_t wgs, int dN1, int dN2) {
+    int m2, int TPW, BagLift bl, int Bg, int64_t wgs, int dN1, int dN2, RowDftNext rd) {
   // MODE 1: dz is read only on its valid region h < dN1, w < dN2 (zero elsewhere: the gradient
   // of a cropped FNO output; see rowdft_mfma_kernel)
   extern __shared__ float sTB[];                    // [KS][NT][64] when LDSB
   const int KS = (m2 + 1) >> 1;
   const int NT = (P2 + 15) >> 4;
-  if (LDSB) {
-    const int ntb = KS * NT * 64;
-    stage_to_lds(sTB, TB, ntb);
+  // RD: the row-DFT twiddle image rd.Tp ([NT][4][Npad][4]) staged after the row-inverse one
+  float* sTp = sTB + (LDSB ? KS * NT * 64 : 0);
+  if (LDSB || RD) {
+    if (LDSB) stage_to_lds(sTB, TB, KS * NT * 64);
+    if (RD) stage_to_lds(sTp, rd.Tp, NT * 16 * rd.Npad);
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
@@ -117,6 +137,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
       grow = bl.grid + (int64_t)h * bl.N2 * 2;
     }
     const int t0 = chunk * TPW, t1 = min(NT, t0 + TPW);
+    f32x4 racc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};     // RD: next layer's spectra
     // epilogue operands of a column tile (raw loads), fetched one tile ahead so their latency
     // overlaps the previous tile's MFMA chain and epilogue
     struct Ops {
@@ -204,7 +225,8 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
 #pragma unroll
       for (int s = 0; s < KSM; ++s)
         if (s < KS) d = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], tb[s * NT * 64], d, 0, 0, 0);
-      if (!pok) continue;
+      float yv[4] = {0.f, 0.f, 0.f, 0.f};           // RD: this lane's field values (channels r)
+      if (pok) {
       if (MODE == 0) {
         if (has_wc) {
           float xv[CM];
@@ -219,11 +241,15 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
             for (int i = 0; i < CM; ++i)
               if (i < C) v = fmaf(wcg[o * C + i], xv[i], v);
             out[rbase + o * HW + w] = v;
+            yv[r] = v;
           }
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (c0 + r < C) out[rbase + (c0 + r) * HW + w] = d[r];
+            if (c0 + r < C) {
+              out[rbase + (c0 + r) * HW + w] = d[r];
+              yv[r] = d[r];
+            }
         }
       } else {
         if (has_wc) {
@@ -249,6 +275,7 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
               }
             } else if (i < C) {
               out[rbase + i * HW + w] = gi;
+              yv[r] = gi;
             }
           }
           if constexpr (WG != 0) {
@@ -263,7 +290,50 @@ __global__ __launch_bounds__(256) void rowinv_mfma_kernel(
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (c0 + r < C) out[rbase + (c0 + r) * HW + w] = d[r];
+            if (c0 + r < C) {
+              out[rbase + (c0 + r) * HW + w] = d[r];
+              yv[r] = d[r];
+            }
+        }
+      }
+      }  // pok
+      if constexpr (RD != 0) {
+        // lane (c16, g4) holds (row g4, channel r, column c16) of the tile; the row DFT wants
+        // lane (r16, kq) to supply A[m = r16][w = 4 kq + s] with m = 4 row + channel
+        // rows of 20 floats: the 64 lanes' stores of one r hit 64 distinct banks, the b128
+        // reads stay 16-B aligned
+        __shared__ float sRD[kW][16 * 20];
+        float* sy = sRD[wave];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sy[(4 * g4 + r) * 20 + c16] = rd.act ? gelu_f(yv[r]) : yv[r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const f32x4 a = *reinterpret_cast<const f32x4*>(sy + c16 * 20 + 4 * g4);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (t * 16 >= rd.Npad) break;
+          const f32x4 b = *reinterpret_cast<const f32x4*>(
+              sTp + (((tile * 4 + g4) * rd.Npad) + t * 16 + c16) * 4);
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            racc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], racc[t], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr (RD != 0) {
+      // D: lane (c16, g4) register r = (row g4, channel r) x spectrum column 16 t + c16
+      if (rok) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int col = t * 16 + c16, k = col >> 1, part = col & 1;
+          if (k >= m2) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r < C) rd.At[((((int64_t)n * m2 + k) * C + r) * P1 + h) * 2 + part] = racc[t][r];
         }
       }
     }
@@ -502,7 +572,8 @@ template <int MODE, int ACT, int WG, int LIFT = 0>
 int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
                   const float* bc, float* out, const float* TB, float* partial, int nblocks,
                   int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{},
-                  int G = 1, int64_t wgs = 0, int dN1 = 0, int dN2 = 0) {
+                  int G = 1, int64_t wgs = 0, int dN1 = 0, int dN2 = 0,
+                  RowDftNext rd = RowDftNext{nullptr, nullptr, 0, 0}) {
   if (dN1 <= 0) dN1 = P1;
   if (dN2 <= 0) dN2 = P2;
   if (dN1 > P1 || dN2 > P2) return (int)hipErrorInvalidValue;
@@ -550,19 +621,45 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
         if (ks <= 8) RW(16, 8); else RW(16, 16);
       }
 #undef RW
-      return (int)hipGetLastError();
+      const int e = (int)hipGetLastError();
+      if (e || !rd.At) return e;
+      return blindno_rowdft(out, rd.At, rd.Tp, Bn, C, P1, P2, m2, rd.act, (void*)st);
     }
+  }
+  // the next layer's row DFT in this pass (whole rows per item, one channel group); otherwise
+  // it runs as its own launch after this one
+  const int NTc = (P2 + 15) / 16;
+  const bool fuse_rd = rd.At != nullptr && ROWINV_FUSE_RD && cm == 4 && g.TPW == NTc &&
+                       2 * m2 <= 32 && G == 1 && !(MODE == 1 && LIFT);
+  if (rd.At && !fuse_rd && (G != 1 || (MODE == 1 && LIFT))) return (int)hipErrorInvalidValue;
+  if (fuse_rd) {
+    sh += sizeof(float) * (size_t)NTc * 16 * rd.Npad;
+    if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+#define RIF(KS_)                                                                             \
+  do {                                                                                       \
+    if (g.ldsb)                                                                              \
+      rowinv_mfma_kernel<4, KS_, MODE, ACT, WG, 1, LIFT, 1><<<nblocks, 256, sh, st>>>(       \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
+          dN2, rd);                                                                          \
+    else                                                                                     \
+      rowinv_mfma_kernel<4, KS_, MODE, ACT, WG, 0, LIFT, 1><<<nblocks, 256, sh, st>>>(       \
+          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
+          dN2, rd);                                                                          \
+  } while (0)
+    if (ks <= 8) RIF(8); else RIF(16);
+#undef RIF
+    return (int)hipGetLastError();
   }
 #define RI(CM_, KS_)                                                                         \
   do {                                                                                       \
     if (g.ldsb)                                                                              \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 1, LIFT><<<nblocks, 256, sh, st>>>(        \
           Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
-          dN2);                                                                              \
+          dN2, rd);                                                                          \
     else                                                                                     \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 0, LIFT><<<nblocks, 256, sh, st>>>(        \
           Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
-          dN2);                                                                              \
+          dN2, rd);                                                                          \
   } while (0)
 #define RI_K(CM_) \
   if (ks <= 8) RI(CM_, 8); else if (ks <= 16) RI(CM_, 16); else RI(CM_, 24);
@@ -575,7 +672,10 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   }
 #undef RI_K
 #undef RI
-  return (int)hipGetLastError();
+  int e = (int)hipGetLastError();
+  if (e || !rd.At) return e;
+  // unfused: the next layer's row DFT of the field just written
+  return blindno_rowdft(out, rd.At, rd.Tp, Bn, C, P1, P2, m2, rd.act, (void*)st);
 }
 
 }  // namespace
@@ -643,6 +743,34 @@ BLINDNO_API int blindno_rowidft_bwd_crop(const float* G, const float* dz, const 
                                 nb0, 1, 0, dN1, dN2);
 }
 
+// blindno_rowidft_bwd_crop plus the row DFT of dx for the previous layer's adjoint
+// (blindno_rowdft(dx, At, Tp, ..., act = 0) in the same pass when the geometry allows)
+BLINDNO_API int blindno_rowidft_bwd_rd(const float* G, const float* dz, const float* wc,
+                                       const float* xsrc, float* dx, const float* tb,
+                                       float* partial, int Bn, int C, int P1, int P2, int m2,
+                                       int act, int dN1, int dN2, float* At, const float* Tp,
+                                       void* stream) {
+  if (dN1 < 1 || dN1 > P1 || dN2 < 1 || dN2 > P2 || !At || !Tp || m2 > P2 / 2 + 1)
+    return (int)hipErrorInvalidValue;
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  hipStream_t st = (hipStream_t)stream;
+  const BagLift nb0{};
+  const RowDftNext rd{At, Tp, ((2 * m2 + 15) / 16) * 16, 0};
+  if (partial) {
+    if (C > 4 || !wc) return (int)hipErrorInvalidValue;
+    if (act)
+      return rowinv_launch<1, 1, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st,
+                                    nb0, 1, 0, dN1, dN2, rd);
+    return rowinv_launch<1, 0, 1>(G, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C, P1, P2, m2, st,
+                                  nb0, 1, 0, dN1, dN2, rd);
+  }
+  if (act)
+    return rowinv_launch<1, 1, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                  nb0, 1, 0, dN1, dN2, rd);
+  return rowinv_launch<1, 0, 0>(G, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                nb0, 1, 0, dN1, dN2, rd);
+}
+
 BLINDNO_API int blindno_rowidft_bwd(const float* G, const float* dz, const float* wc,
                                     const float* xsrc, float* dx, const float* tb,
                                     float* partial, int Bn, int C, int P1, int P2, int m2,
@@ -664,6 +792,40 @@ BLINDNO_API int blindno_rowidft_epi_lift(const float* Z, const float* X, const i
   const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
   return rowinv_launch<0, 0, 0, 1>(Z, nullptr, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2,
                                    m2, (hipStream_t)stream, bl);
+}
+
+// blindno_rowidft_epi_lift plus the next layer's row DFT of its input GELU(z) (act = 1) or z
+// (act = 0): At / Tp as blindno_rowdft's, in the same pass when the geometry allows
+BLINDNO_API int blindno_rowidft_epi_lift_rd(const float* Z, const float* X, const int* idx,
+                                            const float* grid, const float* w0, const float* b0,
+                                            const float* wc, const float* bc, float* z,
+                                            const float* tb, int B, int T, int L, int N1, int N2,
+                                            int C, int P1, int P2, int m2, float* At,
+                                            const float* Tp, int act, void* stream) {
+  if (!wc || !bc || C > 4 || N1 > P1 || N2 > P2 || !At || !Tp || m2 > P2 / 2 + 1)
+    return (int)hipErrorInvalidValue;
+  const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
+  const int Bn = B * L;
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  const RowDftNext rd{At, Tp, ((2 * m2 + 15) / 16) * 16, act};
+  return rowinv_launch<0, 0, 0, 1>(Z, nullptr, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2,
+                                   m2, (hipStream_t)stream, bl, 1, 0, 0, 0, rd);
+}
+
+// blindno_rowidft_epi plus the next layer's row DFT of f(z) (f = GELU when act_next)
+BLINDNO_API int blindno_rowidft_epi_rd(const float* Z, const float* x, const float* wc,
+                                       const float* bc, float* z, const float* tb, int Bn, int C,
+                                       int P1, int P2, int m2, int act, float* At, const float* Tp,
+                                       int act_next, void* stream) {
+  if (!At || !Tp || m2 > P2 / 2 + 1) return (int)hipErrorInvalidValue;
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  hipStream_t st = (hipStream_t)stream;
+  const RowDftNext rd{At, Tp, ((2 * m2 + 15) / 16) * 16, act_next};
+  if (act)
+    return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                  BagLift{}, 1, 0, 0, 0, rd);
+  return rowinv_launch<0, 0, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1, P2, m2, st,
+                                BagLift{}, 1, 0, 0, 0, rd);
 }
 
 BLINDNO_API int blindno_rowidft_bwd_lift(const float* G, const float* dz, const float* X,

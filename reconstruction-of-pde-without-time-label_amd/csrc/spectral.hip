@@ -44,7 +44,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // STAGE: the twiddle image is staged in LDS by every workgroup; otherwise the B operands are
 // read from the global image (L1/L2-resident) -- when each wave runs about one work item the
 // staging is as many bytes as the wave's own x rows and costs a full latency up front.
-template <int NT, int ALIGNED, bool STAGE>
+#ifndef ROWDFT_PRELOAD
+#define ROWDFT_PRELOAD 0
+#endif
+constexpr int kRowdftPre = 10;
+template <int NT, int ALIGNED, bool STAGE, bool PRE>
 __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
                                                           float* __restrict__ At,
                                                           const float* __restrict__ Tp,
@@ -84,6 +88,31 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
         for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
       }
     };
+    if constexpr (PRE) {
+      // all K blocks of the tile issued up front (KB <= kRowdftPre): the whole row segment is
+      // in flight at once instead of two blocks (the x stream is latency-bound otherwise)
+      float ap[kRowdftPre][4];
+#pragma unroll
+      for (int kb = 0; kb < kRowdftPre; ++kb)
+        if (kb < KB) load_a(kb, ap[kb]);
+#pragma unroll
+      for (int kb = 0; kb < kRowdftPre; ++kb) {
+        if (kb < KB) {
+          if (act) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) ap[kb][s] = gelu_f(ap[kb][s]);
+          }
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const f32x4 b = *reinterpret_cast<const f32x4*>(
+                tsrc + (((kb * 4 + kq) * Npad) + (t0 + t) * 16 + r16) * 4);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[kb][s], b[s], acc[t], 0, 0, 0);
+          }
+        }
+      }
+    } else {
     float a1[4], a2[4] = {0.f, 0.f, 0.f, 0.f};
     load_a(0, a1);
     if (KB > 1) load_a(1, a2);
@@ -104,6 +133,7 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
         for (int s = 0; s < 4; ++s)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc[t], 0, 0, 0);
       }
+    }
     }
     // D layout: lane holds rows 4*(l>>4) + r (r < 4), column l & 15
 #pragma unroll
@@ -134,7 +164,7 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
 // 1-channel snapshot is transformed, and it is read straight out of the bag tensor
 // X (B, T, N1, N2) through the bag's index list (snapshot n = b L + l -> X[b][idx[l]]), so
 // neither the gathered bag, the concatenated input nor x0 is ever materialised.
-template <int NT, int ALIGNED>
+template <int NT, int ALIGNED, bool PRE = ROWDFT_PRELOAD != 0>
 // b0 != nullptr: Gt holds the row spectra Dg[k][j][h] of the three grid/bias planes (gx, gy,
 // 1 on the crop) instead, and the grid/bias part is formed here as
 // W0[c,1] Dg[k][0] + W0[c,2] Dg[k][1] + b0[c] Dg[k][2] (Dg depends on the grid only, so it is
@@ -168,9 +198,8 @@ __global__ __launch_bounds__(256) void rowdft_bag_lift_kernel(
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int kb = 0; kb < KB; ++kb) {
+    auto load_a = [&](int kb, float (&a)[4]) {
       const int w0c = kb * 16 + kq * 4;
-      float a[4];
       if (ALIGNED && w0c + 3 < N2) {
         const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0c) : make_float4(0.f, 0.f, 0.f, 0.f);
         a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
@@ -178,11 +207,29 @@ __global__ __launch_bounds__(256) void rowdft_bag_lift_kernel(
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = (rok && w0c + s < N2) ? xr[w0c + s] : 0.f;
       }
+    };
+    auto mma = [&](int kb, const float (&a)[4]) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const f32x4 bt = *reinterpret_cast<const f32x4*>(smT + (((kb * 4 + kq) * Npad) + (t0 + t) * 16 + r16) * 4);
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bt[s], acc[t], 0, 0, 0);
+      }
+    };
+    if (PRE && KB <= kRowdftPre) {
+      // the snapshot row's K blocks all in flight at once (as rowdft_mfma_kernel PRE)
+      float ap[kRowdftPre][4];
+#pragma unroll
+      for (int kb = 0; kb < kRowdftPre; ++kb)
+        if (kb < KB) load_a(kb, ap[kb]);
+#pragma unroll
+      for (int kb = 0; kb < kRowdftPre; ++kb)
+        if (kb < KB) mma(kb, ap[kb]);
+    } else {
+      for (int kb = 0; kb < KB; ++kb) {
+        float a[4];
+        load_a(kb, a);
+        mma(kb, a);
       }
     }
 #pragma unroll
@@ -751,15 +798,17 @@ BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, 
   // stage the twiddle image only when the waves reuse it (>= ROWDFT_STAGE_ITEMS work items
   // per wave)
   const bool stage = nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * blocks;
-#define RD(NT_, AL_)                                                                        \
+  const bool pre = ROWDFT_PRELOAD && KB <= kRowdftPre;
+#define RD3(NT_, AL_, PR_)                                                                  \
   do {                                                                                      \
     if (stage)                                                                              \
-      rowdft_mfma_kernel<NT_, AL_, true><<<blocks, 256, sh, st>>>(                          \
+      rowdft_mfma_kernel<NT_, AL_, true, PR_><<<blocks, 256, sh, st>>>(                     \
           x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
     else                                                                                    \
-      rowdft_mfma_kernel<NT_, AL_, false><<<blocks, 256, 0, st>>>(                          \
+      rowdft_mfma_kernel<NT_, AL_, false, PR_><<<blocks, 256, 0, st>>>(                     \
           x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
   } while (0)
+#define RD(NT_, AL_) do { if (pre) RD3(NT_, AL_, true); else RD3(NT_, AL_, false); } while (0)
 #define RD_AL(NT_) \
   if (aligned) RD(NT_, 1); else RD(NT_, 0);
   switch (nt) {
@@ -770,6 +819,7 @@ BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, 
   }
 #undef RD_AL
 #undef RD
+#undef RD3
   return (int)hipGetLastError();
 }
 

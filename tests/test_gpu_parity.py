@@ -338,6 +338,43 @@ def test_crop_valid_region_kernels(C, m, N, Bn):
     assert K1 > 0
 
 
+@pytest.mark.parametrize("C,m,P,Bn", [(4, 12, 160, 104), (3, 16, 150, 112), (4, 12, 160, 8),
+                                      (4, 20, 96, 180)])
+def test_rowinv_fused_next_rowdft(C, m, P, Bn):
+    """blindno_rowidft_epi_rd / blindno_rowidft_bwd_rd (the next layer's row DFT taken in the row
+    inverse's pass) vs the same row inverse followed by blindno_rowdft on its output: the field
+    is identical and the spectra agree to fp32 rounding (the same MFMA chain order over the same
+    operands; 2e-6 relative).  Cases: fused (whole rows per item, Bn P / 4 >= 4096), a ragged
+    last column tile (P = 150), the small-bag and m2 > 16 fallbacks (separate row DFT launch).
+    The in-pass variant is compiled in with ROWINV_FUSE_RD=1 (rowinv.hip; off by default, see
+    DESIGN.md's measured table); without it the entries launch the row DFT themselves."""
+    from blindno import ops
+    g = torch.Generator(device="cuda").manual_seed(C * 100 + m)
+    Z = torch.randn(Bn, P, m, C, 2, device="cuda", generator=g) * 0.1
+    x = torch.randn(Bn, C, P, P, device="cuda", generator=g)
+    cw = torch.randn(C, C, 1, 1, device="cuda", generator=g) * 0.3
+    cb = torch.randn(C, device="cuda", generator=g) * 0.1
+    for act in (0, 1):
+        for act_next in (0, 1):
+            z_ref = ops.k_rowidft_epi(Z, x, cw, cb, Bn, C, P, P, m, act)
+            a_ref = ops.k_rowdft(z_ref, Bn, C, P, P, m, act_next)
+            z, a = ops.k_rowidft_epi_rd(Z, x, cw, cb, Bn, C, P, P, m, act, act_next)
+            torch.cuda.synchronize()
+            assert torch.equal(z, z_ref)
+            assert rel_l2(a.cpu().numpy(), a_ref.cpu().numpy()) <= 2e-6
+    dz = torch.randn(Bn, C, P, P, device="cuda", generator=g)
+    N = P - 20
+    for wg in (False, True):
+        r_ref = ops.k_rowidft_bwd(Z, dz, cw, x, Bn, C, P, P, m, 1, wg, valid=(N, N))
+        a_ref = ops.k_rowdft(r_ref[0], Bn, C, P, P, m, 0)
+        r = ops.k_rowidft_bwd(Z, dz, cw, x, Bn, C, P, P, m, 1, wg, valid=(N, N), rd=True)
+        torch.cuda.synchronize()
+        assert torch.equal(r[0], r_ref[0])
+        if wg:
+            assert torch.equal(r[1], r_ref[1]) and torch.equal(r[2], r_ref[2])
+        assert rel_l2(r[3].cpu().numpy(), a_ref.cpu().numpy()) <= 2e-6
+
+
 @pytest.mark.parametrize("C,act,G", [(12, 1, 2), (12, 0, 1), (8, 1, 1), (3, 1, 1)])
 def test_conv_wgrad_vs_fp64(C, act, G):
     """1x1-conv weight / bias gradient of an FNO layer (blindno_conv_wgrad_g: the heads' C = 12
