@@ -68,8 +68,12 @@ struct RowDftNext {
 // channel group (C <= 4) and 2 m2 <= 32: each column tile's 4 rows x 4 channels x 16 columns go
 // through a wave-private LDS tile into the A-operand order of the row DFT and are accumulated
 // into two 16-column MFMA tiles against rowdft's twiddle image rd.Tp ([KB][4][Npad][4]).
+// minimum resident workgroups (= waves per SIMD) the register allocation must allow
+#ifndef ROWINV_MFMA_WAVES
+#define ROWINV_MFMA_WAVES 1
+#endif
 template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB, int LIFT, int RD = 0>
-__global__ __launch_bounds__(256) void rowinv_mfma_kernel(
+__global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int C, int P1, int P2,
