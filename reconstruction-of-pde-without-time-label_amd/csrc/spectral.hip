@@ -314,6 +314,13 @@ __device__ __forceinline__ void load4c(const float2* src, int len, bool vec, flo
 // layers launch one workgroup per (sample, mode) pair -- one wave per SIMD -- so a one-block
 // lookahead leaves each step waiting a full memory latency (measured ~16 us for 10 steps)
 constexpr int kFullHB = 10;
+// unroll of the mix's input-channel loop (weight loads in flight per output)
+#ifndef COLMIX_UNROLL
+#define COLMIX_UNROLL 4
+#endif
+#ifndef COLMIX_C12
+#define COLMIX_C12 1
+#endif
 // the column inverse fused into the column-DFT / mix workgroups (coldft_mix_kernel FUSE)
 #ifndef COLPASS_FUSE
 #define COLPASS_FUSE 0
@@ -474,8 +481,7 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
         re *= hinv;
         im *= hinv;
       } else {
-#pragma unroll 4
-        for (int c = 0; c < Cin; ++c) {
+        auto mac = [&](int c) {
           const float2 a = xp[c * LDX];
           const float2 w = wload(c);
           if (DIR == 0) {
@@ -485,6 +491,15 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
             re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
             im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
           }
+        };
+        if (COLMIX_C12 && Cin == 12) {
+          // the 12-channel heads: every weight load of the output in flight at once (the
+          // small head launches are bound by these L2 round trips; same summation order)
+#pragma unroll
+          for (int c = 0; c < 12; ++c) mac(c);
+        } else {
+#pragma unroll COLMIX_UNROLL
+          for (int c = 0; c < Cin; ++c) mac(c);
         }
       }
       if (DIR == 0) {
