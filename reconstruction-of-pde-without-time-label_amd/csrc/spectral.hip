@@ -37,6 +37,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef ROWDFT_STAGE_ITEMS
 #define ROWDFT_STAGE_ITEMS 1
 #endif
+#ifndef ROWDFT_STAGE_RATIO
+#define ROWDFT_STAGE_RATIO 0
+#endif
 // Valid region (N1v, N2v): only rows h < N1v and columns w < N2v of each P1 x P2 plane are
 // read, the rest counts as zero -- for the gradient of a cropped FNO output (2d_FPE/
 // FNOModules.py:234), which is zero on the padding by construction, so the producer
@@ -812,7 +815,11 @@ BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, 
   hipStream_t st = (hipStream_t)stream;
   // stage the twiddle image only when the waves reuse it (>= ROWDFT_STAGE_ITEMS work items
   // per wave)
-  const bool stage = nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * blocks;
+  // ... and when a workgroup's x stream is at least twice the image (the heads' 64-column image
+  // is as large as their rows: staging it costs a full round trip for nothing, r02 kbench)
+  const int64_t x_per_block = ((nwork + blocks - 1) / blocks) * 16 * KB * 16 * (int64_t)sizeof(float);
+  const bool stage = nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * blocks &&
+                     (!ROWDFT_STAGE_RATIO || 2 * (int64_t)sh <= x_per_block);
   const bool pre = ROWDFT_PRELOAD && KB <= kRowdftPre;
 #define RD3(NT_, AL_, PR_)                                                                  \
   do {                                                                                      \
