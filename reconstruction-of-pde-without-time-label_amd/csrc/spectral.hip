@@ -321,6 +321,10 @@ constexpr int kFullHB = 10;
 #ifndef COLMIX_UNROLL
 #define COLMIX_UNROLL 4
 #endif
+// 16-row DFT tiles a column-pass workgroup aims at (pairs per workgroup grow until reached)
+#ifndef COLPASS_WAVE_TILES
+#define COLPASS_WAVE_TILES 4
+#endif
 #ifndef COLMIX_C12
 #define COLMIX_C12 1
 #endif
@@ -919,7 +923,7 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
     return (int)hipErrorInvalidValue;
   // pairs per workgroup: enough 16-row tiles for the four waves, tiles filled
   int G = 1;
-  while (((G * cin + 15) / 16) * Jt < 4 && G * cin < 64) ++G;
+  while (((G * cin + 15) / 16) * Jt < COLPASS_WAVE_TILES && G * cin < 64) ++G;
   G = ((G * cin + 15) / 16) * 16 / cin;
   if (G < 1) G = 1;
   const bool fuse = COLPASS_FUSE != 0;
