@@ -312,6 +312,10 @@ int blindno_mse(const float* p, const float* t, float* partial, float* grad, int
  * blindno_mse's per-block partials). */
 int blindno_mse_finish(const float* partial, int nblk, int64_t n, float* loss,
                        blindno_stream_t stream);
+/* blindno_mse_finish that also adds the loss to *acc (a training loop's running loss sum, one
+ * launch instead of a separate add); acc may be NULL. */
+int blindno_mse_finish_acc(const float* partial, int nblk, int64_t n, float* loss, float* acc,
+                           blindno_stream_t stream);
 
 /* Per-row sums of squares in fp64 for relative-L2 metrics (2d_FPE/train_fno.py:160-163,
  * eval_fno.py:124-128, 2d_Non_conservative_FPE/compute_time_error.py:321-333).

@@ -49,6 +49,7 @@ SIGNATURES = {
     "blindno_bagmean_bwd": "pppiiiiis",
     "blindno_mse": "pppplips",
     "blindno_mse_finish": "pilps",
+    "blindno_mse_finish_acc": "pilpps",
     "blindno_rowsq": "pppiiiiiis",
     "blindno_adam": "pppplffffffs",
     "blindno_gpe_solve": "ppppddiiipppiiis",

@@ -1188,7 +1188,7 @@ class MSEFn(torch.autograd.Function):
     """nn.MSELoss() (mean reduction) with a fused gradient kernel."""
 
     @staticmethod
-    def forward(ctx, pred, target):
+    def forward(ctx, pred, target, acc=None):
         require_device(pred, target)
         pred, target = _c(pred), _c(target)
         n = pred.numel()
@@ -1197,7 +1197,8 @@ class MSEFn(torch.autograd.Function):
         call("blindno_mse", ptr(pred), ptr(target), ptr(partial), None, n, nblk, None,
              stream_ptr())
         loss = _empty((), like=pred)
-        call("blindno_mse_finish", ptr(partial), nblk, n, ptr(loss), stream_ptr())
+        # acc (float32 scalar, optional): the loss is also added to it in the same launch
+        call("blindno_mse_finish_acc", ptr(partial), nblk, n, ptr(loss), ptr(acc), stream_ptr())
         ctx.save_for_backward(pred, target)
         return loss
 
@@ -1211,11 +1212,14 @@ class MSEFn(torch.autograd.Function):
         g = _c(g.reshape(1))
         call("blindno_mse", ptr(pred), ptr(target), ptr(partial), ptr(grad), n, nblk, ptr(g),
              stream_ptr())
-        return grad, None
+        return grad, None, None
 
 
-def mse_loss(pred, target):
-    return MSEFn.apply(pred, target)
+def mse_loss(pred, target, acc=None):
+    """nn.MSELoss()(pred, target); ``acc`` (float32 scalar tensor): add the loss value to it."""
+    if acc is not None and (acc.dtype != F32 or acc.numel() != 1 or acc.device != pred.device):
+        raise BlindnoError("mse_loss: acc must be a float32 scalar on the prediction's device")
+    return MSEFn.apply(pred, target, acc)
 
 
 # ---------------------------------------------------------------------------- metrics

@@ -219,6 +219,8 @@ class GraphedBagStep:
             self.side = torch.cuda.Stream(x.device)
         self.x, self.y, self.grid = x, y, grid
         self.loss_acc = loss_acc
+        # the seed gradient of loss.backward() (a static scalar: no fill kernel per replay)
+        self._one = torch.ones((), dtype=torch.float32, device=x.device)
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs = {}
         self.idx = {}
@@ -234,14 +236,22 @@ class GraphedBagStep:
         self._ev = [None] * len(self._ring)
         self._k = 0
 
+    def _loss(self, out, accumulate):
+        """The step's loss; with the fused MSE the running loss sum is accumulated by the loss
+        kernel itself (no separate add launch)."""
+        acc = self.loss_acc if accumulate else None
+        if acc is not None and self.loss_fn is ops.mse_loss:
+            return self.loss_fn(out, self.y, acc), False
+        return self.loss_fn(out, self.y), acc is not None
+
     def _body(self, L, accumulate=True):
         bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
         out = self.model(self.x, self.grid, bag_idx=bag)
-        loss = self.loss_fn(out, self.y)
+        loss, add = self._loss(out, accumulate)
         with ops.deferred_reductions():               # one batched gradient finalisation
-            loss.backward()
+            loss.backward(self._one)
         self.opt.gather_grads()
-        if accumulate and self.loss_acc is not None:
+        if add:
             self.loss_acc.add_(loss.detach())
         return out.detach(), loss.detach()
 
@@ -252,11 +262,11 @@ class GraphedBagStep:
         h = self.model.forward_encoder(self.x, self.grid, bag_idx=bag)
         hd = h.detach().requires_grad_(True)
         out = self.model.forward_heads(hd)
-        loss = self.loss_fn(out, self.y)
+        loss, add = self._loss(out, accumulate)
         with ops.deferred_reductions():
-            loss.backward()
+            loss.backward(self._one)
         self.opt.gather_grads(self.head_params)
-        if accumulate and self.loss_acc is not None:
+        if add:
             self.loss_acc.add_(loss.detach())
         return h, hd, out.detach(), loss.detach()
 

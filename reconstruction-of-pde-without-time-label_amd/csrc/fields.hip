@@ -714,7 +714,8 @@ __global__ __launch_bounds__(kBlock) void mse_kernel(const float* __restrict__ p
 // single-workgroup launch (instead of a torch sum and a torch division)
 __global__ __launch_bounds__(kBlock) void mse_finish_kernel(const float* __restrict__ partial,
                                                             int nblk, int64_t n,
-                                                            float* __restrict__ loss) {
+                                                            float* __restrict__ loss,
+                                                            float* __restrict__ lsum) {
   __shared__ float red[kBlock];
   float acc = 0.f;
   for (int i = threadIdx.x; i < nblk; i += kBlock) acc += partial[i];
@@ -724,7 +725,11 @@ __global__ __launch_bounds__(kBlock) void mse_finish_kernel(const float* __restr
     if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) loss[0] = red[0] / (float)n;
+  if (threadIdx.x == 0) {
+    const float l = red[0] / (float)n;
+    loss[0] = l;
+    if (lsum) lsum[0] += l;                      // running loss sum of a training loop
+  }
 }
 
 // Row r holds n points of `stride` floats: out[2r] = sum (a[.+off_a] - b[.+off_b])^2,
@@ -1062,11 +1067,16 @@ BLINDNO_API int blindno_bagmean_bwd(const float* dy, const float* w, float* s, i
   return (int)hipGetLastError();
 }
 
+BLINDNO_API int blindno_mse_finish_acc(const float* partial, int nblk, int64_t n, float* loss,
+                                       float* acc, void* stream) {
+  if (nblk < 1 || n < 1) return (int)hipErrorInvalidValue;
+  mse_finish_kernel<<<1, kBlock, 0, (hipStream_t)stream>>>(partial, nblk, n, loss, acc);
+  return (int)hipGetLastError();
+}
+
 BLINDNO_API int blindno_mse_finish(const float* partial, int nblk, int64_t n, float* loss,
                                    void* stream) {
-  if (nblk < 1 || n < 1) return (int)hipErrorInvalidValue;
-  mse_finish_kernel<<<1, kBlock, 0, (hipStream_t)stream>>>(partial, nblk, n, loss);
-  return (int)hipGetLastError();
+  return blindno_mse_finish_acc(partial, nblk, n, loss, nullptr, stream);
 }
 
 BLINDNO_API int blindno_mse(const float* p, const float* t, float* partial, float* grad,
