@@ -130,7 +130,7 @@ def main():
     from blindno import timing
     from blindno.nio import draw_bag_distinct as draw_distinct
     from blindno.train import (DataParallel, FlatAdam, GraphedBagStep, grid1d, grid2d,
-                               synthetic_bags)
+                               shard_bag_ids, synthetic_bags)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -171,7 +171,7 @@ def main():
 
     # one global bag-keyed dataset of a.bags bags; rank r holds {i : i mod world = r}
     gshape = (N, N) if cfg["dim"] == 2 else (N,)
-    my_ids = list(range(rank, max(a.bags, B * world), world))
+    my_ids = shard_bag_ids(a.bags, B, rank, world)
     n_local = len(my_ids)
     X, Y = synthetic_bags(n_local, T, gshape, out_ch, seed=seed, device=dev, bag_ids=my_ids)
     grid = grid2d(N, N, dev) if cfg["dim"] == 2 else grid1d(N, dev)
@@ -181,8 +181,7 @@ def main():
     xb = torch.empty((B,) + tuple(X.shape[1:]), device=dev)
     yb = torch.empty((B,) + tuple(Y.shape[1:]), device=dev)
     graphed = None
-    # one graph per bag size (device-resident bag indices); the NIO branch (D) stays eager: its
-    # MIOpen convolutions allocate workspace per call
+    # one graph per bag size (device-resident bag indices)
     if not a.no_graph and a.config in ("A", "B", "C", "E", "C_attn", "U", "U_NC", "U1"):
         # one HIP graph per bag size L = randint(50, T) (captured here, before the warm-up; the
         # numpy draw below stays the reference's: L and idx are drawn on the host every step)
@@ -198,7 +197,9 @@ def main():
 
     hostp = {"batch_select": 0.0, "draw": 0.0, "step": 0.0, "n": 0}
 
-    def step(i, eager=False):
+    n_loss = [0]             # steps whose loss went into loss_acc (the kernel-timer steps do not)
+
+    def step(i, eager=False, count_loss=True):
         t0_ = time.perf_counter()
         j = (i * B) % (n_local - B + 1)
         ids = order[j:j + B]
@@ -209,6 +210,7 @@ def main():
             idx = (draw_distinct if a.config == "C_attn" else blindno.draw_bag)(T)[1]
             t2_ = time.perf_counter()
             graphed.step(idx)
+            n_loss[0] += 1
             t3_ = time.perf_counter()
             hostp["batch_select"] += t1_ - t0_
             hostp["draw"] += t2_ - t1_
@@ -220,7 +222,9 @@ def main():
         loss.backward()
         dp.step()
         opt.zero_grad()
-        loss_acc.add_(loss.detach())
+        if count_loss:
+            loss_acc.add_(loss.detach())
+            n_loss[0] += 1
 
     for i in range(a.warmup):
         tw = time.perf_counter()
@@ -240,8 +244,16 @@ def main():
     hostp.update(batch_select=0.0, draw=0.0, step=0.0, n=0)
     if graphed is not None:
         graphed.host_times = {}
+        if world > 1:
+            graphed.ar_events = []
+    # per-step GPU time on the main stream (N > 1: per-rank min / max in the line)
+    sev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if world > 1 else None
+    if sev:
+        sev[0].record()
     for i in range(a.steps):
         step(a.warmup + i)
+        if sev:
+            sev[i + 1].record()
     t_enq = time.perf_counter() - t0          # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
@@ -252,7 +264,7 @@ def main():
         # HIP events on its stream over a few eager steps right after the timed region
         timer.start()
         for i in range(a.timer_steps):
-            step(a.warmup + a.steps + i, eager=True)
+            step(a.warmup + a.steps + i, eager=True, count_loss=False)
     if timer:
         timer.stop()
     dtt = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -260,6 +272,30 @@ def main():
         dist.all_reduce(dtt, op=dist.ReduceOp.MAX)
     dt = float(dtt)
     value = world * B * a.steps / dt
+    dist_info = None
+    if world > 1:
+        # self-validating N > 1 line: who ran, over what, and where the time went per rank
+        st = [sev[i].elapsed_time(sev[i + 1]) for i in range(a.steps)]
+        ar = graphed.allreduce_ms() if graphed is not None else {}
+        mine = torch.tensor([min(st), max(st), sum(st) / len(st), dt * 1e3 / a.steps,
+                             sum(ar.values())], device=dev, dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        try:
+            rccl = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception:  # noqa: BLE001 (gloo rehearsal builds)
+            rccl = None
+        dist_info = {
+            "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+            "rccl_version": rccl,
+            "per_rank_step_ms": [{"rank": r, "min": round(float(t[0]), 4), "max": round(float(t[1]), 4),
+                                  "mean": round(float(t[2]), 4), "wall_mean": round(float(t[3]), 4),
+                                  "allreduce_ms": round(float(t[4]), 4)} for r, t in enumerate(allr)],
+            "allreduce_bytes_per_step": int(4 * opt.grad.numel()),
+            "allreduce_ms_per_step_rank0": {k: round(v, 4) for k, v in ar.items()},
+            "allreduce_timing": "HIP events on the issuing stream around each bucketed all_reduce",
+        }
+    loss_mean = float(loss_acc) / max(1, n_loss[0])      # before the parity leg's replay adds to it
 
     if rank == 0:
         res = {
@@ -287,6 +323,8 @@ def main():
                                   ("; two graphs per step, heads' gradient all-reduce overlapped "
                                    "with the encoder backward" if graphed.overlap else ""))},
         }
+        if dist_info is not None:
+            res["dist"] = dist_info
         if timer:
             res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS,
                                              traffic_per_point=timing.pmc_traffic(ROOT, timing.DOMINANT)
@@ -307,7 +345,7 @@ def main():
                 res["parity"] = parity_check(a.config, model, graphed, opt, xb, yb, grid, T, mix=mix)
             if a.config == "C" and not a.no_cpu:
                 res["cpu_baseline"] = cpu_baseline(a.config, model, xb, yb, grid, T, budget=a.cpu_seconds)
-        res["loss_mean"] = float(loss_acc) / (a.warmup + a.steps)
+        res["loss_mean"] = loss_mean
         res["host_enqueue_ms_per_step"] = round(1000.0 * t_enq / a.steps, 4)
         if hostp["n"]:
             hb = {k: round(1e6 * hostp[k] / hostp["n"], 1) for k in ("batch_select", "draw", "step")}
@@ -492,7 +530,7 @@ def cpu_baseline(cfg_name, model, xb, yb, grid, T, budget):
         Ls.append(int(L))
         n += 1
         el = time.perf_counter() - t0
-        if el >= budget or n >= 200:
+        if (el >= budget and n >= 10) or n >= 200:
             break
     B = x.shape[0]
     return {"value": round(n * B / el, 4), "unit": "snapshot-bags/s", "cores": threads, "kind": "port",

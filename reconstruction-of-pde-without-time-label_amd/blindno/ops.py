@@ -220,6 +220,18 @@ def deferred_reductions():
         _DEFER = prev
 
 
+@contextlib.contextmanager
+def immediate_reductions():
+    """Suspend deferred_reductions() for code that reads the reductions' results right away
+    (the torch.ops.blindno backward formulas)."""
+    global _DEFER
+    prev, _DEFER = _DEFER, None
+    try:
+        yield
+    finally:
+        _DEFER = prev
+
+
 def reduce_partials(partial: torch.Tensor, nchunk: int, np_: int) -> torch.Tensor:
     out = _empty(np_, like=partial)
     if _DEFER is not None:

@@ -38,6 +38,16 @@ from ._lib import call, ptr, query, stream_ptr
 F32 = torch.float32
 
 
+def _immediate(bwd):
+    """Autograd formula wrapper: the operator's backward runs with reduction deferral
+    suspended (ops.deferred_reductions, which GraphedBagStep wraps around backward(), would
+    otherwise hand back unwritten reduction buffers that the backward clones or slices)."""
+    def run(ctx, *grads):
+        with ops.immediate_reductions():
+            return bwd(ctx, *grads)
+    return run
+
+
 # ---------------------------------------------------------------------------- spectral conv 2D
 def _spec2d_geom(x, w1):
     Bn, Ci, P1, P2 = x.shape
@@ -93,7 +103,7 @@ def _spec2d_bwd(ctx, gy, gX):
     return dx, dw1, dw2
 
 
-spectral_conv2d.register_autograd(_spec2d_bwd, setup_context=_spec2d_setup)
+spectral_conv2d.register_autograd(_immediate(_spec2d_bwd), setup_context=_spec2d_setup)
 
 
 # ---------------------------------------------------------------------------- spectral conv 1D
@@ -147,7 +157,7 @@ def _spec1d_bwd(ctx, gy, gX):
     return dx, dw
 
 
-spectral_conv1d.register_autograd(_spec1d_bwd, setup_context=_spec1d_setup)
+spectral_conv1d.register_autograd(_immediate(_spec1d_bwd), setup_context=_spec1d_setup)
 
 
 # ---------------------------------------------------------------------------- FNO bodies
@@ -220,7 +230,7 @@ def _fno2d_grad(ctx, gout):
     return g[0], list(g[1:]), None, None, None
 
 
-fno2d.register_autograd(_fno2d_grad, setup_context=_fno2d_setup)
+fno2d.register_autograd(_immediate(_fno2d_grad), setup_context=_fno2d_setup)
 
 
 @custom_op("blindno::fno1d", mutates_args=())
@@ -257,7 +267,7 @@ def _fno1d_grad(ctx, gout):
     return g[0], list(g[1:]), None, None
 
 
-fno1d.register_autograd(_fno1d_grad, setup_context=_fno1d_setup)
+fno1d.register_autograd(_immediate(_fno1d_grad), setup_context=_fno1d_setup)
 
 
 # ---------------------------------------------------------------------------- projection MLP
@@ -315,7 +325,7 @@ def _proj_grad(ctx, gout):
     return dz, dw1, db1, dw2, db2, None, None
 
 
-project_mlp.register_autograd(_proj_grad, setup_context=_proj_setup)
+project_mlp.register_autograd(_immediate(_proj_grad), setup_context=_proj_setup)
 
 
 # ---------------------------------------------------------------------------- bag mean, conv, loss
@@ -354,7 +364,7 @@ def _bag_grad(ctx, gy):
     return torch.ops.blindno.bag_mean_backward(gy, w.detach(), *ctx.Ld), None, None, None
 
 
-bag_mean.register_autograd(_bag_grad, setup_context=_bag_setup)
+bag_mean.register_autograd(_immediate(_bag_grad), setup_context=_bag_setup)
 
 
 @custom_op("blindno::conv2d", mutates_args=())
@@ -406,7 +416,7 @@ def _conv_grad(ctx, dy):
     return dx, dw, (db if has_b else None), None, None
 
 
-conv2d.register_autograd(_conv_grad, setup_context=_conv_setup)
+conv2d.register_autograd(_immediate(_conv_grad), setup_context=_conv_setup)
 
 
 @custom_op("blindno::mse_loss", mutates_args=())
@@ -446,7 +456,7 @@ def _mse_grad(ctx, g):
     return torch.ops.blindno.mse_loss_backward(g, pred, target), None
 
 
-mse_loss.register_autograd(_mse_grad, setup_context=_mse_setup)
+mse_loss.register_autograd(_immediate(_mse_grad), setup_context=_mse_setup)
 
 
 @custom_op("blindno::time_averaged_relative_l2", mutates_args=())
@@ -496,7 +506,7 @@ def _dw_grad(ctx, gy):
     return dx, dw, db
 
 
-depthwise_conv.register_autograd(_dw_grad, setup_context=_dw_setup)
+depthwise_conv.register_autograd(_immediate(_dw_grad), setup_context=_dw_setup)
 
 
 @custom_op("blindno::convnext_pointwise", mutates_args=())
@@ -534,7 +544,7 @@ def _cnx_grad(ctx, gy):
     return dxd, gy, dlw, dlb, dw1, db1, dw2, db2
 
 
-convnext_pointwise.register_autograd(_cnx_grad, setup_context=_cnx_setup)
+convnext_pointwise.register_autograd(_immediate(_cnx_grad), setup_context=_cnx_setup)
 
 
 @custom_op("blindno::max_pool", mutates_args=())
@@ -569,7 +579,7 @@ def _mp_grad(ctx, gy, garg):
     return torch.ops.blindno.max_pool_backward(gy, arg, *ctx.geom), None, None
 
 
-max_pool.register_autograd(_mp_grad, setup_context=_mp_setup)
+max_pool.register_autograd(_immediate(_mp_grad), setup_context=_mp_setup)
 
 
 @custom_op("blindno::conv_transpose", mutates_args=())
@@ -602,7 +612,7 @@ def _ct_grad(ctx, gy):
     return dx, dw, db, None, None
 
 
-conv_transpose.register_autograd(_ct_grad, setup_context=_ct_setup)
+conv_transpose.register_autograd(_immediate(_ct_grad), setup_context=_ct_setup)
 
 
 @custom_op("blindno::temporal_attention_mean", mutates_args=())
@@ -640,7 +650,7 @@ def _ta_grad(ctx, gY, gstate):
     return dX, dlw, dlb, None
 
 
-temporal_attention_mean.register_autograd(_ta_grad, setup_context=_ta_setup)
+temporal_attention_mean.register_autograd(_immediate(_ta_grad), setup_context=_ta_setup)
 
 
 REGISTERED = ("spectral_conv2d", "spectral_conv1d", "fno2d", "fno1d", "project_mlp", "bag_mean", "conv2d",

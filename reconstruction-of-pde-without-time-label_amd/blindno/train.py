@@ -240,7 +240,8 @@ class GraphedBagStep:
         """The step's loss; with the fused MSE the running loss sum is accumulated by the loss
         kernel itself (no separate add launch)."""
         acc = self.loss_acc if accumulate else None
-        if acc is not None and self.loss_fn is ops.mse_loss:
+        if (acc is not None and self.loss_fn is ops.mse_loss and acc.dtype == torch.float32
+                and acc.device == self.y.device and acc.dim() == 0):
             return self.loss_fn(out, self.y, acc), False
         return self.loss_fn(out, self.y), acc is not None
 
@@ -276,6 +277,18 @@ class GraphedBagStep:
             h.backward(hd.grad)
         self.opt.gather_grads(self.enc_params)
 
+    def _buffers(self):
+        """Copies of the model's buffers (BatchNorm running statistics and counters): the eager
+        warm-up before a capture is a train-mode forward that would update them once more than
+        the reference's training does; they are restored after it."""
+        return [(b, b.detach().clone()) for b in self.model.buffers()]
+
+    @staticmethod
+    def _restore(saved):
+        with torch.no_grad():
+            for b, c in saved:
+                b.copy_(c)
+
     def capture(self, L: int):
         if L in self.graphs:
             return
@@ -286,12 +299,14 @@ class GraphedBagStep:
         self.blob[L] = blob
         self.idx[L] = blob[:L]
         self.lw[L] = blob[L:].view(torch.float32)
+        saved = self._buffers()
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                 # eager warm-up: caches, lazy init
             self._body(L, accumulate=False)           # (its loss is not a training step's)
             self.opt.zero_grad()
         torch.cuda.current_stream().wait_stream(side)
+        self._restore(saved)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.pool):
             # static output / loss of the graph: valid after each replay of this key
@@ -305,6 +320,7 @@ class GraphedBagStep:
         self.blob[L] = blob
         self.idx[L] = blob[:L]
         self.lw[L] = blob[L:].view(torch.float32)
+        saved = self._buffers()
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                 # eager warm-up of both halves
@@ -313,6 +329,7 @@ class GraphedBagStep:
             self.opt.zero_grad()
         del h, hd
         torch.cuda.current_stream().wait_stream(side)
+        self._restore(saved)
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(ga, pool=self.pool):
             h, hd, self.out[L], self.loss[L] = self._body_a(L)
@@ -350,7 +367,10 @@ class GraphedBagStep:
             t1 = time.perf_counter()
             self.graphs[key].replay()
             t2 = time.perf_counter()
-            self.dp.reduce_and_step()
+            e = self._ar_begin("all")
+            self.dp.reduce_range(0, self.opt.grad.numel())
+            self._ar_end(e)
+            self.opt.step(grad_scale=1.0 / self.dp.world, gather=False)
             if ht is not None:     # host-side breakdown (bench.py host_us_per_step)
                 t3 = time.perf_counter()
                 for k, v in (("stage", t1 - t0), ("replay", t2 - t1), ("reduce_adam", t3 - t2)):
@@ -362,12 +382,42 @@ class GraphedBagStep:
         ga.replay()
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
+            e = self._ar_begin("heads (side stream, beside the encoder backward)")
             self.dp.reduce_range(*self.head_span)
+            self._ar_end(e)
         gb.replay()
+        e = self._ar_begin("encoder")
         self.dp.reduce_range(*self.enc_span)
+        self._ar_end(e)
         main.wait_stream(self.side)
         self.opt.step(grad_scale=1.0 / self.dp.world, gather=False)
         return key
+
+    # all-reduce timing (bench.py at N > 1): HIP events recorded on the stream that issues the
+    # collective, around it; ar_events is None (off) or a list of (name, start, end)
+    ar_events = None
+
+    def _ar_begin(self, name):
+        if self.ar_events is None or self.dp.world <= 1:
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return name, e0
+
+    def _ar_end(self, e):
+        if e is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.ar_events.append((e[0], e[1], e1))
+
+    def allreduce_ms(self):
+        """Mean all-reduce time per step by piece (ms), from ar_events (after a synchronize)."""
+        tot, cnt = {}, {}
+        for name, e0, e1 in self.ar_events or []:
+            tot[name] = tot.get(name, 0.0) + e0.elapsed_time(e1)
+            cnt[name] = cnt.get(name, 0) + 1
+        return {k: tot[k] / cnt[k] for k in tot}
 
     def replay(self, idx) -> int:
         """Stage the bag and replay its graph (forward, loss, backward, gradient gather into
@@ -410,6 +460,14 @@ class GraphedBagStep:
         ev.record()
         self._ev[k] = ev
         return L
+
+
+def shard_bag_ids(n_bags: int, per_rank_batch: int, rank: int, world: int):
+    """Bag-keyed data-parallel sharding (the reference's accelerate sampler
+    splits one dataset over the processes): rank r of ``world`` owns the global bags
+    {i : i mod world = r} of a set of max(n_bags, B * world) bags -- disjoint shards whose
+    union is the N = 1 set, so the data does not depend on the world size."""
+    return list(range(rank, max(n_bags, per_rank_batch * world), world))
 
 
 def synthetic_bags(n_bags: int, T: int, grid_shape, out_ch: int, seed: int, device,

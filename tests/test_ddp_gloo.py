@@ -100,3 +100,64 @@ def test_synthetic_bag_set_is_keyed_by_bag_id():
             ids = list(range(r, 8, world))
             xr, yr = synthetic_bags(len(ids), 3, (4, 5), 2, seed=1234, device="cpu", bag_ids=ids)
             assert torch.equal(xr, X[ids]) and torch.equal(yr, Y[ids])
+
+
+def _shard_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            import sys
+            root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            sys.path.insert(0, os.path.join(root, "reconstruction-of-pde-without-time-label_amd"))
+            from blindno.train import shard_bag_ids, synthetic_bags
+            n_bags, B = 22, 4
+            ids = shard_bag_ids(n_bags, B, rank, world)
+            X, Y = synthetic_bags(len(ids), 3, (4, 5), 2, seed=1234, device="cpu", bag_ids=ids)
+            # every rank's ids and per-bag checksums, gathered over the process group
+            n = torch.tensor([len(ids)])
+            ns = [torch.zeros_like(n) for _ in range(world)]
+            dist.all_gather(ns, n)
+            m = int(max(int(t) for t in ns))
+            pad = torch.full((m,), -1, dtype=torch.int64)
+            pad[:len(ids)] = torch.tensor(ids)
+            cs = torch.zeros(m, dtype=torch.float64)
+            cs[:len(ids)] = X.double().sum(dim=(1, 2, 3)) + Y.double().sum(dim=(1, 2, 3))
+            gi = [torch.zeros_like(pad) for _ in range(world)]
+            gc = [torch.zeros_like(cs) for _ in range(world)]
+            dist.all_gather(gi, pad)
+            dist.all_gather(gc, cs)
+            q.put((rank, [t.numpy().copy() for t in gi], [t.numpy().copy() for t in gc]))
+        finally:
+            dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, repr(e), None))
+        raise
+
+
+def test_bag_sharding_gloo_world4():
+    """bench.py's bag-keyed sharding at world 4 (gloo, CPU): the ranks' shards are disjoint,
+    their union is the N = 1 bag set, and every bag's content equals the N = 1 set's."""
+    from blindno.train import shard_bag_ids, synthetic_bags
+    world = 4
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    assert all(r[2] is not None for r in res), res
+    gi, gc = res[0][1], res[0][2]
+    ids = [int(i) for a in gi for i in a if i >= 0]
+    sums = {int(i): float(c) for a, b in zip(gi, gc) for i, c in zip(a, b) if i >= 0}
+    full = shard_bag_ids(22, 4, 0, 1)
+    assert sorted(ids) == full and len(ids) == len(set(ids))
+    X, Y = synthetic_bags(len(full), 3, (4, 5), 2, seed=1234, device="cpu")
+    ref = X.double().sum(dim=(1, 2, 3)) + Y.double().sum(dim=(1, 2, 3))
+    for i in full:
+        assert sums[i] == float(ref[i])

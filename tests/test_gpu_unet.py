@@ -227,9 +227,12 @@ def test_perminv_unet_attn_vs_oracle(case, dim, variant, train):
     print(f"[{case}] fwd {rel_l2(yo, o64):.2e} worst grad / bar {worst[0]:.2f} ({worst[1]})")
 
 
-def test_unet_graph_replay_matches_eager():
+@pytest.mark.parametrize("kind", ["attn", "nc"])
+def test_unet_graph_replay_matches_eager(kind):
     """Three graphed training steps (train.GraphedBagStep: one graph per bag size) of the 2D
-    UNet against three eager ones: parameters within 1e-6."""
+    UNet against three eager ones: parameters within 1e-6, and the BatchNorm buffers
+    (running statistics and num_batches_tracked) as the eager steps leave them -- the capture's
+    eager warm-up must not update them."""
     import blindno
     from blindno import unet
     from blindno.train import DataParallel, FlatAdam, GraphedBagStep, trained_parameters
@@ -239,10 +242,13 @@ def test_unet_graph_replay_matches_eager():
     y = torch.randn(B, N, N, 2, device="cuda")
     rs = np.random.RandomState(7)
     bags = [rs.choice(T, rs.randint(50, T)) for _ in range(3)]
-    finals = []
+    finals, bufs = [], []
     for graphed in (False, True):
         torch.manual_seed(1)
-        m = unet.PermInvUNet_attn(1, 2, 1, 4, (N, N)).cuda().train()
+        if kind == "attn":
+            m = unet.PermInvUNet_attn(1, 2, 1, 4, (N, N)).cuda().train()
+        else:
+            m = unet.PermInvUNet_attn_NC(1, 2, 1, 4, (N, N)).cuda().train()
         opt = FlatAdam(trained_parameters(m), lr=5e-4)
         if graphed:
             dp = DataParallel(opt)
@@ -259,7 +265,15 @@ def test_unet_graph_replay_matches_eager():
                 opt.zero_grad()
         torch.cuda.synchronize()
         finals.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu())
+        bufs.append({k: b.detach().cpu().clone() for k, b in m.named_buffers()})
     assert rel_l2(finals[1].numpy(), finals[0].numpy()) <= 1e-6
+    assert bufs[0].keys() == bufs[1].keys() and len(bufs[0]) > 0
+    for k in bufs[0]:
+        a, b = bufs[1][k], bufs[0][k]
+        if a.is_floating_point():
+            assert rel_l2(a.double().numpy(), b.double().numpy()) <= 1e-6, k
+        else:
+            assert torch.equal(a, b), (k, a, b)
 
 
 @pytest.mark.parametrize("kind", ["bag_V", "bag_GPE"])
