@@ -83,6 +83,29 @@ int blindno_project_bwd_w(const float* z, const float* w1, const float* b1, cons
                           int nchunk, int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd,
                           int Cout, int ostride, int ooff, int dout_div, blindno_stream_t stream);
 
+/* Bag-level projection of the snapshot encoder (NIOFP2D_FNO's FNO_input projection fused with
+ * the bag mean that consumes it: 2d_FPE/FNOModules.py:234-239 + 2d_FPE/NIOModules.py:569-575).
+ * z (B U, C, P1, P2): the last encoder layer of the U snapshots of each of B bags (snapshot
+ * n = b U + l), lw (U) the snapshot weights (multiplicity / L; NULL: 1/U).  C <= 4, Hd = 128,
+ * Cout = 1, U <= 1024.  Forward writes
+ *   ubar (B, Ho Wo) = sum_l lw_l (fc2(GELU(fc1(z_l))))   (the bag mean of the projections),
+ *   stats (blindno_project_bag_stats_floats(B, Ho, Wo) floats): per 16-point tile the bag-level
+ *         sums A = sum lw GELU(h), S = sum lw GELU'(h), Q = sum lw GELU'(h) z^T,
+ *   v (B U, C, P1, P2) on the crop: W1^T (w2 * GELU'(h)) per snapshot point.
+ * Backward: gs (B, Ho Wo) = the gradient of ubar; writes dz = lw_l gs v on the crop and
+ * per-workgroup partials [dW1 (Hd*C) | db1 (Hd) | dW2 (Hd) | db2] into partial[nchunk][...],
+ * nchunk = blindno_project_bag_bwd_nchunk(B, Ho, Wo) (any value >= 1). */
+int64_t blindno_project_bag_stats_floats(int B, int Ho, int Wo);
+int blindno_project_bag_bwd_nchunk(int B, int Ho, int Wo);
+int blindno_project_bag_fwd(const float* z, const float* w1, const float* b1, const float* w2,
+                            const float* b2, const float* lw, float* ubar, float* stats,
+                            float* v, int B, int U, int C, int P1, int P2, int Ho, int Wo, int Hd,
+                            blindno_stream_t stream);
+int blindno_project_bag_bwd(const float* stats, const float* gs, const float* w2, const float* lw,
+                            const float* v, float* dz, float* partial, int nchunk, int B, int U,
+                            int C, int P1, int P2, int Ho, int Wo, int Hd,
+                            blindno_stream_t stream);
+
 /* --- truncated spectral transforms --------------------------------------------------- */
 
 /* Row (last-axis) forward DFT of the first m2 modes: torch.fft.rfft2/rfft first stage

@@ -71,6 +71,10 @@ SIGNATURES = {
     "blindno_conv_wgrad_g": "pppiiiiiiis",
     "blindno_bagmean_fwd_w": "pppppp" + "iiiii" + "s",
     "blindno_project_bwd_w": "pppppppp" + "i" + "iiiiiiiiiii" + "s",
+    "blindno_project_bag_stats_floats": "iii",
+    "blindno_project_bag_bwd_nchunk": "iii",
+    "blindno_project_bag_fwd": "ppppppppp" + "iiiiiiii" + "s",
+    "blindno_project_bag_bwd": "ppppppp" + "i" + "iiiiiiii" + "s",
     "blindno_pack_w2d_2": "ppppp" + "iiiii" + "s",
     "blindno_unpack_w2d_2": "ppppp" + "iiiii" + "s",
     "blindno_bn_act_nslices": "iii",

@@ -28,6 +28,12 @@ F32 = torch.float32
 # keeps the mode it was captured with).
 MIX_F16 = False
 
+# The fused snapshot encoder's projection + bag mean at bag level (csrc/bagproj.hip): the
+# forward leaves per-(bag, point) sufficient statistics and the backward reduces them instead
+# of recomputing fc1 / GELU / GELU' per snapshot point.  False: the per-snapshot projection
+# kernels (csrc/project.hip) and the bag-mean kernel, as before.
+BAG_STATS = True
+
 
 def set_mix_precision(name: str) -> None:
     global MIX_F16
@@ -1014,14 +1020,27 @@ class BagEncoderFn(torch.autograd.Function):
             zs.append(z)
         fc1w, fc1b, fc2w, fc2b = prm[2 + 4 * n:6 + 4 * n]
         Hd, Cout = fc1w.shape[0], fc2w.shape[0]
-        u = _empty(Bn, Ho, Wo, Cout, like=X)
-        call("blindno_project_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b), ptr(u),
-             Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, stream_ptr())
         S = Ho * Wo
         width = bw.shape[0]
         h = _empty(B, S, width, like=X)
-        call("blindno_bagmean_fwd_w", ptr(u), ptr(grid), ptr(bw), ptr(bb), ptr(lw), ptr(h), B, L, S, 2,
-             width, stream_ptr())
+        ctx.bag = None
+        if BAG_STATS and Hd == 128 and Cout == 1 and L <= 1024:
+            # projection + bag mean at bag level: the backward becomes a reduction of the
+            # statistics the forward leaves (csrc/bagproj.hip)
+            ubar = _empty(B, S, like=X)
+            stats = _empty(query("blindno_project_bag_stats_floats", B, Ho, Wo), like=X)
+            v = _empty(Bn, C, P1, P2, like=X)
+            call("blindno_project_bag_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b),
+                 ptr(lw), ptr(ubar), ptr(stats), ptr(v), B, L, C, P1, P2, Ho, Wo, Hd, stream_ptr())
+            call("blindno_bagmean_fwd_w", ptr(ubar), ptr(grid), ptr(bw), ptr(bb), None, ptr(h), B, 1, S,
+                 2, width, stream_ptr())
+            ctx.bag = (stats, v)
+        else:
+            u = _empty(Bn, Ho, Wo, Cout, like=X)
+            call("blindno_project_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b), ptr(u),
+                 Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, stream_ptr())
+            call("blindno_bagmean_fwd_w", ptr(u), ptr(grid), ptr(bw), ptr(bb), ptr(lw), ptr(h), B, L, S,
+                 2, width, stream_ptr())
         ctx.meta, ctx.n, ctx.dims = meta, n, (B, T, L, N1, N2, C, P1, P2, Ho, Wo, Hd, Cout, width)
         ctx.lw = lw
         ctx.save_for_backward(X, idx_t, grid, bw, *Xs, *Wts, *zs, *prm)
@@ -1041,8 +1060,10 @@ class BagEncoderFn(torch.autograd.Function):
         # bag mean: every snapshot of bag b receives the same gradient s[b]
         sgr = _empty(B, S, like=gh)
         lw = ctx.lw
-        call("blindno_bagmean_bwd", ptr(gh), ptr(bw), ptr(sgr), B, S, 2, width, 1 if lw is not None else L,
-             stream_ptr())
+        bag = ctx.bag
+        ctx.bag = None
+        call("blindno_bagmean_bwd", ptr(gh), ptr(bw), ptr(sgr), B, S, 2, width,
+             1 if (lw is not None or bag is not None) else L, stream_ptr())
         # projection (dout read per bag: dout_div = L)
         off_fc1 = 2 + 4 * n
         fc1w, fc1b, fc2w = prm[off_fc1:off_fc1 + 3]
@@ -1054,7 +1075,12 @@ class BagEncoderFn(torch.autograd.Function):
         np_p = Hd * C + Hd + Cout * Hd + Cout
         nchunk = query("blindno_project_bwd_nchunk", Bn, Ho, Wo)
         partial = _empty(nchunk, np_p, like=gh)
-        if lw is not None:
+        if bag is not None:
+            nchunk = query("blindno_project_bag_bwd_nchunk", B, Ho, Wo)
+            partial = _empty(nchunk, np_p, like=gh)
+            call("blindno_project_bag_bwd", ptr(bag[0]), ptr(sgr), ptr(fc2w), ptr(lw), ptr(bag[1]),
+                 ptr(dz), ptr(partial), nchunk, B, L, C, P1, P2, Ho, Wo, Hd, stream_ptr())
+        elif lw is not None:
             call("blindno_project_bwd_w", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(sgr), ptr(lw),
                  ptr(dz), ptr(partial), nchunk, Bn, C, P1, P2, Ho, Wo, Hd, Cout, Cout, 0, L, stream_ptr())
         else:

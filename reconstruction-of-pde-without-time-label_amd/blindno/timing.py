@@ -18,9 +18,9 @@ from . import _lib
 # projection kernels are VALU-issue-bound on exactly that work, so their flop fraction is the
 # fraction of the fp32 peak spent on the layer's matrix arithmetic, nothing more.
 GELU_FLOPS = 0
-# the snapshot encoder's projection backward: blindno_project_bwd_w when the bag is
-# deduplicated (distinct snapshots + multiplicity weights), blindno_project_bwd otherwise
-DOMINANT = os.environ.get("BLINDNO_TIMED_KERNEL", "blindno_project_bwd")
+# the snapshot encoder's bag-level projection forward (csrc/bagproj.hip): the largest kernel of a
+# config-C step (the per-snapshot projection backward, blindno_project_bwd[_w], before it)
+DOMINANT = os.environ.get("BLINDNO_TIMED_KERNEL", "blindno_project_bag_fwd")
 _VARIANTS = {"blindno_project_bwd": ("blindno_project_bwd", "blindno_project_bwd_w")}
 
 
@@ -63,6 +63,18 @@ def cost(name, args):
         # dW2 (2 Cout); GELU / GELU' uncharged
         return (8 * pts * C + 4 * (pts // max(1, dout_div)) * Cout,
                 pts * Hd * (6 * C + 4 * Cout + 1 + 2 * GELU_FLOPS))
+    if name == "blindno_project_bag_fwd":
+        B, U, C, P1, P2, Ho, Wo, Hd = (_i(args, k) for k in range(9, 17))
+        pts, bpts = B * U * Ho * Wo, B * Ho * Wo
+        # read z, write v (crop), write the statistics (16 floats x 768 per 16-point tile) and
+        # ubar; per snapshot point and hidden unit: fc1 (2C), lw GELU into A (2), lw GELU' into
+        # S (2), GELU' z into Q (2C), (w2 W1) GELU' into v (2C); GELU / GELU' uncharged
+        return (8 * pts * C + 4 * ((bpts + 15) // 16) * 16 * Hd * 6 + 4 * bpts,
+                pts * Hd * (6 * C + 4 + 2 * GELU_FLOPS))
+    if name == "blindno_project_bag_bwd":
+        B, U, C, P1, P2, Ho, Wo, Hd = (_i(args, k) for k in range(8, 16))
+        pts, bpts = B * U * Ho * Wo, B * Ho * Wo
+        return 8 * pts * C + 4 * ((bpts + 15) // 16) * 16 * Hd * 6 + 4 * bpts, 2 * bpts * Hd * 6
     if name == "blindno_conv_wgrad":
         nchunk, Bn, C, P1, P2 = (_i(args, k) for k in range(3, 8))
         pts = Bn * P1 * P2
@@ -92,6 +104,8 @@ def pmc_traffic(root: str, name: str):
 
 
 def points(name, args):
+    if name == "blindno_project_bag_fwd":
+        return _i(args, 9) * _i(args, 10) * _i(args, 14) * _i(args, 15)
     if name in ("blindno_project_bwd", "blindno_project_bwd_w", "blindno_project_fwd"):
         o = {"blindno_project_bwd": 8, "blindno_project_bwd_w": 9, "blindno_project_fwd": 6}[name]
         Bn, Ho, Wo = _i(args, o), _i(args, o + 4), _i(args, o + 5)

@@ -30,7 +30,8 @@ CXXFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUD
 # per-file extra flags.  project.hip: its packed fp32 math is written explicitly (the SLP
 # vectoriser's own packing is off), and MFMA results go straight to VGPRs (no
 # v_accvgpr_read between the fc1 MFMA and the GELU that consumes it)
-FILE_FLAGS = {"project.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
+FILE_FLAGS = {"project.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+              "bagproj.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def _hipcc():

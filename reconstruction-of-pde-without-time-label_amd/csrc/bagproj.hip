@@ -1,0 +1,377 @@
+// Bag-level projection of the snapshot encoder: the FNO_input projection (crop -> fc1 -> GELU
+// -> fc2, 2d_FPE/FNOModules.py:234-239) of every snapshot of a bag fused with the fixed-weight
+// bag mean that consumes it (2d_FPE/NIOModules.py:569-575), with the backward reduced to
+// bag-level sufficient statistics.
+//
+// The bag mean hands every snapshot l of bag b the same upstream gradient up to its weight:
+// dy[l, p] = lw_l ghat[b, p] (ghat = W'[:, 2] . dL/dh[b, p], lw_l = multiplicity / L).  With
+// h = W1 z + b1 per snapshot point, a = GELU(h) and g = GELU'(h), every parameter gradient is
+// therefore a ghat-weighted sum of per-(bag, point) statistics that the forward forms while h
+// is in registers:
+//     A[k] = sum_l lw_l a_k,   S[k] = sum_l lw_l g_k,   Q[k][c] = sum_l lw_l g_k z_c,
+//     dW2 = sum_bp ghat A,  db1 = w2 * sum_bp ghat S,  dW1 = w2 * sum_bp ghat Q,
+//     db2 = sum_bp ghat * sum_l lw_l,
+// and the input gradient is dz[l, p, c] = lw_l ghat[b, p] v[l, p, c] with v = W1^T (w2 * g).
+// The forward's output is the bag mean of the projections itself,
+//     ubar[b, p] = sum_l lw_l (w2 . a_l + b2) = w2 . A + b2 sum_l lw_l,
+// so no per-snapshot output is written, and the backward reads 3 KB of statistics per (bag,
+// point) instead of recomputing fc1, GELU and GELU' for every snapshot point.
+//
+// Forward layout ("hidden x points", one v_mfma_f32_16x16x4f32 per 16 x 16 tile, K = C <= 4):
+//     H (16 hid x 16 pts) = W1 (16 hid x C) . Z (C x 16 pts)
+// lane l holds h for hidden units 4 (l >> 4) + r (r < 4) and point l & 15, so the lane's Q
+// update needs only its own point's C channels and v reduces over the 4 lane groups (a
+// reduce-scatter of 3 shuffles) instead of over 16 lanes.  A workgroup owns a 16-point tile;
+// its 4 waves split the 128 hidden units (2 tiles each, weights in registers) and walk the
+// bag's snapshots in chunks staged through LDS, where the waves' v partials are also summed.
+#include "common.h"
+#include "blindno.h"
+#include "gelu_pk.h"
+
+using namespace blindno;
+using namespace blindno::gelu_pk;
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kHd = 128;            // fc1 = Linear(width, 128)
+constexpr int kSC = 16;             // snapshots per LDS chunk
+constexpr int kNStat = 6;           // A, S, Q_0..Q_3
+constexpr int kTileF4 = (kHd / 16) * kNStat * 64;   // float4 slots per 16-point tile: 3072
+constexpr int kMaxU = 1024;
+#ifndef BAGPROJ_FWD_WAVES
+#define BAGPROJ_FWD_WAVES 2
+#endif
+
+// point f of the flattened (bag, crop point) space -> offset of (bag b, snapshot 0, channel 0,
+// row h, column w) in z (B U, C, P1, P2); 32-bit (the launchers bound the field below 2^31)
+struct BagGeom {
+  unsigned npts, S, Wo, P2, HW, C, U;
+  FastDiv dS, dWo;
+  __device__ __forceinline__ unsigned base(unsigned f) const {
+    const unsigned b = dS.div(f), s = f - b * S;
+    const unsigned h = dWo.div(s), w = s - h * Wo;
+    return b * U * C * HW + h * P2 + w;
+  }
+};
+
+__global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
+    const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ lw,
+    float* __restrict__ ubar, float* __restrict__ stats, float* __restrict__ v, BagGeom g) {
+  __shared__ float slw[kMaxU];
+  __shared__ float zs[kSC][16][4];            // [snapshot][point][channel]
+  __shared__ float zw[kSC][16][4];            // the same times lw_l (Q's operand)
+  __shared__ float vred[4][kSC][64];          // [wave][snapshot][16 channel + point]
+  __shared__ float ured[4][16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = uniform_int(tid >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const int C = (int)g.C, U = (int)g.U;
+  for (int l = tid; l < U; l += 256) slw[l] = lw ? lw[l] : 1.0f / (float)U;
+
+  // this wave's hidden tiles t = 2 wave + tt: fc1 A operand (k-scaled), bias rows, the rows of
+  // (w2 * W1) that form v, and w2 for ubar
+  float wa[2], bb[2][4], wr[2][4][4], w2r[2][4];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int k0 = 16 * (2 * wave + tt);
+    wa[tt] = g4 < C ? kK * w1[(k0 + c16) * C + g4] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 4 * g4 + r;
+      bb[tt][r] = kK * b1[k];
+      w2r[tt][r] = w2[k];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wr[tt][r][c] = c < C ? w2[k] * w1[k * C + c] : 0.f;
+    }
+  }
+  // the loop evaluates Phi - 1/2 (no +1/2: one packed add per pair less); the 1/2 parts are
+  // added back here and at the statistics write (below):  v gets 1/2 sum_k (w2 W1)[k] per lane
+  float vinit[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float a = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a += wr[tt][r][c];
+    vinit[c] = 0.5f * a;
+  }
+  __syncthreads();
+  float lsum = 0.f;                            // sum_l lw_l, same order in every thread
+  for (int l = 0; l < U; ++l) lsum += slw[l];
+  const float b2l = b2[0] * lsum;
+
+  // staging / v-output role of this thread: point tid & 15 (= the compute lane's c16),
+  // channel (tid >> 4) & 3, snapshots (tid >> 6) + 4 i of each chunk
+  const int cs = (tid >> 4) & 3, ls = tid >> 6;
+  const unsigned ntiles = (g.npts + 15) / 16;
+  for (unsigned tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const unsigned f = tile * 16 + (unsigned)c16;
+    const bool ok = f < g.npts;
+    const unsigned bo = g.base(ok ? f : 0u);
+    f32x2 A[2][2], S[2][2], Q[2][4][2];
+    float4 zbar = {0.f, 0.f, 0.f, 0.f};         // sum_l lw_l z_l of point c16
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        A[tt][i] = S[tt][i] = (f32x2){0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) Q[tt][c][i] = (f32x2){0.f, 0.f};
+      }
+    for (int l0 = 0; l0 < U; l0 += kSC) {
+      const int nl = U - l0 < kSC ? U - l0 : kSC;
+      __syncthreads();                         // previous chunk's zs / vred readers are done
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int l = ls + 4 * i;
+        const float zv = (ok && l < nl && cs < C) ? z[bo + (unsigned)((l0 + l) * C + cs) * g.HW] : 0.f;
+        zs[l][c16][cs] = zv;
+        zw[l][c16][cs] = zv * slw[l0 + l < U ? l0 + l : 0];
+      }
+      __syncthreads();
+      for (int l = 0; l < nl; ++l) {
+        const float4 zc = *reinterpret_cast<const float4*>(&zw[l][c16][0]);
+        const float az = zs[l][c16][g4];
+        const f32x2 wl = splat2(slw[l0 + l]);
+        zbar.x += zc.x; zbar.y += zc.y; zbar.z += zc.z; zbar.w += zc.w;
+        f32x2 vp[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) vp[c] = (f32x2){vinit[c], 0.f};
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          f32x4 d = {bb[tt][0], bb[tt][1], bb[tt][2], bb[tt][3]};
+          d = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[tt], az, d, 0, 0, 0);
+          const f32x2 h[2] = {{d[0], d[1]}, {d[2], d[3]}};
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            f32x2 ep;
+            const f32x2 sg = norm_cdf_pair_pdf_centered(h[i], ep);   // Phi - 1/2
+            const f32x2 gd = pk_fma(h[i], ep, sg);                  // GELU' - 1/2
+            A[tt][i] = pk_fma(wl, h[i] * sg, A[tt][i]);             // lw k h (Phi - 1/2)
+            S[tt][i] = pk_fma(wl, gd, S[tt][i]);
+            Q[tt][0][i] = pk_fma(gd, splat2(zc.x), Q[tt][0][i]);
+            Q[tt][1][i] = pk_fma(gd, splat2(zc.y), Q[tt][1][i]);
+            Q[tt][2][i] = pk_fma(gd, splat2(zc.z), Q[tt][2][i]);
+            Q[tt][3][i] = pk_fma(gd, splat2(zc.w), Q[tt][3][i]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              vp[c] = pk_fma(gd, (f32x2){wr[tt][2 * i][c], wr[tt][2 * i + 1][c]}, vp[c]);
+          }
+        }
+        // v over this wave's 32 hidden units: sum the pair, then reduce-scatter over the 4 lane
+        // groups so that group g4 keeps channel g4 of point c16
+        const float v0 = vp[0].x + vp[0].y, v1 = vp[1].x + vp[1].y;
+        const float v2 = vp[2].x + vp[2].y, v3 = vp[3].x + vp[3].y;
+        const bool hi = (g4 & 2) != 0;
+        const float k0 = hi ? v2 : v0, k1 = hi ? v3 : v1;
+        const float s0 = hi ? v0 : v2, s1 = hi ? v1 : v3;
+        const float r0 = k0 + __shfl_xor(s0, 32, 64);
+        const float r1 = k1 + __shfl_xor(s1, 32, 64);
+        const bool odd = (g4 & 1) != 0;
+        vred[wave][l][lane] = (odd ? r1 : r0) + __shfl_xor(odd ? r0 : r1, 16, 64);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int l = ls + 4 * i;
+        if (ok && l < nl && cs < C)
+          v[bo + (unsigned)((l0 + l) * C + cs) * g.HW] =
+              ((vred[0][l][lane] + vred[1][l][lane]) + vred[2][l][lane]) + vred[3][l][lane];
+      }
+    }
+    // statistics of this tile: slot ((t 6 + comp) 64 + lane) holds hidden 16 t + 4 g4 + r
+    // (r = the float4 component) of point c16
+    float4* st = reinterpret_cast<float4*>(stats) + (size_t)tile * kTileF4 + lane;
+    // the 1/2 parts: A += 1/2 sum_l lw_l h_l = 1/2 (W1 zbar + b1 sum lw), S += 1/2 sum lw,
+    // Q_c += 1/2 zbar_c
+    float up = 0.f;
+    const float zb[4] = {zbar.x, zbar.y, zbar.z, zbar.w};
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * wave + tt;
+      float av[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * t + 4 * g4 + r;
+        float hb = b1[k] * lsum;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hb = c < C ? fmaf(w1[k * C + c], zb[c], hb) : hb;
+        const float acc = r == 0 ? A[tt][0].x : (r == 1 ? A[tt][0].y : (r == 2 ? A[tt][1].x : A[tt][1].y));
+        av[r] = fmaf(kInvK, acc, 0.5f * hb);
+      }
+      const float4 a4 = {av[0], av[1], av[2], av[3]};
+      up += (w2r[tt][0] * a4.x + w2r[tt][1] * a4.y) + (w2r[tt][2] * a4.z + w2r[tt][3] * a4.w);
+      st[(t * kNStat + 0) * 64] = a4;
+      const float hs = 0.5f * lsum;
+      st[(t * kNStat + 1) * 64] = (float4){S[tt][0].x + hs, S[tt][0].y + hs, S[tt][1].x + hs, S[tt][1].y + hs};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float hz = 0.5f * zb[c];
+        st[(t * kNStat + 2 + c) * 64] =
+            (float4){Q[tt][c][0].x + hz, Q[tt][c][0].y + hz, Q[tt][c][1].x + hz, Q[tt][c][1].y + hz};
+      }
+    }
+    up += __shfl_xor(up, 16, 64);
+    up += __shfl_xor(up, 32, 64);
+    if (g4 == 0) ured[wave][c16] = up;
+    __syncthreads();
+    if (tid < 16 && ok) ubar[f] = (((ured[0][tid] + ured[1][tid]) + ured[2][tid]) + ured[3][tid]) + b2l;
+  }
+}
+
+// Backward: ghat-weighted reduction of the statistics (thread tid owns float4 slots tid + 256 j
+// of every tile, all of point tid & 15) into one partial per workgroup
+//     [dW1 (Hd C) | db1 (Hd) | dW2 (Hd) | db2]
+// and dz = lw_l ghat v on the crop.
+__global__ __launch_bounds__(256) void bagproj_bwd_kernel(
+    const float* __restrict__ stats, const float* __restrict__ gs, const float* __restrict__ w2,
+    const float* __restrict__ lw, const float* __restrict__ v, float* __restrict__ dz,
+    float* __restrict__ partial, BagGeom g) {
+  constexpr int kJ = kTileF4 / 256;          // 12 slots per thread
+  __shared__ float slw[kMaxU];
+  __shared__ float4 red[kJ * 4][4];          // [t 6 + comp][g4] -> r
+  __shared__ float sgs;
+  const int tid = threadIdx.x, lane = tid & 63, c16 = lane & 15;
+  const int C = (int)g.C, U = (int)g.U;
+  for (int l = tid; l < U; l += 256) slw[l] = lw ? lw[l] : 1.0f / (float)U;
+  __syncthreads();
+  float4 acc[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) acc[j] = (float4){0.f, 0.f, 0.f, 0.f};
+  float gsum = 0.f;
+  const int cs = (tid >> 4) & 3, ls = tid >> 6;
+  const unsigned ntiles = (g.npts + 15) / 16;
+  for (unsigned tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const unsigned f = tile * 16 + (unsigned)c16;
+    const bool ok = f < g.npts;
+    const float gh = ok ? gs[f] : 0.f;
+    const float4* st = reinterpret_cast<const float4*>(stats) + (size_t)tile * kTileF4 + tid;
+    float4 sv[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) sv[j] = st[256 * j];
+    if (tid < 16) gsum += gh;
+    if (ok && cs < C) {
+      const unsigned bo = g.base(f) + (unsigned)cs * g.HW;
+      int l = ls;
+      for (; l + 12 < U; l += 16) {                // four loads in flight per thread
+        float vv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vv[i] = v[bo + (unsigned)((l + 4 * i) * C) * g.HW];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dz[bo + (unsigned)((l + 4 * i) * C) * g.HW] = slw[l + 4 * i] * gh * vv[i];
+      }
+      for (; l < U; l += 4) {
+        const unsigned o = bo + (unsigned)(l * C) * g.HW;
+        dz[o] = slw[l] * gh * v[o];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      acc[j].x = fmaf(gh, sv[j].x, acc[j].x);
+      acc[j].y = fmaf(gh, sv[j].y, acc[j].y);
+      acc[j].z = fmaf(gh, sv[j].z, acc[j].z);
+      acc[j].w = fmaf(gh, sv[j].w, acc[j].w);
+    }
+  }
+  // sum over the 16 points (lanes c16) in a fixed butterfly order
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+#pragma unroll
+    for (int m = 1; m <= 8; m <<= 1) {
+      acc[j].x += __shfl_xor(acc[j].x, m, 64);
+      acc[j].y += __shfl_xor(acc[j].y, m, 64);
+      acc[j].z += __shfl_xor(acc[j].z, m, 64);
+      acc[j].w += __shfl_xor(acc[j].w, m, 64);
+    }
+    if (c16 == 0) red[(tid >> 6) + 4 * j][(tid >> 4) & 3] = acc[j];
+  }
+  if (tid < 64) {
+    float s = gsum;
+#pragma unroll
+    for (int m = 1; m <= 8; m <<= 1) s += __shfl_xor(s, m, 64);
+    if (tid == 0) sgs = s;
+  }
+  __syncthreads();
+  float lsum = 0.f;
+  for (int l = 0; l < U; ++l) lsum += slw[l];
+  const int np_ = kHd * C + 2 * kHd + 1;
+  float* pp = partial + (size_t)blockIdx.x * np_;
+  for (int e = tid; e < np_; e += 256) {
+    float val;
+    int k, comp;
+    if (e < kHd * C) {
+      k = e / C;
+      comp = 2 + e % C;
+    } else if (e < kHd * C + kHd) {
+      k = e - kHd * C;
+      comp = 1;
+    } else if (e < kHd * C + 2 * kHd) {
+      k = e - kHd * C - kHd;
+      comp = 0;
+    } else {
+      pp[e] = sgs * lsum;
+      continue;
+    }
+    const float4 q = red[(k >> 4) * kNStat + comp][(k >> 2) & 3];
+    const int r = k & 3;
+    val = r == 0 ? q.x : (r == 1 ? q.y : (r == 2 ? q.z : q.w));
+    pp[e] = comp == 0 ? val : w2[k] * val;
+  }
+}
+
+bool bag_geom(int B, int U, int C, int P1, int P2, int Ho, int Wo, int Hd, BagGeom& g) {
+  if (B < 1 || U < 1 || U > kMaxU || C < 1 || C > 4 || Hd != kHd || Ho < 1 || Wo < 1 || Ho > P1 ||
+      Wo > P2)
+    return false;
+  if ((int64_t)B * U * C * P1 * P2 >= INT32_MAX || (int64_t)B * Ho * Wo >= INT32_MAX) return false;
+  g.npts = (unsigned)(B * Ho * Wo);
+  g.S = (unsigned)(Ho * Wo);
+  g.Wo = (unsigned)Wo;
+  g.P2 = (unsigned)P2;
+  g.HW = (unsigned)(P1 * P2);
+  g.C = (unsigned)C;
+  g.U = (unsigned)U;
+  g.dS = FastDiv::make(g.S);
+  g.dWo = FastDiv::make(g.Wo);
+  return true;
+}
+
+}  // namespace
+
+BLINDNO_API int64_t blindno_project_bag_stats_floats(int B, int Ho, int Wo) {
+  return ((int64_t)B * Ho * Wo + 15) / 16 * (int64_t)kTileF4 * 4;
+}
+
+BLINDNO_API int blindno_project_bag_bwd_nchunk(int B, int Ho, int Wo) {
+  const int64_t tiles = ((int64_t)B * Ho * Wo + 15) / 16;
+  return (int)(tiles < 1 ? 1 : (tiles > 1024 ? 1024 : tiles));
+}
+
+BLINDNO_API int blindno_project_bag_fwd(const float* z, const float* w1, const float* b1,
+                                        const float* w2, const float* b2, const float* lw,
+                                        float* ubar, float* stats, float* v, int B, int U, int C,
+                                        int P1, int P2, int Ho, int Wo, int Hd, void* stream) {
+  BagGeom g;
+  if (!bag_geom(B, U, C, P1, P2, Ho, Wo, Hd, g) || !z || !ubar || !stats || !v)
+    return (int)hipErrorInvalidValue;
+  const unsigned ntiles = (g.npts + 15) / 16;
+  bagproj_fwd_kernel<<<ntiles, 256, 0, (hipStream_t)stream>>>(z, w1, b1, w2, b2, lw, ubar, stats,
+                                                              v, g);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_project_bag_bwd(const float* stats, const float* gs, const float* w2,
+                                        const float* lw, const float* v, float* dz,
+                                        float* partial, int nchunk, int B, int U, int C, int P1,
+                                        int P2, int Ho, int Wo, int Hd, void* stream) {
+  BagGeom g;
+  if (!bag_geom(B, U, C, P1, P2, Ho, Wo, Hd, g) || !stats || !gs || !v || !dz || !partial ||
+      nchunk < 1)
+    return (int)hipErrorInvalidValue;
+  bagproj_bwd_kernel<<<nchunk, 256, 0, (hipStream_t)stream>>>(stats, gs, w2, lw, v, dz, partial, g);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,81 @@
+// Packed-fp32 exact-erf GELU / GELU' on k-scaled pre-activations, shared by the projection
+// kernels (project.hip, bagproj.hip).
+#pragma once
+#include "common.h"
+
+namespace blindno {
+namespace gelu_pk {
+
+// GELU on k-scaled pre-activations.  W1 and b1 are staged multiplied by k = sqrt(log2(e)/2),
+// so the MFMA yields hk = k h and e^{-h^2/2} = 2^{-(hk)^2} costs one multiply and one v_exp;
+// with half = erfc(|h|/sqrt2)/2 (A&S 7.1.26, common.h) GELU(h) = (max(hk, 0) - |hk| half)/k,
+// and the 1/k is folded into W2 (forward) or applied once to the accumulated sums (backward).
+constexpr float kK = 0.84932180028801904f;        // sqrt(log2(e) / 2)
+constexpr float kInvK = 1.1774100225154747f;
+constexpr float kT = 0.27273748087922245f;        // A&S p / (sqrt2 k)
+// kp = 1 / (sqrt(2 pi) k) = 0.46971863934982566 (folded into norm_cdf_pair_pdf)
+
+// Two GELUs per lane-instruction: the polynomial / product steps as packed fp32 (v_pk_fma_f32,
+// v_pk_mul_f32 on <2 x float>); the transcendentals, |hk| (a free VOP3 source modifier on the
+// scalar fma) and the sign transfer (v_bfi_b32) stay scalar.  With half = erfc(|h|/sqrt2)/2,
+//     s = copysign(1/2 - half, h),   Phi(h) = 1/2 + s,
+// so no compare/select and no max is needed: k GELU(h) = hk Phi(h), GELU'(h) = Phi + h phi(h).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+
+__device__ __forceinline__ f32x2 splat2(float v) { return (f32x2){v, v}; }
+
+// Phi(h) (as cdf) and e = e^{-h^2/2} for a pair of k-scaled pre-activations
+__device__ __forceinline__ f32x2 norm_cdf_pair(f32x2 hk, f32x2& e) {
+  const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(hk.x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk.y), kT, 1.0f))};
+  const f32x2 sq = hk * hk;
+  e = (f32x2){__builtin_amdgcn_exp2f(-sq.x), __builtin_amdgcn_exp2f(-sq.y)};
+  f32x2 q = pk_fma(t, splat2(0.5307027145f), splat2(-0.7265760135f));
+  q = pk_fma(t, q, splat2(0.7107068705f));
+  q = pk_fma(t, q, splat2(-0.142248368f));
+  q = pk_fma(t, q, splat2(0.127414796f));
+  const f32x2 m = pk_fma(-(q * t), e, splat2(0.5f));          // 1/2 - half
+  const f32x2 sgn = {copysignf(m.x, hk.x), copysignf(m.y, hk.y)};
+  return sgn + splat2(0.5f);
+}
+
+// Backward variant: Phi(h) and ep = phi_k(h) = kp e^{-h^2/2} (kp = 1/(sqrt(2 pi) k)), so that
+// GELU'(h) = Phi + hk ep is one fma: the exp argument carries log2(kp) and the polynomial
+// coefficients carry 1/kp (half = q' t ep).
+constexpr float kLog2Kp = -1.0901312512086083f;
+__device__ __forceinline__ f32x2 norm_cdf_pair_pdf(f32x2 hk, f32x2& ep) {
+  const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(hk.x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk.y), kT, 1.0f))};
+  const f32x2 ea = pk_fma(-hk, hk, splat2(kLog2Kp));
+  ep = (f32x2){__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  f32x2 q = pk_fma(t, splat2(1.129831073415752f), splat2(-1.5468324069611348f));
+  q = pk_fma(t, q, splat2(1.513048048260859f));
+  q = pk_fma(t, q, splat2(-0.3028373926078324f));
+  q = pk_fma(t, q, splat2(0.27125769625911544f));
+  const f32x2 m = pk_fma(-(q * t), ep, splat2(0.5f));         // 1/2 - half
+  const f32x2 sgn = {copysignf(m.x, hk.x), copysignf(m.y, hk.y)};
+  return sgn + splat2(0.5f);
+}
+
+
+// norm_cdf_pair_pdf without the final + 1/2: Phi(h) - 1/2 (the bag-level projection adds the
+// halves back once per point, csrc/bagproj.hip)
+__device__ __forceinline__ f32x2 norm_cdf_pair_pdf_centered(f32x2 hk, f32x2& ep) {
+  const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(hk.x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk.y), kT, 1.0f))};
+  const f32x2 ea = pk_fma(-hk, hk, splat2(kLog2Kp));
+  ep = (f32x2){__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  f32x2 q = pk_fma(t, splat2(1.129831073415752f), splat2(-1.5468324069611348f));
+  q = pk_fma(t, q, splat2(1.513048048260859f));
+  q = pk_fma(t, q, splat2(-0.3028373926078324f));
+  q = pk_fma(t, q, splat2(0.27125769625911544f));
+  const f32x2 m = pk_fma(-(q * t), ep, splat2(0.5f));         // 1/2 - half
+  return (f32x2){copysignf(m.x, hk.x), copysignf(m.y, hk.y)};
+}
+
+}  // namespace gelu_pk
+}  // namespace blindno

@@ -306,6 +306,39 @@ def test_dedup_bag_matches_full_bag(dim):
         assert rel_l2(a, b) <= 1e-5
 
 
+@pytest.mark.parametrize("N,B,dedup", [(32, 3, True), (30, 3, False), (61, 2, True)])
+def test_bag_stats_projection_matches_per_snapshot(N, B, dedup):
+    """The encoder's projection + bag mean at bag level (csrc/bagproj.hip: the forward leaves
+    per-(bag, point) sums of GELU, GELU' and GELU' z; the backward reduces them) against the
+    per-snapshot projection kernels plus the bag-mean kernel on the same bag.  N = 30 and 61 make
+    the 16-point tiles straddle bags (Ho Wo % 16 != 0)."""
+    from blindno import NIOFP2D_FNO, nio, ops
+    torch.manual_seed(9)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 6, 8, 2).cuda().train()
+    x = torch.randn(B, 60, N, N, device="cuda")
+    gx, gy = np.meshgrid(np.linspace(-1, 1, N, dtype=np.float32),
+                         np.linspace(-1, 1, N, dtype=np.float32), indexing="ij")
+    grid = torch.tensor(np.stack([gx, gy], 2)).cuda()
+    idx = np.random.RandomState(3).choice(60, 57)
+    res = []
+    for bag_stats in (True, False):
+        ops.BAG_STATS = bag_stats
+        nio.DEDUP_BAGS = dedup
+        try:
+            m.zero_grad()
+            out = m(x, grid, bag_idx=idx)
+            (out * torch.linspace(-1, 1, out.numel(), device="cuda").view_as(out)).sum().backward()
+            res.append((out.detach().cpu().numpy(), [p.grad.cpu().numpy() for p in m.FNO_input.parameters()]))
+        finally:
+            ops.BAG_STATS = True
+            nio.DEDUP_BAGS = True
+    e_out = rel_l2(res[0][0], res[1][0])
+    e_g = [rel_l2(a, b) for a, b in zip(res[0][1], res[1][1])]
+    print(f"bag-level vs per-snapshot projection: out {e_out:.2e}, FNO_input grads max {max(e_g):.2e}")
+    assert e_out <= 1e-6
+    assert max(e_g) <= 1e-5
+
+
 @pytest.mark.parametrize("C,m,N,Bn", [(4, 12, 128, 12), (4, 12, 61, 3), (3, 5, 30, 5)])
 def test_crop_valid_region_kernels(C, m, N, Bn):
     """blindno_rowdft_crop / blindno_rowidft_bwd_crop (the encoder adjoint's dz read only on the

@@ -71,6 +71,25 @@ def main():
                                                   ptr(dz), ptr(part), nch, Bn, C, P, P, N, N, 128, Cout, Cout, 0, div,
                                                   stream_ptr()),
              8 * pts * C + 4 * (pts // div) * Cout)
+        if tag == "input":
+            # bag-level projection (csrc/bagproj.hip): B = 4 bags of U = 75 snapshots
+            Bb, U = 4, Bn // 4
+            lw = torch.full((U,), 1.0 / U, device=dev)
+            ubar = torch.empty(Bb, N * N, device=dev)
+            stats = torch.empty(query("blindno_project_bag_stats_floats", Bb, N, N), device=dev)
+            vv = torch.empty_like(z)
+            gsb = torch.randn(Bb, N * N, device=dev)
+            nbc = query("blindno_project_bag_bwd_nchunk", Bb, N, N)
+            pb = torch.empty(nbc, 128 * C + 2 * 128 + 1, device=dev)
+            sbytes = stats.numel() * 4
+            case("project_bag_fwd[input]", lambda: call("blindno_project_bag_fwd", ptr(z), ptr(w1), ptr(b1), ptr(w2),
+                                                        ptr(b2), ptr(lw), ptr(ubar), ptr(stats), ptr(vv), Bb, U, C,
+                                                        P, P, N, N, 128, stream_ptr()),
+                 8 * pts * C + sbytes)
+            case("project_bag_bwd[input]", lambda: call("blindno_project_bag_bwd", ptr(stats), ptr(gsb), ptr(w2),
+                                                        ptr(lw), ptr(vv), ptr(dz), ptr(pb), nbc, Bb, U, C, P, P, N,
+                                                        N, 128, stream_ptr()),
+                 8 * pts * C + sbytes)
         # spectral pieces of one layer
         sh = ops.SpecShape(Bn, C, C, P, P, m, m, 2)
         w = torch.rand(C, C, m, m, 2, device=dev) / (C * C)

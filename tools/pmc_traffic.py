@@ -30,6 +30,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NPTS = 300 * 128 * 128
 # ABI entry -> kernel-name pattern of its [input] kbench case (grid-size filter below)
 KERNELS = {
+    "blindno_project_bag_fwd": r"bagproj_fwd_kernel",
+    "blindno_project_bag_bwd": r"bagproj_bwd_kernel",
     "blindno_project_bwd": r"project_bwd_mfma_kernel<4,",
     "blindno_project_fwd": r"project_fwd_mfma_kernel<4,",
     "blindno_rowdft": r"rowdft_mfma_kernel<",
