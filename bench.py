@@ -182,7 +182,7 @@ def main():
     yb = torch.empty((B,) + tuple(Y.shape[1:]), device=dev)
     graphed = None
     # one graph per bag size (device-resident bag indices)
-    if not a.no_graph and a.config in ("A", "B", "C", "E", "C_attn", "U", "U_NC", "U1"):
+    if not a.no_graph:
         # one HIP graph per bag size L = randint(50, T) (captured here, before the warm-up; the
         # numpy draw below stays the reference's: L and idx are drawn on the host every step)
         graphed = GraphedBagStep(model, blindno.mse_loss, opt, dp, xb, yb, grid, loss_acc,
@@ -358,10 +358,14 @@ def main():
 
 
 def spectral_roofline(model, grid, B, T, N, dev):
-    """HBM roofline of one FNO_input spectral layer (the north star's 'spectral-conv kernel'):
-    row DFT + column pass + inverse row transform with its epilogue, at the mean bag size
-    (L = 75), timed with HIP events on the launch stream; algorithmic bytes per SURVEY.md 8d:
-    4 Bn Ci P^2 (read x) + 4 Bn Co P^2 (write y) + 16 Ci Co m1 m2 (weights)."""
+    """HBM roofline of one FNO_input spectral layer (the north star's 'spectral-conv kernel') at
+    the mean bag size (L = 75), timed with HIP events on the launch stream; algorithmic bytes per
+    SURVEY.md 8d: 4 Bn Ci P^2 (read x) + 4 Bn Co P^2 (write y) + 16 Ci Co m1 m2 (weights).
+
+    Headline form = the layer as the step chains it: column pass + row inverse with the conv /
+    bias / GELU epilogue and the NEXT layer's row DFT in the same pass (blindno_rowidft_epi_rd;
+    the first layer's row DFT is the bag-lift one).  The unchained form (row DFT + column pass +
+    row inverse, three passes over the field's spectra, x read twice) is reported beside it."""
     from blindno import ops
     fno = model.FNO_input
     C, m = fno.width, fno.modes1
@@ -373,32 +377,44 @@ def spectral_roofline(model, grid, B, T, N, dev):
     cw, cb = fno.conv_list[1].weight.detach(), fno.conv_list[1].bias.detach()
     sh = ops.SpecShape(Bn, C, C, P, P, m, m, 2)
     Wt = ops.pack_weights((w1.detach(), w2.detach()), P, 2)
+    At = ops.k_rowdft(x, Bn, C, P, P, m, 1)
 
-    def layer():
+    def chained():
+        _, Z = ops.k_colpass(At, Wt, Bn, C, C, P, m, m, P, 0)
+        return ops.k_rowidft_epi_rd(Z, x, cw, cb, Bn, C, P, P, m, 1, 1)
+
+    def unchained():
         _, Z = ops.spec_forward(x, 1, Wt, sh)
         return ops.k_rowidft_epi(Z, x, cw, cb, Bn, C, P, P, m, 1)
 
-    for _ in range(3):
-        layer()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 10
-    ev0.record()
-    for _ in range(reps):
-        layer()
-    ev1.record()
-    torch.cuda.synchronize()
-    ms = ev0.elapsed_time(ev1) / reps
+    def timed(layer):
+        for _ in range(3):
+            layer()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        ev0.record()
+        for _ in range(reps):
+            layer()
+        ev1.record()
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / reps
+
     nbytes = 4 * Bn * C * P * P * 2 + 16 * C * C * m * m
-    gbs = nbytes / (ms * 1e-3) / 1e9
-    res = {"kernels": "blindno_rowdft + blindno_colpass + blindno_rowidft_epi (one FNO_input layer)",
+    ms, ms_u = timed(chained), timed(unchained)
+    gbs, gbs_u = nbytes / (ms * 1e-3) / 1e9, nbytes / (ms_u * 1e-3) / 1e9
+    res = {"kernels": "blindno_colpass + blindno_rowidft_epi_rd (one chained FNO_input layer: the next "
+                      "layer's row DFT taken in the row-inverse pass)",
            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_per_layer": round(ms, 4),
-           "algorithmic_bytes": int(nbytes), "snapshots": Bn, "traffic": None}
+           "algorithmic_bytes": int(nbytes), "snapshots": Bn, "traffic": None,
+           "unchained": {"kernels": "blindno_rowdft + blindno_colpass + blindno_rowidft_epi",
+                         "achieved": round(gbs_u, 1), "frac": round(gbs_u / HBM_PEAK_GBS, 4),
+                         "ms_per_layer": round(ms_u, 4)}}
     # measured HBM bytes of the same layer shape (Bn = 300: tools/kbench.py "[input]" under
     # tools/pmc_kbench.sh -> profiles/pmc_traffic.json)
     from blindno import timing
-    parts = {k: timing.pmc_record(ROOT, k) for k in ("blindno_rowdft", "coldft_mix (blindno_colpass)",
-                                                      "colidft (blindno_colpass)", "blindno_rowidft_epi")}
+    parts = {k: timing.pmc_record(ROOT, k) for k in ("coldft_mix (blindno_colpass)",
+                                                      "colidft (blindno_colpass)", "blindno_rowidft_epi_rd")}
     if Bn == 300 and all(v is not None for v in parts.values()):
         res["traffic"] = int(sum(v["hbm_bytes_per_dispatch"] for v in parts.values()))
         res["traffic_by_kernel"] = {k: v["hbm_bytes_per_dispatch"] for k, v in parts.items()}

@@ -183,6 +183,12 @@ int blindno_rowidft_bwd_crop(const float* G, const float* dz, const float* wc, c
                              float* dx, const float* tb, float* partial, int Bn, int C, int P1,
                              int P2, int m2, int act, int dN1, int dN2, blindno_stream_t stream);
 int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2);
+/* Kernel selection of the C = 4 row inverses above (no reference counterpart; A/B measurement
+ * and cross-checks): on = 1 (default, or environment BLINDNO_ROWFUSE unset / not "0") runs the
+ * transposed whole-row kernel for C == 4, m2 % 4 == 0, m2 <= 16, P1 % 16 == 0, P2 % 32 == 0;
+ * 0 the general kernel.  Returns the previous setting.  Not thread-safe against launches; the
+ * partial count of blindno_rowidft_bwd_nchunk follows the setting. */
+int blindno_set_rowfuse(int on);
 /* Layer chaining (the FNO layer loop, 2d_FPE/FNOModules.py:226-232): the next spectral layer's
  * row DFT of the field a row inverse produces, taken in the same pass -- At / Tp exactly as
  * blindno_rowdft(field, At, Tp, Bn, C, P1, P2, m2, act_next) would take them (m2 of the next

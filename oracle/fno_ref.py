@@ -328,7 +328,7 @@ _ENC2D_BLOCKS = [
 
 
 def encoder2d(p: Dict[str, torch.Tensor], x: torch.Tensor,
-              masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+              masks: Optional[Sequence[torch.Tensor]] = None, record: Optional[list] = None) -> torch.Tensor:
     """Encoder2D.forward (train-mode BatchNorm), 2d_FPE/Baselines.py:203-249.
 
     ConvBlock = Conv2d -> BatchNorm2d (batch statistics) -> LeakyReLU(0.2)
@@ -339,6 +339,7 @@ def encoder2d(p: Dict[str, torch.Tensor], x: torch.Tensor,
     is piecewise linear, its gradient jumps across a branch, and a pre-activation within fp32
     rounding of 0 can land on either side in two correct evaluations; with the checked path's own
     branches the comparison is of one linear piece (tests/test_gpu_encoder.py, test_gpu_configs.py).
+    ``record`` (optional list): receives this evaluation's own branch masks (pre-activation > 0).
     """
     B, L = x.shape[:2]
     h = x.reshape(B * L, *x.shape[2:]).to(DT)
@@ -347,6 +348,8 @@ def encoder2d(p: Dict[str, torch.Tensor], x: torch.Tensor,
                      stride=stride, padding=pad)
         h = F.batch_norm(h, None, None, p[f"{name}.layers.1.weight"].to(DT),
                          p[f"{name}.layers.1.bias"].to(DT), training=True, eps=1e-5)
+        if record is not None:
+            record.append(h.detach() > 0)
         h = F.leaky_relu(h, 0.2) if masks is None else torch.where(masks[k], h, 0.2 * h)
     h = h.flatten(1).view(B, L, -1)
     return _linear(h, p, "linear")

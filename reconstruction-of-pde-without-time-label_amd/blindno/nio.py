@@ -290,7 +290,7 @@ class NIOFP2D(nn.Module):
         B, _, nx, ny = x.shape
         u = self.deeponet(x.unsqueeze(2), grid.reshape(-1, 2))     # (B, L, nx*ny)
         h = _bag_mean_2d(self, u, grid, B, L, nx, ny)
-        return torch.cat([getattr(self, n)(h) for n in self._heads], dim=-1)
+        return _run_heads(self, h)          # the two FNO heads as one grouped launch chain
 
 
 class NIOFP(nn.Module):

@@ -13,6 +13,14 @@ Reference loops (one per experiment; the flat module-level scripts):
                                             results_fno/
   1d_GPE/train_fno_GPE.py:75-205           NIOFP_FNO(3,20,40,1) head fno_V, bs 32, lr 1e-3,
                                             eval every 10, results_GPE_fno/
+  --model nio (the DeepONet-branch NIO, train_nio*.py):
+  2d_FPE/train_nio.py:62-267 and            NIOFP2D(2,3,100,25,3,12,32,2) (NC: heads fno_Fx/fno_Fy),
+  2d_Non_conservative_FPE/train_nio.py:      bs 4, lr 5e-4, eval every 5, result_2d_nio/
+    60-236
+  1d_FPE/train_nio.py:60-200                NIOFP(1,3,100,25,3,30,15,2), bs 32, lr 1e-3, eval every
+                                            10, results_nio/
+  1d_GPE/train_nio_GPE.py:80-212            NIOFP_schrodinger(1,3,100,25,3,20,40,1), bs 32, lr 1e-3,
+                                            eval every 10, results_GPE_nio/
 
 What is kept from the reference, exactly:
   * dataset scaling / z-scoring (``blindno.data``, bit-pinned to the reference classes) and the
@@ -71,9 +79,30 @@ def _experiments(model: str = "fno"):
     """The reference's train_*.py configurations.  ``model="unet"``: the attention-UNet scripts
     (2d_FPE/train_unet.py:62-110, 2d_Non_conservative_FPE/train_unet.py:60-110,
     1d_FPE/train_unet_bag.py:61-92, 1d_GPE/train_unet_GPE.py:80-110): same loop, metric quirk
-    and best-checkpoint rule as train_fno.py, their own model / lr / batch / result directory."""
+    and best-checkpoint rule as train_fno.py, their own model / lr / batch / result directory.
+    ``model="nio"``: the DeepONet-branch NIO scripts (train_nio*.py, module docstring); the
+    branch's train-mode BatchNorm takes its statistics over the drawn bag with its repeats, so
+    these graphs are keyed by the drawn L (no deduplication)."""
     from . import data, nio, unet
     from .encoders import Encoder2D
+    all4 = ("train_losses", "test_losses", "test_losses_drift", "test_losses_diffusion")
+    if model == "nio":
+        def nio2d(heads):
+            return lambda n, dev: nio.NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, heads=heads,
+                                              branch_last_kernel=Encoder2D.kernel_for_grid(n))
+        return {
+            "2d_FPE": Experiment("2d_FPE", 2, data.TrajectoryDataset2D, nio2d(("fno_drift", "fno_diffusion")),
+                                 5e-4, 4, 5, "result_2d_nio", True, all4),
+            "2d_Non_conservative_FPE": Experiment(
+                "2d_Non_conservative_FPE", 2, data.TrajectoryDataset2DForce, nio2d(("fno_Fx", "fno_Fy")),
+                5e-4, 4, 5, "result_2d_nio", True, all4),
+            "1d_FPE": Experiment("1d_FPE", 1, data.TrajectoryDataset1D,
+                                 lambda n, dev: nio.NIOFP(1, 3, 100, 25, 3, 30, 15, 2, dev), 1e-3, 32, 10,
+                                 "results_nio", True, all4),
+            "1d_GPE": Experiment("1d_GPE", 1, data.ParameterDataset,
+                                 lambda n, dev: nio.NIOFP_schrodinger(1, 3, 100, 25, 3, 20, 40, 1, dev), 1e-3,
+                                 32, 10, "results_GPE_nio", False),
+        }
     if model == "unet":
         all4 = ("train_losses", "test_losses", "test_losses_drift", "test_losses_diffusion")
         return {
@@ -95,12 +124,12 @@ def _experiments(model: str = "fno"):
     def nio2d(heads):
         return lambda n, dev: nio.NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2, heads=heads,
                                               branch_last_kernel=Encoder2D.kernel_for_grid(n))
-    all4 = ("train_losses", "test_losses", "test_losses_drift", "test_losses_diffusion")
     return {
         "2d_FPE": Experiment("2d_FPE", 2, data.TrajectoryDataset2D, nio2d(("fno_drift", "fno_diffusion")),
                              5e-4, 4, 5, "result_2d_fno", True, all4),
         "2d_Non_conservative_FPE": Experiment("2d_Non_conservative_FPE", 2, data.TrajectoryDataset2DForce,
-                                              nio2d(("fno_Fx", "fno_Fy")), 5e-4, 4, 5, "result_2d_fno", True),
+                                              nio2d(("fno_Fx", "fno_Fy")), 5e-4, 4, 5, "result_2d_fno", True,
+                                              all4),
         "1d_FPE": Experiment("1d_FPE", 1, data.TrajectoryDataset1D,
                              lambda n, dev: nio.NIOFP_FNO(3, 30, 15, 2, dev), 1e-3, 32, 10, "results_fno", True,
                              all4),
@@ -280,8 +309,9 @@ class Trainer:
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--experiment", choices=sorted(_experiments()), default="2d_FPE")
-    ap.add_argument("--model", choices=["fno", "unet"], default="fno",
-                    help="fno: train_fno*.py (NIO-FNO); unet: train_unet*.py (attention UNet)")
+    ap.add_argument("--model", choices=["fno", "unet", "nio"], default="fno",
+                    help="fno: train_fno*.py (NIO-FNO); unet: train_unet*.py (attention UNet); "
+                         "nio: train_nio*.py (DeepONet-branch NIO)")
     ap.add_argument("--data", required=True, help="the experiment's dataset file (npz, or the GPE .npy dict)")
     ap.add_argument("--outdir", default=None, help="result directory (default: the reference's)")
     ap.add_argument("--epochs", type=int, default=400)

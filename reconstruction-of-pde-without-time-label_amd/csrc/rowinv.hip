@@ -26,11 +26,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW = 4;      // waves per workgroup
 
-// lookahead of the adjoint's epilogue operands for the narrow (C <= 4) fields
-#ifndef ROWINV_PRE_BWD
-#define ROWINV_PRE_BWD 0
-#endif
-
 // Snapshot-encoder lift source (LIFT kernels): the layer input is x0 = fc0([u, gx, gy]),
 // zero outside the N1 x N2 crop, recomputed from the bag tensor instead of being stored.
 struct BagLift {
@@ -50,9 +45,6 @@ struct RowDftNext {
   const float* Tp;
   int Npad, act;
 };
-#ifndef ROWINV_FUSE_RD
-#define ROWINV_FUSE_RD 0
-#endif
 
 // MODE 0 (forward epilogue): z = acc + bc + Wc f(x)                (f = GELU if ACT)
 // MODE 1 (adjoint):          dx = (acc + Wc^T dz) * (ACT ? GELU'(xsrc) : 1)
@@ -62,32 +54,20 @@ struct RowDftNext {
 // x0 for the conv term, MODE 1 (with WG, ACT 0, C <= 4) recomputes it for dWc and, instead of
 // writing dx0, reduces fc0's gradient dW0[c][j] = sum dx0[c] [u, gx, gy]_j, db0[c] = sum dx0[c]
 // over the crop into partial[..][C*C + C + 4 C] (after the conv terms).
-// RD: the row DFT of the NEXT spectral layer (rowdft_mfma_kernel, spectral.hip) is taken in the
-// same pass from the field this kernel produces (MODE 0: f(z) with f = GELU when rd.act; MODE 1:
-// dx), so that field is not read back from HBM.  Needs whole rows per work item (TPW = NT), one
-// channel group (C <= 4) and 2 m2 <= 32: each column tile's 4 rows x 4 channels x 16 columns go
-// through a wave-private LDS tile into the A-operand order of the row DFT and are accumulated
-// into two 16-column MFMA tiles against rowdft's twiddle image rd.Tp ([KB][4][Npad][4]).
-// minimum resident workgroups (= waves per SIMD) the register allocation must allow
-#ifndef ROWINV_MFMA_WAVES
-#define ROWINV_MFMA_WAVES 1
-#endif
-template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB, int LIFT, int RD = 0>
-__global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
+// (The next layer's row DFT in the same pass is rowfuse_kernel's, below.)
+template <int CM, int KSM, int MODE, int ACT, int WG, int LDSB, int LIFT>
+__global__ __launch_bounds__(256) void rowinv_mfma_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int C, int P1, int P2,
-    int m2, int TPW, BagLift bl, int Bg, int64_t wgs, int dN1, int dN2, RowDftNext rd) {
+    int m2, int TPW, BagLift bl, int Bg, int64_t wgs, int dN1, int dN2) {
   // MODE 1: dz is read only on its valid region h < dN1, w < dN2 (zero elsewhere: the gradient
   // of a cropped FNO output; see rowdft_mfma_kernel)
   extern __shared__ float sTB[];                    // [KS][NT][64] when LDSB
   const int KS = (m2 + 1) >> 1;
   const int NT = (P2 + 15) >> 4;
-  // RD: the row-DFT twiddle image rd.Tp ([NT][4][Npad][4]) staged after the row-inverse one
-  float* sTp = sTB + (LDSB ? KS * NT * 64 : 0);
-  if (LDSB || RD) {
-    if (LDSB) stage_to_lds(sTB, TB, KS * NT * 64);
-    if (RD) stage_to_lds(sTp, rd.Tp, NT * 16 * rd.Npad);
+  if (LDSB) {
+    stage_to_lds(sTB, TB, KS * NT * 64);
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
@@ -141,7 +121,6 @@ __global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
       grow = bl.grid + (int64_t)h * bl.N2 * 2;
     }
     const int t0 = chunk * TPW, t1 = min(NT, t0 + TPW);
-    f32x4 racc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};     // RD: next layer's spectra
     // epilogue operands of a column tile (raw loads), fetched one tile ahead so their latency
     // overlaps the previous tile's MFMA chain and epilogue
     struct Ops {
@@ -174,7 +153,7 @@ __global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
     };
     // (forward epilogue of narrow fields only: the adjoint's and the 12-channel heads' larger
     // operand sets cost more occupancy than the lookahead gains -- measured)
-    constexpr bool kPre = (MODE == 0 && CM <= 8) || (ROWINV_PRE_BWD && MODE == 1 && CM <= 4);
+    constexpr bool kPre = MODE == 0 && CM <= 8;
     Ops nx;
     if (kPre) load_ops(t0, nx);
     for (int tile = t0; tile < t1; ++tile) {
@@ -229,7 +208,6 @@ __global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
 #pragma unroll
       for (int s = 0; s < KSM; ++s)
         if (s < KS) d = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], tb[s * NT * 64], d, 0, 0, 0);
-      float yv[4] = {0.f, 0.f, 0.f, 0.f};           // RD: this lane's field values (channels r)
       if (pok) {
       if (MODE == 0) {
         if (has_wc) {
@@ -245,14 +223,12 @@ __global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
             for (int i = 0; i < CM; ++i)
               if (i < C) v = fmaf(wcg[o * C + i], xv[i], v);
             out[rbase + o * HW + w] = v;
-            yv[r] = v;
           }
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (c0 + r < C) {
               out[rbase + (c0 + r) * HW + w] = d[r];
-              yv[r] = d[r];
             }
         }
       } else {
@@ -279,7 +255,6 @@ __global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
               }
             } else if (i < C) {
               out[rbase + i * HW + w] = gi;
-              yv[r] = gi;
             }
           }
           if constexpr (WG != 0) {
@@ -296,50 +271,10 @@ __global__ __launch_bounds__(256, ROWINV_MFMA_WAVES) void rowinv_mfma_kernel(
           for (int r = 0; r < 4; ++r)
             if (c0 + r < C) {
               out[rbase + (c0 + r) * HW + w] = d[r];
-              yv[r] = d[r];
             }
         }
       }
       }  // pok
-      if constexpr (RD != 0) {
-        // lane (c16, g4) holds (row g4, channel r, column c16) of the tile; the row DFT wants
-        // lane (r16, kq) to supply A[m = r16][w = 4 kq + s] with m = 4 row + channel
-        // rows of 20 floats: the 64 lanes' stores of one r hit 64 distinct banks, the b128
-        // reads stay 16-B aligned
-        __shared__ float sRD[kW][16 * 20];
-        float* sy = sRD[wave];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sy[(4 * g4 + r) * 20 + c16] = rd.act ? gelu_f(yv[r]) : yv[r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const f32x4 a = *reinterpret_cast<const f32x4*>(sy + c16 * 20 + 4 * g4);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          if (t * 16 >= rd.Npad) break;
-          const f32x4 b = *reinterpret_cast<const f32x4*>(
-              sTp + (((tile * 4 + g4) * rd.Npad) + t * 16 + c16) * 4);
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-            racc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], racc[t], 0, 0, 0);
-        }
-      }
-    }
-    if constexpr (RD != 0) {
-      // D: lane (c16, g4) register r = (row g4, channel r) x spectrum column 16 t + c16
-      if (rok) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int col = t * 16 + c16, k = col >> 1, part = col & 1;
-          if (k >= m2) continue;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (r < C) rd.At[((((int64_t)n * m2 + k) * C + r) * P1 + h) * 2 + part] = racc[t][r];
-        }
-      }
     }
   }
   if (WG) {
@@ -509,6 +444,317 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
   }
 }
 
+// ------------------------------------------------------------ transposed row inverse (C = 4)
+// The snapshot encoder's layers (FNO_input: C = 4, m2 = 12, P2 = 160 at 128^2), whole rows per
+// work item.  The row inverse is taken TRANSPOSED: for a block of 16 rows (sample n, rows
+// h0 .. h0 + 15) and a 16-column tile t,
+//     D_c[w][h] = sum_kk T'[kk][w] Z[n][h][kk][c]        (A = twiddles, B = the spectrum)
+// so the D layout puts 4 CONSECUTIVE columns w = 16 t + 4 (l>>4) + r of one row h = h0 + (l&15)
+// in lane l.  Consequences:
+//   * every field operand and result of the epilogue is one 16-B access per channel (a wave
+//     instruction covers 16 rows x 64 contiguous bytes; the next tile's instruction the other
+//     half of each 128-B line), where the untransposed kernel above issues 4-B accesses;
+//   * the field values a lane produces are exactly the operand the next layer's row DFT takes
+//     from that lane (rowdft_mfma_kernel's k order w = 16 kb + 4 kq + s), so the RD fusion runs
+//     straight from registers, with no LDS transposition (the earlier RD variant's cost);
+//   * the row DFT is taken transposed as well (D = T^T f(y)^T): lane l then holds spectrum
+//     columns k' = 16 nt + 4 (l>>4) + r of row h, i.e. whole (Re, Im) pairs, stored as float2.
+// K order of the row inverse: lane group g = l>>4 supplies kk = S g + s' (s' < S = m2 / 2), i.e.
+// the S/2 complex modes S g / 2 .. of all 4 channels: 4 S contiguous floats of the spectrum row
+// (one float4 per K step).  The twiddle image of the untransposed kernel (twiddle_rowinv, K order
+// 4 s + g) is permuted into this order while it is staged.
+// MODE / ACT / WG / LIFT as rowinv_mfma_kernel; RD: 0 none, 1 next row DFT of the field, 2 of
+// GELU(field).  S = m2 / 2 (m2 % 4 == 0, m2 <= 16); P1 % 16 == 0, P2 % 32 == 0.
+#ifndef ROWFUSE_BLOCKS
+#define ROWFUSE_BLOCKS 512
+#endif
+// NH column tiles per step (1 or 2): with NH = 2 lane group g owns the 8 consecutive columns
+// w = 32 st + 8 g + 4 hf + r of a 32-column step (hf: the step's two MFMA tiles), so the two
+// 16-B accesses a lane issues per channel and step are adjacent and each pair of wave
+// instructions covers whole 128-B lines of 16 rows (NH = 1: 64-B half lines, the other halves
+// one step later).  The MFMA row i of tile (st, hf) is column w = 16 NH st + 4 NH (i>>2) + 4 hf
+// + (i&3); the staged twiddle images follow that order.
+// (per mode: the adjoint carries twice the operands, so NH = 2 costs it occupancy)
+#ifndef ROWFUSE_NH0
+#define ROWFUSE_NH0 2
+#endif
+#ifndef ROWFUSE_NH1
+#define ROWFUSE_NH1 1
+#endif
+template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH>
+__global__ __launch_bounds__(256) void rowfuse_kernel(
+    const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
+    const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
+    const float* __restrict__ TB, float* __restrict__ partial, int Bn, int P1, int P2,
+    BagLift bl, int dN1, int dN2, RowDftNext rd) {
+  constexpr int C = 4;
+  constexpr int m2 = 2 * S;
+  constexpr int NNT = (4 * S + 15) / 16;          // 16-column tiles of the next row DFT
+  constexpr int Npad = 16 * NNT;
+  const int NT = P2 >> 4;                           // MFMA column tiles (NT % NH == 0)
+  extern __shared__ float lds[];
+  float* sA = lds;                                  // [NT][64 lanes][S]
+  float* sT = lds + NT * 64 * S;                    // RD: [NT][4][Npad][4] (rowdft's image)
+  for (int e = threadIdx.x; e < NT * 64 * S; e += blockDim.x) {
+    const int t = e / (64 * S), rem = e - t * (64 * S);
+    const int ln = rem / S, sp = rem - ln * S;
+    const int kk = S * (ln >> 4) + sp;
+    const int w = 16 * NH * (t / NH) + 4 * NH * ((ln & 15) >> 2) + 4 * (t % NH) + (ln & 3);
+    sA[e] = TB[((kk >> 2) * NT + (w >> 4)) * 64 + (kk & 3) * 16 + (w & 15)];
+  }
+  if (RD) stage_to_lds(sT, rd.Tp, NT * 16 * Npad);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int c16 = lane & 15, g = lane >> 4;
+  const int HB = P1 >> 4;
+  const int nitems = Bn * HB;
+  const int HW = P1 * P2;                           // field < 2^31 elements (launcher)
+  const int NS = NT / NH;                           // steps per row block
+  const bool has_wc = wc != nullptr;
+  float W[C][C], bv[C], w0[C][3], b0[C];
+#pragma unroll
+  for (int o = 0; o < C; ++o) {
+    bv[o] = (MODE == 0 && has_wc && bc) ? bc[o] : 0.f;
+#pragma unroll
+    for (int i = 0; i < C; ++i) W[o][i] = has_wc ? wc[o * C + i] : 0.f;
+    b0[o] = LIFT ? bl.b0[o] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) w0[o][j] = LIFT ? bl.w0[o * 3 + j] : 0.f;
+  }
+  constexpr int NWC = WG ? C * C + C : 0;          // [o][i] dWc, then dbc
+  constexpr int NWL = (LIFT && MODE == 1) ? 4 * C : 0;   // [c][j] dW0, then db0
+  constexpr int NW = NWC + NWL > 0 ? NWC + NWL : 1;
+  float wacc[NW];
+#pragma unroll
+  for (int e = 0; e < NW; ++e) wacc[e] = 0.f;
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  for (int item = blockIdx.x * kW + wave; item < nitems; item += gridDim.x * kW) {
+    const int n = item / HB;
+    const int h = ((item - n * HB) << 4) + c16;
+    float zb[C][S];
+    {
+      const f32x4* zr = reinterpret_cast<const f32x4*>(Z + (int64_t)(n * P1 + h) * (m2 * C * 2) + 4 * S * g);
+      float zz[4 * S];
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        const f32x4 v = zr[q];
+        zz[4 * q] = v.x; zz[4 * q + 1] = v.y; zz[4 * q + 2] = v.z; zz[4 * q + 3] = v.w;
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int sp = 0; sp < S; ++sp) zb[c][sp] = zz[((sp >> 1) * C + c) * 2 + (sp & 1)];
+    }
+    const int64_t fbase = (int64_t)n * C * HW + (int64_t)h * P2;
+    const float* urow = bl.X;
+    const float* grow = bl.grid;
+    const bool lrow = LIFT && h < bl.N1;
+    if (LIFT && lrow) {
+      const int b = n / bl.L, l = n - (n / bl.L) * bl.L;
+      urow = bl.X + (((int64_t)b * bl.T + bl.idx[l]) * bl.N1 + h) * bl.N2;
+      grow = bl.grid + (int64_t)h * bl.N2 * 2;
+    }
+    const bool drow = MODE == 0 || h < dN1;
+    // field operands of one step: 16-B loads from clamped offsets, then selects
+    struct Ops {
+      f32x4 a[C][NH];      // MODE 0: layer input x; MODE 1: dz of every output channel
+      f32x4 s[C][NH];      // MODE 1: the layer input (GELU' / dWc)
+      f32x4 u[NH], g0[NH], g1[NH];   // LIFT: snapshot and grid (gx, gy interleaved)
+      bool lok[NH];
+    };
+    auto load = [&](int st, Ops& o) {
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        const int w = 16 * NH * st + 4 * NH * g + 4 * hf;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          o.a[c][hf] = zero4;
+          o.s[c][hf] = zero4;
+          if (MODE == 0 && !LIFT && has_wc) o.a[c][hf] = *reinterpret_cast<const f32x4*>(xs + fbase + c * HW + w);
+          if (MODE == 1 && has_wc) {
+            const bool ok = drow && w < dN2;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(dz + (ok ? fbase + c * HW + w : 0));
+            o.a[c][hf] = ok ? v : zero4;
+          }
+          if (MODE == 1 && !LIFT && (ACT || WG))
+            o.s[c][hf] = *reinterpret_cast<const f32x4*>(xs + fbase + c * HW + w);
+        }
+        o.lok[hf] = false;
+        o.u[hf] = o.g0[hf] = o.g1[hf] = zero4;
+        if (LIFT) {
+          o.lok[hf] = lrow && w < bl.N2;
+          const int wl = o.lok[hf] ? w : 0;
+          const f32x4 u = *reinterpret_cast<const f32x4*>(urow + wl);
+          const f32x4 g0 = *reinterpret_cast<const f32x4*>(grow + 2 * wl);
+          const f32x4 g1 = *reinterpret_cast<const f32x4*>(grow + 2 * wl + 4);
+          o.u[hf] = o.lok[hf] ? u : zero4;
+          o.g0[hf] = o.lok[hf] ? g0 : zero4;
+          o.g1[hf] = o.lok[hf] ? g1 : zero4;
+        }
+      }
+    };
+    f32x4 racc[C][NNT];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int nt = 0; nt < NNT; ++nt) racc[c][nt] = zero4;
+    Ops cur;
+    load(0, cur);
+    for (int st = 0; st < NS; ++st) {
+      Ops nxt;
+      load(st + 1 < NS ? st + 1 : st, nxt);         // one step ahead (the last re-reads its own)
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        const int t = st * NH + hf;
+        float av[S];
+        const float2* ta = reinterpret_cast<const float2*>(sA + (t * 64 + lane) * S);
+#pragma unroll
+        for (int q = 0; q < S / 2; ++q) {
+          const float2 v = ta[q];
+          av[2 * q] = v.x;
+          av[2 * q + 1] = v.y;
+        }
+        f32x4 d[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          d[c] = zero4;
+#pragma unroll
+          for (int sp = 0; sp < S; ++sp) d[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[sp], zb[c][sp], d[c], 0, 0, 0);
+        }
+        const int w = 16 * NH * st + 4 * NH * g + 4 * hf;
+        f32x4 ya[C];                                // RD operand (this lane's field values)
+        // LIFT: the lifted field x0 = fc0([u, gx, gy]) at the lane's 4 points (0 off the crop)
+        auto x0 = [&](int c, int r) -> float {
+          const float gx = r < 2 ? cur.g0[hf][2 * r] : cur.g1[hf][2 * r - 4];
+          const float gy = r < 2 ? cur.g0[hf][2 * r + 1] : cur.g1[hf][2 * r - 3];
+          return cur.lok[hf] ? fmaf(w0[c][0], cur.u[hf][r], fmaf(w0[c][1], gx, fmaf(w0[c][2], gy, b0[c]))) : 0.f;
+        };
+        if (MODE == 0) {
+          f32x4 xin[C];
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              xin[c][r] = LIFT ? x0(c, r) : (ACT ? gelu_f(cur.a[c][hf][r]) : cur.a[c][hf][r]);
+#pragma unroll
+          for (int o = 0; o < C; ++o) {
+            f32x4 y = d[o];
+            if (has_wc) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float v = y[r] + bv[o];
+#pragma unroll
+                for (int i = 0; i < C; ++i) v = fmaf(W[o][i], xin[i][r], v);
+                y[r] = v;
+              }
+            }
+            *reinterpret_cast<f32x4*>(out + fbase + o * HW + w) = y;
+            if (RD) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) ya[o][r] = RD == 2 ? gelu_f(y[r]) : y[r];
+            }
+          }
+        } else {
+          if (WG) {
+#pragma unroll
+            for (int o = 0; o < C; ++o)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) wacc[C * C + o] += cur.a[o][hf][r];
+          }
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            f32x4 dg = d[c];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float v = dg[r];
+              if (has_wc) {
+#pragma unroll
+                for (int o = 0; o < C; ++o) v = fmaf(W[o][c], cur.a[o][hf][r], v);
+              }
+              float ain;
+              if (LIFT) {
+                ain = x0(c, r);
+              } else if (ACT) {
+                float dgl;
+                gelu_both(cur.s[c][hf][r], ain, dgl);
+                v *= dgl;
+              } else {
+                ain = cur.s[c][hf][r];
+              }
+              if (WG) {
+#pragma unroll
+                for (int o = 0; o < C; ++o) wacc[o * C + c] = fmaf(cur.a[o][hf][r], ain, wacc[o * C + c]);
+              }
+              if (LIFT) {
+                if (cur.lok[hf]) {
+                  const float gx = r < 2 ? cur.g0[hf][2 * r] : cur.g1[hf][2 * r - 4];
+                  const float gy = r < 2 ? cur.g0[hf][2 * r + 1] : cur.g1[hf][2 * r - 3];
+                  wacc[NWC + 3 * c] = fmaf(v, cur.u[hf][r], wacc[NWC + 3 * c]);
+                  wacc[NWC + 3 * c + 1] = fmaf(v, gx, wacc[NWC + 3 * c + 1]);
+                  wacc[NWC + 3 * c + 2] = fmaf(v, gy, wacc[NWC + 3 * c + 2]);
+                  wacc[NWC + 3 * C + c] += v;
+                }
+              }
+              dg[r] = v;
+            }
+            if (!LIFT) *reinterpret_cast<f32x4*>(out + fbase + c * HW + w) = dg;
+            if (RD) ya[c] = dg;
+          }
+        }
+        if (RD) {
+          // next layer's row DFT, transposed: A = its twiddles (lane: column k' = 16 nt + c16;
+          // K = w = 16 kb + 4 kq + s of rowdft's image), B = the field values this lane holds
+          const int kb = (16 * NH * st + 4 * NH * g + 4 * hf) >> 4, kq = (NH * g + hf) & 3;
+#pragma unroll
+          for (int nt = 0; nt < NNT; ++nt) {
+            const f32x4 tb = *reinterpret_cast<const f32x4*>(sT + ((kb * 4 + kq) * Npad + 16 * nt + c16) * 4);
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+              for (int s = 0; s < 4; ++s)
+                racc[c][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[s], ya[c][s], racc[c][nt], 0, 0, 0);
+          }
+        }
+      }
+      cur = nxt;
+    }
+    if (RD) {
+      // lane: row h, spectrum columns k' = 16 nt + 4 g + r -> modes 8 nt + 2 g + r/2 (Re, Im)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int nt = 0; nt < NNT; ++nt)
+#pragma unroll
+          for (int rp = 0; rp < 2; ++rp) {
+            const int k = 8 * nt + 2 * g + rp;
+            if (k < m2)
+              *reinterpret_cast<float2*>(rd.At + ((((int64_t)n * m2 + k) * C + c) * P1 + h) * 2) =
+                  make_float2(racc[c][nt][2 * rp], racc[c][nt][2 * rp + 1]);
+          }
+    }
+  }
+  if (WG || NWL) {
+    // block reduction of the per-lane partials -> partial[blockIdx.x][np] (np = C*C + C, + 4 C
+    // for LIFT: dW0 (C x 3) then db0 (C)), index = wacc index
+    __syncthreads();
+    float* red = lds;
+    constexpr int np = NWC + NWL;
+#pragma unroll
+    for (int e = 0; e < np; ++e) {
+      const float s = wave_sum(wacc[e]);
+      if (lane == 0) red[wave * np + e] = s;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+      float s = 0.f;
+      for (int wv = 0; wv < kW; ++wv) s += red[wv * np + p];
+      partial[(int64_t)blockIdx.x * np + p] = s;
+    }
+  }
+}
+
 }  // namespace
 
 namespace blindno {
@@ -547,8 +793,33 @@ struct RowinvGeom {
 #define ROWINV_WIDE_ITEMS 2048
 #endif
 
+// shapes the transposed C = 4 kernel (rowfuse_kernel) takes; BLINDNO_ROWFUSE=0 turns it off
+int g_rowfuse = -1;                                 // -1: from the environment on first use
+bool rowfuse_on() {
+  if (g_rowfuse < 0) {
+    const char* e = getenv("BLINDNO_ROWFUSE");
+    g_rowfuse = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_rowfuse != 0;
+}
+bool rowfuse_shape(int Bn, int C, int P1, int P2, int m2) {
+  return rowfuse_on() && C == 4 && m2 >= 4 && m2 <= 16 && m2 % 4 == 0 && P1 % 16 == 0 &&
+         P2 % 32 == 0 &&
+         2 * m2 <= P2 && Bn > 0 && (int64_t)Bn * C * P1 * P2 < INT32_MAX;
+}
+
 RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   RowinvGeom g;
+  if (rowfuse_shape(Bn, C, P1, P2, m2)) {
+    // whole 16-row blocks per work item, one per wave; partials are per workgroup
+    g.TPW = P2 / 16;
+    g.nitems = Bn * (P1 / 16);
+    const int b = (g.nitems + kW - 1) / kW;
+    g.blocks = b < ROWFUSE_BLOCKS ? b : ROWFUSE_BLOCKS;
+    g.ldsb = false;
+    g.lds = 0;
+    return g;
+  }
   const int KS = (m2 + 1) / 2, NT = (P2 + 15) / 16;
   const int NG = (C + 3) / 4;
   const int64_t base = (int64_t)((Bn * P1 + 3) / 4) * NG;
@@ -598,6 +869,32 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   const int cm = C <= 4 ? 4 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
   const int ks = (m2 + 1) / 2;
   if (ks > 24) return (int)hipErrorInvalidValue;               // m2 <= 48
+  {
+    // the transposed C = 4 kernel: 16-B field accesses need aligned bases and a crop width
+    // (dz's valid region, the snapshot) in whole float4s
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool rd_ok = !rd.At || rd.Npad == 16 * ((2 * m2 + 15) / 16);
+    if (rowfuse_shape(Bn, C, P1, P2, m2) && G == 1 && al(Z) && al(xs) && al(dz) && al(out) &&
+        dN2 % 4 == 0 && rd_ok && (!LIFT || (bl.N2 % 4 == 0 && al(bl.X) && al(bl.grid)))) {
+      const int NT = P2 / 16, S = m2 / 2;
+      size_t shf = sizeof(float) * ((size_t)NT * 64 * S + (rd.At ? (size_t)NT * 16 * rd.Npad : 0));
+      const size_t red = sizeof(float) * (size_t)kW * (C * C + C + 4 * C);
+      if (shf < red) shf = red;
+      if (shf > 160 * 1024) return (int)hipErrorInvalidValue;
+#define RF(RD_, S_)                                                                            \
+  rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1>          \
+      <<<nblocks, 256, shf, st>>>(                                                             \
+      Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, dN2, rd)
+#define RF_S(RD_) \
+  do { if (S == 2) RF(RD_, 2); else if (S == 4) RF(RD_, 4); else if (S == 6) RF(RD_, 6); else RF(RD_, 8); } while (0)
+      if (!rd.At) RF_S(0);
+      else if (rd.act) RF_S(2);
+      else RF_S(1);
+#undef RF_S
+#undef RF
+      return (int)hipGetLastError();
+    }
+  }
   if constexpr (!WG && !LIFT) {
     // wide fields with the spectrum in A-tile order (rowinv_tile_layout; full-field dz only)
     if (rowinv_tile_layout(Bn, C, P1, P2, m2) && dN1 == P1 && dN2 == P2) {
@@ -630,40 +927,18 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       return blindno_rowdft(out, rd.At, rd.Tp, Bn, C, P1, P2, m2, rd.act, (void*)st);
     }
   }
-  // the next layer's row DFT in this pass (whole rows per item, one channel group); otherwise
-  // it runs as its own launch after this one
-  const int NTc = (P2 + 15) / 16;
-  const bool fuse_rd = rd.At != nullptr && ROWINV_FUSE_RD && cm == 4 && g.TPW == NTc &&
-                       2 * m2 <= 32 && G == 1 && !(MODE == 1 && LIFT);
-  if (rd.At && !fuse_rd && (G != 1 || (MODE == 1 && LIFT))) return (int)hipErrorInvalidValue;
-  if (fuse_rd) {
-    sh += sizeof(float) * (size_t)NTc * 16 * rd.Npad;
-    if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
-#define RIF(KS_)                                                                             \
-  do {                                                                                       \
-    if (g.ldsb)                                                                              \
-      rowinv_mfma_kernel<4, KS_, MODE, ACT, WG, 1, LIFT, 1><<<nblocks, 256, sh, st>>>(       \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
-          dN2, rd);                                                                          \
-    else                                                                                     \
-      rowinv_mfma_kernel<4, KS_, MODE, ACT, WG, 0, LIFT, 1><<<nblocks, 256, sh, st>>>(       \
-          Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
-          dN2, rd);                                                                          \
-  } while (0)
-    if (ks <= 8) RIF(8); else RIF(16);
-#undef RIF
-    return (int)hipGetLastError();
-  }
+  // the next layer's row DFT otherwise runs as its own launch after this one
+  if (rd.At && (G != 1 || (MODE == 1 && LIFT))) return (int)hipErrorInvalidValue;
 #define RI(CM_, KS_)                                                                         \
   do {                                                                                       \
     if (g.ldsb)                                                                              \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 1, LIFT><<<nblocks, 256, sh, st>>>(        \
           Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
-          dN2, rd);                                                                          \
+          dN2);                                                                              \
     else                                                                                     \
       rowinv_mfma_kernel<CM_, KS_, MODE, ACT, WG, 0, LIFT><<<nblocks, 256, sh, st>>>(        \
           Z, xs, dz, wc, bc, out, TB, partial, Bn, C, P1, P2, m2, g.TPW, bl, Bg, wgs, dN1,   \
-          dN2, rd);                                                                          \
+          dN2);                                                                              \
   } while (0)
 #define RI_K(CM_) \
   if (ks <= 8) RI(CM_, 8); else if (ks <= 16) RI(CM_, 16); else RI(CM_, 24);
@@ -705,6 +980,12 @@ BLINDNO_API int blindno_rowidft_epi(const float* Z, const float* x, const float*
 
 BLINDNO_API int blindno_spectrum_tile_layout(int Bn, int C, int P1, int P2, int m2) {
   return rowinv_tile_layout(Bn, C, P1, P2, m2) ? 1 : 0;
+}
+
+BLINDNO_API int blindno_set_rowfuse(int on) {
+  const int prev = rowfuse_on() ? 1 : 0;
+  g_rowfuse = on ? 1 : 0;
+  return prev;
 }
 
 BLINDNO_API int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2) {

@@ -37,9 +37,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef ROWDFT_STAGE_ITEMS
 #define ROWDFT_STAGE_ITEMS 1
 #endif
-#ifndef ROWDFT_STAGE_RATIO
-#define ROWDFT_STAGE_RATIO 0
-#endif
 // Valid region (N1v, N2v): only rows h < N1v and columns w < N2v of each P1 x P2 plane are
 // read, the rest counts as zero -- for the gradient of a cropped FNO output (2d_FPE/
 // FNOModules.py:234), which is zero on the padding by construction, so the producer
@@ -47,11 +44,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // STAGE: the twiddle image is staged in LDS by every workgroup; otherwise the B operands are
 // read from the global image (L1/L2-resident) -- when each wave runs about one work item the
 // staging is as many bytes as the wave's own x rows and costs a full latency up front.
-#ifndef ROWDFT_PRELOAD
-#define ROWDFT_PRELOAD 0
-#endif
-constexpr int kRowdftPre = 10;
-template <int NT, int ALIGNED, bool STAGE, bool PRE>
+template <int NT, int ALIGNED, bool STAGE>
 __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
                                                           float* __restrict__ At,
                                                           const float* __restrict__ Tp,
@@ -91,31 +84,6 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
         for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
       }
     };
-    if constexpr (PRE) {
-      // all K blocks of the tile issued up front (KB <= kRowdftPre): the whole row segment is
-      // in flight at once instead of two blocks (the x stream is latency-bound otherwise)
-      float ap[kRowdftPre][4];
-#pragma unroll
-      for (int kb = 0; kb < kRowdftPre; ++kb)
-        if (kb < KB) load_a(kb, ap[kb]);
-#pragma unroll
-      for (int kb = 0; kb < kRowdftPre; ++kb) {
-        if (kb < KB) {
-          if (act) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) ap[kb][s] = gelu_f(ap[kb][s]);
-          }
-#pragma unroll
-          for (int t = 0; t < NT; ++t) {
-            const f32x4 b = *reinterpret_cast<const f32x4*>(
-                tsrc + (((kb * 4 + kq) * Npad) + (t0 + t) * 16 + r16) * 4);
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[kb][s], b[s], acc[t], 0, 0, 0);
-          }
-        }
-      }
-    } else {
     float a1[4], a2[4] = {0.f, 0.f, 0.f, 0.f};
     load_a(0, a1);
     if (KB > 1) load_a(1, a2);
@@ -136,7 +104,6 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
         for (int s = 0; s < 4; ++s)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc[t], 0, 0, 0);
       }
-    }
     }
     // D layout: lane holds rows 4*(l>>4) + r (r < 4), column l & 15
 #pragma unroll
@@ -167,7 +134,7 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
 // 1-channel snapshot is transformed, and it is read straight out of the bag tensor
 // X (B, T, N1, N2) through the bag's index list (snapshot n = b L + l -> X[b][idx[l]]), so
 // neither the gathered bag, the concatenated input nor x0 is ever materialised.
-template <int NT, int ALIGNED, bool PRE = ROWDFT_PRELOAD != 0>
+template <int NT, int ALIGNED>
 // b0 != nullptr: Gt holds the row spectra Dg[k][j][h] of the three grid/bias planes (gx, gy,
 // 1 on the crop) instead, and the grid/bias part is formed here as
 // W0[c,1] Dg[k][0] + W0[c,2] Dg[k][1] + b0[c] Dg[k][2] (Dg depends on the grid only, so it is
@@ -219,21 +186,10 @@ __global__ __launch_bounds__(256) void rowdft_bag_lift_kernel(
         for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bt[s], acc[t], 0, 0, 0);
       }
     };
-    if (PRE && KB <= kRowdftPre) {
-      // the snapshot row's K blocks all in flight at once (as rowdft_mfma_kernel PRE)
-      float ap[kRowdftPre][4];
-#pragma unroll
-      for (int kb = 0; kb < kRowdftPre; ++kb)
-        if (kb < KB) load_a(kb, ap[kb]);
-#pragma unroll
-      for (int kb = 0; kb < kRowdftPre; ++kb)
-        if (kb < KB) mma(kb, ap[kb]);
-    } else {
-      for (int kb = 0; kb < KB; ++kb) {
-        float a[4];
-        load_a(kb, a);
-        mma(kb, a);
-      }
+    for (int kb = 0; kb < KB; ++kb) {
+      float a[4];
+      load_a(kb, a);
+      mma(kb, a);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -328,10 +284,6 @@ constexpr int kFullHB = 10;
 #ifndef COLMIX_C12
 #define COLMIX_C12 1
 #endif
-// the column inverse fused into the column-DFT / mix workgroups (coldft_mix_kernel FUSE)
-#ifndef COLPASS_FUSE
-#define COLPASS_FUSE 0
-#endif
 // H16 (config E, blindno.ops.set_mix_precision("fp16")): the channel mix takes fp16 operands
 // with fp32 accumulation -- each complex multiply-add is two v_dot2c_f32_f16 (packed fp16
 // pairs, exact products, fp32 sum).  The column spectra are block-scaled first: the workgroup's
@@ -342,10 +294,7 @@ constexpr int kFullHB = 10;
 // batch of complex GEMVs (one Ci x Co matrix per kept mode, one row per sample), which would
 // fill a quarter of an MFMA tile at best.
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-// FUSE: the column inverse runs in the same workgroup on its own pairs (Y stays in LDS; the
-// colidft launch and the Y round trip disappear): Z[n][h][k][o] = sum_j Y[o][j] conj(F[h][j])
-// as a complex GEMM with M = the pairs' (p, o) rows, N = 16-row h tiles, K = the kept rows.
-template <int DIR, bool FULL, bool H16, bool FUSE>
+template <int DIR, bool FULL, bool H16>
 __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restrict__ At,
                                                          const float2* __restrict__ Wt,
                                                          const f32x4* __restrict__ FB,
@@ -353,10 +302,9 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
                                                          float2* __restrict__ Y, int npairs,
                                                          int Ci, int Co, int P1, int m1, int m2,
                                                          int P2, int G, int vec, int Bg,
-                                                         int64_t wtgs, const f32x4* __restrict__ GB,
-                                                         float2* __restrict__ Z, int tiled) {
+                                                         int64_t wtgs) {
   // grouped launches: samples n of weight group n / Bg use Wt + (n / Bg) wtgs (in floats)
-  extern __shared__ float2 sX[];                  // [G Cin][K1p + 1] (+ FUSE: [G Cout][K1p + 1])
+  extern __shared__ float2 sX[];                  // [G Cin][K1p + 1]
   const int K1 = kept_rows_count(m1, P1);
   const int Jt = (K1 + 15) >> 4, K1p = Jt * 16, LDX = K1p + 1;
   const int Cin = DIR == 0 ? Ci : Co;
@@ -515,55 +463,9 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
         im *= sc;
       }
     }
-    if constexpr (FUSE) sX[(G * Cin + p * Cout + o) * LDX + j] = make_float2(re, im);
-    else Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
+    Y[((int64_t)(q0 + p) * Cout + o) * K1p + j] = make_float2(re, im);
   };
   for (int e = threadIdx.x; e < nout; e += blockDim.x) mix_one(e);
-  if constexpr (FUSE) {
-    __syncthreads();
-    const float2* sY = sX + G * Cin * LDX;
-    const int rowsY = np * Cout;
-    const int MtY = (rowsY + 15) >> 4;
-    const int Ht = (P1 + 15) >> 4;
-    for (int item = wave; item < MtY * Ht; item += 4) {
-      const int mt = item / Ht, ht = item % Ht;
-      const int row = mt * 16 + r16;
-      const bool rok = row < rowsY;
-      const float2* yr = sY + (rok ? row : 0) * LDX;
-      const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
-      f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
-      for (int jb = 0; jb < Jt; ++jb) {
-        float re[4], im[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const float2 v = rok ? yr[jb * 16 + kq * 4 + s] : make_float2(0.f, 0.f);
-          re[s] = v.x;
-          im[s] = v.y;
-        }
-        cmfma4(re, im, gb[jb * 128], gb[jb * 128 + 1], dr, di);
-      }
-      const int h = ht * 16 + r16;
-      if (h >= P1) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rowD = mt * 16 + kq * 4 + r;
-        if (rowD >= rowsY) continue;
-        const int p = rowD / Cout, o = rowD - p * Cout;
-        const int q = q0 + p, n = q / m2, k = q - n * m2;
-        if (!tiled) {
-          Z[(((int64_t)n * P1 + h) * m2 + k) * Cout + o] = make_float2(dr[r], di[r]);
-        } else {
-          // A-tile order of the wide row inverse (as colidft_kernel writes it)
-          const int gr = n * P1 + h;
-          const int c16 = 4 * (gr & 3) + (o & 3);
-          float* zt = reinterpret_cast<float*>(Z) +
-                      ((int64_t)((gr >> 2) * (Cout >> 2) + (o >> 2)) * (m2 >> 1) + (k >> 1)) * 64;
-          zt[32 * (k & 1) + c16] = dr[r];
-          zt[32 * (k & 1) + 16 + c16] = di[r];
-        }
-      }
-    }
-  }
 }
 
 // Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
@@ -819,22 +721,16 @@ BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, 
   hipStream_t st = (hipStream_t)stream;
   // stage the twiddle image only when the waves reuse it (>= ROWDFT_STAGE_ITEMS work items
   // per wave)
-  // ... and when a workgroup's x stream is at least twice the image (the heads' 64-column image
-  // is as large as their rows: staging it costs a full round trip for nothing, r02 kbench)
-  const int64_t x_per_block = ((nwork + blocks - 1) / blocks) * 16 * KB * 16 * (int64_t)sizeof(float);
-  const bool stage = nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * blocks &&
-                     (!ROWDFT_STAGE_RATIO || 2 * (int64_t)sh <= x_per_block);
-  const bool pre = ROWDFT_PRELOAD && KB <= kRowdftPre;
-#define RD3(NT_, AL_, PR_)                                                                  \
+  const bool stage = nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * blocks;
+#define RD(NT_, AL_)                                                                        \
   do {                                                                                      \
     if (stage)                                                                              \
-      rowdft_mfma_kernel<NT_, AL_, true, PR_><<<blocks, 256, sh, st>>>(                     \
+      rowdft_mfma_kernel<NT_, AL_, true><<<blocks, 256, sh, st>>>(                          \
           x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
     else                                                                                    \
-      rowdft_mfma_kernel<NT_, AL_, false, PR_><<<blocks, 256, 0, st>>>(                     \
+      rowdft_mfma_kernel<NT_, AL_, false><<<blocks, 256, 0, st>>>(                          \
           x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
   } while (0)
-#define RD(NT_, AL_) do { if (pre) RD3(NT_, AL_, true); else RD3(NT_, AL_, false); } while (0)
 #define RD_AL(NT_) \
   if (aligned) RD(NT_, 1); else RD(NT_, 0);
   switch (nt) {
@@ -845,7 +741,6 @@ BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, 
   }
 #undef RD_AL
 #undef RD
-#undef RD3
   return (int)hipGetLastError();
 }
 
@@ -926,8 +821,7 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   while (((G * cin + 15) / 16) * Jt < COLPASS_WAVE_TILES && G * cin < 64) ++G;
   G = ((G * cin + 15) / 16) * 16 / cin;
   if (G < 1) G = 1;
-  const bool fuse = COLPASS_FUSE != 0;
-  const size_t sh = sizeof(float2) * (size_t)G * (cin + (fuse ? cout : 0)) * (K1p + 1);
+  const size_t sh = sizeof(float2) * (size_t)G * cin * (K1p + 1);
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
   const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
   hipStream_t st = (hipStream_t)stream;
@@ -935,12 +829,10 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
   // full operand prefetch when the launch is too small to hide latency with waves
   const bool full = (P1 + 15) / 16 <= kFullHB && (int64_t)g1.x * 4 < 4096;
-#define CM4_(D_, F_, H_, U_)                                                                \
-  coldft_mix_kernel<D_, F_, H_, U_><<<g1, 256, sh, st>>>(                                   \
+#define CM3_(D_, F_, H_)                                                                    \
+  coldft_mix_kernel<D_, F_, H_><<<g1, 256, sh, st>>>(                                       \
       (const float2*)At, (const float2*)Wt, (const f32x4*)FB, (float2*)Xs, (float2*)Y,     \
-      (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg, wtgs, (const f32x4*)GB, (float2*)Z, \
-      tiled)
-#define CM3_(D_, F_, H_) do { if (fuse) CM4_(D_, F_, H_, true); else CM4_(D_, F_, H_, false); } while (0)
+      (int)npairs, Ci, Co, P1, m1, m2, P2, G, vec, Bg, wtgs)
 #define CM_(D_, F_) do { if (h16) CM3_(D_, F_, true); else CM3_(D_, F_, false); } while (0)
   if (dir == 0) {
     if (full) CM_(0, true); else CM_(0, false);
@@ -949,9 +841,8 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   }
 #undef CM_
 #undef CM3_
-#undef CM4_
   int e = (int)hipGetLastError();
-  if (e || fuse) return e;
+  if (e) return e;
   const int Ht = (P1 + 15) / 16;
   const int Mt = (m2 * cout + 15) / 16;
   const dim3 g2((unsigned)(Bn * Ht), (unsigned)((Mt + 3) / 4));

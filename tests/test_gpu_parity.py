@@ -376,11 +376,11 @@ def test_crop_valid_region_kernels(C, m, N, Bn):
 def test_rowinv_fused_next_rowdft(C, m, P, Bn):
     """blindno_rowidft_epi_rd / blindno_rowidft_bwd_rd (the next layer's row DFT taken in the row
     inverse's pass) vs the same row inverse followed by blindno_rowdft on its output: the field
-    is identical and the spectra agree to fp32 rounding (the same MFMA chain order over the same
-    operands; 2e-6 relative).  Cases: fused (whole rows per item, Bn P / 4 >= 4096), a ragged
-    last column tile (P = 150), the small-bag and m2 > 16 fallbacks (separate row DFT launch).
-    The in-pass variant is compiled in with ROWINV_FUSE_RD=1 (rowinv.hip; off by default, see
-    DESIGN.md's measured table); without it the entries launch the row DFT themselves."""
+    agrees to the last bit or two (the fused and unfused template instances of the transposed
+    C = 4 kernel are compiled separately; 1e-7 relative) and the spectra to fp32 rounding (2e-6
+    relative).  Cases: the transposed whole-row kernel (C = 4, m = 12, P = 160), a ragged last
+    column tile (P = 150), the small-bag case and the m2 > 16 fallback (general kernel plus a
+    separate row DFT launch)."""
     from blindno import ops
     g = torch.Generator(device="cuda").manual_seed(C * 100 + m)
     Z = torch.randn(Bn, P, m, C, 2, device="cuda", generator=g) * 0.1
@@ -393,7 +393,7 @@ def test_rowinv_fused_next_rowdft(C, m, P, Bn):
             a_ref = ops.k_rowdft(z_ref, Bn, C, P, P, m, act_next)
             z, a = ops.k_rowidft_epi_rd(Z, x, cw, cb, Bn, C, P, P, m, act, act_next)
             torch.cuda.synchronize()
-            assert torch.equal(z, z_ref)
+            assert rel_l2(z.cpu().numpy(), z_ref.cpu().numpy()) <= 1e-7
             assert rel_l2(a.cpu().numpy(), a_ref.cpu().numpy()) <= 2e-6
     dz = torch.randn(Bn, C, P, P, device="cuda", generator=g)
     N = P - 20
@@ -402,9 +402,10 @@ def test_rowinv_fused_next_rowdft(C, m, P, Bn):
         a_ref = ops.k_rowdft(r_ref[0], Bn, C, P, P, m, 0)
         r = ops.k_rowidft_bwd(Z, dz, cw, x, Bn, C, P, P, m, 1, wg, valid=(N, N), rd=True)
         torch.cuda.synchronize()
-        assert torch.equal(r[0], r_ref[0])
+        assert rel_l2(r[0].cpu().numpy(), r_ref[0].cpu().numpy()) <= 1e-7
         if wg:
-            assert torch.equal(r[1], r_ref[1]) and torch.equal(r[2], r_ref[2])
+            assert rel_l2(r[1].cpu().numpy(), r_ref[1].cpu().numpy()) <= 1e-7
+            assert rel_l2(r[2].cpu().numpy(), r_ref[2].cpu().numpy()) <= 1e-7
         assert rel_l2(r[3].cpu().numpy(), a_ref.cpu().numpy()) <= 2e-6
 
 

@@ -91,3 +91,28 @@ def test_trainer_unet_2d(tmp_path):
     sd = torch.load(os.path.join(out, ckpts[0]), weights_only=True)
     m = exp.model(52, "cuda")
     m.load_state_dict(sd)
+
+
+def test_trainer_nio_2d(tmp_path):
+    """train_nio.py's loop (2d_FPE/train_nio.py:62-267: NIOFP2D with the Encoder2D branch, bs 4,
+    lr 5e-4, StepLR, best checkpoint in result_2d_nio) through the native trainer: one HIP graph
+    per drawn bag size L (the branch's train-mode BatchNorm takes its statistics over the bag
+    with its repeats, so no deduplication), the two-channel metric, all four loss files."""
+    from blindno import trainer
+    data = str(tmp_path / "ds.npz")
+    _npz_2d(data, M=10, T=56, N=61)
+    out = str(tmp_path / "result_2d_nio")
+    exp = trainer._experiments("nio")["2d_FPE"]
+    assert exp.result_dir == "result_2d_nio" and exp.lr == 5e-4 and exp.batch == 4
+    t = trainer.Trainer(exp, data, out, torch.device("cuda"), epochs=2, save_interval=1, log=lambda s: None)
+    assert not t.graphed.dedup
+    hist = t.fit()
+    assert len(hist["train_losses"]) == 2 and all(np.isfinite(hist["train_losses"]))
+    assert all(np.isfinite(hist["test_losses"]))
+    for k in ("train_losses", "test_losses", "test_losses_drift", "test_losses_diffusion"):
+        assert np.load(os.path.join(out, k + ".npy")).shape == (2,)
+    ckpts = [f for f in os.listdir(out) if f.startswith("model_checkpoint_best_")]
+    assert ckpts == [f"model_checkpoint_best_{min(hist['test_losses']):.6f}.pt"]
+    sd = torch.load(os.path.join(out, ckpts[0]), weights_only=True)
+    m = exp.model(61, "cuda")
+    m.load_state_dict(sd)

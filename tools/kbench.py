@@ -90,6 +90,11 @@ def main():
                                                         ptr(lw), ptr(vv), ptr(dz), ptr(pb), nbc, Bb, U, C, P, P, N,
                                                         N, 128, stream_ptr()),
                  8 * pts * C + sbytes)
+        if tag == "input":
+            # calibration: the device's own copy of one field (read + write, the streaming ceiling
+            # of an epilogue that reads x and writes z)
+            zc = torch.empty_like(z)
+            case("copy_field[input]", lambda: zc.copy_(z), 2 * 4 * z.numel())
         # spectral pieces of one layer
         sh = ops.SpecShape(Bn, C, C, P, P, m, m, 2)
         w = torch.rand(C, C, m, m, 2, device=dev) / (C * C)
@@ -103,6 +108,20 @@ def main():
         cb = torch.randn(C, device=dev) * 0.1
         case(f"rowidft_epi[{tag}]", lambda: ops.k_rowidft_epi(Z, z, cw, cb, Bn, C, P, P, m, 1), 2 * fld)
         case(f"rowidft_bwd[{tag}]", lambda: ops.k_rowidft_bwd(Z, z, cw, z, Bn, C, P, P, m, 1, C <= 4), 3 * fld)
+        if C <= 4:
+            # layer chaining: the next row DFT in the row-inverse pass (+ its spectrum bytes)
+            spb = 8 * Bn * m * C * P
+            case(f"rowidft_epi_rd[{tag}]", lambda: ops.k_rowidft_epi_rd(Z, z, cw, cb, Bn, C, P, P, m, 1, 1),
+                 2 * fld + 2 * spb)
+            case(f"rowidft_bwd_rd_crop[{tag}]",
+                 lambda: ops.k_rowidft_bwd(Z, z, cw, z, Bn, C, P, P, m, 1, True, (N, N), rd=True),
+                 fld * (2 + (N * N) / (P * P)) + 2 * spb)
+
+            def layer():
+                _, Zl = ops.k_colpass(At, Wt, Bn, C, C, P, m, m, P, 0)
+                return ops.k_rowidft_epi_rd(Zl, z, cw, cb, Bn, C, P, P, m, 1, 1)
+            # SURVEY 8d's algorithmic bytes of one layer: read x, write y, the weights
+            case(f"layer_colpass+epi_rd[{tag}]", layer, 2 * fld + 16 * C * C * m * m)
         if C > 4:
             case(f"conv_wgrad[{tag}]", lambda: ops.k_conv_wgrad(z, z, Bn, C, P, P, 1), 2 * fld)
         inp = torch.randn(Bn, N, N, 3 if tag == "input" else C, device=dev)

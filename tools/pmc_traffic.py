@@ -35,8 +35,10 @@ KERNELS = {
     "blindno_project_bwd": r"project_bwd_mfma_kernel<4,",
     "blindno_project_fwd": r"project_fwd_mfma_kernel<4,",
     "blindno_rowdft": r"rowdft_mfma_kernel<",
-    "blindno_rowidft_epi": r"rowinv_mfma_kernel<4, 8, 0,",
-    "blindno_rowidft_bwd": r"rowinv_mfma_kernel<4, 8, 1,",
+    "blindno_rowidft_epi": r"rowfuse_kernel<0, 1, 0, 0, 0,",
+    "blindno_rowidft_epi_rd": r"rowfuse_kernel<0, 1, 0, 0, 2,",
+    "blindno_rowidft_bwd": r"rowfuse_kernel<1, 1, 1, 0, 0,",
+    "blindno_rowidft_bwd_rd_crop": r"rowfuse_kernel<1, 1, 1, 0, 1,",
     "coldft_mix (blindno_colpass)": r"coldft_mix_kernel<0,",
     "colidft (blindno_colpass)": r"colidft_kernel",
 }
