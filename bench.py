@@ -234,7 +234,9 @@ def main():
             print(f"[bench] warmup step {i}: {time.perf_counter() - tw:.3f}s", file=sys.stderr, flush=True)
     timer = None
     if not a.no_kernel_timer:
-        timer = timing.KernelTimer(timing.DOMINANT)
+        # the dominant kernel: the bag-level projection (configs with the fused snapshot encoder);
+        # config D: its snapshot CNN's implicit-GEMM convolutions as one family
+        timer = timing.KernelTimer("blindno_conv2d" if a.config == "D" else timing.DOMINANT)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

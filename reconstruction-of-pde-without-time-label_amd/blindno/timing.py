@@ -21,7 +21,16 @@ GELU_FLOPS = 0
 # the snapshot encoder's bag-level projection forward (csrc/bagproj.hip): the largest kernel of a
 # config-C step (the per-snapshot projection backward, blindno_project_bwd[_w], before it)
 DOMINANT = os.environ.get("BLINDNO_TIMED_KERNEL", "blindno_project_bag_fwd")
-_VARIANTS = {"blindno_project_bwd": ("blindno_project_bwd", "blindno_project_bwd_w")}
+_VARIANTS = {"blindno_project_bwd": ("blindno_project_bwd", "blindno_project_bwd_w"),
+             # config D's snapshot CNN: every implicit-GEMM convolution of a step (forward, input
+             # gradient, weight gradient; csrc/conv.hip), reported as one family
+             "blindno_conv2d": ("blindno_conv2d_fwd", "blindno_conv2d_bwd_data", "blindno_conv2d_bwd_weight")}
+# families whose roofline aggregates every launch (sum of flops / sum of time)
+_FAMILIES = ("blindno_conv2d",)
+
+
+def _conv_out(n, k, s, p):
+    return (n + 2 * p - k) // s + 1
 
 
 def _i(args, k):
@@ -75,6 +84,16 @@ def cost(name, args):
         B, U, C, P1, P2, Ho, Wo, Hd = (_i(args, k) for k in range(8, 16))
         pts, bpts = B * U * Ho * Wo, B * Ho * Wo
         return 8 * pts * C + 4 * ((bpts + 15) // 16) * 16 * Hd * 6 + 4 * bpts, 2 * bpts * Hd * 6
+    if name in ("blindno_conv2d_fwd", "blindno_conv2d_bwd_data", "blindno_conv2d_bwd_weight"):
+        o = {"blindno_conv2d_fwd": 4, "blindno_conv2d_bwd_data": 3, "blindno_conv2d_bwd_weight": 5}[name]
+        N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw = (_i(args, k) for k in range(o, o + 11))
+        Ho, Wo = _conv_out(Hi, KH, sh, ph), _conv_out(Wi, KW, sw, pw)
+        K = Ci * KH * KW + (1 if name == "blindno_conv2d_bwd_weight" else 0)   # + the bias column
+        # FMA-only flops of the GEMM (the adjoint's FMAs equal the forward's); bytes: the
+        # operands and the result once each
+        flops = 2 * N * Co * Ho * Wo * K
+        nbytes = 4 * (N * Ci * Hi * Wi + N * Co * Ho * Wo + Co * K)
+        return nbytes, flops
     if name == "blindno_conv_wgrad":
         nchunk, Bn, C, P1, P2 = (_i(args, k) for k in range(3, 8))
         pts = Bn * P1 * P2
@@ -152,8 +171,11 @@ class KernelTimer:
                  traffic_per_point=None):
         if not self.recs:
             return None
-        bmax = max(r[2] for r in self.recs)
-        sel = [r for r in self.recs if 4 * r[2] >= bmax]
+        if self.name in _FAMILIES:
+            sel = self.recs                        # every launch of the family
+        else:
+            bmax = max(r[2] for r in self.recs)
+            sel = [r for r in self.recs if 4 * r[2] >= bmax]
         n = len(sel)
         ms = sum(a.elapsed_time(b) for a, b, *_ in sel) / n
         bytes_per = sum(r[2] for r in sel) / n
@@ -166,14 +188,18 @@ class KernelTimer:
             # the roof the kernel's arithmetic intensity puts it under
             ridge = flop_peak_tflops * 1e12 / (hbm_peak_gbs * 1e9)
             bound = "mfma" if flops_per / max(1.0, bytes_per) > ridge else "hbm"
+        fam = ({"family": list(self.entries), "aggregate": "sum of flops / sum of launch times"}
+               if self.name in _FAMILIES else {})
         if bound == "hbm":
             return {"kernel": self.name, "bound": "hbm", "achieved": round(gbs, 2), "peak": hbm_peak_gbs,
                     "unit": "GB/s", "frac": round(gbs / hbm_peak_gbs, 4), "traffic": traffic,
-                    "launches": n, "avg_ms": round(ms, 5), "algorithmic_bytes_per_launch": int(bytes_per)}
+                    "launches": n, "avg_ms": round(ms, 5), "algorithmic_bytes_per_launch": int(bytes_per),
+                    **fam}
+        note = ("FMA-only flops of the implicit GEMMs (one FMA = 2); fp32 operands on the fp32 matrix "
+                "cores" if self.name in _FAMILIES else
+                "FMA-only flops (one FMA = 2; exact-erf GELU / GELU' evaluation not charged); the kernel "
+                "is fp32 VALU-issue-bound on that GELU work; gfx950 fp32 vector peak = fp32 MFMA peak")
         return {"kernel": self.name, "bound": "mfma", "achieved": round(tfs, 3), "peak": flop_peak_tflops,
                 "unit": "TFLOP/s", "frac": round(tfs / flop_peak_tflops, 4), "traffic": traffic,
                 "launches": n, "avg_ms": round(ms, 5), "algorithmic_flops_per_launch": int(flops_per),
-                "algorithmic_bytes_per_launch": int(bytes_per),
-                "note": "FMA-only flops (one FMA = 2; exact-erf GELU / GELU' evaluation not charged); the "
-                        "kernel is fp32 VALU-issue-bound on that GELU work; gfx950 fp32 vector peak = "
-                        "fp32 MFMA peak"}
+                "algorithmic_bytes_per_launch": int(bytes_per), "note": note, **fam}

@@ -468,6 +468,9 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
 #ifndef ROWFUSE_BLOCKS
 #define ROWFUSE_BLOCKS 512
 #endif
+#ifndef ROWFUSE_ZPRE
+#define ROWFUSE_ZPRE 0
+#endif
 // NH column tiles per step (1 or 2): with NH = 2 lane group g owns the 8 consecutive columns
 // w = 32 st + 8 g + 4 hf + r of a 32-column step (hf: the step's two MFMA tiles), so the two
 // 16-B accesses a lane issues per channel and step are adjacent and each pair of wave
@@ -481,7 +484,9 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
 #ifndef ROWFUSE_NH1
 #define ROWFUSE_NH1 1
 #endif
-template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH>
+// HW: the layer has its 1x1 conv (wc != NULL) -- a compile-time flag: a runtime test around each
+// operand load made hipcc branch around the loads and count their waits conservatively.
+template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH, bool HW_ = true>
 __global__ __launch_bounds__(256) void rowfuse_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
@@ -511,7 +516,7 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
   const int nitems = Bn * HB;
   const int HW = P1 * P2;                           // field < 2^31 elements (launcher)
   const int NS = NT / NH;                           // steps per row block
-  const bool has_wc = wc != nullptr;
+  constexpr bool has_wc = HW_;
   float W[C][C], bv[C], w0[C][3], b0[C];
 #pragma unroll
   for (int o = 0; o < C; ++o) {
@@ -529,16 +534,35 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
 #pragma unroll
   for (int e = 0; e < NW; ++e) wacc[e] = 0.f;
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  for (int item = blockIdx.x * kW + wave; item < nitems; item += gridDim.x * kW) {
+  // the spectrum rows (B operand) of a work item: 4 S contiguous floats per lane; the next
+  // item's are loaded while this one runs (ROWFUSE_ZPRE), so only a wave's first item waits
+  auto load_z = [&](int item, f32x4 (&zr)[S]) {
+    const int it = item < nitems ? item : nitems - 1;
+    const int n = it / HB;
+    const int h = ((it - n * HB) << 4) + c16;
+    const f32x4* src = reinterpret_cast<const f32x4*>(Z + (int64_t)(n * P1 + h) * (m2 * C * 2) + 4 * S * g);
+#pragma unroll
+    for (int q = 0; q < S; ++q) zr[q] = src[q];
+  };
+  f32x4 znext[S];
+  const int item0 = blockIdx.x * kW + wave;
+  if (ROWFUSE_ZPRE) load_z(item0, znext);
+  for (int item = item0; item < nitems; item += gridDim.x * kW) {
     const int n = item / HB;
     const int h = ((item - n * HB) << 4) + c16;
     float zb[C][S];
     {
-      const f32x4* zr = reinterpret_cast<const f32x4*>(Z + (int64_t)(n * P1 + h) * (m2 * C * 2) + 4 * S * g);
+      f32x4 zcur[S];
+      if (ROWFUSE_ZPRE) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) zcur[q] = znext[q];
+      } else {
+        load_z(item, zcur);
+      }
       float zz[4 * S];
 #pragma unroll
       for (int q = 0; q < S; ++q) {
-        const f32x4 v = zr[q];
+        const f32x4 v = zcur[q];
         zz[4 * q] = v.x; zz[4 * q + 1] = v.y; zz[4 * q + 2] = v.z; zz[4 * q + 3] = v.w;
       }
 #pragma unroll
@@ -599,11 +623,8 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int nt = 0; nt < NNT; ++nt) racc[c][nt] = zero4;
-    Ops cur;
-    load(0, cur);
-    for (int st = 0; st < NS; ++st) {
-      Ops nxt;
-      load(st + 1 < NS ? st + 1 : st, nxt);         // one step ahead (the last re-reads its own)
+    // one step of MFMA tiles + epilogue on the operands ``cur`` (loaded one step earlier)
+    auto step = [&](const int st, const Ops& cur) {
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
         const int t = st * NH + hf;
@@ -717,7 +738,24 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
           }
         }
       }
-      cur = nxt;
+    };
+    // ping-pong operand buffers: the loads of step st + 1 are in flight while step st computes,
+    // and no register copy of a pending load forces an early wait (a rotating cur = next copy
+    // made hipcc wait for the prefetch inside the same step)
+    // (sched_barrier: keep each prefetch issued where it is written -- the scheduler otherwise
+    // sinks the loads next to their first use)
+    Ops bufA, bufB;
+    load(0, bufA);
+    if (ROWFUSE_ZPRE) load_z(item + gridDim.x * kW, znext);   // after this item's first loads
+    for (int st = 0; st < NS; st += 2) {
+      load(st + 1 < NS ? st + 1 : st, bufB);
+      __builtin_amdgcn_sched_barrier(0);
+      step(st, bufA);
+      if (st + 1 < NS) {
+        load(st + 2 < NS ? st + 2 : st + 1, bufA);
+        __builtin_amdgcn_sched_barrier(0);
+        step(st + 1, bufB);
+      }
     }
     if (RD) {
       // lane: row h, spectrum columns k' = 16 nt + 4 g + r -> modes 8 nt + 2 g + r/2 (Re, Im)
@@ -882,9 +920,16 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       if (shf < red) shf = red;
       if (shf > 160 * 1024) return (int)hipErrorInvalidValue;
 #define RF(RD_, S_)                                                                            \
-  rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1>          \
-      <<<nblocks, 256, shf, st>>>(                                                             \
-      Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, dN2, rd)
+  do {                                                                                         \
+    if (wc)                                                                                    \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1, true>  \
+          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+                                      dN2, rd);                                                \
+    else                                                                                       \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1, false> \
+          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+                                      dN2, rd);                                                \
+  } while (0)
 #define RF_S(RD_) \
   do { if (S == 2) RF(RD_, 2); else if (S == 4) RF(RD_, 4); else if (S == 6) RF(RD_, 6); else RF(RD_, 8); } while (0)
       if (!rd.At) RF_S(0);
