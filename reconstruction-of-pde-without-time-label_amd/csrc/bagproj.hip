@@ -65,6 +65,10 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
   __shared__ float zw[kSC][16][4];            // the same times lw_l (Q's operand)
   __shared__ float vred[4][kSC][64];          // [wave][snapshot][16 channel + point]
   __shared__ float ured[4][16];
+  // the rows of (w2 W1) that form v, per wave and lane group: [wave][g4][tt][i][c] as (r = 2 i,
+  // 2 i + 1) pairs -- read back as broadcasts instead of held in 32 VGPRs per lane (the register
+  // budget of 3 resident waves per SIMD)
+  __shared__ float2 swr[4][4][2][2][4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = uniform_int(tid >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
@@ -73,7 +77,8 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
 
   // this wave's hidden tiles t = 2 wave + tt: fc1 A operand (k-scaled), bias rows, the rows of
   // (w2 * W1) that form v, and w2 for ubar
-  float wa[2], bb[2][4], wr[2][4][4], w2r[2][4];
+  float wa[2], bb[2][4], w2r[2][4];
+  float vinit[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int k0 = 16 * (2 * wave + tt);
@@ -84,21 +89,20 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
       bb[tt][r] = kK * b1[k];
       w2r[tt][r] = w2[k];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) wr[tt][r][c] = c < C ? w2[k] * w1[k * C + c] : 0.f;
+      for (int c = 0; c < 4; ++c) {
+        const float wrv = c < C ? w2[k] * w1[k * C + c] : 0.f;
+        // the loop evaluates Phi - 1/2 (no +1/2: one packed add per pair less); the 1/2 parts
+        // are added back here and at the statistics write (below): v gets 1/2 sum_k (w2 W1)[k]
+        vinit[c] += wrv;
+        if (c16 == 0) {
+          float2& e = swr[wave][g4][tt][r >> 1][c];
+          if (r & 1) e.y = wrv; else e.x = wrv;
+        }
+      }
     }
   }
-  // the loop evaluates Phi - 1/2 (no +1/2: one packed add per pair less); the 1/2 parts are
-  // added back here and at the statistics write (below):  v gets 1/2 sum_k (w2 W1)[k] per lane
-  float vinit[4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    float a = 0.f;
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) a += wr[tt][r][c];
-    vinit[c] = 0.5f * a;
-  }
+  for (int c = 0; c < 4; ++c) vinit[c] *= 0.5f;
   __syncthreads();
   float lsum = 0.f;                            // sum_l lw_l, same order in every thread
   for (int l = 0; l < U; ++l) lsum += slw[l];
@@ -134,6 +138,10 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
       }
       __syncthreads();
       for (int l = 0; l < nl; ++l) {
+        // an opaque zero offset for the swr reads: keeps them in the loop (hoisted, they would
+        // occupy the 32 VGPRs they exist to save)
+        int zo;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
         const float4 zc = *reinterpret_cast<const float4*>(&zw[l][c16][0]);
         const float az = zs[l][c16][g4];
         const f32x2 wl = splat2(slw[l0 + l]);
@@ -157,9 +165,12 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
             Q[tt][1][i] = pk_fma(gd, splat2(zc.y), Q[tt][1][i]);
             Q[tt][2][i] = pk_fma(gd, splat2(zc.z), Q[tt][2][i]);
             Q[tt][3][i] = pk_fma(gd, splat2(zc.w), Q[tt][3][i]);
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-              vp[c] = pk_fma(gd, (f32x2){wr[tt][2 * i][c], wr[tt][2 * i + 1][c]}, vp[c]);
+            const float4* wq = reinterpret_cast<const float4*>(&swr[wave][g4][tt][i][0]) + zo;
+            const float4 wq0 = wq[0], wq1 = wq[1];
+            vp[0] = pk_fma(gd, (f32x2){wq0.x, wq0.y}, vp[0]);
+            vp[1] = pk_fma(gd, (f32x2){wq0.z, wq0.w}, vp[1]);
+            vp[2] = pk_fma(gd, (f32x2){wq1.x, wq1.y}, vp[2]);
+            vp[3] = pk_fma(gd, (f32x2){wq1.z, wq1.w}, vp[3]);
           }
         }
         // v over this wave's 32 hidden units: sum the pair, then reduce-scatter over the 4 lane
