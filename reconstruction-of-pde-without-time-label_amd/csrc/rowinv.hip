@@ -486,7 +486,8 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
 #endif
 // HW: the layer has its 1x1 conv (wc != NULL) -- a compile-time flag: a runtime test around each
 // operand load made hipcc branch around the loads and count their waits conservatively.
-template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH, bool HW_ = true>
+// NSC: steps per row block as a compile-time constant (P2 / (16 NH)), 0 = a runtime loop.
+template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH, bool HW_ = true, int NSC = 0>
 __global__ __launch_bounds__(256) void rowfuse_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
@@ -744,17 +745,27 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
     // made hipcc wait for the prefetch inside the same step)
     // (sched_barrier: keep each prefetch issued where it is written -- the scheduler otherwise
     // sinks the loads next to their first use)
-    Ops bufA, bufB;
-    load(0, bufA);
+    Ops buf[2];
+    load(0, buf[0]);
     if (ROWFUSE_ZPRE) load_z(item + gridDim.x * kW, znext);   // after this item's first loads
-    for (int st = 0; st < NS; st += 2) {
-      load(st + 1 < NS ? st + 1 : st, bufB);
-      __builtin_amdgcn_sched_barrier(0);
-      step(st, bufA);
-      if (st + 1 < NS) {
-        load(st + 2 < NS ? st + 2 : st + 1, bufA);
+    if constexpr (NSC > 0) {
+      // the step count is a compile-time constant: straight-line steps, the waits counted exactly
+#pragma unroll
+      for (int st = 0; st < NSC; ++st) {
+        if (st + 1 < NSC) load(st + 1, buf[(st + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
-        step(st + 1, bufB);
+        step(st, buf[st & 1]);
+      }
+    } else {
+      for (int st = 0; st < NS; st += 2) {
+        load(st + 1 < NS ? st + 1 : st, buf[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        step(st, buf[0]);
+        if (st + 1 < NS) {
+          load(st + 2 < NS ? st + 2 : st + 1, buf[0]);
+          __builtin_amdgcn_sched_barrier(0);
+          step(st + 1, buf[1]);
+        }
       }
     }
     if (RD) {
@@ -919,14 +930,22 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       const size_t red = sizeof(float) * (size_t)kW * (C * C + C + 4 * C);
       if (shf < red) shf = red;
       if (shf > 160 * 1024) return (int)hipErrorInvalidValue;
+      constexpr int NHm = MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1;
+      // P2 = 160 (the encoder at 128^2), forward: the step loop fully unrolled (the adjoint's
+      // larger operand set and in-pass weight-gradient sums spill when unrolled: runtime loop)
+      const bool p160 = P2 == 160 && MODE == 0;
 #define RF(RD_, S_)                                                                            \
   do {                                                                                         \
-    if (wc)                                                                                    \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1, true>  \
+    if (wc && p160)                                                                            \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, true, MODE == 0 ? 160 / (16 * NHm) : 0> \
+          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+                                      dN2, rd);                                                \
+    else if (wc)                                                                               \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, true>                                  \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd);                                                \
     else                                                                                       \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1, false> \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, false>                                 \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd);                                                \
   } while (0)
