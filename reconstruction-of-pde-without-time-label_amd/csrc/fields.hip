@@ -119,6 +119,99 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_kernel(const float* __rest
   }
 }
 
+// Wide lifts of the FNO heads (Cin, C <= 16, Cin % 4 == 0; two heads grouped): one thread per
+// point of the padded P1 x P2 grid, every channel in registers, the weights of all groups in LDS
+// (broadcast reads), the point's Cin inputs as float4 loads, 32-bit index math with launch-
+// invariant divisors.  Forward writes all C channels of x0 (zero on the padding); the input
+// gradient sums the groups' fields: d_in[n'][h][w][j] = sum_g sum_c W_g[c][j] dx0[g Bg + n'][c].
+constexpr int kLiftMaxG = 4, kLiftMaxC = 16;
+template <int CIN, int CM>
+__global__ __launch_bounds__(kBlock) void lift_fwd_wide_kernel(
+    const float* __restrict__ in, const float* __restrict__ w0, const float* __restrict__ b0,
+    float* __restrict__ x0, int Bn, int N1, int N2, int C, int P1, int P2, int Bg, int G,
+    int64_t wgs, FastDiv dHW, FastDiv dP2) {
+  __shared__ float sw[kLiftMaxG][CM * CIN + CM];
+  for (int e = threadIdx.x; e < G * (CM * CIN + CM); e += blockDim.x) {
+    const int g = e / (CM * CIN + CM), q = e - g * (CM * CIN + CM);
+    float v = 0.f;
+    if (q < CM * CIN) {
+      const int c = q / CIN, j = q - c * CIN;
+      v = c < C ? w0[g * wgs + c * CIN + j] : 0.f;
+    } else if (q - CM * CIN < C) {
+      v = b0[g * wgs + q - CM * CIN];
+    }
+    sw[g][q] = v;
+  }
+  __syncthreads();
+  const unsigned HW = (unsigned)(P1 * P2);
+  const unsigned total = (unsigned)Bn * HW;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const unsigned n = dHW.div(idx), s = idx - n * HW;
+    const unsigned h = dP2.div(s), w = s - h * (unsigned)P2;
+    float* xp = x0 + (size_t)n * C * HW + s;
+    if (h >= (unsigned)N1 || w >= (unsigned)N2) {
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C) xp[(size_t)c * HW] = 0.f;
+      continue;
+    }
+    const int g = G > 1 ? (int)(n / (unsigned)Bg) : 0;
+    const unsigned ni = n - (unsigned)g * (unsigned)Bg;
+    const float4* ip = reinterpret_cast<const float4*>(in + ((size_t)(ni * N1 + h) * N2 + w) * CIN);
+    float v[CIN];
+#pragma unroll
+    for (int q = 0; q < CIN / 4; ++q) {
+      const float4 t = ip[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    }
+    const float* wg = sw[g];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c >= C) break;
+      float a = wg[CM * CIN + c];
+#pragma unroll
+      for (int j = 0; j < CIN; ++j) a = fmaf(wg[c * CIN + j], v[j], a);
+      xp[(size_t)c * HW] = a;
+    }
+  }
+}
+
+template <int CIN, int CM>
+__global__ __launch_bounds__(kBlock) void lift_bwd_in_wide_kernel(
+    const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in, int Bn,
+    int N1, int N2, int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2) {
+  __shared__ float sw[kLiftMaxG][CM * CIN];
+  for (int e = threadIdx.x; e < G * CM * CIN; e += blockDim.x) {
+    const int g = e / (CM * CIN), q = e - g * (CM * CIN);
+    const int c = q / CIN, j = q - c * CIN;
+    sw[g][q] = c < C ? w0[g * wgs + c * CIN + j] : 0.f;
+  }
+  __syncthreads();
+  const unsigned S = (unsigned)(N1 * N2), HW = (unsigned)(P1 * P2);
+  const unsigned total = (unsigned)Bn * S;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const unsigned n = dS.div(idx), s = idx - n * S;
+    const unsigned h = dN2.div(s), w = s - h * (unsigned)N2;
+    float acc[CIN];
+#pragma unroll
+    for (int j = 0; j < CIN; ++j) acc[j] = 0.f;
+    for (int g = 0; g < G; ++g) {
+      const float* dp = dx0 + ((size_t)(g * Bn + n) * C) * HW + h * (unsigned)P2 + w;
+      const float* wg = sw[g];
+#pragma unroll
+      for (int c = 0; c < CM; ++c) {
+        if (c >= C) break;
+        const float d = dp[(size_t)c * HW];
+#pragma unroll
+        for (int j = 0; j < CIN; ++j) acc[j] = fmaf(wg[c * CIN + j], d, acc[j]);
+      }
+    }
+    float4* op = reinterpret_cast<float4*>(d_in + (size_t)idx * CIN);
+#pragma unroll
+    for (int q = 0; q < CIN / 4; ++q) op[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+  }
+}
+
 // Tiled outer-product reductions: partial[block][a*Cb + b] = sum_p A[a][p] B[b][p] and
 // partial[block][Ca*Cb + a] = sum_p A[a][p] over the block's tile of TP points, staged in
 // LDS with coalesced loads (rows padded by one float: conflict-free column sweeps).
@@ -806,6 +899,15 @@ BLINDNO_API int blindno_lift_fwd_g(const float* in, const float* w0, const float
   hipStream_t st = (hipStream_t)stream;
   const int Bg = G > 1 ? Bn / G : Bn;
   if (G == 1) wgs = 0;
+  const int64_t npts = (int64_t)Bn * P1 * P2;
+  if (Cin == 12 && C > 4 && C <= kLiftMaxC && G <= kLiftMaxG && npts * (C > Cin ? C : Cin) < INT32_MAX &&
+      (((uintptr_t)in) & 15) == 0) {
+    // the heads (width 12): thread per point, weights in LDS (lift_fwd_wide_kernel)
+    lift_fwd_wide_kernel<12, 16><<<grid_for(npts, kBlock, 8192), kBlock, 0, st>>>(
+        in, w0, b0, x0, Bn, N1, N2, C, P1, P2, Bg, G, wgs, FastDiv::make((unsigned)(P1 * P2)),
+        FastDiv::make((unsigned)P2));
+    return (int)hipGetLastError();
+  }
   if (C > 4 && C <= 16) {         // wide lifts (the heads): one thread per point, all channels
     const int64_t pts = (int64_t)Bn * P1 * P2;
     lift_fwd_pt_kernel<16><<<grid_for(4 * pts, kBlock, 65536), kBlock, 0, st>>>(
@@ -838,8 +940,15 @@ BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const floa
   hipStream_t st = (hipStream_t)stream;
   if (d_in) {
     const int64_t total = (int64_t)Bg * N1 * N2 * Cin;
-    lift_bwd_in_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(
-        dx0, w0, d_in, Bg, N1, N2, Cin, C, P1, P2, G, G > 1 ? wgs : 0);
+    if (Cin == 12 && C <= kLiftMaxC && G <= kLiftMaxG && (int64_t)Bn * C * P1 * P2 < INT32_MAX &&
+        total < INT32_MAX && (((uintptr_t)d_in) & 15) == 0) {
+      lift_bwd_in_wide_kernel<12, 16><<<grid_for((int64_t)Bg * N1 * N2, kBlock, 8192), kBlock, 0, st>>>(
+          dx0, w0, d_in, Bg, N1, N2, C, P1, P2, G, G > 1 ? wgs : 0,
+          FastDiv::make((unsigned)(N1 * N2)), FastDiv::make((unsigned)N2));
+    } else {
+      lift_bwd_in_kernel<<<grid_for(total, kBlock, 65536), kBlock, 0, st>>>(
+          dx0, w0, d_in, Bg, N1, N2, Cin, C, P1, P2, G, G > 1 ? wgs : 0);
+    }
   }
   if (partial) {
     if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)

@@ -34,6 +34,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef ROWDFT_MAX_BLOCKS
 #define ROWDFT_MAX_BLOCKS 4096
 #endif
+// work items the row DFT aims at when splitting a row tile's column tiles over waves
+#ifndef ROWDFT_MIN_WORK
+#define ROWDFT_MIN_WORK 4096
+#endif
 #ifndef ROWDFT_STAGE_ITEMS
 #define ROWDFT_STAGE_ITEMS 1
 #endif
@@ -712,7 +716,7 @@ BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, 
   const int nrt = (nrows + 15) / 16;
   int nt = ntiles;
   if (nt > 4) nt = 4;
-  while (nt > 1 && (int64_t)nrt * ((ntiles + nt - 1) / nt) < 4096) nt >>= 1;
+  while (nt > 1 && (int64_t)nrt * ((ntiles + nt - 1) / nt) < ROWDFT_MIN_WORK) nt >>= 1;
   while (ntiles % nt) --nt;
   const int groups = ntiles / nt;
   const int64_t nwork = (int64_t)nrt * groups;
@@ -767,7 +771,7 @@ BLINDNO_API int blindno_rowdft_bag_lift_dg(const float* X, const int* idx, const
   const int nrt = (nrows + 15) / 16;
   int nt = ntiles;
   if (nt > 4) nt = 4;
-  while (nt > 1 && (int64_t)nrt * ((ntiles + nt - 1) / nt) < 4096) nt >>= 1;
+  while (nt > 1 && (int64_t)nrt * ((ntiles + nt - 1) / nt) < ROWDFT_MIN_WORK) nt >>= 1;
   while (ntiles % nt) --nt;
   const int groups = ntiles / nt;
   const int64_t nwork = (int64_t)nrt * groups;

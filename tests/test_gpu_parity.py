@@ -462,3 +462,39 @@ def test_lift_wgrad_vs_fp64(C, Cin, N, G):
         b = d.sum(dim=(0, 2, 3))
         assert rel_l2(got[gi, :C * Cin].numpy(), w.reshape(-1).numpy()) <= 5e-5
         assert rel_l2(got[gi, C * Cin:].numpy(), b.numpy()) <= 5e-5
+
+
+@pytest.mark.parametrize("N,G", [(128, 2), (61, 1), (64, 2)])
+def test_head_lift_fwd_and_input_grad_vs_fp64(N, G):
+    """The heads' fc0 + pad (blindno_lift_fwd_g, width 12 -> 12: the thread-per-point kernel with
+    the weights in LDS) and its input gradient (blindno_lift_bwd_g, d_in summed over the grouped
+    heads) vs float64 (2d_FPE/FNOModules.py:219-224): x0 = pad(W0 in + b0), zero on the padding;
+    d_in[n][h][w][j] = sum_g sum_c W_g[c][j] dx0[g Bg + n][c][h][w] on the crop."""
+    from blindno import ops
+    from blindno._lib import call, ptr, stream_ptr
+    C = Cin = 12
+    Bg, P = 4, N + ops.pad_amount(N)
+    g = torch.Generator(device="cuda").manual_seed(N + G)
+    inp = torch.randn(Bg, N, N, Cin, device="cuda", generator=g)
+    w0 = torch.randn(G, C, Cin, device="cuda", generator=g)
+    b0 = torch.randn(G, C, device="cuda", generator=g)
+    x0 = torch.full((G * Bg, C, P, P), float("nan"), device="cuda")
+    call("blindno_lift_fwd_g", ptr(inp), ptr(w0), ptr(b0), ptr(x0), G, C * Cin, G * Bg, N, N, Cin, C, P, P,
+         stream_ptr())
+    dx0 = torch.randn(G * Bg, C, P, P, device="cuda", generator=g)
+    d_in = torch.empty(Bg, N, N, Cin, device="cuda")
+    call("blindno_lift_bwd_g", ptr(dx0), ptr(inp), ptr(w0), ptr(d_in), None, 0, G, C * Cin, G * Bg, N, N, Cin,
+         C, P, P, stream_ptr())
+    torch.cuda.synchronize()
+    i64, w64, b64 = inp.double().cpu(), w0.double().cpu(), b0.double().cpu()
+    ref = torch.zeros(G * Bg, C, P, P, dtype=torch.float64)
+    for gi in range(G):
+        ref[gi * Bg:(gi + 1) * Bg, :, :N, :N] = (torch.einsum("nhwj,cj->nchw", i64, w64[gi])
+                                                 + b64[gi][None, :, None, None])
+    got = x0.double().cpu()
+    assert torch.isfinite(got).all()                     # the padding is written (zeros)
+    assert float(got[:, :, N:, :].abs().max()) == 0.0 and float(got[:, :, :, N:].abs().max()) == 0.0
+    assert rel_l2(got.numpy(), ref.numpy()) <= 1e-6
+    d64 = dx0.double().cpu()[:, :, :N, :N]
+    dref = sum(torch.einsum("nchw,cj->nhwj", d64[gi * Bg:(gi + 1) * Bg], w64[gi]) for gi in range(G))
+    assert rel_l2(d_in.double().cpu().numpy(), dref.numpy()) <= 1e-6
