@@ -471,6 +471,10 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
 #ifndef ROWFUSE_ZPRE
 #define ROWFUSE_ZPRE 0
 #endif
+// operand prefetch (ping-pong buffers) in the adjoint
+#ifndef ROWFUSE_PF1
+#define ROWFUSE_PF1 1
+#endif
 // NH column tiles per step (1 or 2): with NH = 2 lane group g owns the 8 consecutive columns
 // w = 32 st + 8 g + 4 hf + r of a 32-column step (hf: the step's two MFMA tiles), so the two
 // 16-B accesses a lane issues per channel and step are adjacent and each pair of wave
@@ -755,6 +759,13 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
         if (st + 1 < NSC) load(st + 1, buf[(st + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         step(st, buf[st & 1]);
+      }
+    } else if (MODE == 1 && !ROWFUSE_PF1) {
+      // the adjoint without operand prefetch (its operand set is twice the forward's; the
+      // registers buy occupancy instead)
+      for (int st = 0; st < NS; ++st) {
+        if (st > 0) load(st, buf[0]);
+        step(st, buf[0]);
       }
     } else {
       for (int st = 0; st < NS; st += 2) {

@@ -36,7 +36,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #endif
 // work items the row DFT aims at when splitting a row tile's column tiles over waves
 #ifndef ROWDFT_MIN_WORK
-#define ROWDFT_MIN_WORK 4096
+#define ROWDFT_MIN_WORK 512
 #endif
 #ifndef ROWDFT_STAGE_ITEMS
 #define ROWDFT_STAGE_ITEMS 1

@@ -478,8 +478,12 @@ def test_head_lift_fwd_and_input_grad_vs_fp64(N, G):
     inp = torch.randn(Bg, N, N, Cin, device="cuda", generator=g)
     w0 = torch.randn(G, C, Cin, device="cuda", generator=g)
     b0 = torch.randn(G, C, device="cuda", generator=g)
+    # grouped weights share one group stride wgs for the weights and the biases (ops packs both
+    # into per-head blocks of that stride)
+    bpk = torch.zeros(G, C * Cin, device="cuda")
+    bpk[:, :C] = b0
     x0 = torch.full((G * Bg, C, P, P), float("nan"), device="cuda")
-    call("blindno_lift_fwd_g", ptr(inp), ptr(w0), ptr(b0), ptr(x0), G, C * Cin, G * Bg, N, N, Cin, C, P, P,
+    call("blindno_lift_fwd_g", ptr(inp), ptr(w0), ptr(bpk), ptr(x0), G, C * Cin, G * Bg, N, N, Cin, C, P, P,
          stream_ptr())
     dx0 = torch.randn(G * Bg, C, P, P, device="cuda", generator=g)
     d_in = torch.empty(Bg, N, N, Cin, device="cuda")

@@ -35,11 +35,11 @@ __global__ void fill_kernel(float* x, long n) {
 
 // MFMA: 4 chains of 6 v_mfma_f32_16x16x4f32 per tile (the row inverse's work), the A operand
 // from an LDS image like the real kernel's twiddles
-template <int D, bool ALU, bool MF = false>
+template <int D, bool ALU, bool MF = false, bool RANDOP = false>
 __global__ __launch_bounds__(256) void frag_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                    int Bn, int P, float w) {
   __shared__ float sA[10 * 64 * 6];
-  for (int e = threadIdx.x; e < 10 * 64 * 6; e += 256) sA[e] = 0.001f * (e % 17);
+  for (int e = threadIdx.x; e < 10 * 64 * 6; e += 256) sA[e] = RANDOP ? __sinf(1.3f * e + 0.7f) : 0.001f * (e % 17);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void frag_kernel(const float* __restrict__ x, 
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int s = 0; s < 6; ++s) zb[c][s] = 0.01f * (c + s + r16);
+          for (int s = 0; s < 6; ++s) zb[c][s] = RANDOP ? cur[c][s & 3] * 0.37f + (float)s : 0.01f * (c + s + r16);
         const float2* ta = reinterpret_cast<const float2*>(sA + (t * 64 + lane) * 6);
         float av[6];
 #pragma unroll
@@ -144,6 +144,8 @@ int main() {
     run(nm, [&] { frag_kernel<1, true, true><<<b, 256>>>(x, y, Bn, P, 0.1f); });
     snprintf(nm, sizeof nm, "frag_mfma_alu<2> b%d", b);
     run(nm, [&] { frag_kernel<2, true, true><<<b, 256>>>(x, y, Bn, P, 0.1f); });
+    snprintf(nm, sizeof nm, "frag_mfma_alu_rand<1> b%d", b);
+    run(nm, [&] { frag_kernel<1, true, true, true><<<b, 256>>>(x, y, Bn, P, 0.1f); });
   }
   hipFree(x);
   hipFree(y);
