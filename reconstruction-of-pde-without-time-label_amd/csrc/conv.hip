@@ -16,13 +16,15 @@
 //         split over blockIdx.z into fixed K ranges; the partials are reduced in a fixed order
 //         afterwards (blindno_reduce_partials).
 //
-// Tiling for CDNA4 wave64: a 256-thread workgroup computes a 64 x 64 tile as 2 x 2 waves of
-// 32 x 32 (2 x 2 MFMA blocks each, 4 accumulator VGPRs per block), K in steps of 16 staged
-// through double-buffered LDS (k-major, rows padded by 16 floats: the four k-groups of a wave's
-// operand read land in disjoint banks).  The next step's global loads are issued before the
-// current step's MFMAs, so their latency hides behind 16 MFMAs per wave.  im2col is never
-// materialised: each loader lane decodes its (channel, tap) / pixel indices with
-// multiply-high divisions by the launch's constants (FastDiv).
+// Tiling for CDNA4 wave64: a 256-thread workgroup computes a BM x BN tile (128 x 128 for the
+// large layers, 64 x 64 otherwise) as 2 x 2 waves of (BM/2) x (BN/2) (up to 4 x 4 MFMA blocks
+// per wave, 4 accumulator VGPRs each), K in steps of 16 staged through double-buffered LDS.
+// The LDS tiles are k-contiguous per row (A[m][k], B[n][k], rows padded to 20 floats) and the
+// MFMA K order is permuted (step s takes k = 4 (lane>>4) + s), so one ds_read_b128 brings a
+// lane's operands of four MFMA steps.  The next step's global loads are issued before the
+// current step's MFMAs, so their latency hides behind 16 (64 x 64) or 64 (128 x 128) MFMAs per
+// wave.  im2col is never materialised: each loader lane decodes its (channel, tap) / pixel
+// indices with multiply-high divisions by the launch's constants (FastDiv).
 #include "common.h"
 #include "blindno.h"
 
@@ -32,8 +34,8 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 64, BN = 64, BK = 16;
-constexpr int SA = BM + 16, SB = BN + 16;      // LDS row strides (floats)
+constexpr int BK = 16;
+constexpr int SK = BK + 4;                     // LDS row stride (floats) of the k-contiguous tiles
 
 enum { FWD = 0, BWD_D = 1, BWD_W = 2 };
 
@@ -155,13 +157,15 @@ __device__ __forceinline__ Tap decode_tap(const ConvArgs& g, int ng) {
   return t;
 }
 
-template <int MODE>
+template <int MODE, int BM, int BN>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict__ pa,
                                                          const float* __restrict__ pb,
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ out, ConvArgs g) {
-  __shared__ float As[2][BK * SA];
-  __shared__ float Bs[2][BK * SB];
+  constexpr int EA = BM / 16, EB = BN * BK / 256;  // loads per thread per K step (A, B)
+  constexpr int MI = BM / 32, NJ = BN / 32;        // MFMA blocks per wave
+  __shared__ float As[2][BM * SK];
+  __shared__ float Bs[2][BN * SK];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uniform_int(tid >> 6);
@@ -178,27 +182,28 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   // loader roles.  A: k = tid % 16 (contiguous in memory for all modes), m = tid / 16 + 16 e.
-  const int ak = tid & 15, am = tid >> 4;
-  // B (FWD / BWD_D): pixel n = tid % 64 fixed for the tile, k = tid / 64 + 4 e.
+  // B (FWD / BWD_D): pixel n = tid % BN fixed for the tile, k = tid / BN + (256 / BN) e.
   // B (BWD_W): pixel k = tid % 16, column n = tid / 16 + 16 e (fixed taps for the tile).
-  const int bn = tid & 63, bk = tid >> 6;
+  const int ak = tid & 15, am = tid >> 4;
+  const int bn = tid % BN, bk = tid / BN;
+  constexpr int KS = 256 / BN;                    // k stride of a thread's B loads
   Pix pix{};
-  Tap taps[4];
+  Tap taps[EB];
   if (MODE != BWD_W) {
     pix = decode_pix<MODE>(g, ph, n0 + bn);
   } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) taps[e] = decode_tap(g, n0 + (tid >> 4) + 16 * e);
+    for (int e = 0; e < EB; ++e) taps[e] = decode_tap(g, n0 + (tid >> 4) + 16 * e);
   }
 
-  float ra[4], rb[4];
+  float ra[EA], rb[EB];
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) ra[e] = load_a<MODE>(pa, g, ph, m0 + am + 16 * e, k0 + ak, kend);
+    for (int e = 0; e < EA; ++e) ra[e] = load_a<MODE>(pa, g, ph, m0 + am + 16 * e, k0 + ak, kend);
     if (MODE != BWD_W) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) rb[e] = load_b_pix<MODE>(pb, g, ph, pix, k0 + bk + 4 * e, kend);
+      for (int e = 0; e < EB; ++e) rb[e] = load_b_pix<MODE>(pb, g, ph, pix, k0 + bk + KS * e, kend);
     } else {
       const int kg = k0 + ak;                          // this thread's pixel
       const bool kok = kg < kend;
@@ -209,7 +214,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
       const int64_t xb = (int64_t)n * g.Ci * g.Hi * g.Wi;
       const int r0 = ho * g.sh - g.ph, c0 = wo * g.sw - g.pw;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < EB; ++e) {
         float v2 = 0.f;
         if (kok && taps[e].kind == 1) {
           const int hi = r0 + taps[e].kh, wi = c0 + taps[e].kw;
@@ -224,21 +229,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) As[buf][ak * SA + am + 16 * e] = ra[e];
+    for (int e = 0; e < EA; ++e) As[buf][(am + 16 * e) * SK + ak] = ra[e];
     if (MODE != BWD_W) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Bs[buf][(bk + 4 * e) * SB + bn] = rb[e];
+      for (int e = 0; e < EB; ++e) Bs[buf][bn * SK + bk + KS * e] = rb[e];
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Bs[buf][ak * SB + (tid >> 4) + 16 * e] = rb[e];
+      for (int e = 0; e < EB; ++e) Bs[buf][((tid >> 4) + 16 * e) * SK + ak] = rb[e];
     }
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) {
     gload(0);
@@ -249,19 +254,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
       if (kt + 1 < nk) gload(kt + 1);
       const float* as = As[cur];
       const float* bs = Bs[cur];
+      // lane (c16, g4) supplies k = 4 g4 + s in MFMA step s: one 16-B read per block
+      f32x4 av[MI], bv[NJ];
 #pragma unroll
-      for (int kk = 0; kk < BK / 4; ++kk) {
-        const int kr = 4 * kk + g4;
-        float av[2], bv[2];
+      for (int i = 0; i < MI; ++i)
+        av[i] = *reinterpret_cast<const f32x4*>(as + (wm * (BM / 2) + i * 16 + c16) * SK + 4 * g4);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) av[i] = as[kr * SA + wm * 32 + i * 16 + c16];
+      for (int j = 0; j < NJ; ++j)
+        bv[j] = *reinterpret_cast<const f32x4*>(bs + (wn * (BN / 2) + j * 16 + c16) * SK + 4 * g4);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bv[j] = bs[kr * SB + wn * 32 + j * 16 + c16];
+      for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-      }
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][s4], bv[j][s4], acc[i][j], 0, 0, 0);
       if (kt + 1 < nk) sstore(cur ^ 1);
       __syncthreads();
     }
@@ -269,35 +276,35 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
 
   // epilogue: lane holds rows 4 g4 + r of column c16 of each 16 x 16 block
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int ng = n0 + wn * 32 + j * 16 + c16;
+  for (int j = 0; j < NJ; ++j) {
+    const int ng = n0 + wn * (BN / 2) + j * 16 + c16;
     if (ng >= g.Ncol) continue;
     if (MODE == BWD_W) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int mg = m0 + wm * 32 + i * 16 + 4 * g4 + r;
+          const int mg = m0 + wm * (BM / 2) + i * 16 + 4 * g4 + r;
           if (mg < g.M) out[((int64_t)blockIdx.z * g.M + mg) * g.Ncol + ng] = acc[i][j][r];
         }
     } else if (MODE == FWD) {
       const int HW = g.Ho * g.Wo;
       const int n = (int)g.dHoWo.div((unsigned)ng), q = ng - n * HW;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int mg = m0 + wm * 32 + i * 16 + 4 * g4 + r;
+          const int mg = m0 + wm * (BM / 2) + i * 16 + 4 * g4 + r;
           if (mg < g.M) out[((int64_t)n * g.M + mg) * HW + q] = acc[i][j][r] + (bias ? bias[mg] : 0.f);
         }
     } else {
       if (ng >= ph.Ncol) continue;
       const int64_t o0 = dx_offset(g, ph, ng, 0), cs = (int64_t)g.Hi * g.Wi;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int mg = m0 + wm * 32 + i * 16 + 4 * g4 + r;
+          const int mg = m0 + wm * (BM / 2) + i * 16 + 4 * g4 + r;
           if (mg < g.M) out[o0 + mg * cs] = acc[i][j][r];
         }
     }
@@ -326,8 +333,36 @@ bool make_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int K
   return true;
 }
 
+// 128 x 128 tiles where the GEMM has the rows and enough column tiles to fill the chip
+// (two workgroups per CU); 64 x 64 otherwise.  BWD_W (split over K) only needs the extents.
+#ifndef CONV_BIG_MIN_TILES
+#define CONV_BIG_MIN_TILES 512
+#endif
+#ifndef CONV_BIG
+#define CONV_BIG 1
+#endif
+bool big_tiles(int mode, int M, int Ncol) {
+  if (!CONV_BIG || M < 128 || Ncol < 128) return false;
+  return mode == BWD_W || (int64_t)cdiv(M, 128) * cdiv(Ncol, 128) >= CONV_BIG_MIN_TILES;
+}
+
+template <int MODE>
+void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
+                  float* out, const ConvArgs& g, hipStream_t st) {
+  if (big_tiles(MODE, M, Ncol)) {
+    g3.x = cdiv(Ncol, 128);
+    g3.y = cdiv(M, 128);
+    conv_igemm_kernel<MODE, 128, 128><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
+  } else {
+    g3.x = cdiv(Ncol, 64);
+    g3.y = cdiv(M, 64);
+    conv_igemm_kernel<MODE, 64, 64><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
+  }
+}
+
 int wgrad_splits(const ConvArgs& g) {
-  const int64_t tiles = (int64_t)cdiv(g.M, BM) * cdiv(g.Ncol, BN);
+  const int T = big_tiles(BWD_W, g.M, g.Ncol) ? 128 : 64;
+  const int64_t tiles = (int64_t)cdiv(g.M, T) * cdiv(g.Ncol, T);
   const int64_t ksteps = cdiv(g.K, BK);
   int64_t s = cdiv(2048, tiles);                 // aim at >= 2048 workgroups
   const int64_t maxs = cdiv(ksteps, 8);          // but >= 8 K-steps per split
@@ -347,8 +382,7 @@ BLINDNO_API int blindno_conv2d_fwd(const float* x, const float* w, const float* 
   g.M = Co;
   g.Ncol = N * g.Ho * g.Wo;
   g.K = Ci * KH * KW;
-  const dim3 grid(cdiv(g.Ncol, BN), cdiv(g.M, BM), 1);
-  conv_igemm_kernel<FWD><<<grid, 256, 0, (hipStream_t)stream>>>(w, x, b, y, g);
+  launch_igemm<FWD>(dim3(1, 1, 1), g.M, g.Ncol, w, x, b, y, g, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
 
@@ -395,8 +429,7 @@ BLINDNO_API int blindno_conv2d_bwd_data(const float* dy, const float* w, float* 
     const hipError_t e = hipMemsetAsync(dx, 0, sizeof(float) * (size_t)N * Ci * Hi * Wi, st);
     if (e != hipSuccess) return (int)e;
   }
-  const dim3 grid(cdiv(maxcol, BN), cdiv(g.M, BM), sh * sw);
-  conv_igemm_kernel<BWD_D><<<grid, 256, 0, st>>>(w, dy, nullptr, dx, g);
+  launch_igemm<BWD_D>(dim3(1, 1, sh * sw), g.M, maxcol, w, dy, nullptr, dx, g, st);
   return (int)hipGetLastError();
 }
 
@@ -424,9 +457,8 @@ BLINDNO_API int blindno_conv2d_bwd_weight(const float* dy, const float* x, float
   g.kchunk = cdiv(cdiv(g.K, nsplit), BK) * BK;
   const int nz = cdiv(g.K, g.kchunk);
   if ((int64_t)g.M * g.Ncol >= INT32_MAX / (nz > 0 ? nz : 1)) return (int)hipErrorInvalidValue;
-  const dim3 grid(cdiv(g.Ncol, BN), cdiv(g.M, BM), nz);
   hipStream_t st = (hipStream_t)stream;
-  conv_igemm_kernel<BWD_W><<<grid, 256, 0, st>>>(dy, x, nullptr, nz > 1 ? partial : dwb, g);
+  launch_igemm<BWD_W>(dim3(1, 1, nz), g.M, g.Ncol, dy, x, nullptr, nz > 1 ? partial : dwb, g, st);
   if (nz > 1) {
     const int e = (int)hipGetLastError();
     if (e) return e;

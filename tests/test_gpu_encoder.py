@@ -92,6 +92,10 @@ CONV_CASES = [
     (3, 64, 61, 31, 128, 3, 3, 2, 2, 1, 1),
     (11, 256, 1, 20, 256, 1, 5, 1, 1, 0, 1),
     (3, 5, 13, 11, 7, 3, 2, 3, 2, 2, 1),
+    # large enough for the 128 x 128 tiles (>= 512 tiles; csrc/conv.hip big_tiles) in the
+    # forward and the input gradient, with a ragged last tile
+    (66, 128, 64, 32, 128, 3, 3, 1, 1, 1, 1),
+    (40, 128, 64, 32, 256, 3, 3, 2, 2, 1, 1),
 ]
 
 
