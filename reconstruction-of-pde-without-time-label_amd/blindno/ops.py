@@ -1291,6 +1291,16 @@ def time_averaged_relative_l2(pt_pred, pt_ref, eps=1e-12):
 
 # ---------------------------------------------------------------------------- NIO encoder blocks
 
+def k_conv2d_bwd_data(dy, weight, g):
+    """Input gradient of a conv2d with geometry g = (N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw):
+    K split (partial slabs reduced in order) where the input pixels are too few to fill the chip."""
+    dx = torch.empty(g[0], g[1], g[2], g[3], dtype=F32, device=dy.device)
+    ns = query("blindno_conv2d_bwd_data_nsplit", *g)
+    part = _empty(ns, dx.numel(), like=dy) if ns > 1 else None
+    call("blindno_conv2d_bwd_data_split", ptr(dy), ptr(weight), ptr(dx), ptr(part), ns, *g, stream_ptr())
+    return dx
+
+
 class Conv2dFn(torch.autograd.Function):
     """nn.Conv2d (bias, groups 1, zero padding) of the NIO encoders' ConvBlocks
     (2d_FPE/Baselines.py:40-52) on the HIP implicit-GEMM kernels (csrc/conv.hip): x (N, Ci, H, W),
@@ -1308,9 +1318,12 @@ class Conv2dFn(torch.autograd.Function):
         ph, pw = padding
         Ho, Wo = (Hi + 2 * ph - KH) // sh + 1, (Wi + 2 * pw - KW) // sw + 1
         y = _empty(N, Co, Ho, Wo, like=x)
-        call("blindno_conv2d_fwd", ptr(x), ptr(weight), ptr(bias), ptr(y), N, Ci, Hi, Wi, Co, KH, KW,
-             sh, sw, ph, pw, stream_ptr())
-        ctx.geom = (N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)
+        g = (N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)
+        ns = query("blindno_conv2d_fwd_nsplit", *g)      # split K for the few-pixel last blocks
+        part = _empty(ns, y.numel(), like=x) if ns > 1 else None
+        call("blindno_conv2d_fwd_split", ptr(x), ptr(weight), ptr(bias), ptr(y), ptr(part), ns, *g,
+             stream_ptr())
+        ctx.geom = g
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, weight)
         return y
@@ -1323,8 +1336,7 @@ class Conv2dFn(torch.autograd.Function):
         dy = _c(dy)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            call("blindno_conv2d_bwd_data", ptr(dy), ptr(weight), ptr(dx), *g, stream_ptr())
+            dx = k_conv2d_bwd_data(dy, weight, g)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             ncol = Ci * KH * KW + 1
             ns = query("blindno_conv2d_wgrad_nsplit", *g)

@@ -24,7 +24,11 @@ DOMINANT = os.environ.get("BLINDNO_TIMED_KERNEL", "blindno_project_bag_fwd")
 _VARIANTS = {"blindno_project_bwd": ("blindno_project_bwd", "blindno_project_bwd_w"),
              # config D's snapshot CNN: every implicit-GEMM convolution of a step (forward, input
              # gradient, weight gradient; csrc/conv.hip), reported as one family
-             "blindno_conv2d": ("blindno_conv2d_fwd", "blindno_conv2d_bwd_data", "blindno_conv2d_bwd_weight")}
+             # (the split-K forms time the partial sums' reduction with their GEMM)
+             "blindno_conv2d": ("blindno_conv2d_fwd", "blindno_conv2d_bwd_data", "blindno_conv2d_bwd_weight",
+                                "blindno_conv2d_fwd_split", "blindno_conv2d_bwd_data_split")}
+_CONV_ARG0 = {"blindno_conv2d_fwd": 4, "blindno_conv2d_bwd_data": 3, "blindno_conv2d_bwd_weight": 5,
+              "blindno_conv2d_fwd_split": 6, "blindno_conv2d_bwd_data_split": 5}
 # families whose roofline aggregates every launch (sum of flops / sum of time)
 _FAMILIES = ("blindno_conv2d",)
 
@@ -84,8 +88,8 @@ def cost(name, args):
         B, U, C, P1, P2, Ho, Wo, Hd = (_i(args, k) for k in range(8, 16))
         pts, bpts = B * U * Ho * Wo, B * Ho * Wo
         return 8 * pts * C + 4 * ((bpts + 15) // 16) * 16 * Hd * 6 + 4 * bpts, 2 * bpts * Hd * 6
-    if name in ("blindno_conv2d_fwd", "blindno_conv2d_bwd_data", "blindno_conv2d_bwd_weight"):
-        o = {"blindno_conv2d_fwd": 4, "blindno_conv2d_bwd_data": 3, "blindno_conv2d_bwd_weight": 5}[name]
+    if name in _CONV_ARG0:
+        o = _CONV_ARG0[name]
         N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw = (_i(args, k) for k in range(o, o + 11))
         Ho, Wo = _conv_out(Hi, KH, sh, ph), _conv_out(Wi, KW, sw, pw)
         K = Ci * KH * KW + (1 if name == "blindno_conv2d_bwd_weight" else 0)   # + the bias column

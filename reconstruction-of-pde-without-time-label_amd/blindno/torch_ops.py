@@ -388,8 +388,7 @@ def conv2d_backward(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: 
     Co, _, KH, KW = w.shape
     g = (N, Ci, Hi, Wi, Co, KH, KW, stride[0], stride[1], padding[0], padding[1])
     dy, x, w = ops._c(dy), ops._c(x), ops._c(w)
-    dx = torch.empty_like(x)
-    call("blindno_conv2d_bwd_data", ptr(dy), ptr(w), ptr(dx), *g, stream_ptr())
+    dx = ops.k_conv2d_bwd_data(dy, w, g)
     ncol = Ci * KH * KW + 1
     ns = query("blindno_conv2d_wgrad_nsplit", *g)
     dwb = ops._empty(Co, ncol, like=dy)

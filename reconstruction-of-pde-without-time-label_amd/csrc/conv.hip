@@ -19,6 +19,10 @@
 // Tiling for CDNA4 wave64: a 256-thread workgroup computes a BM x BN tile (128 x 128 for the
 // large layers, 64 x 64 otherwise) as 2 x 2 waves of (BM/2) x (BN/2) (up to 4 x 4 MFMA blocks
 // per wave, 4 accumulator VGPRs each), K in steps of 16 staged through double-buffered LDS.
+// Where the channel count is a multiple of 16, the forward and the input gradient can order K
+// tap-major (k = tap x C + c: no index divisions in the loop; see launch_igemm for where it is
+// used), and layers whose output pixels leave the chip short of workgroups split K into
+// partial slabs summed in a fixed order (blindno_conv2d_{fwd,bwd_data}_split).
 // The LDS tiles are k-contiguous per row (A[m][k], B[n][k], rows padded to 20 floats) and the
 // MFMA K order is permuted (step s takes k = 4 (lane>>4) + s), so one ds_read_b128 brings a
 // lane's operands of four MFMA steps.  The next step's global loads are issued before the
@@ -34,8 +38,23 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// MFMA shape: v_mfma_f32_16x16x4f32 (4 accumulators per lane).  The 32x32x2 form with the same
+// wave tile measured the same (r03r: 39.1 vs 38.8 ms over the encoder's layers).
+constexpr int MF = 16;
+using Acc = f32x4;
+constexpr int NR = 4;                             // accumulator registers per block
+constexpr int KPL = 4;                            // k per lane in a 16-k chunk
+__device__ __forceinline__ Acc mfma_step(float a, float b, Acc c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// row of accumulator register r in a block for lane group gm
+__device__ __forceinline__ int acc_row(int r, int gm) { return 4 * gm + r; }
+
+// K per step and LDS row stride (floats) of the k-contiguous tiles.  BK = 32 (one barrier per 32
+// k, 2 workgroups per CU) and a conflict-free-read stride of 24 measured slower / the same
+// (r03q); the row stride 20 keeps the B tile's 16-B stores conflict-free.
 constexpr int BK = 16;
-constexpr int SK = BK + 4;                     // LDS row stride (floats) of the k-contiguous tiles
+constexpr int SK = BK + 4;
 
 enum { FWD = 0, BWD_D = 1, BWD_W = 2 };
 
@@ -51,7 +70,9 @@ struct Phase {
 struct ConvArgs {
   int N, Ci, Hi, Wi, Co, Ho, Wo, KH, KW, sh, sw, ph, pw;
   int M, Ncol, K;               // GEMM sizes of this mode
-  int kchunk;                   // BWD_W: K per split (multiple of BK)
+  int kchunk;                   // K per split (multiple of BK; FWD / BWD_D: >= K unless split)
+  int nph;                      // BWD_D: stride-phase classes (blockIdx.z = class + nph split)
+  int64_t slab;                 // FWD / BWD_D split: floats per partial output slab
   FastDiv dKHW, dKW, dHoWo, dWo, dHiWi, dWi;
   Phase phase[kMaxPhases];      // BWD_D
 };
@@ -157,34 +178,37 @@ __device__ __forceinline__ Tap decode_tap(const ConvArgs& g, int ng) {
   return t;
 }
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, bool TM = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict__ pa,
                                                          const float* __restrict__ pb,
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ out, ConvArgs g) {
-  constexpr int EA = BM / 16, EB = BN * BK / 256;  // loads per thread per K step (A, B)
-  constexpr int MI = BM / 32, NJ = BN / 32;        // MFMA blocks per wave
+  constexpr int EA = BM * BK / 256, EB = BN * BK / 256;  // loads per thread per K step (A, B)
+  constexpr int AR = 256 / BK;                     // A rows (BWD_W: B columns) per load round
+  constexpr int MI = BM / 2 / MF, NJ = BN / 2 / MF;  // MFMA blocks per wave
   __shared__ float As[2][BM * SK];
   __shared__ float Bs[2][BN * SK];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uniform_int(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int c16 = lane & 15, g4 = lane >> 4;
+  const int cm = lane % MF, gm = lane / MF;         // block row / column, k group
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const Phase& ph = g.phase[MODE == BWD_D ? blockIdx.z : 0];
+  // blockIdx.z: the K split (FWD, BWD_W), or class + nph x split (BWD_D).  Split FWD / BWD_D
+  // launches write partial output slabs (out + split x slab), reduced afterwards in split order;
+  // a split past a class's K writes its zeros (every slab covers every pixel)
+  const int split = MODE == BWD_D ? (int)blockIdx.z / g.nph : (int)blockIdx.z;
+  const Phase& ph = g.phase[MODE == BWD_D ? (int)blockIdx.z - split * g.nph : 0];
   if (MODE == BWD_D && n0 >= ph.Ncol) return;        // this class has fewer pixels (whole block)
-  int kbeg = 0, kend = MODE == BWD_D ? ph.K : g.K;
-  if (MODE == BWD_W) {
-    kbeg = blockIdx.z * g.kchunk;
-    kend = min(g.K, kbeg + g.kchunk);
-  }
+  const int kbeg = split * g.kchunk;
+  const int kend = min(MODE == BWD_D ? ph.K : g.K, kbeg + g.kchunk);
+  if (MODE != BWD_W) out += split * g.slab;
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   // loader roles.  A: k = tid % 16 (contiguous in memory for all modes), m = tid / 16 + 16 e.
   // B (FWD / BWD_D): pixel n = tid % BN fixed for the tile, k = tid / BN + (256 / BN) e.
   // B (BWD_W): pixel k = tid % 16, column n = tid / 16 + 16 e (fixed taps for the tile).
-  const int ak = tid & 15, am = tid >> 4;
+  const int ak = tid % BK, am = tid / BK;
   const int bn = tid % BN, bk = tid / BN;
   constexpr int KS = 256 / BN;                    // k stride of a thread's B loads
   Pix pix{};
@@ -193,14 +217,81 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
     pix = decode_pix<MODE>(g, ph, n0 + bn);
   } else {
 #pragma unroll
-    for (int e = 0; e < EB; ++e) taps[e] = decode_tap(g, n0 + (tid >> 4) + 16 * e);
+    for (int e = 0; e < EB; ++e) taps[e] = decode_tap(g, n0 + am + AR * e);
+  }
+
+  // Tap-major K order (TM; FWD with Ci % 16 == 0, BWD_D with Co % 16 == 0): k = tap x C + c, so
+  // the 16 k of a K-step share one tap and the channel advances by 16 per step.  The tap and
+  // channel are uniform per step, each thread's A / B offsets are fixed per tile plus a uniform
+  // part, and the only per-element work left is one add (and, for B, the padding select) --
+  // no index divisions in the loop.  A rows past M read a clamped row (their results are never
+  // stored); B columns whose tap falls in the padding read 0.
+  // Offsets are 32-bit byte offsets from the uniform base (tensors < 2^30 floats, checked on the
+  // host), so the loads take the scalar-base + vector-offset form.
+  unsigned aoff[EA];
+  int boff = 0, bstride = 0, tc = 0, t1 = 0, t2 = 0;   // uniform: channel, tap row, tap col
+  bool bok = false;                                    // this step's tap inside the image
+  if constexpr (TM) {
+    const int KHW = g.KH * g.KW;
+    const int C = MODE == FWD ? g.Ci : g.Co;
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int mg = min(m0 + am + AR * e, g.M - 1);
+      aoff[e] = 4u * (unsigned)(MODE == FWD ? mg * g.K + ak * KHW : (ak * g.Ci + mg) * KHW);
+    }
+    const int cs = MODE == FWD ? g.Hi * g.Wi : g.Ho * g.Wo;   // B's channel stride
+    boff = (int)pix.base + bk * EB * cs;             // this thread's EB consecutive channels
+    bstride = cs;
+    const int tap = kbeg / C;
+    tc = kbeg - tap * C;
+    const int ntw = MODE == FWD ? g.KW : ph.nKw;
+    t1 = tap / ntw;
+    t2 = tap - t1 * ntw;
   }
 
   float ra[EA], rb[EB];
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK;
+    if constexpr (TM) {
+      const int KHW = g.KH * g.KW;
+      int hi, wi, u, cu;
+      if (MODE == FWD) {
+        hi = pix.r + t1;
+        wi = pix.c + t2;
+        u = tc * KHW + t1 * g.KW + t2;
+        cu = tc * g.Hi * g.Wi + hi * g.Wi + wi;
+      } else {
+        hi = pix.r - t1;
+        wi = pix.c - t2;
+        u = tc * g.Ci * KHW + (ph.ah + g.sh * t1) * g.KW + ph.aw + g.sw * t2;
+        cu = tc * g.Ho * g.Wo + hi * g.Wo + wi;
+      }
+      const int Hb = MODE == FWD ? g.Hi : g.Ho, Wb = MODE == FWD ? g.Wi : g.Wo;
+      bok = pix.ok && (unsigned)hi < (unsigned)Hb && (unsigned)wi < (unsigned)Wb;
+      const unsigned bo = bok ? 4u * (unsigned)(boff + cu) : 0u;
+      const char* ca = reinterpret_cast<const char*>(pa) + 4u * (unsigned)u;
+      const char* cb = reinterpret_cast<const char*>(pb);
 #pragma unroll
-    for (int e = 0; e < EA; ++e) ra[e] = load_a<MODE>(pa, g, ph, m0 + am + 16 * e, k0 + ak, kend);
+      for (int e = 0; e < EA; ++e) ra[e] = *reinterpret_cast<const float*>(ca + aoff[e]);
+      // the padding select happens at the LDS store (after the MFMAs), not here, so the
+      // loads stay in flight
+#pragma unroll
+      for (int e = 0; e < EB; ++e) rb[e] = *reinterpret_cast<const float*>(cb + (bo + 4u * (unsigned)(e * bstride)));
+      // next step: channel + 16, carrying into the tap
+      const int C = MODE == FWD ? g.Ci : g.Co;
+      const int ntw = MODE == FWD ? g.KW : ph.nKw;
+      tc += BK;
+      if (tc == C) {
+        tc = 0;
+        if (++t2 == ntw) {
+          t2 = 0;
+          ++t1;
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int e = 0; e < EA; ++e) ra[e] = load_a<MODE>(pa, g, ph, m0 + am + AR * e, k0 + ak, kend);
     if (MODE != BWD_W) {
 #pragma unroll
       for (int e = 0; e < EB; ++e) rb[e] = load_b_pix<MODE>(pb, g, ph, pix, k0 + bk + KS * e, kend);
@@ -229,21 +320,33 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][(am + 16 * e) * SK + ak] = ra[e];
-    if (MODE != BWD_W) {
+    for (int e = 0; e < EA; ++e) As[buf][(am + AR * e) * SK + ak] = ra[e];
+    if constexpr (TM) {
+      // k = bk EB + e: 16-B stores of consecutive k; 8 lanes of consecutive rows cover all 32
+      // banks (row stride SK = 20 / 36 floats), so the stores are conflict-free
+#pragma unroll
+      for (int q = 0; q < EB / 4; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = bok ? rb[4 * q + r] : 0.f;
+        *reinterpret_cast<f32x4*>(&Bs[buf][bn * SK + bk * EB + 4 * q]) = v;
+      }
+    } else if (MODE != BWD_W) {
 #pragma unroll
       for (int e = 0; e < EB; ++e) Bs[buf][bn * SK + bk + KS * e] = rb[e];
     } else {
 #pragma unroll
-      for (int e = 0; e < EB; ++e) Bs[buf][((tid >> 4) + 16 * e) * SK + ak] = rb[e];
+      for (int e = 0; e < EB; ++e) Bs[buf][(am + AR * e) * SK + ak] = rb[e];
     }
   };
 
-  f32x4 acc[MI][NJ];
+  Acc acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
 
   if (nk > 0) {
     gload(0);
@@ -254,37 +357,44 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
       if (kt + 1 < nk) gload(kt + 1);
       const float* as = As[cur];
       const float* bs = Bs[cur];
-      // lane (c16, g4) supplies k = 4 g4 + s in MFMA step s: one 16-B read per block
-      f32x4 av[MI], bv[NJ];
+      // lane (cm, gm) supplies k = 16 kq + KPL gm + s in MFMA step s: KPL / 4 16-B reads per
+      // block (the MFMA K order is permuted consistently for A and B)
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
-        av[i] = *reinterpret_cast<const f32x4*>(as + (wm * (BM / 2) + i * 16 + c16) * SK + 4 * g4);
+      for (int kq = 0; kq < BK / 16; ++kq) {
+        f32x4 av[MI][KPL / 4], bv[NJ][KPL / 4];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        bv[j] = *reinterpret_cast<const f32x4*>(bs + (wn * (BN / 2) + j * 16 + c16) * SK + 4 * g4);
+        for (int q = 0; q < KPL / 4; ++q) {
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
+          for (int i = 0; i < MI; ++i)
+            av[i][q] = *reinterpret_cast<const f32x4*>(as + (wm * (BM / 2) + i * MF + cm) * SK + 16 * kq + KPL * gm + 4 * q);
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][s4], bv[j][s4], acc[i][j], 0, 0, 0);
+            bv[j][q] = *reinterpret_cast<const f32x4*>(bs + (wn * (BN / 2) + j * MF + cm) * SK + 16 * kq + KPL * gm + 4 * q);
+        }
+#pragma unroll
+        for (int st = 0; st < KPL; ++st)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              acc[i][j] = mfma_step(av[i][st >> 2][st & 3], bv[j][st >> 2][st & 3], acc[i][j]);
+      }
       if (kt + 1 < nk) sstore(cur ^ 1);
       __syncthreads();
     }
   }
 
-  // epilogue: lane holds rows 4 g4 + r of column c16 of each 16 x 16 block
+  // epilogue: lane holds rows acc_row(r, gm) of column cm of each MF x MF block
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int ng = n0 + wn * (BN / 2) + j * 16 + c16;
+    const int ng = n0 + wn * (BN / 2) + j * MF + cm;
     if (ng >= g.Ncol) continue;
     if (MODE == BWD_W) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int mg = m0 + wm * (BM / 2) + i * 16 + 4 * g4 + r;
+        for (int r = 0; r < NR; ++r) {
+          const int mg = m0 + wm * (BM / 2) + i * MF + acc_row(r, gm);
           if (mg < g.M) out[((int64_t)blockIdx.z * g.M + mg) * g.Ncol + ng] = acc[i][j][r];
         }
     } else if (MODE == FWD) {
@@ -293,9 +403,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int mg = m0 + wm * (BM / 2) + i * 16 + 4 * g4 + r;
-          if (mg < g.M) out[((int64_t)n * g.M + mg) * HW + q] = acc[i][j][r] + (bias ? bias[mg] : 0.f);
+        for (int r = 0; r < NR; ++r) {
+          const int mg = m0 + wm * (BM / 2) + i * MF + acc_row(r, gm);
+          if (mg < g.M) out[((int64_t)n * g.M + mg) * HW + q] = acc[i][j][r] + (bias && split == 0 ? bias[mg] : 0.f);
         }
     } else {
       if (ng >= ph.Ncol) continue;
@@ -303,8 +413,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int mg = m0 + wm * (BM / 2) + i * 16 + 4 * g4 + r;
+        for (int r = 0; r < NR; ++r) {
+          const int mg = m0 + wm * (BM / 2) + i * MF + acc_row(r, gm);
           if (mg < g.M) out[o0 + mg * cs] = acc[i][j][r];
         }
     }
@@ -324,6 +434,8 @@ bool make_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int K
   g.N = N; g.Ci = Ci; g.Hi = Hi; g.Wi = Wi; g.Co = Co; g.Ho = Ho; g.Wo = Wo;
   g.KH = KH; g.KW = KW; g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw;
   g.kchunk = 0;
+  g.nph = 1;
+  g.slab = 0;
   g.dKHW = FastDiv::make((unsigned)(KH * KW));
   g.dKW = FastDiv::make((unsigned)KW);
   g.dHoWo = FastDiv::make((unsigned)(Ho * Wo));
@@ -346,18 +458,59 @@ bool big_tiles(int mode, int M, int Ncol) {
   return mode == BWD_W || (int64_t)cdiv(M, 128) * cdiv(Ncol, 128) >= CONV_BIG_MIN_TILES;
 }
 
-template <int MODE>
-void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
-                  float* out, const ConvArgs& g, hipStream_t st) {
+#ifndef CONV_TM
+#define CONV_TM 1
+#endif
+template <int MODE, bool TM>
+void launch_igemm_t(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
+                    float* out, const ConvArgs& g, hipStream_t st) {
   if (big_tiles(MODE, M, Ncol)) {
     g3.x = cdiv(Ncol, 128);
     g3.y = cdiv(M, 128);
-    conv_igemm_kernel<MODE, 128, 128><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
+    conv_igemm_kernel<MODE, 128, 128, TM><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
   } else {
     g3.x = cdiv(Ncol, 64);
     g3.y = cdiv(M, 64);
-    conv_igemm_kernel<MODE, 64, 64><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
+    conv_igemm_kernel<MODE, 64, 64, TM><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
   }
+}
+
+// the tap-major loaders where the K-step channel blocks are whole (C % 16 == 0)
+template <int MODE>
+void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
+                  float* out, const ConvArgs& g, hipStream_t st) {
+  const int64_t big = (int64_t)1 << 30;   // byte offsets in 32 bits
+  // where it pays (measured, profiles/r03/r03q_kbench_conv_variants.txt): the input gradient
+  // with >= 128 input channels (-10 %), the stride-1 forward on >= 128 output pixels per image
+  // (-3..5 %; on the 8 x 4 outputs of the last blocks the tap-major order revisits each weight
+  // line once per tap, 1.6x slower there, and the stride-2 forwards lose a little)
+  const bool pays = CONV_TM == 2 ||
+                    (MODE == FWD ? g.sh * g.sw == 1 && g.Ho * g.Wo >= 128 : g.Ci >= 128);
+  const bool tm = CONV_TM && pays && MODE != BWD_W && (MODE == FWD ? g.Ci : g.Co) % BK == 0 &&
+                  (int64_t)g.N * g.Ci * g.Hi * g.Wi < big && (int64_t)g.N * g.Co * g.Ho * g.Wo < big &&
+                  (int64_t)g.Co * g.Ci * g.KH * g.KW < big;
+  if constexpr (MODE != BWD_W) {
+    if (tm) return launch_igemm_t<MODE, true>(g3, M, Ncol, pa, pb, bias, out, g, st);
+  }
+  launch_igemm_t<MODE, false>(g3, M, Ncol, pa, pb, bias, out, g, st);
+}
+
+// FWD / BWD_D: split K when the output tiles leave the chip short of workgroups (the encoder's
+// last layers: a few thousand output pixels, K = 512 x 9).  Aim at >= 1024 workgroups with
+// >= 16 K-steps per split.
+#ifndef CONV_SPLIT
+#define CONV_SPLIT 1
+#endif
+int dk_splits(int mode, int M, int Ncol, int K, int classes) {
+  if (!CONV_SPLIT) return 1;
+  const int T = big_tiles(mode, M, Ncol) ? 128 : 64;
+  const int64_t tiles = (int64_t)cdiv(M, T) * cdiv(Ncol, T) * classes;
+  if (tiles >= 512) return 1;
+  int64_t s = cdiv(1024, tiles);
+  const int64_t maxs = cdiv(K, 16 * BK);
+  if (s > maxs) s = maxs;
+  if (s > 16) s = 16;
+  return (int)(s < 1 ? 1 : s);
 }
 
 int wgrad_splits(const ConvArgs& g) {
@@ -373,34 +526,32 @@ int wgrad_splits(const ConvArgs& g) {
 
 }  // namespace
 
-BLINDNO_API int blindno_conv2d_fwd(const float* x, const float* w, const float* b, float* y, int N,
-                                   int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
-                                   int ph, int pw, void* stream) {
-  ConvArgs g;
-  if (!x || !w || !y || !make_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw))
-    return (int)hipErrorInvalidValue;
+namespace {
+
+bool fwd_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
+              int ph, int pw) {
+  if (!make_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)) return false;
   g.M = Co;
   g.Ncol = N * g.Ho * g.Wo;
   g.K = Ci * KH * KW;
-  launch_igemm<FWD>(dim3(1, 1, 1), g.M, g.Ncol, w, x, b, y, g, (hipStream_t)stream);
-  return (int)hipGetLastError();
+  g.kchunk = cdiv(g.K, BK) * BK;
+  g.slab = (int64_t)N * Co * g.Ho * g.Wo;
+  return true;
 }
 
-BLINDNO_API int blindno_conv2d_bwd_data(const float* dy, const float* w, float* dx, int N, int Ci,
-                                        int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
-                                        int ph, int pw, void* stream) {
-  ConvArgs g;
-  if (!dy || !w || !dx || sh * sw > kMaxPhases ||
-      !make_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw))
-    return (int)hipErrorInvalidValue;
+// stride-phase classes of BWD_D; returns the largest class's pixel count, *uncovered when some
+// pixels' classes have no taps (they receive no gradient: only when the stride exceeds the
+// kernel extent)
+int bwd_data_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh,
+                  int sw, int ph, int pw, bool* uncovered) {
+  if (sh * sw > kMaxPhases || !make_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)) return -1;
   g.M = Ci;
   g.Ncol = N * Hi * Wi;
   g.K = Co * KH * KW;
-  // stride-phase classes; pixels of a class whose taps are all off the kernel (nKh or nKw = 0)
-  // receive no gradient, so they are zeroed first (only possible when the stride exceeds the
-  // kernel extent)
-  int maxcol = 1;
-  bool uncovered = false;
+  g.nph = sh * sw;
+  g.slab = (int64_t)N * Ci * Hi * Wi;
+  int maxcol = 1, maxk = BK;
+  *uncovered = false;
   for (int ah = 0; ah < sh; ++ah)
     for (int aw = 0; aw < sw; ++aw) {
       Phase& p = g.phase[ah * sw + aw];
@@ -416,21 +567,95 @@ BLINDNO_API int blindno_conv2d_bwd_data(const float* dy, const float* w, float* 
       p.ow0 = (p.wi0 + pw - aw) / sw;
       p.Ncol = N * p.Hc * p.Wc;
       p.K = Co * p.nKh * p.nKw;
-      if (p.K == 0 && p.Ncol > 0) uncovered = true;
+      if (p.K == 0 && p.Ncol > 0) *uncovered = true;
       if (p.K == 0) p.Ncol = 0;
       p.dHcWc = FastDiv::make((unsigned)(p.Hc * p.Wc > 0 ? p.Hc * p.Wc : 1));
       p.dWc = FastDiv::make((unsigned)(p.Wc > 0 ? p.Wc : 1));
       p.dKhw = FastDiv::make((unsigned)(p.nKh * p.nKw > 0 ? p.nKh * p.nKw : 1));
       p.dKw = FastDiv::make((unsigned)(p.nKw > 0 ? p.nKw : 1));
       if (p.Ncol > maxcol) maxcol = p.Ncol;
+      if (p.K > maxk) maxk = p.K;
     }
+  g.kchunk = cdiv(maxk, BK) * BK;
+  return maxcol;
+}
+
+// the K range of each of nsplit splits (multiple of BK); the number of splits that remain
+int set_split(ConvArgs& g, int nsplit) {
+  const int kmax = g.kchunk;
+  g.kchunk = cdiv(cdiv(kmax, nsplit), BK) * BK;
+  return cdiv(kmax, g.kchunk);
+}
+
+}  // namespace
+
+BLINDNO_API int blindno_conv2d_fwd_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,
+                                          int sh, int sw, int ph, int pw) {
+  ConvArgs g;
+  if (!fwd_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)) return -1;
+  return dk_splits(FWD, g.M, g.Ncol, g.K, 1);
+}
+
+BLINDNO_API int blindno_conv2d_fwd_split(const float* x, const float* w, const float* b, float* y,
+                                         float* partial, int nsplit, int N, int Ci, int Hi, int Wi,
+                                         int Co, int KH, int KW, int sh, int sw, int ph, int pw,
+                                         void* stream) {
+  ConvArgs g;
+  if (!x || !w || !y || nsplit < 1 || (nsplit > 1 && !partial) ||
+      !fwd_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw))
+    return (int)hipErrorInvalidValue;
+  const int nz = set_split(g, nsplit);
+  if (nz > 1 && g.slab >= INT32_MAX / nz) return (int)hipErrorInvalidValue;
+  launch_igemm<FWD>(dim3(1, 1, nz), g.M, g.Ncol, w, x, b, nz > 1 ? partial : y, g, (hipStream_t)stream);
+  const int e = (int)hipGetLastError();
+  if (e || nz == 1) return e;
+  return blindno_reduce_partials(partial, y, nz, (int)g.slab, stream);
+}
+
+BLINDNO_API int blindno_conv2d_fwd(const float* x, const float* w, const float* b, float* y, int N,
+                                   int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
+                                   int ph, int pw, void* stream) {
+  return blindno_conv2d_fwd_split(x, w, b, y, nullptr, 1, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw,
+                                  stream);
+}
+
+BLINDNO_API int blindno_conv2d_bwd_data_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,
+                                               int sh, int sw, int ph, int pw) {
+  ConvArgs g;
+  bool unc;
+  const int maxcol = bwd_data_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw, &unc);
+  if (maxcol < 0) return -1;
+  return dk_splits(BWD_D, g.M, maxcol, g.kchunk, g.nph);
+}
+
+BLINDNO_API int blindno_conv2d_bwd_data_split(const float* dy, const float* w, float* dx,
+                                              float* partial, int nsplit, int N, int Ci, int Hi,
+                                              int Wi, int Co, int KH, int KW, int sh, int sw, int ph,
+                                              int pw, void* stream) {
+  ConvArgs g;
+  bool uncovered;
+  if (!dy || !w || !dx || nsplit < 1 || (nsplit > 1 && !partial)) return (int)hipErrorInvalidValue;
+  const int maxcol = bwd_data_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw, &uncovered);
+  if (maxcol < 0) return (int)hipErrorInvalidValue;
+  const int nz = set_split(g, nsplit);
+  if (nz > 1 && g.slab >= INT32_MAX / nz) return (int)hipErrorInvalidValue;
+  float* out = nz > 1 ? partial : dx;
   hipStream_t st = (hipStream_t)stream;
   if (uncovered) {
-    const hipError_t e = hipMemsetAsync(dx, 0, sizeof(float) * (size_t)N * Ci * Hi * Wi, st);
+    const hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)g.slab * nz, st);
     if (e != hipSuccess) return (int)e;
   }
-  launch_igemm<BWD_D>(dim3(1, 1, sh * sw), g.M, maxcol, w, dy, nullptr, dx, g, st);
-  return (int)hipGetLastError();
+  launch_igemm<BWD_D>(dim3(1, 1, g.nph * nz), g.M, maxcol, w, dy, nullptr, out, g, st);
+  const int e = (int)hipGetLastError();
+  if (e || nz == 1) return e;
+  return blindno_reduce_partials(partial, dx, nz, (int)g.slab, stream);
+}
+
+BLINDNO_API int blindno_conv2d_bwd_data(const float* dy, const float* w, float* dx, int N, int Ci,
+                                        int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
+                                        int ph, int pw, void* stream) {
+  return blindno_conv2d_bwd_data_split(dy, w, dx, nullptr, 1, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph,
+                                       pw, stream);
 }
 
 BLINDNO_API int blindno_conv2d_wgrad_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,

@@ -123,6 +123,55 @@ def test_conv2d_matches_fp64(case):
     assert torch.equal(y.detach(), y2)
 
 
+SPLIT_CASES = [
+    (9, 512, 4, 2, 512, 4, 2, 1, 1, 0, 0),    # the 1x1-output last block: split by default
+    (9, 512, 4, 2, 512, 3, 3, 2, 2, 1, 1),
+    (3, 5, 13, 11, 7, 3, 2, 3, 2, 2, 1),
+    (4, 6, 9, 10, 5, 1, 1, 3, 2, 0, 0),       # stride > kernel: pixels with no taps (zero dx)
+]
+
+
+@pytest.mark.parametrize("case", SPLIT_CASES)
+def test_conv2d_split_k(case):
+    """blindno_conv2d_{fwd,bwd_data}_split at explicit split counts (1, 2, 3, the default) vs fp64;
+    nsplit = 1 is bit-identical to the unsplit entries."""
+    from blindno import ops
+    from blindno._lib import call, ptr, query, stream_ptr
+    N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw = case
+    torch.manual_seed(sum(case) + 1)
+    x = torch.randn(N, Ci, Hi, Wi, device="cuda", dtype=torch.float64)
+    w = torch.randn(Co, Ci, KH, KW, device="cuda", dtype=torch.float64) / (Ci * KH * KW) ** 0.5
+    b = torch.randn(Co, device="cuda", dtype=torch.float64)
+    y64 = F.conv2d(x, w, b, stride=(sh, sw), padding=(ph, pw))
+    dy64 = torch.randn_like(y64)
+    x64 = x.clone().requires_grad_(True)
+    F.conv2d(x64, w, b, stride=(sh, sw), padding=(ph, pw)).backward(dy64)
+    xs, ws, bs, dys = x.float(), w.float(), b.float(), dy64.float()
+    g = case
+    y1 = torch.empty_like(y64, dtype=torch.float32)
+    call("blindno_conv2d_fwd", ptr(xs), ptr(ws), ptr(bs), ptr(y1), *g, stream_ptr())
+    dx1 = torch.empty_like(xs)
+    call("blindno_conv2d_bwd_data", ptr(dys), ptr(ws), ptr(dx1), *g, stream_ptr())
+    splits = sorted({1, 2, 3, query("blindno_conv2d_fwd_nsplit", *g), query("blindno_conv2d_bwd_data_nsplit", *g)})
+    for ns in splits:
+        y = torch.full_like(y1, float("nan"))
+        part = torch.full((ns, y.numel()), float("nan"), device="cuda")
+        call("blindno_conv2d_fwd_split", ptr(xs), ptr(ws), ptr(bs), ptr(y), ptr(part), ns, *g, stream_ptr())
+        dx = torch.full_like(xs, float("nan"))
+        partd = torch.full((ns, dx.numel()), float("nan"), device="cuda")
+        call("blindno_conv2d_bwd_data_split", ptr(dys), ptr(ws), ptr(dx), ptr(partd), ns, *g, stream_ptr())
+        torch.cuda.synchronize()
+        assert rel_l2(y.cpu().numpy(), y64.cpu().numpy()) <= 1e-5, ns
+        assert rel_l2(dx.cpu().numpy(), x64.grad.cpu().numpy()) <= 1e-5, ns
+        if ns == 1:
+            assert torch.equal(y, y1) and torch.equal(dx, dx1)
+        # deterministic at every split count
+        y2 = torch.empty_like(y)
+        call("blindno_conv2d_fwd_split", ptr(xs), ptr(ws), ptr(bs), ptr(y2), ptr(part), ns, *g, stream_ptr())
+        assert torch.equal(y, y2)
+    print(f"splits {splits}")
+
+
 def _branch_masks(enc):
     """Forward hooks recording each ConvBlock's LeakyReLU branch (output > 0 <=> pre-activation > 0)."""
     masks, hooks = [], []

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-layer timing of config D's snapshot CNN (Encoder2D at 128^2, Bn = 300 snapshots): each
 ConvBlock's convolution forward, input gradient and weight gradient (C ABI, HIP events), with
-the FMA-only TFLOP/s of each launch.  python tools/kbench_conv.py [Bn]"""
+the FMA-only TFLOP/s of each launch.  python tools/kbench_conv.py [Bn] [layer-regex] [mode-regex]"""
+import re
 import os
 import sys
 
@@ -36,11 +37,17 @@ def timeit(fn, iters=5):
 
 def main():
     Bn = int(sys.argv[1]) if len(sys.argv) > 1 else 300
-    blindno.load_library()
+    lpat = sys.argv[2] if len(sys.argv) > 2 else ""
+    mpat = sys.argv[3] if len(sys.argv) > 3 else ""
+    lib = blindno.load_library()
+    split = hasattr(lib, "blindno_conv2d_fwd_split")   # older variant libraries: unsplit entries
     H, W = 128, 128
     tot_t = tot_f = 0.0
     for name, Ci, Co, (KH, KW), (sh, sw), (ph, pw) in LAYERS:
         Ho, Wo = (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+        if lpat and not re.fullmatch(lpat, name):
+            H, W = Ho, Wo
+            continue
         x = torch.randn(Bn, Ci, H, W, device="cuda")
         w = torch.randn(Co, Ci, KH, KW, device="cuda") * 0.05
         b = torch.randn(Co, device="cuda")
@@ -53,10 +60,25 @@ def main():
         part = torch.empty(max(ns, 1), Co * (Ci * KH * KW + 1), device="cuda")
         fl = 2.0 * Bn * Co * Ho * Wo * Ci * KH * KW
         row = [name]
-        for kind, fn in (("fwd", lambda: call("blindno_conv2d_fwd", ptr(x), ptr(w), ptr(b), ptr(y), *g, stream_ptr())),
-                         ("bwd_data", lambda: call("blindno_conv2d_bwd_data", ptr(dy), ptr(w), ptr(dx), *g, stream_ptr())),
+        if name == "cb1":
+            row[0] += " (dx unused in the step)"
+        if split:   # split-K forms with the library's default split counts
+            nf, nd = query("blindno_conv2d_fwd_nsplit", *g), query("blindno_conv2d_bwd_data_nsplit", *g)
+            pf = torch.empty(nf, y.numel(), device="cuda")
+            pd = torch.empty(nd, dx.numel(), device="cuda")
+            fwd = lambda: call("blindno_conv2d_fwd_split", ptr(x), ptr(w), ptr(b), ptr(y), ptr(pf), nf, *g,  # noqa: E731
+                               stream_ptr())
+            bwd = lambda: call("blindno_conv2d_bwd_data_split", ptr(dy), ptr(w), ptr(dx), ptr(pd), nd, *g,  # noqa: E731
+                               stream_ptr())
+            row[0] += f" [{nf},{nd}]"
+        else:
+            fwd = lambda: call("blindno_conv2d_fwd", ptr(x), ptr(w), ptr(b), ptr(y), *g, stream_ptr())  # noqa: E731
+            bwd = lambda: call("blindno_conv2d_bwd_data", ptr(dy), ptr(w), ptr(dx), *g, stream_ptr())  # noqa: E731
+        for kind, fn in (("fwd", fwd), ("bwd_data", bwd),
                          ("bwd_w", lambda: call("blindno_conv2d_bwd_weight", ptr(dy), ptr(x), ptr(dwb), ptr(part), ns, *g,
                                                 stream_ptr()))):
+            if mpat and not re.fullmatch(mpat, kind):
+                continue
             us = timeit(fn)
             tot_t += us
             tot_f += fl
