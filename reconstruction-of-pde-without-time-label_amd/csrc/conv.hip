@@ -249,6 +249,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
     t2 = tap - t1 * ntw;
   }
 
+  // register staging: loads run one K-step ahead of the MFMAs (two steps ahead, with two
+  // register sets, costs the 128 x 128 kernels an occupancy step: 3-8 % slower, r03t)
   float ra[EA], rb[EB];
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK;

@@ -22,6 +22,10 @@ head -30 gpurun_out/step_breakdown_$TAG.txt
 python3 tools/trace_kernel_avg.py gpurun_out/prof_$TAG/run_kernel_trace.csv bagproj_fwd 4 > gpurun_out/dominant_check_$TAG.txt 2>&1 || true
 cat gpurun_out/dominant_check_$TAG.txt
 rm -f gpurun_out/prof_$TAG/run_kernel_trace.csv
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profD_$TAG -o run \
+  -- python3 bench.py --config D --steps 4 --warmup 2 --no-cpu --no-parity > gpurun_out/profD_$TAG.log 2>&1 || { echo "rocprof D failed"; exit 1; }
+rm -f gpurun_out/profD_$TAG/run_kernel_trace.csv
+head -12 gpurun_out/profD_$TAG/run_kernel_stats.csv | cut -c1-160
 bash tools/pmc_kbench.sh $TAG "\[input\]" || exit 1
 python3 tools/pmc_traffic.py gpurun_out/pmck_$TAG > gpurun_out/pmc_traffic_$TAG.json || exit 1
 find gpurun_out/pmck_$TAG -name "*.csv" -size +8M -delete
