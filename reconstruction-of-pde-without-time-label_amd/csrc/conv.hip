@@ -447,17 +447,18 @@ bool make_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int K
   return true;
 }
 
-// 128 x 128 tiles where the GEMM has the rows and enough column tiles to fill the chip
-// (two workgroups per CU); 64 x 64 otherwise.  BWD_W (split over K) only needs the extents.
+// 128 x 128 tiles where the GEMM has the rows and enough column tiles (over all stride-phase
+// classes) to fill the chip -- two workgroups per CU; 64 x 64 otherwise.  BWD_W (split over K)
+// only needs the extents, and so does a forward with >= 4 column tiles, whose K split then
+// fills the chip (dk_splits; the 8 x 4 and 4 x 2 outputs of the last blocks, r03z: -4 / -9 %).
+// The input gradient keeps 64 x 64 rather than split its classes' uneven K (r03z: 1.5x slower).
 #ifndef CONV_BIG_MIN_TILES
 #define CONV_BIG_MIN_TILES 512
 #endif
-#ifndef CONV_BIG
-#define CONV_BIG 1
-#endif
-bool big_tiles(int mode, int M, int Ncol) {
-  if (!CONV_BIG || M < 128 || Ncol < 128) return false;
-  return mode == BWD_W || (int64_t)cdiv(M, 128) * cdiv(Ncol, 128) >= CONV_BIG_MIN_TILES;
+bool big_tiles(int mode, int M, int Ncol, int classes) {
+  if (M < 128 || Ncol < 128) return false;
+  if (mode == BWD_W || (mode == FWD && Ncol >= 512)) return true;
+  return (int64_t)cdiv(M, 128) * cdiv(Ncol, 128) * classes >= CONV_BIG_MIN_TILES;
 }
 
 #ifndef CONV_TM
@@ -466,7 +467,7 @@ bool big_tiles(int mode, int M, int Ncol) {
 template <int MODE, bool TM>
 void launch_igemm_t(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
                     float* out, const ConvArgs& g, hipStream_t st) {
-  if (big_tiles(MODE, M, Ncol)) {
+  if (big_tiles(MODE, M, Ncol, MODE == BWD_D ? g.nph : 1)) {
     g3.x = cdiv(Ncol, 128);
     g3.y = cdiv(M, 128);
     conv_igemm_kernel<MODE, 128, 128, TM><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
@@ -505,7 +506,7 @@ void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, co
 #endif
 int dk_splits(int mode, int M, int Ncol, int K, int classes) {
   if (!CONV_SPLIT) return 1;
-  const int T = big_tiles(mode, M, Ncol) ? 128 : 64;
+  const int T = big_tiles(mode, M, Ncol, classes) ? 128 : 64;
   const int64_t tiles = (int64_t)cdiv(M, T) * cdiv(Ncol, T) * classes;
   if (tiles >= 512) return 1;
   int64_t s = cdiv(1024, tiles);
@@ -516,7 +517,7 @@ int dk_splits(int mode, int M, int Ncol, int K, int classes) {
 }
 
 int wgrad_splits(const ConvArgs& g) {
-  const int T = big_tiles(BWD_W, g.M, g.Ncol) ? 128 : 64;
+  const int T = big_tiles(BWD_W, g.M, g.Ncol, 1) ? 128 : 64;
   const int64_t tiles = (int64_t)cdiv(g.M, T) * cdiv(g.Ncol, T);
   const int64_t ksteps = cdiv(g.K, BK);
   int64_t s = cdiv(2048, tiles);                 // aim at >= 2048 workgroups
