@@ -461,6 +461,14 @@ bool big_tiles(int mode, int M, int Ncol, int classes) {
   return (int64_t)cdiv(M, 128) * cdiv(Ncol, 128) * classes >= CONV_BIG_MIN_TILES;
 }
 
+// 64 x 128 tiles for the input gradients with 64 input channels and many columns (the second
+// block's, r03zb: 1.85 -> 1.40 ms with the tap-major order; the first block's forward, memory-
+// bound, gains nothing)
+bool wide_tiles(int mode, int M, int Ncol, int classes) {
+  if (mode != BWD_D || M > 64 || M < 48) return false;
+  return (int64_t)cdiv(Ncol, 128) * classes >= CONV_BIG_MIN_TILES;
+}
+
 #ifndef CONV_TM
 #define CONV_TM 1
 #endif
@@ -471,6 +479,10 @@ void launch_igemm_t(dim3 g3, int M, int Ncol, const float* pa, const float* pb, 
     g3.x = cdiv(Ncol, 128);
     g3.y = cdiv(M, 128);
     conv_igemm_kernel<MODE, 128, 128, TM><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
+  } else if (wide_tiles(MODE, M, Ncol, MODE == BWD_D ? g.nph : 1)) {
+    g3.x = cdiv(Ncol, 128);
+    g3.y = cdiv(M, 64);
+    conv_igemm_kernel<MODE, 64, 128, TM><<<g3, 256, 0, st>>>(pa, pb, bias, out, g);
   } else {
     g3.x = cdiv(Ncol, 64);
     g3.y = cdiv(M, 64);
@@ -483,12 +495,12 @@ template <int MODE>
 void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
                   float* out, const ConvArgs& g, hipStream_t st) {
   const int64_t big = (int64_t)1 << 30;   // byte offsets in 32 bits
-  // where it pays (measured, profiles/r03/r03q_kbench_conv_variants.txt): the input gradient
-  // with >= 128 input channels (-10 %), the stride-1 forward on >= 128 output pixels per image
+  // where it pays (measured, profiles/r03/r03q_kbench_conv_variants.txt, r03zb): the input
+  // gradient with >= 64 input channels (-10 %; -24 % at 64 with the 64 x 128 tiles), the stride-1 forward on >= 128 output pixels per image
   // (-3..5 %; on the 8 x 4 outputs of the last blocks the tap-major order revisits each weight
   // line once per tap, 1.6x slower there, and the stride-2 forwards lose a little)
   const bool pays = CONV_TM == 2 ||
-                    (MODE == FWD ? g.sh * g.sw == 1 && g.Ho * g.Wo >= 128 : g.Ci >= 128);
+                    (MODE == FWD ? g.sh * g.sw == 1 && g.Ho * g.Wo >= 128 : g.Ci >= 64);
   const bool tm = CONV_TM && pays && MODE != BWD_W && (MODE == FWD ? g.Ci : g.Co) % BK == 0 &&
                   (int64_t)g.N * g.Ci * g.Hi * g.Wi < big && (int64_t)g.N * g.Co * g.Ho * g.Wo < big &&
                   (int64_t)g.Co * g.Ci * g.KH * g.KW < big;
@@ -506,8 +518,9 @@ void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, co
 #endif
 int dk_splits(int mode, int M, int Ncol, int K, int classes) {
   if (!CONV_SPLIT) return 1;
-  const int T = big_tiles(mode, M, Ncol, classes) ? 128 : 64;
-  const int64_t tiles = (int64_t)cdiv(M, T) * cdiv(Ncol, T) * classes;
+  const bool big = big_tiles(mode, M, Ncol, classes);
+  const int TM_ = big ? 128 : 64, TN = big || wide_tiles(mode, M, Ncol, classes) ? 128 : 64;
+  const int64_t tiles = (int64_t)cdiv(M, TM_) * cdiv(Ncol, TN) * classes;
   if (tiles >= 512) return 1;
   int64_t s = cdiv(1024, tiles);
   const int64_t maxs = cdiv(K, 16 * BK);

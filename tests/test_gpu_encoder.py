@@ -96,6 +96,10 @@ CONV_CASES = [
     # forward and the input gradient, with a ragged last tile
     (66, 128, 64, 32, 128, 3, 3, 1, 1, 1, 1),
     (40, 128, 64, 32, 256, 3, 3, 2, 2, 1, 1),
+    # 64 x 128 tiles (64-row GEMMs with >= 512 column tiles): the first block's forward and the
+    # second block's input gradient
+    (12, 1, 128, 128, 64, 1, 7, 1, 2, 0, 3),
+    (9, 64, 128, 64, 128, 3, 3, 2, 2, 1, 1),
 ]
 
 
