@@ -480,22 +480,28 @@ int blindno_conv2d_wgrad_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, i
 int blindno_conv2d_bwd_weight(const float* dy, const float* x, float* dwb, float* partial,
                               int nsplit, int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,
                               int sh, int sw, int ph, int pw, blindno_stream_t stream);
-/* Split-K forms of fwd / bwd_data for layers whose output leaves the chip short of workgroups
- * (the encoder's last blocks: a few thousand output pixels against K = 512 x 9): K is cut into
- * nsplit ranges whose partial outputs (partial: nsplit * |y| or nsplit * |dx| floats) are
- * summed in split order (deterministic).  nsplit from the *_nsplit queries (1: no scratch, the
- * same result as the unsplit entries; any other nsplit >= 1 is valid too). */
+/* Split-K / re-laid-out-weight forms of fwd / bwd_data.  K is cut into nsplit ranges whose
+ * partial outputs (partial: nsplit * |y| or nsplit * |dx| floats) are summed in split order
+ * (deterministic) -- for the layers whose output leaves the chip short of workgroups (the
+ * encoder's last blocks); nsplit from the *_nsplit queries (1: no partial scratch, the same
+ * result as the plain entries; any nsplit >= 1 is valid).  wscratch (may be NULL):
+ * blindno_conv2d_wscratch_floats(mode 0 = fwd | 1 = bwd_data, ...) floats, where the weights
+ * are re-laid out tap-major first so the GEMM's weight loads are contiguous (0 floats: not
+ * used for this layer).  The result does not depend on wscratch. */
 int blindno_conv2d_fwd_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh,
                               int sw, int ph, int pw);
-int blindno_conv2d_fwd_split(const float* x, const float* w, const float* b, float* y,
-                             float* partial, int nsplit, int N, int Ci, int Hi, int Wi, int Co,
-                             int KH, int KW, int sh, int sw, int ph, int pw,
-                             blindno_stream_t stream);
 int blindno_conv2d_bwd_data_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh,
                                    int sw, int ph, int pw);
+int blindno_conv2d_wscratch_floats(int mode, int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,
+                                   int sh, int sw, int ph, int pw);
+int blindno_conv2d_fwd_split(const float* x, const float* w, const float* b, float* y,
+                             float* partial, int nsplit, float* wscratch, int N, int Ci, int Hi,
+                             int Wi, int Co, int KH, int KW, int sh, int sw, int ph, int pw,
+                             blindno_stream_t stream);
 int blindno_conv2d_bwd_data_split(const float* dy, const float* w, float* dx, float* partial,
-                                  int nsplit, int N, int Ci, int Hi, int Wi, int Co, int KH,
-                                  int KW, int sh, int sw, int ph, int pw, blindno_stream_t stream);
+                                  int nsplit, float* wscratch, int N, int Ci, int Hi, int Wi,
+                                  int Co, int KH, int KW, int sh, int sw, int ph, int pw,
+                                  blindno_stream_t stream);
 
 /* ---- whole-op spectral convolutions for C / C++ hosts (no Python needed) ---------------
  * SpectralConv2d.forward / backward (2d_FPE/FNOModules.py:156-178: rfft2 -> corner mix with

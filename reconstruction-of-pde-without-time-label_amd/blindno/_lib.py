@@ -94,9 +94,10 @@ SIGNATURES = {
     "blindno_conv2d_wgrad_nsplit": "iiiiiiiiiii",
     "blindno_conv2d_bwd_weight": "pppp" + "i" + "iiiiiiiiiii" + "s",
     "blindno_conv2d_fwd_nsplit": "iiiiiiiiiii",
-    "blindno_conv2d_fwd_split": "ppppp" + "i" + "iiiiiiiiiii" + "s",
+    "blindno_conv2d_fwd_split": "ppppp" + "i" + "p" + "iiiiiiiiiii" + "s",
     "blindno_conv2d_bwd_data_nsplit": "iiiiiiiiiii",
-    "blindno_conv2d_bwd_data_split": "pppp" + "i" + "iiiiiiiiiii" + "s",
+    "blindno_conv2d_bwd_data_split": "pppp" + "i" + "p" + "iiiiiiiiiii" + "s",
+    "blindno_conv2d_wscratch_floats": "i" + "iiiiiiiiiii",
     # whole-op spectral convolutions (C hosts); int64_t byte queries
     "blindno_spectral2d_tables_bytes": "iiii",
     "blindno_spectral2d_tables_init": "piiii",

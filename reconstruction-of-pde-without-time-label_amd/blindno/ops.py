@@ -1297,8 +1297,15 @@ def k_conv2d_bwd_data(dy, weight, g):
     dx = torch.empty(g[0], g[1], g[2], g[3], dtype=F32, device=dy.device)
     ns = query("blindno_conv2d_bwd_data_nsplit", *g)
     part = _empty(ns, dx.numel(), like=dy) if ns > 1 else None
-    call("blindno_conv2d_bwd_data_split", ptr(dy), ptr(weight), ptr(dx), ptr(part), ns, *g, stream_ptr())
+    call("blindno_conv2d_bwd_data_split", ptr(dy), ptr(weight), ptr(dx), ptr(part), ns,
+         ptr(_wscratch(1, g, dy)), *g, stream_ptr())
     return dx
+
+
+def _wscratch(mode, g, like):
+    """Scratch for the tap-major weight re-layout of a conv2d launch (None where unused)."""
+    n = query("blindno_conv2d_wscratch_floats", mode, *g)
+    return _empty(n, like=like) if n > 0 else None
 
 
 class Conv2dFn(torch.autograd.Function):
@@ -1321,8 +1328,8 @@ class Conv2dFn(torch.autograd.Function):
         g = (N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)
         ns = query("blindno_conv2d_fwd_nsplit", *g)      # split K for the few-pixel last blocks
         part = _empty(ns, y.numel(), like=x) if ns > 1 else None
-        call("blindno_conv2d_fwd_split", ptr(x), ptr(weight), ptr(bias), ptr(y), ptr(part), ns, *g,
-             stream_ptr())
+        call("blindno_conv2d_fwd_split", ptr(x), ptr(weight), ptr(bias), ptr(y), ptr(part), ns,
+             ptr(_wscratch(0, g, x)), *g, stream_ptr())
         ctx.geom = g
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, weight)

@@ -28,7 +28,7 @@ _VARIANTS = {"blindno_project_bwd": ("blindno_project_bwd", "blindno_project_bwd
              "blindno_conv2d": ("blindno_conv2d_fwd", "blindno_conv2d_bwd_data", "blindno_conv2d_bwd_weight",
                                 "blindno_conv2d_fwd_split", "blindno_conv2d_bwd_data_split")}
 _CONV_ARG0 = {"blindno_conv2d_fwd": 4, "blindno_conv2d_bwd_data": 3, "blindno_conv2d_bwd_weight": 5,
-              "blindno_conv2d_fwd_split": 6, "blindno_conv2d_bwd_data_split": 5}
+              "blindno_conv2d_fwd_split": 7, "blindno_conv2d_bwd_data_split": 6}
 # families whose roofline aggregates every launch (sum of flops / sum of time)
 _FAMILIES = ("blindno_conv2d",)
 

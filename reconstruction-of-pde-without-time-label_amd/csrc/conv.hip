@@ -73,6 +73,7 @@ struct ConvArgs {
   int kchunk;                   // K per split (multiple of BK; FWD / BWD_D: >= K unless split)
   int nph;                      // BWD_D: stride-phase classes (blockIdx.z = class + nph split)
   int64_t slab;                 // FWD / BWD_D split: floats per partial output slab
+  int wt;                       // BWD_D tap-major: the weights come as Wt[tap][ci][co]
   FastDiv dKHW, dKW, dHoWo, dWo, dHiWi, dWi;
   Phase phase[kMaxPhases];      // BWD_D
 };
@@ -237,7 +238,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
       const int mg = min(m0 + am + AR * e, g.M - 1);
-      aoff[e] = 4u * (unsigned)(MODE == FWD ? mg * g.K + ak * KHW : (ak * g.Ci + mg) * KHW);
+      // g.wt: the weights were re-laid out tap-major (FWD Wf[co][tap][ci], BWD_D
+      // Wt[tap][ci][co]), so a row's 16 k of a step are 64 contiguous bytes
+      aoff[e] = 4u * (unsigned)(MODE == FWD ? (g.wt ? mg * g.K + ak : mg * g.K + ak * KHW)
+                                : (g.wt ? mg * g.Co + ak : (ak * g.Ci + mg) * KHW));
     }
     const int cs = MODE == FWD ? g.Hi * g.Wi : g.Ho * g.Wo;   // B's channel stride
     boff = (int)pix.base + bk * EB * cs;             // this thread's EB consecutive channels
@@ -260,12 +264,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
       if (MODE == FWD) {
         hi = pix.r + t1;
         wi = pix.c + t2;
-        u = tc * KHW + t1 * g.KW + t2;
+        u = g.wt ? (t1 * g.KW + t2) * g.Ci + tc : tc * KHW + t1 * g.KW + t2;
         cu = tc * g.Hi * g.Wi + hi * g.Wi + wi;
       } else {
         hi = pix.r - t1;
         wi = pix.c - t2;
-        u = tc * g.Ci * KHW + (ph.ah + g.sh * t1) * g.KW + ph.aw + g.sw * t2;
+        const int tap = (ph.ah + g.sh * t1) * g.KW + ph.aw + g.sw * t2;
+        u = g.wt ? tap * g.Ci * g.Co + tc : tc * g.Ci * KHW + tap;
         cu = tc * g.Ho * g.Wo + hi * g.Wo + wi;
       }
       const int Hb = MODE == FWD ? g.Hi : g.Ho, Wb = MODE == FWD ? g.Wi : g.Wo;
@@ -423,6 +428,32 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   }
 }
 
+// Tap-major weight layouts of the A operand (one pass over the weights, <= 9.4 MB):
+//   FWD   W[co][ci][tap] -> Wf[co][tap][ci]   (k = tap Ci + ci contiguous per output channel)
+//   BWD_D W[co][ci][tap] -> Wt[tap][ci][co]   (k = co contiguous per (tap, input channel))
+// Without them the tap-major loaders read 16 k of a step at a stride of KH KW (forward) or
+// Ci KH KW (input gradient) floats, a cache line per lane: the input gradient ran 71 -> 101
+// TFLOP/s with the re-layout (r03zd).
+template <int MODE>
+__global__ void weight_relayout_kernel(const float* __restrict__ w, float* __restrict__ wt, int Co,
+                                       int Ci, int KHW) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;     // output index
+  if (i >= Co * Ci * KHW) return;
+  int co, ci, tap;
+  if (MODE == FWD) {
+    ci = i % Ci;
+    const int r = i / Ci;
+    tap = r % KHW;
+    co = r / KHW;
+  } else {
+    co = i % Co;
+    const int r = i / Co;
+    ci = r % Ci;
+    tap = r / Ci;
+  }
+  wt[i] = w[((int64_t)co * Ci + ci) * KHW + tap];
+}
+
 bool make_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
                int ph, int pw) {
   if (N < 1 || Ci < 1 || Hi < 1 || Wi < 1 || Co < 1 || KH < 1 || KW < 1 || sh < 1 || sw < 1 ||
@@ -438,6 +469,7 @@ bool make_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int K
   g.kchunk = 0;
   g.nph = 1;
   g.slab = 0;
+  g.wt = 0;
   g.dKHW = FastDiv::make((unsigned)(KH * KW));
   g.dKW = FastDiv::make((unsigned)KW);
   g.dHoWo = FastDiv::make((unsigned)(Ho * Wo));
@@ -490,24 +522,39 @@ void launch_igemm_t(dim3 g3, int M, int Ncol, const float* pa, const float* pb, 
   }
 }
 
-// the tap-major loaders where the K-step channel blocks are whole (C % 16 == 0)
+// the tap-major loaders where the K-step channel blocks are whole (C % 16 == 0) and the tensors'
+// byte offsets fit 32 bits
+bool use_tm(int mode, const ConvArgs& g) {
+  const int64_t big = (int64_t)1 << 30;
+  // where it pays (measured, profiles/r03/r03ze_conv_weight_relayout_ab.txt): with the weights
+  // re-laid out, every input gradient and every forward with >= 16 output pixels per image (the
+  // 4 x 2 and 1 x 1 outputs of the last blocks keep the channel-major order: -8 / -16 % there)
+  const bool pays = CONV_TM == 2 || mode == BWD_D || g.Ho * g.Wo >= 16;
+  return CONV_TM && pays && mode != BWD_W && (mode == FWD ? g.Ci : g.Co) % BK == 0 &&
+         (int64_t)g.N * g.Ci * g.Hi * g.Wi < big && (int64_t)g.N * g.Co * g.Ho * g.Wo < big &&
+         (int64_t)g.Co * g.Ci * g.KH * g.KW < big;
+}
+
 template <int MODE>
 void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
                   float* out, const ConvArgs& g, hipStream_t st) {
-  const int64_t big = (int64_t)1 << 30;   // byte offsets in 32 bits
-  // where it pays (measured, profiles/r03/r03q_kbench_conv_variants.txt, r03zb): the input
-  // gradient with >= 64 input channels (-10 %; -24 % at 64 with the 64 x 128 tiles), the stride-1 forward on >= 128 output pixels per image
-  // (-3..5 %; on the 8 x 4 outputs of the last blocks the tap-major order revisits each weight
-  // line once per tap, 1.6x slower there, and the stride-2 forwards lose a little)
-  const bool pays = CONV_TM == 2 ||
-                    (MODE == FWD ? g.sh * g.sw == 1 && g.Ho * g.Wo >= 128 : g.Ci >= 64);
-  const bool tm = CONV_TM && pays && MODE != BWD_W && (MODE == FWD ? g.Ci : g.Co) % BK == 0 &&
-                  (int64_t)g.N * g.Ci * g.Hi * g.Wi < big && (int64_t)g.N * g.Co * g.Ho * g.Wo < big &&
-                  (int64_t)g.Co * g.Ci * g.KH * g.KW < big;
   if constexpr (MODE != BWD_W) {
-    if (tm) return launch_igemm_t<MODE, true>(g3, M, Ncol, pa, pb, bias, out, g, st);
+    if (use_tm(MODE, g)) return launch_igemm_t<MODE, true>(g3, M, Ncol, pa, pb, bias, out, g, st);
   }
   launch_igemm_t<MODE, false>(g3, M, Ncol, pa, pb, bias, out, g, st);
+}
+
+// the weights in the tap-major layout of `mode` into wscratch (when given and the launch uses
+// the tap-major loaders): returns the A operand to use
+template <int MODE>
+const float* relayout_weights(const float* w, float* wscratch, ConvArgs& g, hipStream_t st) {
+  g.wt = 0;
+  if (!wscratch || !use_tm(MODE, g)) return w;
+  const int KHW = g.KH * g.KW;
+  const int total = g.Co * g.Ci * KHW;
+  weight_relayout_kernel<MODE><<<cdiv(total, 256), 256, 0, st>>>(w, wscratch, g.Co, g.Ci, KHW);
+  g.wt = 1;
+  return wscratch;
 }
 
 // FWD / BWD_D: split K when the output tiles leave the chip short of workgroups (the encoder's
@@ -612,17 +659,33 @@ BLINDNO_API int blindno_conv2d_fwd_nsplit(int N, int Ci, int Hi, int Wi, int Co,
   return dk_splits(FWD, g.M, g.Ncol, g.K, 1);
 }
 
+BLINDNO_API int blindno_conv2d_wscratch_floats(int mode, int N, int Ci, int Hi, int Wi, int Co,
+                                               int KH, int KW, int sh, int sw, int ph, int pw) {
+  ConvArgs g;
+  bool unc;
+  if (mode == FWD) {
+    if (!fwd_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)) return -1;
+  } else if (mode == BWD_D) {
+    if (bwd_data_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw, &unc) < 0) return -1;
+  } else {
+    return -1;
+  }
+  return use_tm(mode, g) ? Co * Ci * KH * KW : 0;
+}
+
 BLINDNO_API int blindno_conv2d_fwd_split(const float* x, const float* w, const float* b, float* y,
-                                         float* partial, int nsplit, int N, int Ci, int Hi, int Wi,
-                                         int Co, int KH, int KW, int sh, int sw, int ph, int pw,
-                                         void* stream) {
+                                         float* partial, int nsplit, float* wscratch, int N, int Ci,
+                                         int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
+                                         int ph, int pw, void* stream) {
   ConvArgs g;
   if (!x || !w || !y || nsplit < 1 || (nsplit > 1 && !partial) ||
       !fwd_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw))
     return (int)hipErrorInvalidValue;
   const int nz = set_split(g, nsplit);
   if (nz > 1 && g.slab >= INT32_MAX / nz) return (int)hipErrorInvalidValue;
-  launch_igemm<FWD>(dim3(1, 1, nz), g.M, g.Ncol, w, x, b, nz > 1 ? partial : y, g, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  const float* wa = relayout_weights<FWD>(w, wscratch, g, st);
+  launch_igemm<FWD>(dim3(1, 1, nz), g.M, g.Ncol, wa, x, b, nz > 1 ? partial : y, g, st);
   const int e = (int)hipGetLastError();
   if (e || nz == 1) return e;
   return blindno_reduce_partials(partial, y, nz, (int)g.slab, stream);
@@ -631,8 +694,8 @@ BLINDNO_API int blindno_conv2d_fwd_split(const float* x, const float* w, const f
 BLINDNO_API int blindno_conv2d_fwd(const float* x, const float* w, const float* b, float* y, int N,
                                    int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
                                    int ph, int pw, void* stream) {
-  return blindno_conv2d_fwd_split(x, w, b, y, nullptr, 1, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw,
-                                  stream);
+  return blindno_conv2d_fwd_split(x, w, b, y, nullptr, 1, nullptr, N, Ci, Hi, Wi, Co, KH, KW, sh, sw,
+                                  ph, pw, stream);
 }
 
 BLINDNO_API int blindno_conv2d_bwd_data_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,
@@ -645,9 +708,9 @@ BLINDNO_API int blindno_conv2d_bwd_data_nsplit(int N, int Ci, int Hi, int Wi, in
 }
 
 BLINDNO_API int blindno_conv2d_bwd_data_split(const float* dy, const float* w, float* dx,
-                                              float* partial, int nsplit, int N, int Ci, int Hi,
-                                              int Wi, int Co, int KH, int KW, int sh, int sw, int ph,
-                                              int pw, void* stream) {
+                                              float* partial, int nsplit, float* wscratch, int N,
+                                              int Ci, int Hi, int Wi, int Co, int KH, int KW, int sh,
+                                              int sw, int ph, int pw, void* stream) {
   ConvArgs g;
   bool uncovered;
   if (!dy || !w || !dx || nsplit < 1 || (nsplit > 1 && !partial)) return (int)hipErrorInvalidValue;
@@ -661,7 +724,8 @@ BLINDNO_API int blindno_conv2d_bwd_data_split(const float* dy, const float* w, f
     const hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)g.slab * nz, st);
     if (e != hipSuccess) return (int)e;
   }
-  launch_igemm<BWD_D>(dim3(1, 1, g.nph * nz), g.M, maxcol, w, dy, nullptr, out, g, st);
+  const float* wa = relayout_weights<BWD_D>(w, wscratch, g, st);
+  launch_igemm<BWD_D>(dim3(1, 1, g.nph * nz), g.M, maxcol, wa, dy, nullptr, out, g, st);
   const int e = (int)hipGetLastError();
   if (e || nz == 1) return e;
   return blindno_reduce_partials(partial, dx, nz, (int)g.slab, stream);
@@ -670,8 +734,8 @@ BLINDNO_API int blindno_conv2d_bwd_data_split(const float* dy, const float* w, f
 BLINDNO_API int blindno_conv2d_bwd_data(const float* dy, const float* w, float* dx, int N, int Ci,
                                         int Hi, int Wi, int Co, int KH, int KW, int sh, int sw,
                                         int ph, int pw, void* stream) {
-  return blindno_conv2d_bwd_data_split(dy, w, dx, nullptr, 1, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph,
-                                       pw, stream);
+  return blindno_conv2d_bwd_data_split(dy, w, dx, nullptr, 1, nullptr, N, Ci, Hi, Wi, Co, KH, KW, sh,
+                                       sw, ph, pw, stream);
 }
 
 BLINDNO_API int blindno_conv2d_wgrad_nsplit(int N, int Ci, int Hi, int Wi, int Co, int KH, int KW,

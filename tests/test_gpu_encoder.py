@@ -129,6 +129,7 @@ def test_conv2d_matches_fp64(case):
 
 SPLIT_CASES = [
     (9, 512, 4, 2, 512, 4, 2, 1, 1, 0, 0),    # the 1x1-output last block: split by default
+    (5, 128, 64, 32, 128, 3, 3, 1, 1, 1, 1),   # tap-major with the weight re-layout (both modes)
     (9, 512, 4, 2, 512, 3, 3, 2, 2, 1, 1),
     (3, 5, 13, 11, 7, 3, 2, 3, 2, 2, 1),
     (4, 6, 9, 10, 5, 1, 1, 3, 2, 0, 0),       # stride > kernel: pixels with no taps (zero dx)
@@ -157,23 +158,33 @@ def test_conv2d_split_k(case):
     dx1 = torch.empty_like(xs)
     call("blindno_conv2d_bwd_data", ptr(dys), ptr(ws), ptr(dx1), *g, stream_ptr())
     splits = sorted({1, 2, 3, query("blindno_conv2d_fwd_nsplit", *g), query("blindno_conv2d_bwd_data_nsplit", *g)})
+    nwf, nwd = (query("blindno_conv2d_wscratch_floats", m, *g) for m in (0, 1))
+    wsf = torch.full((max(1, nwf),), float("nan"), device="cuda")
+    wsd = torch.full((max(1, nwd),), float("nan"), device="cuda")
     for ns in splits:
-        y = torch.full_like(y1, float("nan"))
-        part = torch.full((ns, y.numel()), float("nan"), device="cuda")
-        call("blindno_conv2d_fwd_split", ptr(xs), ptr(ws), ptr(bs), ptr(y), ptr(part), ns, *g, stream_ptr())
-        dx = torch.full_like(xs, float("nan"))
-        partd = torch.full((ns, dx.numel()), float("nan"), device="cuda")
-        call("blindno_conv2d_bwd_data_split", ptr(dys), ptr(ws), ptr(dx), ptr(partd), ns, *g, stream_ptr())
-        torch.cuda.synchronize()
-        assert rel_l2(y.cpu().numpy(), y64.cpu().numpy()) <= 1e-5, ns
-        assert rel_l2(dx.cpu().numpy(), x64.grad.cpu().numpy()) <= 1e-5, ns
-        if ns == 1:
-            assert torch.equal(y, y1) and torch.equal(dx, dx1)
-        # deterministic at every split count
-        y2 = torch.empty_like(y)
-        call("blindno_conv2d_fwd_split", ptr(xs), ptr(ws), ptr(bs), ptr(y2), ptr(part), ns, *g, stream_ptr())
-        assert torch.equal(y, y2)
-    print(f"splits {splits}")
+        for use_ws in (False, True):   # the weight re-layout changes the loads, not the result
+            y = torch.full_like(y1, float("nan"))
+            part = torch.full((ns, y.numel()), float("nan"), device="cuda")
+            call("blindno_conv2d_fwd_split", ptr(xs), ptr(ws), ptr(bs), ptr(y), ptr(part), ns,
+                 ptr(wsf) if use_ws else None, *g, stream_ptr())
+            dx = torch.full_like(xs, float("nan"))
+            partd = torch.full((ns, dx.numel()), float("nan"), device="cuda")
+            call("blindno_conv2d_bwd_data_split", ptr(dys), ptr(ws), ptr(dx), ptr(partd), ns,
+                 ptr(wsd) if use_ws else None, *g, stream_ptr())
+            torch.cuda.synchronize()
+            assert rel_l2(y.cpu().numpy(), y64.cpu().numpy()) <= 1e-5, ns
+            assert rel_l2(dx.cpu().numpy(), x64.grad.cpu().numpy()) <= 1e-5, ns
+            if ns == 1 and not use_ws:
+                assert torch.equal(y, y1) and torch.equal(dx, dx1)
+            if use_ws:
+                assert torch.equal(y, y_nows) and torch.equal(dx, dx_nows), ns
+            y_nows, dx_nows = y, dx
+            # deterministic at every split count
+            y2 = torch.empty_like(y)
+            call("blindno_conv2d_fwd_split", ptr(xs), ptr(ws), ptr(bs), ptr(y2), ptr(part), ns,
+                 ptr(wsf) if use_ws else None, *g, stream_ptr())
+            assert torch.equal(y, y2)
+    print(f"splits {splits}, weight scratch {nwf} / {nwd} floats")
 
 
 def _branch_masks(enc):

@@ -40,7 +40,7 @@ def main():
     lpat = sys.argv[2] if len(sys.argv) > 2 else ""
     mpat = sys.argv[3] if len(sys.argv) > 3 else ""
     lib = blindno.load_library()
-    split = hasattr(lib, "blindno_conv2d_fwd_split")   # older variant libraries: unsplit entries
+    split = hasattr(lib, "blindno_conv2d_wscratch_floats")   # older libraries: the plain entries
     H, W = 128, 128
     tot_t = tot_f = 0.0
     for name, Ci, Co, (KH, KW), (sh, sw), (ph, pw) in LAYERS:
@@ -66,10 +66,12 @@ def main():
             nf, nd = query("blindno_conv2d_fwd_nsplit", *g), query("blindno_conv2d_bwd_data_nsplit", *g)
             pf = torch.empty(nf, y.numel(), device="cuda")
             pd = torch.empty(nd, dx.numel(), device="cuda")
-            fwd = lambda: call("blindno_conv2d_fwd_split", ptr(x), ptr(w), ptr(b), ptr(y), ptr(pf), nf, *g,  # noqa: E731
-                               stream_ptr())
-            bwd = lambda: call("blindno_conv2d_bwd_data_split", ptr(dy), ptr(w), ptr(dx), ptr(pd), nd, *g,  # noqa: E731
-                               stream_ptr())
+            wsf = torch.empty(max(1, query("blindno_conv2d_wscratch_floats", 0, *g)), device="cuda")
+            wsd = torch.empty(max(1, query("blindno_conv2d_wscratch_floats", 1, *g)), device="cuda")
+            fwd = lambda: call("blindno_conv2d_fwd_split", ptr(x), ptr(w), ptr(b), ptr(y), ptr(pf), nf,  # noqa: E731
+                               ptr(wsf), *g, stream_ptr())
+            bwd = lambda: call("blindno_conv2d_bwd_data_split", ptr(dy), ptr(w), ptr(dx), ptr(pd), nd,  # noqa: E731
+                               ptr(wsd), *g, stream_ptr())
             row[0] += f" [{nf},{nd}]"
         else:
             fwd = lambda: call("blindno_conv2d_fwd", ptr(x), ptr(w), ptr(b), ptr(y), *g, stream_ptr())  # noqa: E731
