@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   unsigned aoff[EA];
   int boff = 0, bstride = 0, tc = 0, t1 = 0, t2 = 0;   // uniform: channel, tap row, tap col
   bool bok = false;                                    // this step's tap inside the image
-  if constexpr (TM) {
+  if constexpr (TM && MODE != BWD_W) {
     const int KHW = g.KH * g.KW;
     const int C = MODE == FWD ? g.Ci : g.Co;
 #pragma unroll
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   float ra[EA], rb[EB];
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK;
-    if constexpr (TM) {
+    if constexpr (TM && MODE != BWD_W) {
       const int KHW = g.KH * g.KW;
       int hi, wi, u, cu;
       if (MODE == FWD) {
@@ -297,8 +297,26 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
       }
       return;
     }
+    if constexpr (TM && MODE == BWD_W) {
+      // vectorised A (dy): thread (row t / 4 + 64 e, pixels 4 (t % 4) .. + 3) -- one 16-B load
+      // per 4 pixels of one plane (HoWo % 4 == 0, the host checks; kend is a multiple of 4)
+      const int kg = k0 + 4 * (tid & 3);
+      const bool kok = kg < kend;
+      const int HoWo = g.Ho * g.Wo;
+      const int v = kok ? kg : 0;
+      const int n = (int)g.dHoWo.div((unsigned)v), q = v - n * HoWo;
 #pragma unroll
-    for (int e = 0; e < EA; ++e) ra[e] = load_a<MODE>(pa, g, ph, m0 + am + AR * e, k0 + ak, kend);
+      for (int e = 0; e < EA / 4; ++e) {
+        const int mg = min(m0 + (tid >> 2) + 64 * e, g.M - 1);
+        const f32x4 a4 = kok ? *reinterpret_cast<const f32x4*>(pa + ((int64_t)n * g.Co + mg) * HoWo + q)
+                             : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ra[4 * e + r] = a4[r];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < EA; ++e) ra[e] = load_a<MODE>(pa, g, ph, m0 + am + AR * e, k0 + ak, kend);
+    }
     if (MODE != BWD_W) {
 #pragma unroll
       for (int e = 0; e < EB; ++e) rb[e] = load_b_pix<MODE>(pb, g, ph, pix, k0 + bk + KS * e, kend);
@@ -327,8 +345,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) As[buf][(am + AR * e) * SK + ak] = ra[e];
-    if constexpr (TM) {
+    for (int e = 0; e < EA; ++e)
+      if constexpr (!(TM && MODE == BWD_W)) As[buf][(am + AR * e) * SK + ak] = ra[e];
+    if constexpr (TM && MODE == BWD_W) {
+#pragma unroll
+      for (int e = 0; e < EA / 4; ++e)
+        *reinterpret_cast<f32x4*>(&As[buf][((tid >> 2) + 64 * e) * SK + 4 * (tid & 3)]) =
+            (f32x4){ra[4 * e], ra[4 * e + 1], ra[4 * e + 2], ra[4 * e + 3]};
+    }
+    if constexpr (TM && MODE != BWD_W) {
       // k = bk EB + e: 16-B stores of consecutive k; 8 lanes of consecutive rows cover all 32
       // banks (row stride SK = 20 / 36 floats), so the stores are conflict-free
 #pragma unroll
@@ -524,13 +549,18 @@ void launch_igemm_t(dim3 g3, int M, int Ncol, const float* pa, const float* pb, 
 
 // the tap-major loaders where the K-step channel blocks are whole (C % 16 == 0) and the tensors'
 // byte offsets fit 32 bits
+#ifndef CONV_VA
+#define CONV_VA 1
+#endif
 bool use_tm(int mode, const ConvArgs& g) {
   const int64_t big = (int64_t)1 << 30;
   // where it pays (measured, profiles/r03/r03ze_conv_weight_relayout_ab.txt): with the weights
   // re-laid out, every input gradient and every forward with >= 16 output pixels per image (the
   // 4 x 2 and 1 x 1 outputs of the last blocks keep the channel-major order: -8 / -16 % there)
   const bool pays = CONV_TM == 2 || mode == BWD_D || g.Ho * g.Wo >= 16;
-  return CONV_TM && pays && mode != BWD_W && (mode == FWD ? g.Ci : g.Co) % BK == 0 &&
+  if (mode == BWD_W)   // vectorised dy loads (16-B aligned planes)
+    return CONV_VA && (g.Ho * g.Wo) % 4 == 0 && (int64_t)g.N * g.Co * g.Ho * g.Wo < big;
+  return CONV_TM && pays && (mode == FWD ? g.Ci : g.Co) % BK == 0 &&
          (int64_t)g.N * g.Ci * g.Hi * g.Wi < big && (int64_t)g.N * g.Co * g.Ho * g.Wo < big &&
          (int64_t)g.Co * g.Ci * g.KH * g.KW < big;
 }
@@ -538,9 +568,7 @@ bool use_tm(int mode, const ConvArgs& g) {
 template <int MODE>
 void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
                   float* out, const ConvArgs& g, hipStream_t st) {
-  if constexpr (MODE != BWD_W) {
-    if (use_tm(MODE, g)) return launch_igemm_t<MODE, true>(g3, M, Ncol, pa, pb, bias, out, g, st);
-  }
+  if (use_tm(MODE, g)) return launch_igemm_t<MODE, true>(g3, M, Ncol, pa, pb, bias, out, g, st);
   launch_igemm_t<MODE, false>(g3, M, Ncol, pa, pb, bias, out, g, st);
 }
 
