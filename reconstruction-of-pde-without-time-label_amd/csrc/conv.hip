@@ -689,6 +689,17 @@ BLINDNO_API int blindno_conv2d_fwd_nsplit(int N, int Ci, int Hi, int Wi, int Co,
   return dk_splits(FWD, g.M, g.Ncol, g.K, 1);
 }
 
+namespace {
+// A convolution whose kernel covers the whole (unpadded) input is a dense layer: its input
+// gradient dX (N, Ci KH KW) = dY (N, Co) W (Co, Ci KH KW) runs as a forward 1x1 convolution of dY
+// with W^T (from the weight scratch) instead of an implicit GEMM whose taps are 1 / (KH KW)
+// inside the image (the 1x1-output last encoder block: 190 -> ~40 us)
+bool full_kernel(int Hi, int Wi, int KH, int KW, int ph, int pw) {
+  return KH == Hi && KW == Wi && ph == 0 && pw == 0 && Hi * Wi > 1;
+}
+
+}  // namespace
+
 BLINDNO_API int blindno_conv2d_wscratch_floats(int mode, int N, int Ci, int Hi, int Wi, int Co,
                                                int KH, int KW, int sh, int sw, int ph, int pw) {
   ConvArgs g;
@@ -697,6 +708,7 @@ BLINDNO_API int blindno_conv2d_wscratch_floats(int mode, int N, int Ci, int Hi, 
     if (!fwd_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw)) return -1;
   } else if (mode == BWD_D) {
     if (bwd_data_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw, &unc) < 0) return -1;
+    if (full_kernel(Hi, Wi, KH, KW, ph, pw)) return Co * Ci * KH * KW;   // W^T
   } else {
     return -1;
   }
@@ -734,6 +746,11 @@ BLINDNO_API int blindno_conv2d_bwd_data_nsplit(int N, int Ci, int Hi, int Wi, in
   bool unc;
   const int maxcol = bwd_data_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw, &unc);
   if (maxcol < 0) return -1;
+  if (full_kernel(Hi, Wi, KH, KW, ph, pw)) {
+    ConvArgs f;
+    if (!fwd_args(f, N, Co, 1, 1, Ci * KH * KW, 1, 1, 1, 1, 0, 0)) return -1;
+    return dk_splits(FWD, f.M, f.Ncol, f.K, 1);
+  }
   return dk_splits(BWD_D, g.M, maxcol, g.kchunk, g.nph);
 }
 
@@ -746,6 +763,21 @@ BLINDNO_API int blindno_conv2d_bwd_data_split(const float* dy, const float* w, f
   if (!dy || !w || !dx || nsplit < 1 || (nsplit > 1 && !partial)) return (int)hipErrorInvalidValue;
   const int maxcol = bwd_data_args(g, N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw, &uncovered);
   if (maxcol < 0) return (int)hipErrorInvalidValue;
+  if (wscratch && full_kernel(Hi, Wi, KH, KW, ph, pw)) {
+    const int K = Ci * KH * KW;
+    ConvArgs f;
+    if (!fwd_args(f, N, Co, 1, 1, K, 1, 1, 1, 1, 0, 0)) return (int)hipErrorInvalidValue;
+    const int nzf = set_split(f, nsplit);
+    if (nzf > 1 && f.slab >= INT32_MAX / nzf) return (int)hipErrorInvalidValue;
+    hipStream_t st = (hipStream_t)stream;
+    // W (Co, K) -> W^T (K, Co): the relayout kernel with one tap and K "input channels"
+    weight_relayout_kernel<BWD_D><<<cdiv(Co * K, 256), 256, 0, st>>>(w, wscratch, Co, K, 1);
+    launch_igemm<FWD>(dim3(1, 1, nzf), f.M, f.Ncol, wscratch, dy, nullptr, nzf > 1 ? partial : dx, f,
+                      st);
+    const int e = (int)hipGetLastError();
+    if (e || nzf == 1) return e;
+    return blindno_reduce_partials(partial, dx, nzf, (int)f.slab, stream);
+  }
   const int nz = set_split(g, nsplit);
   if (nz > 1 && g.slab >= INT32_MAX / nz) return (int)hipErrorInvalidValue;
   float* out = nz > 1 ? partial : dx;
