@@ -340,7 +340,7 @@ def main():
                     rec["source"])
             if a.config in ("C", "E"):
                 res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
-        if world == 1 and a.config in ("A", "B", "C", "E"):
+        if world == 1 and a.config in ("A", "B", "C", "D", "E"):
             # the reference's CPU path on the same weights / inputs: accuracy parity of the
             # benched step (the "rel-L2 drift error" half of BASELINE's metric), then its timing
             if not a.no_parity:
@@ -461,6 +461,8 @@ def parity_check(cfg_name, model, graphed, opt, xb, yb, grid, T, seed=4321, mix=
     and the worst per-tensor gradient rel-L2; also the reference fp32 path's own distance to
     fp64 (its conditioning floor).  Pass: GPU vs fp64 within SURVEY.md 8c (fields 1e-5,
     gradients 1e-4) and GPU vs the reference's fp32 fields within 1e-5."""
+    if cfg_name == "D":
+        return parity_check_nio(model, graphed, opt, xb, yb, grid, T, seed)
     rs = np.random.RandomState(seed)
     L = rs.randint(50, T)
     idx = rs.choice(T, L)
@@ -525,6 +527,92 @@ def parity_check(cfg_name, model, graphed, opt, xb, yb, grid, T, seed=4321, mix=
            "tolerance": {"fields": 1e-5, "grads": 1e-4} if mix == "fp32" else dict(MIX16_TOL, mix="fp16")}
     tf, tg = (1e-5, 1e-4) if mix == "fp32" else (MIX16_TOL["fields"], MIX16_TOL["grads"])
     res["pass"] = bool(gpu64["fwd"] <= tf and gw <= tg and gpu32["fwd"] <= tf)
+    return res
+
+
+def parity_check_nio(model, graphed, opt, xb, yb, grid, T, seed):
+    """Config D's parity leg: the benched NIOFP2D step (a HIP graph per drawn L, train-mode
+    BatchNorm inside it) on one recorded draw vs (1) the reference's fp32 CPU step
+    (oracle.cpu_ref.niofp2d_fft: F.conv2d / F.batch_norm / addmm, its own LeakyReLU branches)
+    and (2) the same step in fp64 on the GPU as the arbiter.  The Encoder2D branch is piecewise
+    linear: a pre-activation within fp32 rounding of 0 may take either LeakyReLU branch in two
+    correct evaluations, so the fp64 arbiter takes the branches the REPLAY took (comparisons
+    captured into a fresh graph of the same step, tests/test_gpu_configs.py::
+    test_config_d_graphed_niofp2d_nc_128) and the count of branches an unconditioned fp64 forward
+    takes differently is reported (bar 1e-5 of all).  Pass: GPU vs fp64 fields 1e-5 and every
+    gradient 1e-4 (conv biases ahead of batch-statistics BatchNorm, whose true gradient is 0,
+    excluded), GPU vs the reference's fp32 fields 1e-5, flips within the bar."""
+    import blindno
+    from oracle import cpu_ref, fno_ref
+    from blindno.train import DataParallel, GraphedBagStep
+    rs = np.random.RandomState(seed)
+    L = rs.randint(50, T)
+    idx = rs.choice(T, L)
+    if graphed is not None:
+        graphed.release()            # the timed region is over: free the graph pool
+    rec = []
+    names = ("convblock1", "convblock2_1", "convblock2_2", "convblock3_1", "convblock3_2", "convblock4_1",
+             "convblock4_2", "convblock7_1", "convblock7_2", "convblock7_3")
+    hooks = [getattr(model.branch, n).register_forward_hook(lambda mod, i, o: rec.append(o.detach() > 0))
+             for n in names]
+    gs = GraphedBagStep(model, blindno.mse_loss, opt, DataParallel(opt), xb, yb, grid)
+    key = gs.replay(idx)
+    torch.cuda.synchronize()
+    for h in hooks:
+        h.remove()
+    masks = rec[-10:]
+    out_gpu, loss_gpu = gs.out[key].clone(), gs.loss[key].clone()
+    pnames = {id(q): k for k, q in model.named_parameters()}
+    grads_gpu = {pnames[id(prm)]: opt.grad[off:off + sz].detach().clone()
+                 for prm, off, sz in zip(opt.params, opt.offsets, opt.sizes)}
+    gs.release()
+    heads = tuple(model._heads)
+    sd = {k: v.detach() for k, v in model.state_dict().items()
+          if v.is_floating_point() and not k.endswith(("running_mean", "running_var"))}
+    p32 = {k: v.cpu().clone().requires_grad_(True) for k, v in sd.items()}
+    out32 = cpu_ref.niofp2d_fft(p32, xb.cpu(), grid.cpu(), idx=list(idx), heads=heads)
+    ((out32 - yb.cpu()) ** 2).mean().backward()
+    p64 = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    own = []
+    with torch.no_grad():
+        fno_ref.encoder2d(fno_ref.sub_params({k: v.detach() for k, v in p64.items()}, "branch"),
+                          xb.double()[:, list(idx)].unsqueeze(2), record=own)
+    flips = sum(int((a != b).sum()) for a, b in zip(masks, own))
+    total = sum(a.numel() for a in masks)
+    del own
+    out64 = cpu_ref.niofp2d_fft(p64, xb.double(), grid.double(), idx=list(idx), heads=heads, branch_masks=masks)
+    loss64 = ((out64 - yb.double()) ** 2).mean()
+    loss64.backward()
+
+    def rel(a, b):
+        a, b = a.double().cpu(), b.double().cpu()
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+    def fields(o, r):
+        return {"fwd": rel(o, r), "Fx": rel(o[..., 0], r[..., 0]), "Fy": rel(o[..., 1], r[..., 1])}
+
+    skip = ("layers.0.bias",)
+    keys = [k for k in grads_gpu if not k.endswith(skip)]
+    gw, gk = max((rel(grads_gpu[k].view(p64[k].shape), p64[k].grad), k) for k in keys)
+    rw, rk = max((rel(p32[k].grad, p64[k].grad), k) for k in keys)
+    gpu64, gpu32, ref64 = fields(out_gpu, out64.detach()), fields(out_gpu, out32.detach()), \
+        fields(out32.detach(), out64.detach())
+    fmt = lambda d: {k: float(f"{v:.3e}") for k, v in d.items()}
+    res = {"bag": {"L": int(L), "distinct": int(len(np.unique(idx))), "graph_key": int(key)},
+           "reference": "the reference's fp32 CPU step (oracle.cpu_ref.niofp2d_fft: F.conv2d, F.batch_norm, "
+                        "addmm, rfft2/irfft2) and the same step in fp64 on the GPU as arbiter (LeakyReLU "
+                        "branches of the replay), same weights / inputs / bag",
+           "drift_rel_l2": float(f"{gpu32['Fx']:.3e}"),
+           "gpu_vs_ref_fp32": fmt(gpu32),
+           "gpu_vs_fp64": dict(fmt(gpu64), grad_max=float(f"{gw:.3e}"), grad_worst=gk,
+                               loss=float(f"{abs(float(loss_gpu) - float(loss64)) / abs(float(loss64)):.3e}")),
+           "ref_fp32_vs_fp64": dict(fmt(ref64), grad_max=float(f"{rw:.3e}"), grad_worst=rk,
+                                    note="the fp32 reference takes its own LeakyReLU branches"),
+           "branch_flips": {"count": int(flips), "of": int(total), "bar": "1e-5 of all"},
+           "grads_excluded": "conv biases ahead of batch-statistics BatchNorm (true gradient 0)",
+           "tolerance": {"fields": 1e-5, "grads": 1e-4}}
+    res["pass"] = bool(gpu64["fwd"] <= 1e-5 and max(gpu64["Fx"], gpu64["Fy"]) <= 1e-5 and gw <= 1e-4
+                       and gpu32["fwd"] <= 1e-5 and flips <= 1e-5 * total)
     return res
 
 

@@ -313,6 +313,24 @@ int blindno_bagmean_fwd_w(const float* u, const float* grid, const float* w, con
 int blindno_bagmean_bwd(const float* dy, const float* w, float* s, int B, int S, int d,
                         int width, int L, blindno_stream_t stream);
 
+/* --- DeepONet combiner fused with the bag mean (NIO models): replaces
+ *     DeepOnetNoBiasOrg.forward, 2d_FPE/DeepONetModules.py:142-151, whose (B, L, S) output the
+ *     bag mean of 2d_FPE/NIOModules.py:66-77 (NC :65-76, 1d_FPE/NIOModules.py:62-77) reads only
+ *     through its mean over the bag ---------------------------------------------------------
+ * w (B, L, P) branch coefficients, basis (S, P) trunk output, b0 (1) device scalar, lw (L)
+ * optional per-snapshot weights (NULL: 1/L).  Forward:
+ *   wbar[b,k] = sum_l lw_l w[b,l,k];  ubar[b,p] = (wbar[b] . basis[p] + b0 sum_l lw_l) * scale
+ * (scale = 1/sqrt(P)); wbar (B, P) is saved for the backward.  Backward from g = dL/dubar
+ * (B, S): dw (B, L, P), dbasis (S, P), db0 (1, NULL: none); partial: nblk * (B P + 1) floats,
+ * nblk = blindno_deeponet_bag_nblk(S).  B <= 64, P <= 64, L <= 1024. */
+int blindno_deeponet_bag_nblk(int S);
+int blindno_deeponet_bag_fwd(const float* w, const float* basis, const float* b0, const float* lw,
+                             float* wbar, float* ubar, int B, int L, int S, int P, float scale,
+                             blindno_stream_t stream);
+int blindno_deeponet_bag_bwd(const float* g, const float* basis, const float* wbar, const float* lw,
+                             float* dw, float* dbasis, float* db0, float* partial, int nblk, int B,
+                             int L, int S, int P, float scale, blindno_stream_t stream);
+
 /* --- token self-attention over the bag (NIOFP2D_FNO_attn, 2d_FPE/NIOModules.py:365-399;
  *     2d_Non_conservative_FPE/NIOModules.py:364-398) ------------------------------------
  * Tokens X[b] = [gx, gy, u_1..u_L] (T = L + 2 <= 256 rows of S points); grid (S, 2)

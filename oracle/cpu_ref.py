@@ -23,7 +23,7 @@ import torch
 from .fno_ref import pad_amount, sub_params
 
 __all__ = ["spectral_conv2d_fft", "spectral_conv1d_fft", "fno2d_fft", "fno1d_fft",
-           "niofp2d_fno_fft", "niofp_fno_fft"]
+           "niofp2d_fno_fft", "niofp_fno_fft", "encoder2d_conv", "niofp2d_fft"]
 
 
 def _gelu(x):
@@ -145,3 +145,59 @@ def niofp_fno_fft(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tenso
     h = _bag_mean(u, gcf, p["fc0.weight"], p["fc0.bias"])
     outs = [fno1d_fft(sub_params(p, hd), h) for hd in heads]
     return torch.cat(outs, dim=-1) if len(outs) > 1 else outs[0]
+
+
+# Encoder2D's ConvBlocks (name, stride, padding), 2d_FPE/Baselines.py:186-249 (the last kernel
+# comes with the weights: grid-adaptive)
+_ENC2D = (("convblock1", (1, 2), (0, 3)), ("convblock2_1", (2, 2), (1, 1)), ("convblock2_2", (1, 1), (1, 1)),
+          ("convblock3_1", (2, 2), (1, 1)), ("convblock3_2", (1, 1), (1, 1)), ("convblock4_1", (2, 2), (1, 1)),
+          ("convblock4_2", (1, 1), (1, 1)), ("convblock7_1", (2, 2), (1, 1)), ("convblock7_2", (2, 2), (1, 1)),
+          ("convblock7_3", (1, 1), (0, 0)))
+
+
+def encoder2d_conv(p: Dict[str, torch.Tensor], x: torch.Tensor,
+                   masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+    """Encoder2D.forward in train mode, 2d_FPE/Baselines.py:203-249, executed as the reference
+    does: ``F.conv2d`` -> ``F.batch_norm`` (batch statistics) -> LeakyReLU(0.2) per ConvBlock
+    (:40-52), then ``linear``.  x (B, L, 1, nx, ny) -> (B, L, n_out).  ``masks``: take each
+    LeakyReLU's branch from the path under test (see ``fno_ref.encoder2d``)."""
+    B, L = x.shape[:2]
+    h = x.reshape(B * L, *x.shape[2:])
+    F = torch.nn.functional
+    for k, (name, stride, pad) in enumerate(_ENC2D):
+        h = F.conv2d(h, p[f"{name}.layers.0.weight"], p[f"{name}.layers.0.bias"], stride=stride, padding=pad)
+        h = F.batch_norm(h, None, None, p[f"{name}.layers.1.weight"], p[f"{name}.layers.1.bias"],
+                         training=True, eps=1e-5)
+        h = F.leaky_relu(h, 0.2) if masks is None else torch.where(masks[k], h, 0.2 * h)
+    return _lin(h.flatten(1).view(B, L, -1), p, "linear")
+
+
+def _ffn(p, x, n_hidden_layers):
+    """FFN.forward, 2d_FPE/DeepONetModules.py:155-185 (leaky_relu 0.01, dropout 0, train-mode
+    BatchNorm1d)."""
+    F = torch.nn.functional
+    h = F.leaky_relu(_lin(x, p, "input_layer"), 0.01)
+    for k in range(n_hidden_layers - 1):
+        h = F.leaky_relu(_lin(h, p, f"hidden_layers.{k}"), 0.01)
+        h = F.batch_norm(h, None, None, p[f"batch_layers.{k}.weight"], p[f"batch_layers.{k}.bias"],
+                         training=True, eps=1e-5)
+    return _lin(h, p, "output_layer")
+
+
+def niofp2d_fft(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
+                idx: Optional[Sequence[int]] = None, n_hidden_layers: int = 3,
+                heads: Sequence[str] = ("fno_drift", "fno_diffusion"),
+                branch_masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+    """NIOFP2D.forward, 2d_FPE/NIOModules.py:47-83 (NC heads fno_Fx/fno_Fy:
+    2d_Non_conservative_FPE/NIOModules.py:46-82): the Encoder2D branch on every drawn snapshot,
+    the FFN trunk on the grid points, DeepOnetNoBiasOrg ``(w @ basis^T + b0) / sqrt(p)``
+    (DeepONetModules.py:142-151), the fixed-weight bag mean, the FNO2d heads."""
+    if idx is not None:
+        x = x[:, torch.as_tensor(list(idx), device=x.device)]
+    B, L, nx, ny = x.shape
+    w = encoder2d_conv(sub_params(p, "branch"), x.unsqueeze(2), branch_masks)
+    basis = _ffn(sub_params(p, "trunk"), grid.reshape(-1, 2), n_hidden_layers)
+    u = ((w @ basis.T + p["deeponet.b0"]) / basis.shape[-1] ** 0.5).view(B, L, nx, ny)
+    gcf = grid.permute(2, 0, 1).unsqueeze(0).expand(B, 2, nx, ny)
+    h = _bag_mean(u, gcf, p["fc0.weight"], p["fc0.bias"])
+    return torch.cat([fno2d_fft(sub_params(p, hd), h) for hd in heads], dim=-1)

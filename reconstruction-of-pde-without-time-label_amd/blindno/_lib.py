@@ -130,6 +130,10 @@ SIGNATURES = {
     "blindno_tok_attn_fwd": "ppppppp" + "iil" + "f" + "s",
     "blindno_tok_attn_bwd_scratch_floats": "ii",
     "blindno_tok_attn_bwd": "pppppppp" + "iil" + "s",
+    # DeepONet combiner + bag mean (csrc/deeponet.hip)
+    "blindno_deeponet_bag_nblk": "i",
+    "blindno_deeponet_bag_fwd": "pppppp" + "iiii" + "f" + "s",
+    "blindno_deeponet_bag_bwd": "pppppppp" + "iiiii" + "f" + "s",
 }
 
 # entry points returning int64_t (byte counts) instead of an error code / int count

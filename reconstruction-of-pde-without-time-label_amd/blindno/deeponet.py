@@ -87,10 +87,32 @@ class _FFNBase(nn.Module):
         self.dropout = nn.Dropout(self.dropout_rate)
 
     def forward(self, x):
+        if self._native_ok(x):
+            return self._forward_native(x)
         x = self.activation(self.input_layer(x))
         for l, b in zip(self.hidden_layers, self.batch_layers):
             x = b(self.activation(self.dropout(l(x))))
         return self.output_layer(x)
+
+    def _native_ok(self, x):
+        return (x.is_cuda and x.dtype == torch.float32 and isinstance(self.activation, nn.LeakyReLU)
+                and (self.dropout.p == 0.0 or not self.training)
+                and all(type(b) is nn.BatchNorm1d for b in self.batch_layers))
+
+    def _forward_native(self, x):
+        """The same layers on libblindno (ops.linear: 1x1-convolution GEMMs; ops.BNActFn with
+        slope 1: BatchNorm1d with batch statistics and running-statistics updates like
+        nn.BatchNorm1d), LeakyReLU as the torch elementwise op: no BLAS library call and no
+        torch reduction, so a step that contains the trunk can be captured in a HIP graph and
+        replayed in any order (tests/test_gpu_graphs.py)."""
+        from . import ops
+        slope = self.activation.negative_slope
+        F = torch.nn.functional
+        x = F.leaky_relu(ops.linear(x, self.input_layer.weight, self.input_layer.bias), slope)
+        for l, b in zip(self.hidden_layers, self.batch_layers):
+            x = F.leaky_relu(ops.linear(x, l.weight, l.bias), slope)
+            x = ops.BNActFn.apply(x, b.weight, b.bias, b, x.shape[0], 1.0)
+        return ops.linear(x, self.output_layer.weight, self.output_layer.bias)
 
 
 class FeedForwardNN(_FFNBase):

@@ -91,7 +91,7 @@ class Encoder2D(nn.Module):
                     self.convblock3_2, self.convblock4_1, self.convblock4_2, self.convblock7_1,
                     self.convblock7_2, self.convblock7_3):
             x = blk(x)
-        return self.linear(x.flatten(1).view(b, L, -1))
+        return ops.linear(x.flatten(1).view(b, L, -1), self.linear.weight, self.linear.bias)
 
 
 class Encoder(nn.Module):
@@ -121,4 +121,4 @@ class Encoder(nn.Module):
             blocks.append(self.final_conv4)
         for blk in blocks:
             x = blk(x)
-        return self.linear(x.reshape(b, L, -1))
+        return ops.linear(x.reshape(b, L, -1), self.linear.weight, self.linear.bias)

@@ -285,11 +285,16 @@ class NIOFP2D(nn.Module):
                                       input_dim=width, output_dim=1))
 
     def forward(self, x, grid, bag_idx=None):
+        """x (B, T, nx, ny), grid (nx, ny, 2) -> (B, nx, ny, 2).  The DeepONet combiner and the
+        bag mean run fused (ops.DeepONetBagFn: the bag mean commutes with w basis^T + b0, so
+        the (B, L, nx ny) field of DeepOnetNoBiasOrg.forward is never formed)."""
         ops.require_device(x, grid)
         x, L, _ = _select(self, x, bag_idx)
         B, _, nx, ny = x.shape
-        u = self.deeponet(x.unsqueeze(2), grid.reshape(-1, 2))     # (B, L, nx*ny)
-        h = _bag_mean_2d(self, u, grid, B, L, nx, ny)
+        w = self.deeponet.branch(x.unsqueeze(2))                   # (B, L, n_basis)
+        basis = self.deeponet.trunk(grid.reshape(-1, 2))           # (nx ny, n_basis)
+        ubar = ops.DeepONetBagFn.apply(w, basis, self.deeponet.b0)
+        h = _bag_mean_2d(self, ubar.view(B, 1, nx * ny), grid, B, 1, nx, ny)
         return _run_heads(self, h)          # the two FNO heads as one grouped launch chain
 
 
@@ -320,8 +325,10 @@ class NIOFP(nn.Module):
         ops.require_device(x, grid)
         x, L, _ = _select(self, x, bag_idx)
         B, _, nx = x.shape
-        u = self.deeponet(x, grid)                                   # (B, L, nx)
-        h = _bag_mean_1d(self, u, grid, B, L, nx)
+        w = self.deeponet.branch(x)                                  # (B, L, n_basis)
+        basis = self.deeponet.trunk(grid)                            # (nx, n_basis)
+        ubar = ops.DeepONetBagFn.apply(w, basis, self.deeponet.b0)  # fused combiner + bag mean
+        h = _bag_mean_1d(self, ubar.view(B, 1, nx), grid, B, 1, nx)
         outs = [getattr(self, n)(h) for n in self._heads]
         return torch.cat(outs, dim=-1) if len(outs) > 1 else outs[0]
 

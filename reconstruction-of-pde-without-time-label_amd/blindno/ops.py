@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import math
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -1165,6 +1166,46 @@ class BagMeanFn(torch.autograd.Function):
         return gu, ggrid, None, None, None
 
 
+class DeepONetBagFn(torch.autograd.Function):
+    """DeepOnetNoBiasOrg (2d_FPE/DeepONetModules.py:142-151) fused with the bag mean that reads
+    its output (2d_FPE/NIOModules.py:66-77): w (B, L, P) branch coefficients, basis (S, P) trunk
+    output, b0 scalar -> ubar (B, S) = mean_l (w_l . basis^T + b0) / sqrt(P), without the
+    (B, L, S) field (csrc/deeponet.hip).  ``lw`` (optional, (L,)): per-snapshot weights."""
+
+    @staticmethod
+    def forward(ctx, w, basis, b0, lw=None):
+        require_device(w, basis, b0)
+        w, basis, b0 = _c(w), _c(basis), _c(b0.reshape(1))
+        B, L, P = w.shape
+        S = basis.shape[0]
+        if basis.shape[1] != P:
+            raise BlindnoError(f"deeponet: branch {tuple(w.shape)} / trunk {tuple(basis.shape)} mismatch")
+        scale = 1.0 / math.sqrt(P)
+        wbar = _empty(B, P, like=w)
+        ubar = _empty(B, S, like=w)
+        call("blindno_deeponet_bag_fwd", ptr(w), ptr(basis), ptr(b0), ptr(lw), ptr(wbar), ptr(ubar),
+             B, L, S, P, scale, stream_ptr())
+        ctx.save_for_backward(basis, wbar)
+        ctx.lw = lw
+        ctx.dims = (B, L, S, P, scale)
+        return ubar
+
+    @staticmethod
+    def backward(ctx, g):
+        basis, wbar = ctx.saved_tensors
+        B, L, S, P, scale = ctx.dims
+        g = _c(g)
+        nblk = query("blindno_deeponet_bag_nblk", S)
+        dw = _empty(B, L, P, like=g)
+        dbasis = _empty(S, P, like=g)
+        db0 = _empty(1, like=g)
+        partial = _empty(nblk * (B * P + 1), like=g)
+        call("blindno_deeponet_bag_bwd", ptr(g), ptr(basis), ptr(wbar), ptr(ctx.lw), ptr(dw), ptr(dbasis),
+             ptr(db0), ptr(partial), nblk, B, L, S, P, scale, stream_ptr())
+        ctx.lw = None
+        return dw, dbasis, db0.reshape(()), None
+
+
 class BagAttnFn(torch.autograd.Function):
     """Token self-attention + fixed-weight fusion of NIOFP2D_FNO_attn
     (2d_FPE/NIOModules.py:365-399): u (B, L, S) encoded snapshots, grid (S, 2) -> (B, S, width).
@@ -1357,6 +1398,18 @@ class Conv2dFn(torch.autograd.Function):
 
 def conv2d(x, weight, bias, stride, padding):
     return Conv2dFn.apply(x, weight, bias, tuple(stride), tuple(padding))
+
+
+def linear(x, weight, bias):
+    """nn.Linear on libblindno: x (..., K) @ weight (N, K)^T + bias as a 1x1 convolution of
+    (rows, K, 1, 1) images (csrc/conv.hip implicit GEMMs: fp32 matrix cores, the bias a GEMM
+    column of the weight gradient, fixed-order split-K) -- no rocBLAS / hipBLASLt and no torch
+    reduction in a captured step.  Used by the NIO branch's final Linear and the FFN trunk
+    (2d_FPE/Baselines.py:202,249; 2d_FPE/DeepONetModules.py:155-185)."""
+    shp = x.shape
+    K, N = shp[-1], weight.shape[0]
+    y = conv2d(x.reshape(-1, K, 1, 1), weight.view(N, K, 1, 1), bias, (1, 1), (0, 0))
+    return y.view(*shp[:-1], N)
 
 
 class BNActFn(torch.autograd.Function):

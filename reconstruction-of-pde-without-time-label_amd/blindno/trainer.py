@@ -73,6 +73,10 @@ class Experiment:
     result_dir: str
     two_channel_metric: bool
     loss_files: Sequence[str] = field(default_factory=lambda: ("train_losses", "test_losses"))
+    # parameters the reference never trains: the FNO-NIO models' unused ``branch`` and their
+    # ``fc0`` read through ``.data``; the NIO models train their branch CNN (2d_FPE/train_nio.py:115,
+    # 1d_FPE/train_nio.py:96: Adam(model.parameters())), so only fc0 is excluded there
+    exclude_prefixes: Sequence[str] = ("branch.", "fc0.")
 
 
 def _experiments(model: str = "fno"):
@@ -92,16 +96,16 @@ def _experiments(model: str = "fno"):
                                               branch_last_kernel=Encoder2D.kernel_for_grid(n))
         return {
             "2d_FPE": Experiment("2d_FPE", 2, data.TrajectoryDataset2D, nio2d(("fno_drift", "fno_diffusion")),
-                                 5e-4, 4, 5, "result_2d_nio", True, all4),
+                                 5e-4, 4, 5, "result_2d_nio", True, all4, ("fc0.",)),
             "2d_Non_conservative_FPE": Experiment(
                 "2d_Non_conservative_FPE", 2, data.TrajectoryDataset2DForce, nio2d(("fno_Fx", "fno_Fy")),
-                5e-4, 4, 5, "result_2d_nio", True, all4),
+                5e-4, 4, 5, "result_2d_nio", True, all4, ("fc0.",)),
             "1d_FPE": Experiment("1d_FPE", 1, data.TrajectoryDataset1D,
                                  lambda n, dev: nio.NIOFP(1, 3, 100, 25, 3, 30, 15, 2, dev), 1e-3, 32, 10,
-                                 "results_nio", True, all4),
+                                 "results_nio", True, all4, ("fc0.",)),
             "1d_GPE": Experiment("1d_GPE", 1, data.ParameterDataset,
                                  lambda n, dev: nio.NIOFP_schrodinger(1, 3, 100, 25, 3, 20, 40, 1, dev), 1e-3,
-                                 32, 10, "results_GPE_nio", False),
+                                 32, 10, "results_GPE_nio", False, exclude_prefixes=("fc0.",)),
         }
     if model == "unet":
         all4 = ("train_losses", "test_losses", "test_losses_drift", "test_losses_diffusion")
@@ -184,7 +188,8 @@ class Trainer:
         np.random.seed(seed + self.rank)
         torch.manual_seed(seed + self.rank)
         self.model = exp.model(n, device).to(device)
-        self.opt = FlatAdam(trained_parameters(self.model), lr=lr or exp.lr)
+        self.opt = FlatAdam(trained_parameters(self.model, exclude_prefixes=exp.exclude_prefixes),
+                            lr=lr or exp.lr)
         self.dp = DataParallel(self.opt)
         self.dp.broadcast_parameters(0)
         world_steps = self.world if scheduler_mode == "reference" else 1

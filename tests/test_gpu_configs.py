@@ -5,7 +5,9 @@ Each test builds the config's model at the reference's own sizes (SURVEY.md sect
 restated"), runs ONE training step on a recorded with-replacement bag draw exactly as
 ``bench.py`` does -- for A, B, C, E: ``train.GraphedBagStep`` (HIP graph per distinct-count
 key, deduplicated bag with multiplicity weights, grouped heads, fused snapshot encoder); for
-D: the eager NIO step -- and compares the step's output and every trained parameter's
+D: ``train.GraphedBagStep`` keyed by the drawn L (no deduplication: the branch's train-mode
+BatchNorm counts the bag's repeats; ``test_config_d_graphed_niofp2d_nc_128``), and the eager
+NIO step beside it -- and compares the step's output and every trained parameter's
 gradient (MSE loss, the reference's criterion) with the float64 oracle (``oracle.fno_ref``)
 evaluated on the same inputs, weights and bag.  The oracle runs in fp64 on the GPU (plain
 torch ops; it shares nothing with the HIP kernels) so the 128^2 / 256^2 cases finish in
@@ -47,13 +49,16 @@ def _oracle_params(model, skip=("branch.",)):
     return out
 
 
-def _check_grads(model, opt, p64, min_count, tol=GRAD_TOL):
-    """Compare the flat gradient buffer the graph filled (``opt.grad``) per parameter tensor."""
+def _check_grads(model, opt, p64, min_count, tol=GRAD_TOL, skip=()):
+    """Compare the flat gradient buffer the graph filled (``opt.grad``) per parameter tensor
+    (names ending in ``skip`` are left out)."""
     names = {id(p): k for k, p in model.named_parameters()}
     n = 0
     worst = 0.0
     for prm, off, sz in zip(opt.params, opt.offsets, opt.sizes):
         k = names[id(prm)]
+        if skip and k.endswith(tuple(skip)):
+            continue
         ref = p64[k].grad
         assert ref is not None, k
         ref = torch.view_as_real(ref) if ref.is_complex() else ref
@@ -227,7 +232,7 @@ def test_config_ab_niofp_fno_1d(cfg):
 def test_config_d_niofp2d_nc_128():
     """Config D: 2d_Non_conservative_FPE NIOFP2D (Encoder2D branch with the grid-adaptive (4,2)
     final kernel, FFN trunk, DeepONet combiner, heads fno_Fx/fno_Fy) at 128^2, B = 2, one
-    recorded draw, eager step as bench.py runs it.
+    recorded draw, eager step (the graphed step bench.py replays: the test below).
 
     The branch is piecewise linear (ten Conv -> BatchNorm -> LeakyReLU blocks): a pre-activation
     within fp32 rounding of 0 can take either branch in two correct evaluations, and one flip
@@ -285,6 +290,88 @@ def test_config_d_niofp2d_nc_128():
         n += 1
     assert n > 60
     print("config D worst grads", sorted(worst)[-5:])
+
+
+def _record_branch_masks(enc, store):
+    """Forward hooks appending each ConvBlock's LeakyReLU branch (output > 0) to ``store``.  Run
+    inside a graph capture, the comparison is a captured kernel: its output tensor is rewritten
+    by every replay of that graph (``store`` keeps the tensors -- and their pool memory -- alive)."""
+    names = ("convblock1", "convblock2_1", "convblock2_2", "convblock3_1", "convblock3_2", "convblock4_1",
+             "convblock4_2", "convblock7_1", "convblock7_2", "convblock7_3")
+    return [getattr(enc, n).register_forward_hook(lambda mod, i, o: store.append(o.detach() > 0))
+            for n in names]
+
+
+@pytest.mark.parametrize("B", [2])
+def test_config_d_graphed_niofp2d_nc_128(B):
+    """Config D as bench.py times it: the NIOFP2D training step replayed from a HIP graph per
+    drawn L (train.GraphedBagStep; BatchNorm in train mode inside the graph, the buffers saved and
+    restored around the capture's warm-up), at 128^2, two recorded draws (two graph keys), output,
+    loss and every trained parameter's gradient (the flat buffer the graph fills) vs the fp64
+    oracle.  The LeakyReLU branches of the fp64 evaluation are those the REPLAY took (recorded by
+    comparisons captured into the graph), with the flip bound of test_config_d_niofp2d_nc_128;
+    SURVEY 8c bars as fixed numbers."""
+    import blindno
+    import oracle
+    from blindno import Encoder2D, NIOFP2D
+    from blindno.train import DataParallel, FlatAdam, GraphedBagStep, trained_parameters
+    heads = ("fno_Fx", "fno_Fy")
+    torch.manual_seed(6)
+    m = NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, heads=heads,
+                branch_last_kernel=Encoder2D.kernel_for_grid(128)).cuda().train()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(B, 100, 128, 128, device="cuda", generator=g)
+    y = torch.randn(B, 128, 128, 2, device="cuda", generator=g)
+    grid = _grid2d(128)
+    opt = FlatAdam(trained_parameters(m, exclude_prefixes=("fc0.",)), lr=5e-4)
+    rec = []
+    hooks = _record_branch_masks(m.branch, rec)
+    gs = GraphedBagStep(m, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+    assert not gs.dedup
+    draws = _draws(100, 13)
+    assert len(draws[0]) != len(draws[1])
+    masks_of = {}
+    for idx in draws:
+        n0 = len(rec)
+        key = gs.replay(idx)
+        assert key == len(idx)
+        if len(rec) > n0:
+            # warm-up (eager) then capture: the last ten are the graph's own mask tensors
+            assert len(rec) - n0 == 20
+            masks_of[key] = rec[-10:]
+    for k in masks_of:
+        assert masks_of[k][0].shape[0] == B * k
+    for idx in draws:
+        key = gs.replay(idx)          # each key replayed again, in the other order
+    for idx in reversed(draws):
+        key = gs.replay(idx)
+        torch.cuda.synchronize()
+        out = gs.out[key].clone()
+        masks = masks_of[key]
+        p = {k: v.detach().double().requires_grad_(True) for k, v in m.state_dict().items()
+             if v.is_floating_point() and not k.endswith(("running_mean", "running_var"))}
+        own = []
+        with torch.no_grad():
+            oracle.fno_ref.encoder2d(oracle.fno_ref.sub_params({k: v.detach() for k, v in p.items()}, "branch"),
+                                     x.double()[:, list(idx)].unsqueeze(2), record=own)
+        flips = sum(int((a != b).sum()) for a, b in zip(masks, own))
+        total = sum(a.numel() for a in masks)
+        print(f"  graphed D L={key}: {flips} of {total} LeakyReLU branches differ from an unconditioned "
+              f"fp64 forward ({flips / total:.2e}, bar 1e-5)")
+        assert flips <= 1e-5 * total, (flips, total)
+        ref = oracle.niofp2d(p, x.double(), grid.double(), idx=idx.tolist(), heads=heads, branch_masks=masks)
+        e_fwd = rel_l2(out.cpu().numpy(), ref.detach().cpu().numpy())
+        e_ch = [rel_l2(out[..., c].cpu().numpy(), ref[..., c].detach().cpu().numpy()) for c in range(2)]
+        print(f"  graphed D L={key}: fwd {e_fwd:.2e}, Fx {e_ch[0]:.2e}, Fy {e_ch[1]:.2e}")
+        assert max([e_fwd] + e_ch) <= FWD_TOL, (e_fwd, e_ch)
+        loss = ((ref - y.double()) ** 2).mean()
+        assert abs(float(gs.loss[key]) - float(loss.detach())) <= FWD_TOL * float(loss.detach())
+        loss.backward()
+        # conv biases ahead of batch-statistics BatchNorm: the true gradient is exactly 0
+        worst = _check_grads(m, opt, p, 60, skip=("layers.0.bias",))
+        print(f"  graphed D L={key}: worst gradient {worst:.2e} (bar {GRAD_TOL})")
+    for h in hooks:
+        h.remove()
 
 
 def test_config_c_after_training_steps():

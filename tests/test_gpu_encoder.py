@@ -247,3 +247,90 @@ def test_encoder2d_matches_fp64():
     for k, b in enc.named_buffers():
         if b.dtype.is_floating_point:
             assert rel_l2(b.cpu().numpy(), b64[k].cpu().numpy()) <= 1e-5, k
+
+
+@pytest.mark.parametrize("M,K,N", [(300, 512, 25), (16384, 2, 100), (16384, 100, 100), (77, 100, 25)])
+def test_linear_matches_fp64(M, K, N):
+    """ops.linear (nn.Linear as a 1x1 convolution on csrc/conv.hip) vs F.linear in fp64: output,
+    input / weight / bias gradients."""
+    from blindno import ops
+    torch.manual_seed(M + K + N)
+    lin = torch.nn.Linear(K, N).cuda()
+    x = torch.randn(M, K, device="cuda", requires_grad=True)
+    y = ops.linear(x, lin.weight, lin.bias)
+    cot = torch.randn_like(y)
+    (y * cot).sum().backward()
+    w64 = lin.weight.detach().double().requires_grad_(True)
+    b64 = lin.bias.detach().double().requires_grad_(True)
+    x64 = x.detach().double().requires_grad_(True)
+    y64 = F.linear(x64, w64, b64)
+    (y64 * cot.double()).sum().backward()
+    assert rel_l2(y.detach().cpu().numpy(), y64.detach().cpu().numpy()) <= 1e-6
+    for got, want in ((x.grad, x64.grad), (lin.weight.grad, w64.grad), (lin.bias.grad, b64.grad)):
+        assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
+
+
+def test_ffn_trunk_native_matches_fp64():
+    """The FFN trunk (2d_FPE/DeepONetModules.py:155-185: Linear -> LeakyReLU(0.01) -> [Linear ->
+    LeakyReLU -> BatchNorm1d (batch statistics)] x 2 -> Linear) on libblindno vs the same module
+    run by torch in fp64: output, every parameter gradient, the input gradient and the running
+    statistics (two steps: they compound)."""
+    import copy
+    from blindno.deeponet import FFN
+    torch.manual_seed(3)
+    f = FFN(2, 25, 3, 100, "leaky_relu", 0.0).cuda().train()
+    ref = copy.deepcopy(f).double()
+    gx, gy = torch.meshgrid(torch.linspace(-1, 1, 128), torch.linspace(-1, 1, 128), indexing="ij")
+    grid = torch.stack([gx, gy], -1).reshape(-1, 2).cuda()
+    for it in range(2):
+        x = grid.clone().requires_grad_(True)
+        assert f._native_ok(x)
+        y = f(x)
+        cot = torch.randn_like(y)
+        f.zero_grad()
+        (y * cot).sum().backward()
+        x64 = grid.double().requires_grad_(True)
+        ref.zero_grad()
+        y64 = ref(x64)
+        (y64 * cot.double()).sum().backward()
+        assert rel_l2(y.detach().cpu().numpy(), y64.detach().cpu().numpy()) <= 1e-5
+        assert rel_l2(x.grad.cpu().numpy(), x64.grad.cpu().numpy()) <= 1e-4
+        p64 = dict(ref.named_parameters())
+        for k, p in f.named_parameters():
+            assert rel_l2(p.grad.cpu().numpy(), p64[k].grad.cpu().numpy()) <= 1e-4, k
+        b64 = dict(ref.named_buffers())
+        for k, b in f.named_buffers():
+            if b.is_floating_point():
+                assert rel_l2(b.cpu().numpy(), b64[k].cpu().numpy()) <= 1e-6, k
+            else:
+                assert int(b) == int(b64[k]) == it + 1, k
+
+
+@pytest.mark.parametrize("B,L,S,weighted", [(4, 75, 16384, False), (2, 51, 80, True), (3, 1, 6400, False)])
+def test_deeponet_bag_matches_fp64(B, L, S, weighted):
+    """ops.DeepONetBagFn (DeepOnetNoBiasOrg + the bag mean that reads it, csrc/deeponet.hip) vs
+    the reference composition in fp64: mean_l ((w basis^T + b0) / sqrt(P)), with 1/L or
+    multiplicity weights; ubar and the gradients of w, basis and b0."""
+    from blindno import ops
+    torch.manual_seed(B * L + S)
+    P = 25
+    w = torch.randn(B, L, P, device="cuda", requires_grad=True)
+    basis = torch.randn(S, P, device="cuda", requires_grad=True)
+    b0 = torch.tensor(0.3, device="cuda", requires_grad=True)
+    lw = None
+    if weighted:
+        c = torch.randint(1, 4, (L,), device="cuda").float()
+        lw = c / c.sum()
+    ubar = ops.DeepONetBagFn.apply(w, basis, b0, lw)
+    cot = torch.randn_like(ubar)
+    (ubar * cot).sum().backward()
+    w64, bs64, b064 = (t.detach().double().requires_grad_(True) for t in (w, basis, b0))
+    u = (w64 @ bs64.T + b064) / P ** 0.5
+    ref = u.mean(1) if lw is None else (u * lw.double().view(1, L, 1)).sum(1)
+    (ref * cot.double()).sum().backward()
+    assert rel_l2(ubar.detach().cpu().numpy(), ref.detach().cpu().numpy()) <= 1e-6
+    for got, want in ((w.grad, w64.grad), (basis.grad, bs64.grad)):
+        assert rel_l2(got.cpu().numpy(), want.cpu().numpy()) <= 1e-6
+    # db0 = sum of B S cotangents / sqrt(P): a cancelling sum, so the bar is relative to its
+    # absolute sum (fp32 accumulation over 1e4-1e5 terms)
+    assert abs(float(b0.grad) - float(b064.grad)) <= 1e-6 * float(cot.double().abs().sum()) / P ** 0.5

@@ -67,6 +67,141 @@ def test_graphed_steps_match_eager(case, overlap):
     assert rel_l2(opt.flat.cpu().numpy(), ropt.flat.cpu().numpy()) <= 1e-6
 
 
+def test_graphed_nio_step_matches_eager():
+    """Config D's benched step (bench.py --config D): NIOFP2D (Encoder2D branch with train-mode
+    BatchNorm and the grid-adaptive (4, 2) last kernel, FFN trunk, DeepONet combiner, heads
+    fno_Fx / fno_Fy) at 128^2, B = 2, replayed from one HIP graph per drawn L (no deduplication:
+    the BatchNorm statistics count the bag's repeats), three draws, against three eager steps.
+    Parameters within 1e-6; BatchNorm running statistics within 1e-6 and num_batches_tracked
+    exactly as the eager steps leave them -- the capture's eager warm-up must not count, and the
+    graph must take each replay's batch statistics, not the captured L's."""
+    import blindno
+    from blindno import Encoder2D, NIOFP2D
+    from blindno.train import DataParallel, FlatAdam, GraphedBagStep, grid2d, trained_parameters
+    B, T, N = 2, 100, 128
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(B, T, N, N, device="cuda", generator=g)
+    y = torch.randn(B, N, N, 2, device="cuda", generator=g)
+    grid = grid2d(N, N, "cuda")
+    rs = np.random.RandomState(5)
+    draws = [rs.choice(T, rs.randint(50, T)) for _ in range(3)]
+    assert len({len(d) for d in draws}) == 3          # three graph keys
+    finals, bufs = [], []
+    for graphed in (False, True):
+        torch.manual_seed(6)
+        m = NIOFP2D(2, 3, 100, 25, 3, 12, 32, 2, heads=("fno_Fx", "fno_Fy"),
+                    branch_last_kernel=Encoder2D.kernel_for_grid(N)).cuda().train()
+        # bench.py config D: everything but fc0 (read through .data) is trained, the branch too
+        params = trained_parameters(m, exclude_prefixes=("fc0.",))
+        assert any(k.startswith("branch.") for k, p in m.named_parameters() if any(p is q for q in params))
+        opt = FlatAdam(params, lr=1e-3)
+        if graphed:
+            gs = GraphedBagStep(m, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+            assert not gs.dedup
+            for idx in draws:
+                gs.step(idx)
+        else:
+            for idx in draws:
+                out = m(x, grid, bag_idx=idx)
+                blindno.mse_loss(out, y).backward()
+                opt.step()
+                opt.zero_grad()
+        torch.cuda.synchronize()
+        finals.append(opt.flat.cpu().numpy().copy())
+        bufs.append({k: b.detach().cpu().clone() for k, b in m.named_buffers()})
+    assert rel_l2(finals[1], finals[0]) <= 1e-6
+    assert bufs[0].keys() == bufs[1].keys() and len(bufs[0]) >= 36      # 10 + 2 BatchNorms x 3
+    for k in bufs[0]:
+        a, b = bufs[1][k], bufs[0][k]
+        if a.is_floating_point():
+            assert rel_l2(a.double().numpy(), b.double().numpy()) <= 1e-6, k
+        else:
+            assert torch.equal(a, b) and int(a) == len(draws), (k, a, b)
+
+
+def _poison_default_pool():
+    """Hand every free block of the caching allocator's default pool (of the sizes a step
+    allocates) to tensors filled with NaN, then free them: a captured graph that still points at
+    default-pool memory it does not own reads NaN afterwards."""
+    torch.cuda.synchronize()
+    blobs = []
+    for mb in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024):
+        for _ in range(8):
+            blobs.append(torch.full((mb << 18,), float("nan"), device="cuda"))
+    for kb in (1, 4, 16, 64, 256):
+        for _ in range(64):
+            blobs.append(torch.full((kb << 8,), float("nan"), device="cuda"))
+    torch.cuda.synchronize()
+    del blobs
+    torch.cuda.synchronize()
+
+
+def _graph_models():
+    import blindno
+    from blindno import Encoder2D, unet
+    torch.manual_seed(3)
+    yield "fno2d", blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, 6, 6, 2), (2, 60, 32, 32), 2
+    torch.manual_seed(4)
+    yield "fno1d", blindno.NIOFP_FNO(3, 30, 15, 2, "cuda"), (4, 80, 64), 2
+    torch.manual_seed(5)
+    yield "nio2d", blindno.NIOFP2D(2, 3, 100, 25, 3, 12, 8, 2, heads=("fno_Fx", "fno_Fy"),
+                                   branch_last_kernel=Encoder2D.kernel_for_grid(64)), (2, 60, 64, 64), 2
+    torch.manual_seed(6)
+    yield "nio1d", blindno.NIOFP(1, 3, 100, 25, 3, 30, 15, 2, "cuda"), (4, 60, 80), 2
+    torch.manual_seed(7)
+    yield "fno2d_attn", blindno.NIOFP2D_FNO_attn(2, 3, 100, 25, 3, 6, 6, 2, 32, 32), (2, 60, 32, 32), 2
+    torch.manual_seed(8)
+    yield "unet2d", unet.PermInvUNet_attn(1, 2, 1, 4, (52, 52)), (2, 60, 52, 52), 2
+
+
+@pytest.mark.parametrize("case", ["fno2d", "fno1d", "nio2d", "nio1d", "fno2d_attn", "unet2d"])
+def test_graph_replays_survive_default_pool_reuse(case):
+    """Every graphed model: two graph keys captured, then the default pool's free blocks are
+    overwritten (NaN) and each key replayed again -- its output and flat gradient must equal an
+    eager step at the same parameters and bag.  A captured graph that reads memory it does not own
+    (a torch op whose capture referenced a default-pool block later freed) fails here; the NIO
+    step did with torch's Linear / matmul reductions in it, before they moved to libblindno."""
+    import blindno
+    from blindno.train import DataParallel, FlatAdam, GraphedBagStep, grid1d, grid2d, trained_parameters
+    name, m, xshape, cout = next(c for c in _graph_models() if c[0] == case)
+    m = m.cuda().train()
+    B, T = xshape[0], xshape[1]
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randn(*xshape, device="cuda", generator=g)
+    y = torch.randn(*((B,) + xshape[2:] + (cout,)), device="cuda", generator=g)
+    grid = grid2d(xshape[2], xshape[3], "cuda") if len(xshape) == 4 else grid1d(xshape[2], "cuda")
+    excl = ("fc0.",) if case.startswith("nio") else ("branch.", "fc0.")
+    opt = FlatAdam(trained_parameters(m, exclude_prefixes=excl), lr=1e-3)
+    gs = GraphedBagStep(m, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+    rs = np.random.RandomState(1)
+    draws = [rs.choice(T, rs.randint(50, T), replace=case != "fno2d_attn") for _ in range(2)]
+
+    def eager(idx):
+        saved = [(b, b.detach().clone()) for b in m.buffers()]
+        opt.zero_grad()
+        out = m(x, grid, bag_idx=idx)
+        blindno.mse_loss(out, y).backward()
+        gg = opt.gather_grads().clone()
+        opt.zero_grad()
+        with torch.no_grad():
+            for b, c in saved:
+                b.copy_(c)
+        return out.detach(), gg
+
+    for idx in draws:
+        gs.replay(idx)
+    _poison_default_pool()
+    for idx in list(draws) + list(reversed(draws)):
+        key = gs.replay(idx)
+        torch.cuda.synchronize()
+        out, grad = gs.out[key].clone(), opt.grad.clone()
+        eo, eg = eager(idx)
+        assert torch.isfinite(grad).all() and torch.isfinite(out).all()
+        assert rel_l2(out.cpu().numpy(), eo.cpu().numpy()) <= 1e-6
+        assert rel_l2(grad.cpu().numpy(), eg.cpu().numpy()) <= 1e-6
+        _poison_default_pool()
+
+
 def test_gather_flat_segments():
     """blindno_gather_flat (FlatAdam's gradient gather): odd offsets, empty and multi-launch
     (> 64 segments) lists, sizes straddling the 2048-element block chunk."""

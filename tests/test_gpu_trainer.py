@@ -106,7 +106,16 @@ def test_trainer_nio_2d(tmp_path):
     assert exp.result_dir == "result_2d_nio" and exp.lr == 5e-4 and exp.batch == 4
     t = trainer.Trainer(exp, data, out, torch.device("cuda"), epochs=2, save_interval=1, log=lambda s: None)
     assert not t.graphed.dedup
+    # the NIO scripts train the branch CNN (2d_FPE/train_nio.py:115: Adam(model.parameters()));
+    # only fc0 (read through .data) stays out of the optimizer
+    names = {id(p): k for k, p in t.model.named_parameters()}
+    trained = {names[id(p)] for p in t.opt.params}
+    assert any(k.startswith("branch.") for k in trained) and not any(k.startswith("fc0.") for k in trained)
+    w0 = t.model.branch.convblock1.layers[0].weight.detach().clone()
+    lin0 = t.model.branch.linear.weight.detach().clone()
     hist = t.fit()
+    assert not torch.equal(w0, t.model.branch.convblock1.layers[0].weight.detach())
+    assert not torch.equal(lin0, t.model.branch.linear.weight.detach())
     assert len(hist["train_losses"]) == 2 and all(np.isfinite(hist["train_losses"]))
     assert all(np.isfinite(hist["test_losses"]))
     for k in ("train_losses", "test_losses", "test_losses_drift", "test_losses_diffusion"):

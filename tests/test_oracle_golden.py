@@ -115,6 +115,33 @@ def test_niofp2d_fno_attn(case, heads):
     _check(g, y, p, {"x": x, "grid": grid})
 
 
+def test_cpu_ref_niofp2d_nc():
+    """cpu_ref.niofp2d_fft (the NIO model as the reference executes it: F.conv2d, F.batch_norm,
+    addmm) on the nio2d_nc_train golden (80^2, Encoder2D branch, FFN trunk, heads Fx/Fy), fp32
+    with the bars of the fp64 oracle's check (BatchNorm over 50 images)."""
+    import json
+    from oracle import cpu_ref
+    g = load_golden("nio2d_nc_train")
+    shapes = [(k, tuple(s)) for k, s in json.loads(str(g["layout_json"]))]
+    st = make_state(shapes, seed=int(g["recipe_seed"]))
+    p = {k: torch.from_numpy(v).float().requires_grad_(v.dtype.kind == "f") for k, v in st.items()}
+    x = torch.from_numpy(g["in.x"]).float()
+    grid = torch.from_numpy(g["in.grid"]).float()
+    y = cpu_ref.niofp2d_fft(p, x, grid, idx=g["idx"].tolist(), heads=("fno_Fx", "fno_Fy"))
+    assert rel_l2(y.detach().numpy(), g["out"]) <= 1e-4
+    (y * torch.from_numpy(g["cot"]).float()).sum().backward()
+    gmax = max(float(v) for k, v in g.items() if k.startswith("gnorm."))
+    n = 0
+    for k, v in g.items():
+        if k.startswith("g."):
+            assert rel_l2(p[k[2:]].grad.numpy(), v) <= 1e-3, k
+            n += 1
+        if k.startswith("gnorm."):
+            got = float(p[k[6:]].grad.norm())
+            assert abs(got - float(v)) <= 1e-3 * abs(float(v)) + 1e-5 * gmax, k
+    assert n > 0
+
+
 @pytest.mark.parametrize("case,heads", [("nio1d_fno_train", ("fno_drift", "fno_diffusion")),
                                         ("nio1d_fno_eval", ("fno_drift", "fno_diffusion")),
                                         ("gpe_nio_fno_train", ("fno_V",))])
