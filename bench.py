@@ -287,7 +287,22 @@ def main():
             rccl = ".".join(str(v) for v in torch.cuda.nccl.version())
         except Exception:  # noqa: BLE001 (gloo rehearsal builds)
             rccl = None
+        # DP replicas must stay identical: compare every rank's parameters with rank 0's
+        ref_flat = opt.flat.clone()
+        dist.broadcast(ref_flat, 0)
+        same = torch.tensor([1 if torch.equal(ref_flat, opt.flat) else 0], device=dev, dtype=torch.int32)
+        maxdiff = (ref_flat - opt.flat).abs().max().reshape(1).double()
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        dist.all_reduce(maxdiff, op=dist.ReduceOp.MAX)
+        del ref_flat
+        ids = torch.tensor([my_ids[0], my_ids[-1], len(my_ids)], device=dev, dtype=torch.int64)
+        all_ids = [torch.zeros_like(ids) for _ in range(world)]
+        dist.all_gather(all_ids, ids)
         dist_info = {
+            "params_identical_across_ranks": bool(int(same) == 1),
+            "params_max_abs_diff_vs_rank0": float(maxdiff),
+            "bag_ids_per_rank": [{"rank": r, "first": int(t[0]), "last": int(t[1]), "count": int(t[2]),
+                                  "rule": "i mod world == rank"} for r, t in enumerate(all_ids)],
             "world_size": dist.get_world_size(), "backend": dist.get_backend(),
             "rccl_version": rccl,
             "per_rank_step_ms": [{"rank": r, "min": round(float(t[0]), 4), "max": round(float(t[1]), 4),
@@ -328,7 +343,10 @@ def main():
         if dist_info is not None:
             res["dist"] = dist_info
         if timer:
+            # the limiter: the bag-level projection is fp32 VALU-issue-bound (PMC valu_issue_util);
+            # the conv family runs on the fp32 matrix cores
             res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS,
+                                             bound="valu" if timer.name == timing.DOMINANT else None,
                                              traffic_per_point=timing.pmc_traffic(ROOT, timing.DOMINANT)
                                              if a.config == "C" else None)
             rec = timing.pmc_record(ROOT, timing.DOMINANT) if a.config == "C" else None
@@ -641,7 +659,13 @@ def cpu_baseline(cfg_name, model, xb, yb, grid, T, budget):
     B = x.shape[0]
     return {"value": round(n * B / el, 4), "unit": "snapshot-bags/s", "cores": threads, "kind": "port",
             "sample": f"{n} train steps x B={B} bags (L={Ls} with replacement, fp32 forward+MSE+backward, "
-                      f"no optimizer) in {el:.1f}s; reference measured 1.29 bags/s on 8 threads (BASELINE.md)"}
+                      f"no optimizer) in {el:.1f}s",
+            # the reference itself cannot travel to the GPU box; its own CPU step was timed in the
+            # build container
+            "reference_measured": {"value": 1.29, "unit": "snapshot-bags/s", "cores": 8,
+                                   "where": "the reference's own CPU step (torch 2.10 CPU, 8 threads) in the "
+                                            "build container, BASELINE.md; the port above runs ~25 % slower "
+                                            "per core"}}
 
 
 if __name__ == "__main__":

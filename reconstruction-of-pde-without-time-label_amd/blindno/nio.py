@@ -321,6 +321,12 @@ class NIOFP(nn.Module):
             setattr(self, name, FNO1d(modes=modes, width=width, n_layers=self.fno_layers,
                                       input_dim=width, output_dim=1, device=self.device))
 
+    @property
+    def unused_prefixes(self):
+        """Parameters that never receive a gradient: the 1d_FPE encoder builds final_conv4 but
+        does not apply it (1d_FPE/Baselines.py:254-287); the reference's Adam skips them."""
+        return () if self.branch.apply_conv4 else ("branch.final_conv4.",)
+
     def forward(self, x, grid, bag_idx=None):
         ops.require_device(x, grid)
         x, L, _ = _select(self, x, bag_idx)

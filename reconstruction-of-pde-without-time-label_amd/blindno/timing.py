@@ -200,10 +200,12 @@ class KernelTimer:
                     "launches": n, "avg_ms": round(ms, 5), "algorithmic_bytes_per_launch": int(bytes_per),
                     **fam}
         note = ("FMA-only flops of the implicit GEMMs (one FMA = 2); fp32 operands on the fp32 matrix "
-                "cores" if self.name in _FAMILIES else
-                "FMA-only flops (one FMA = 2; exact-erf GELU / GELU' evaluation not charged); the kernel "
-                "is fp32 VALU-issue-bound on that GELU work; gfx950 fp32 vector peak = fp32 MFMA peak")
-        return {"kernel": self.name, "bound": "mfma", "achieved": round(tfs, 3), "peak": flop_peak_tflops,
+                "cores (the NIO path's Linear layers run as 1x1 convolutions and are in the family)"
+                if self.name in _FAMILIES else
+                "FMA-only flops (one FMA = 2; exact-erf GELU / GELU' evaluation not charged); the measured "
+                "limiter is fp32 VALU issue on that GELU work (valu_issue_util); gfx950 fp32 vector peak = "
+                "fp32 MFMA peak = 157.3 TFLOP/s")
+        return {"kernel": self.name, "bound": bound, "achieved": round(tfs, 3), "peak": flop_peak_tflops,
                 "unit": "TFLOP/s", "frac": round(tfs / flop_peak_tflops, 4), "traffic": traffic,
                 "launches": n, "avg_ms": round(ms, 5), "algorithmic_flops_per_launch": int(flops_per),
                 "algorithmic_bytes_per_launch": int(bytes_per), "note": note, **fam}

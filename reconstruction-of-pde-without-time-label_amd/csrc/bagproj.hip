@@ -21,9 +21,10 @@
 //     H (16 hid x 16 pts) = W1 (16 hid x C) . Z (C x 16 pts)
 // lane l holds h for hidden units 4 (l >> 4) + r (r < 4) and point l & 15, so the lane's Q
 // update needs only its own point's C channels and v reduces over the 4 lane groups (a
-// reduce-scatter of 3 shuffles) instead of over 16 lanes.  A workgroup owns a 16-point tile;
+// reduce-scatter of 3 lane swaps) instead of over 16 lanes.  A workgroup owns a 16-point tile;
 // its 4 waves split the 128 hidden units (2 tiles each, weights in registers) and walk the
-// bag's snapshots in chunks staged through LDS, where the waves' v partials are also summed.
+// bag's snapshots in double-buffered chunks staged through LDS, where the waves' v partials are
+// also summed.
 #include "common.h"
 #include "blindno.h"
 #include "gelu_pk.h"
@@ -36,7 +37,6 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kHd = 128;            // fc1 = Linear(width, 128)
-constexpr int kSC = 16;             // snapshots per LDS chunk
 constexpr int kNStat = 6;           // A, S, Q_0..Q_3
 constexpr int kTileF4 = (kHd / 16) * kNStat * 64;   // float4 slots per 16-point tile: 3072
 constexpr int kMaxU = 1024;
@@ -56,29 +56,45 @@ struct BagGeom {
   }
 };
 
+// The forward.  Per (snapshot, point, hidden unit) the GELU / GELU' and statistics arithmetic;
+// around it (round 4; round 3's kernel: 340 -> 328 us at config C):
+//   * v's reduce-scatter over the 4 lane groups with v_permlane32_swap / v_permlane16_swap (3
+//     swaps + 3 adds, no LDS round trip, no lane-index arithmetic) instead of ds_bpermute;
+//   * v's 1/2 sum_k (w2 W1)[k] part added once at the store (the accumulation starts with a
+//     multiply), zbar summed by the staging threads, w2 re-read at the statistics write:
+//     no per-snapshot register moves and 20 fewer live VGPRs;
+//   * double-buffered 8-snapshot chunks: one barrier per chunk instead of three per 16.
+constexpr int kSC2 = 8;
+
+__device__ __forceinline__ float swap_sum32(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ float swap_sum16(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ lw,
     float* __restrict__ ubar, float* __restrict__ stats, float* __restrict__ v, BagGeom g) {
   __shared__ float slw[kMaxU];
-  __shared__ float zs[kSC][16][4];            // [snapshot][point][channel]
-  __shared__ float zw[kSC][16][4];            // the same times lw_l (Q's operand)
-  __shared__ float vred[4][kSC][64];          // [wave][snapshot][16 channel + point]
+  __shared__ float zs[2][kSC2][16][4];        // [buffer][snapshot][point][channel]
+  __shared__ float zw[2][kSC2][16][4];        // the same times lw_l (Q's operand)
+  __shared__ float vred[2][4][kSC2][64];      // [buffer][wave][snapshot][16 channel + point]
+  __shared__ float zbr[4][64];                // zbar partials [ls][16 cs + point]
+  __shared__ float vpart[16][4];              // per (wave, g4): 1/2 sum over its 8 hidden of (w2 W1)[k][c]
+  __shared__ float vhalf[4];                  // 1/2 sum_k (w2 W1)[k][c]
   __shared__ float ured[4][16];
-  // the rows of (w2 W1) that form v, per wave and lane group: [wave][g4][tt][i][c] as (r = 2 i,
-  // 2 i + 1) pairs -- read back as broadcasts instead of held in 32 VGPRs per lane (the register
-  // budget of 3 resident waves per SIMD)
   __shared__ float2 swr[4][4][2][2][4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = uniform_int(tid >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
   const int C = (int)g.C, U = (int)g.U;
   for (int l = tid; l < U; l += 256) slw[l] = lw ? lw[l] : 1.0f / (float)U;
-
-  // this wave's hidden tiles t = 2 wave + tt: fc1 A operand (k-scaled), bias rows, the rows of
-  // (w2 * W1) that form v, and w2 for ubar
-  float wa[2], bb[2][4], w2r[2][4];
-  float vinit[4] = {0.f, 0.f, 0.f, 0.f};
+  float wa[2], bb[2][4], vloc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int k0 = 16 * (2 * wave + tt);
@@ -87,23 +103,27 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
     for (int r = 0; r < 4; ++r) {
       const int k = k0 + 4 * g4 + r;
       bb[tt][r] = kK * b1[k];
-      w2r[tt][r] = w2[k];
+      if (c16 == 0) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float wrv = c < C ? w2[k] * w1[k * C + c] : 0.f;
-        // the loop evaluates Phi - 1/2 (no +1/2: one packed add per pair less); the 1/2 parts
-        // are added back here and at the statistics write (below): v gets 1/2 sum_k (w2 W1)[k]
-        vinit[c] += wrv;
-        if (c16 == 0) {
+        for (int c = 0; c < 4; ++c) {
+          const float wrv = c < C ? w2[k] * w1[k * C + c] : 0.f;
+          vloc[c] += wrv;
           float2& e = swr[wave][g4][tt][r >> 1][c];
           if (r & 1) e.y = wrv; else e.x = wrv;
         }
       }
     }
   }
+  if (c16 == 0) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c) vinit[c] *= 0.5f;
+    for (int c = 0; c < 4; ++c) vpart[4 * wave + g4][c] = 0.5f * vloc[c];
+  }
   __syncthreads();
+  if (tid < 4) {
+    float acc = 0.f;
+    for (int j = 0; j < 16; ++j) acc += vpart[j][tid];
+    vhalf[tid] = acc;                          // read after the first chunk's barrier
+  }
   float lsum = 0.f;                            // sum_l lw_l, same order in every thread
   for (int l = 0; l < U; ++l) lsum += slw[l];
   const float b2l = b2[0] * lsum;
@@ -111,13 +131,44 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
   // staging / v-output role of this thread: point tid & 15 (= the compute lane's c16),
   // channel (tid >> 4) & 3, snapshots (tid >> 6) + 4 i of each chunk
   const int cs = (tid >> 4) & 3, ls = tid >> 6;
+  const int nch = (U + kSC2 - 1) / kSC2;
   const unsigned ntiles = (g.npts + 15) / 16;
   for (unsigned tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const unsigned f = tile * 16 + (unsigned)c16;
     const bool ok = f < g.npts;
     const unsigned bo = g.base(ok ? f : 0u);
+    float zbp = 0.f;                           // sum over this thread's staged snapshots of lw z
+    // staging is split so that the next chunk's global loads are in flight during this
+    // chunk's compute: load() into registers, store() into the LDS buffer after the compute
+    float zn[kSC2 / 4];
+    auto load = [&](int ch) {
+#pragma unroll
+      for (int i = 0; i < kSC2 / 4; ++i) {
+        const int lg = ch * kSC2 + ls + 4 * i;
+        zn[i] = (ok && lg < U && cs < C) ? z[bo + (unsigned)(lg * C + cs) * g.HW] : 0.f;
+      }
+    };
+    auto store = [&](int ch, int buf) {
+#pragma unroll
+      for (int i = 0; i < kSC2 / 4; ++i) {
+        const int l = ls + 4 * i, lg = ch * kSC2 + l;
+        const float wv = zn[i] * slw[lg < U ? lg : 0];
+        zs[buf][l][c16][cs] = zn[i];
+        zw[buf][l][c16][cs] = wv;
+        zbp += wv;
+      }
+    };
+    auto vwrite = [&](int ch, int buf) {
+#pragma unroll
+      for (int i = 0; i < kSC2 / 4; ++i) {
+        const int l = ls + 4 * i, lg = ch * kSC2 + l;
+        if (ok && lg < U && cs < C)
+          v[bo + (unsigned)(lg * C + cs) * g.HW] =
+              (((vred[buf][0][l][lane] + vred[buf][1][l][lane]) + vred[buf][2][l][lane]) +
+               vred[buf][3][l][lane]) + vhalf[cs];
+      }
+    };
     f32x2 A[2][2], S[2][2], Q[2][4][2];
-    float4 zbar = {0.f, 0.f, 0.f, 0.f};         // sum_l lw_l z_l of point c16
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -126,29 +177,20 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
 #pragma unroll
         for (int c = 0; c < 4; ++c) Q[tt][c][i] = (f32x2){0.f, 0.f};
       }
-    for (int l0 = 0; l0 < U; l0 += kSC) {
-      const int nl = U - l0 < kSC ? U - l0 : kSC;
-      __syncthreads();                         // previous chunk's zs / vred readers are done
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int l = ls + 4 * i;
-        const float zv = (ok && l < nl && cs < C) ? z[bo + (unsigned)((l0 + l) * C + cs) * g.HW] : 0.f;
-        zs[l][c16][cs] = zv;
-        zw[l][c16][cs] = zv * slw[l0 + l < U ? l0 + l : 0];
-      }
-      __syncthreads();
+    load(0);
+    store(0, 0);
+    if (nch > 1) load(1);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      const int buf = ch & 1, l0 = ch * kSC2;
+      const int nl = U - l0 < kSC2 ? U - l0 : kSC2;
       for (int l = 0; l < nl; ++l) {
-        // an opaque zero offset for the swr reads: keeps them in the loop (hoisted, they would
-        // occupy the 32 VGPRs they exist to save)
-        int zo;
+        int zo;                                // opaque zero: keeps the swr reads in the loop
         asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
-        const float4 zc = *reinterpret_cast<const float4*>(&zw[l][c16][0]);
-        const float az = zs[l][c16][g4];
+        const float4 zc = *reinterpret_cast<const float4*>(&zw[buf][l][c16][0]);
+        const float az = zs[buf][l][c16][g4];
         const f32x2 wl = splat2(slw[l0 + l]);
-        zbar.x += zc.x; zbar.y += zc.y; zbar.z += zc.z; zbar.w += zc.w;
         f32x2 vp[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) vp[c] = (f32x2){vinit[c], 0.f};
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
           f32x4 d = {bb[tt][0], bb[tt][1], bb[tt][2], bb[tt][3]};
@@ -167,40 +209,42 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
             Q[tt][3][i] = pk_fma(gd, splat2(zc.w), Q[tt][3][i]);
             const float4* wq = reinterpret_cast<const float4*>(&swr[wave][g4][tt][i][0]) + zo;
             const float4 wq0 = wq[0], wq1 = wq[1];
-            vp[0] = pk_fma(gd, (f32x2){wq0.x, wq0.y}, vp[0]);
-            vp[1] = pk_fma(gd, (f32x2){wq0.z, wq0.w}, vp[1]);
-            vp[2] = pk_fma(gd, (f32x2){wq1.x, wq1.y}, vp[2]);
-            vp[3] = pk_fma(gd, (f32x2){wq1.z, wq1.w}, vp[3]);
+            const f32x2 q0 = {wq0.x, wq0.y}, q1 = {wq0.z, wq0.w}, q2 = {wq1.x, wq1.y}, q3 = {wq1.z, wq1.w};
+            if (tt == 0 && i == 0) {
+              vp[0] = gd * q0; vp[1] = gd * q1; vp[2] = gd * q2; vp[3] = gd * q3;
+            } else {
+              vp[0] = pk_fma(gd, q0, vp[0]);
+              vp[1] = pk_fma(gd, q1, vp[1]);
+              vp[2] = pk_fma(gd, q2, vp[2]);
+              vp[3] = pk_fma(gd, q3, vp[3]);
+            }
           }
         }
-        // v over this wave's 32 hidden units: sum the pair, then reduce-scatter over the 4 lane
-        // groups so that group g4 keeps channel g4 of point c16
-        const float v0 = vp[0].x + vp[0].y, v1 = vp[1].x + vp[1].y;
-        const float v2 = vp[2].x + vp[2].y, v3 = vp[3].x + vp[3].y;
-        const bool hi = (g4 & 2) != 0;
-        const float k0 = hi ? v2 : v0, k1 = hi ? v3 : v1;
-        const float s0 = hi ? v0 : v2, s1 = hi ? v1 : v3;
-        const float r0 = k0 + __shfl_xor(s0, 32, 64);
-        const float r1 = k1 + __shfl_xor(s1, 32, 64);
-        const bool odd = (g4 & 1) != 0;
-        vred[wave][l][lane] = (odd ? r1 : r0) + __shfl_xor(odd ? r0 : r1, 16, 64);
+        // v over this wave's 32 hidden units, reduce-scattered over the 4 lane groups: lanes
+        // 0-31 / 32-63 first (channels 0, 1 / 2, 3), then the 16-lane rows, so that group g4
+        // keeps channel g4 of point c16
+        const float a = swap_sum32(vp[0].x + vp[0].y, vp[2].x + vp[2].y);
+        const float b = swap_sum32(vp[1].x + vp[1].y, vp[3].x + vp[3].y);
+        vred[buf][wave][l][lane] = swap_sum16(a, b);
       }
+      if (ch + 1 < nch) {
+        store(ch + 1, buf ^ 1);                // its loads were issued one chunk ago
+        if (ch + 2 < nch) load(ch + 2);
+      }
+      if (ch >= 1) vwrite(ch - 1, buf ^ 1);
       __syncthreads();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int l = ls + 4 * i;
-        if (ok && l < nl && cs < C)
-          v[bo + (unsigned)((l0 + l) * C + cs) * g.HW] =
-              ((vred[0][l][lane] + vred[1][l][lane]) + vred[2][l][lane]) + vred[3][l][lane];
-      }
     }
+    vwrite(nch - 1, (nch - 1) & 1);
+    zbr[ls][lane] = zbp;
+    __syncthreads();
     // statistics of this tile: slot ((t 6 + comp) 64 + lane) holds hidden 16 t + 4 g4 + r
     // (r = the float4 component) of point c16
     float4* st = reinterpret_cast<float4*>(stats) + (size_t)tile * kTileF4 + lane;
-    // the 1/2 parts: A += 1/2 sum_l lw_l h_l = 1/2 (W1 zbar + b1 sum lw), S += 1/2 sum lw,
-    // Q_c += 1/2 zbar_c
+    float zb[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      zb[c] = ((zbr[0][16 * c + c16] + zbr[1][16 * c + c16]) + zbr[2][16 * c + c16]) + zbr[3][16 * c + c16];
     float up = 0.f;
-    const float zb[4] = {zbar.x, zbar.y, zbar.z, zbar.w};
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
       const int t = 2 * wave + tt;
@@ -215,7 +259,8 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
         av[r] = fmaf(kInvK, acc, 0.5f * hb);
       }
       const float4 a4 = {av[0], av[1], av[2], av[3]};
-      up += (w2r[tt][0] * a4.x + w2r[tt][1] * a4.y) + (w2r[tt][2] * a4.z + w2r[tt][3] * a4.w);
+      const int kb = 16 * t + 4 * g4;
+      up += (w2[kb] * a4.x + w2[kb + 1] * a4.y) + (w2[kb + 2] * a4.z + w2[kb + 3] * a4.w);
       st[(t * kNStat + 0) * 64] = a4;
       const float hs = 0.5f * lsum;
       st[(t * kNStat + 1) * 64] = (float4){S[tt][0].x + hs, S[tt][0].y + hs, S[tt][1].x + hs, S[tt][1].y + hs};
@@ -371,7 +416,7 @@ BLINDNO_API int blindno_project_bag_fwd(const float* z, const float* w1, const f
     return (int)hipErrorInvalidValue;
   const unsigned ntiles = (g.npts + 15) / 16;
   bagproj_fwd_kernel<<<ntiles, 256, 0, (hipStream_t)stream>>>(z, w1, b1, w2, b2, lw, ubar, stats,
-                                                              v, g);
+                                                               v, g);
   return (int)hipGetLastError();
 }
 

@@ -86,6 +86,13 @@ def main():
                                                         ptr(b2), ptr(lw), ptr(ubar), ptr(stats), ptr(vv), Bb, U, C,
                                                         P, P, N, N, 128, stream_ptr()),
                  8 * pts * C + sbytes)
+            # the benched step's bag: ~52 distinct snapshots of a randint(50, 100) draw
+            U52 = 52
+            lw52 = torch.full((U52,), 1.0 / U52, device=dev)
+            case("project_bag_fwd[u52]", lambda: call("blindno_project_bag_fwd", ptr(z), ptr(w1), ptr(b1), ptr(w2),
+                                                      ptr(b2), ptr(lw52), ptr(ubar), ptr(stats), ptr(vv), Bb, U52, C,
+                                                      P, P, N, N, 128, stream_ptr()),
+                 8 * Bb * U52 * N * N * C + sbytes)
             case("project_bag_bwd[input]", lambda: call("blindno_project_bag_bwd", ptr(stats), ptr(gsb), ptr(w2),
                                                         ptr(lw), ptr(vv), ptr(dz), ptr(pb), nbc, Bb, U, C, P, P, N,
                                                         N, 128, stream_ptr()),
