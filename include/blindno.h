@@ -189,6 +189,10 @@ int blindno_rowidft_bwd_nchunk(int Bn, int C, int P1, int P2, int m2);
  * 0 the general kernel.  Returns the previous setting.  Not thread-safe against launches; the
  * partial count of blindno_rowidft_bwd_nchunk follows the setting. */
 int blindno_set_rowfuse(int on);
+/* The fused column pass (one launch per layer: column DFT, mix and column inverse with the
+ * spectrum in LDS) on (1) or the split coldft_mix + colidft kernels (0); returns the previous
+ * setting.  Default on; BLINDNO_COLFUSE=0 in the environment turns it off. */
+int blindno_set_colfuse(int on);
 /* Layer chaining (the FNO layer loop, 2d_FPE/FNOModules.py:226-232): the next spectral layer's
  * row DFT of the field a row inverse produces, taken in the same pass -- At / Tp exactly as
  * blindno_rowdft(field, At, Tp, Bn, C, P1, P2, m2, act_next) would take them (m2 of the next

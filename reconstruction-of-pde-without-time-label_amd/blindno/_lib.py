@@ -59,6 +59,7 @@ SIGNATURES = {
     "blindno_conv_wgrad_nchunk": "iii",
     "blindno_rowidft_bwd_nchunk": "iiiii",
     "blindno_set_rowfuse": "i",
+    "blindno_set_colfuse": "i",
     "blindno_project_bwd_nchunk": "iii",
     "blindno_mix_wgrad_nsplit": "iiiii",
     "blindno_lift_fwd_g": "ppppiliiiiiiis",

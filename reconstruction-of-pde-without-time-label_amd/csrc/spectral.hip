@@ -472,6 +472,185 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
   for (int e = threadIdx.x; e < nout; e += blockDim.x) mix_one(e);
 }
 
+// The fused column pass (default for fp32 mixes of up to 16 channels and K1 <= 64 kept rows):
+// coldft_mix + colidft in ONE workgroup per 16-row M tile (G = 16 / Cin (sample, mode) pairs of
+// Cin channels), so the spectrum Y never leaves LDS and each layer pays one launch:
+//   1. column DFT X = At F on the matrix cores; the 4 waves split the K1p / 16 column tiles and,
+//      when there are fewer than 4 tiles, the P1 rows into KS chunks (partials summed in LDS,
+//      fixed order); every chunk's operands are loaded before its first MFMA;
+//   2. the per-mode channel mix (as coldft_mix) from LDS into LDS;
+//   3. column inverse Z = Y conj(F) on the matrix cores, the 4 waves over the P1 / 16 row tiles.
+// Same twiddle images (FB, GB) and the same summation order within each K chunk as the split
+// kernels; Xs (the saved spectrum) is written as before, Y is not.
+template <int DIR, int HBC>
+__global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__ At,
+                                                      const float2* __restrict__ Wt,
+                                                      const f32x4* __restrict__ FB,
+                                                      const f32x4* __restrict__ GB,
+                                                      float2* __restrict__ Xs,
+                                                      float2* __restrict__ Z, int npairs, int Ci,
+                                                      int Co, int P1, int m1, int m2, int P2, int G,
+                                                      int KS, int vec, int Bg, int64_t wtgs,
+                                                      int tiled) {
+  constexpr int kLd = 65;                          // LDS row stride (float2) for K1p <= 64
+  // DFT partials, chunk kc in columns [kc K1p, (kc + 1) K1p) (KS K1p <= 64), then Y
+  __shared__ float2 sP[16][kLd];
+  __shared__ float2 sX[16][kLd];
+  const int K1 = kept_rows_count(m1, P1);
+  const int Jt = (K1 + 15) >> 4, K1p = Jt * 16;
+  const int Cin = DIR == 0 ? Ci : Co;
+  const int Cout = DIR == 0 ? Co : Ci;
+  const int HB = (P1 + 15) >> 4;
+  const int q0 = blockIdx.x * G;
+  const int np = min(G, npairs - q0);
+  const int rows = np * Cin, orows = np * Cout;
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_int(threadIdx.x >> 6);
+  const int r16 = lane & 15, kq = lane >> 4;
+  const float inv = 1.0f / ((float)P1 * (float)P2);
+
+  // ---- 1. column DFT: unit u = (tile jt, chunk kc), u = wave, wave + 4, ...
+  const int HBc = (HB + KS - 1) / KS;
+  {
+    const bool rok = r16 < rows;
+    const float2* ar = At + ((int64_t)q0 * Cin + (rok ? r16 : 0)) * P1;
+    for (int u = wave; u < Jt * KS; u += 4) {
+      const int jt = u % Jt, kc = u / Jt;
+      const int hb0 = kc * HBc;
+      const int nhb = min(HBc, HB - hb0);
+      const f32x4* fb = FB + ((int64_t)jt * HB * 64 + lane) * 2;
+      float are[HBC][4], aim[HBC][4];
+      f32x4 af0[HBC], af1[HBC];
+#pragma unroll
+      for (int i = 0; i < HBC; ++i) {
+        if (i < nhb) {
+          const int h1 = (hb0 + i) * 16 + kq * 4;
+          load4c(ar + h1, rok ? P1 - h1 : 0, vec, are[i], aim[i]);
+          af0[i] = fb[(hb0 + i) * 128];
+          af1[i] = fb[(hb0 + i) * 128 + 1];
+        }
+      }
+      f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < HBC; ++i)
+        if (i < nhb) cmfma4(are[i], aim[i], af0[i], af1[i], dr, di);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sP[kq * 4 + r][kc * K1p + jt * 16 + r16] = make_float2(dr[r], di[r]);
+    }
+  }
+  __syncthreads();
+  // chunk sum in order, the adjoint's c_k / (P1 P2) scale, the saved spectrum
+  for (int e = threadIdx.x; e < 16 * K1p; e += 256) {
+    const int row = e / K1p, j = e - row * K1p;
+    float2 v = sP[row][j];
+    for (int kc = 1; kc < KS; ++kc) {
+      const float2 w = sP[row][kc * K1p + j];
+      v.x += w.x;
+      v.y += w.y;
+    }
+    if (row < rows) {
+      if (DIR == 1) {
+        const float sc = c2r_weight((q0 + row / Cin) % m2, P2) * inv;
+        v.x *= sc;
+        v.y *= sc;
+      }
+      if (j < K1) Xs[((int64_t)q0 * Cin + row) * K1 + j] = v;
+    }
+    sX[row][j] = v;
+  }
+  __syncthreads();
+
+  // ---- 2. the mix: Y[p o][j] into sP (rows >= orows and columns >= K1 zero)
+  for (int e = threadIdx.x; e < 16 * K1p; e += 256) {
+    const int o = e % Cout;                       // output channel fastest: contiguous weights
+    const int t = e / Cout;
+    const int j = t % K1p, p = t / K1p;
+    const int orow = p * Cout + o;
+    if (orow >= 16) continue;
+    float re = 0.f, im = 0.f;
+    if (p < np && j < K1) {
+      const int k = (q0 + p) % m2;
+      const float2* wg = wtgs ? reinterpret_cast<const float2*>(
+                                    reinterpret_cast<const float*>(Wt) + ((q0 + p) / m2 / Bg) * wtgs)
+                              : Wt;
+      const float2* wj = wg + ((int64_t)k * K1 + j) * Ci * Co;
+      const float2* xp = &sX[p * Cin][j];
+#pragma unroll 4
+      for (int c = 0; c < Cin; ++c) {
+        const float2 a = xp[c * kLd];
+        const float2 w = DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
+        if (DIR == 0) {
+          re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
+          im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
+        } else {                                    // conj(w) * a
+          re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
+          im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+        }
+      }
+      if (DIR == 0) {
+        const float sc = c2r_weight(k, P2) * inv;
+        re *= sc;
+        im *= sc;
+      }
+    }
+    sP[orow][j] = make_float2(re, im);
+  }
+  // rows past G Cout (e.g. 12-channel pairs) are zero: the inverse's A operand reads all 16
+  for (int e = threadIdx.x; e < 16 * K1p; e += 256) {
+    const int row = e / K1p;
+    if (row >= min(16, (16 / Cout) * Cout)) sP[row][e - row * K1p] = make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+
+  // ---- 3. column inverse: D[orow][h] = sum_j Y[orow][j] conj F[h][j], h tiles over the waves
+  const int Ht = HB;
+  const int R = m2 * Cout;
+  for (int ht = wave; ht < Ht; ht += 4) {
+    const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
+    f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
+    // every j block's twiddles in flight before the first MFMA (Jt <= 4)
+    f32x4 g0[4], g1[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+      if (jb < Jt) {
+        g0[jb] = gb[jb * 128];
+        g1[jb] = gb[jb * 128 + 1];
+      }
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      if (jb >= Jt) break;
+      float re[4], im[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float2 v = sP[r16][jb * 16 + kq * 4 + s];
+        re[s] = v.x;
+        im[s] = v.y;
+      }
+      cmfma4(re, im, g0[jb], g1[jb], dr, di);
+    }
+    const int h = ht * 16 + r16;
+    if (h >= P1) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int orow = kq * 4 + r;
+      if (orow >= orows) continue;
+      const int p = orow / Cout, o = orow - p * Cout;
+      const int q = q0 + p, n = q / m2, k = q - n * m2;
+      const float2 v = make_float2(dr[r], di[r]);
+      if (!tiled) {
+        Z[((int64_t)n * P1 + h) * R + k * Cout + o] = v;
+      } else {
+        const int gr = n * P1 + h;
+        const int c16 = 4 * (gr & 3) + (o & 3);
+        float* zt = reinterpret_cast<float*>(Z) +
+                    ((int64_t)((gr >> 2) * (Cout >> 2) + (o >> 2)) * (m2 >> 1) + (k >> 1)) * 64;
+        zt[32 * (k & 1) + c16] = v.x;
+        zt[32 * (k & 1) + 16 + c16] = v.y;
+      }
+    }
+  }
+}
+
 // Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
 // tile, 64 spectrum rows (k, o)); one 16-row MFMA tile per wave; the result is transposed
 // through LDS so that each h row of Z is written as one contiguous run.  tiled: Z in the
@@ -802,6 +981,22 @@ BLINDNO_API int blindno_rowdft_bag_lift(const float* X, const int* idx, const fl
                                     m2, stream);
 }
 
+// BLINDNO_COLFUSE=0 (or blindno_set_colfuse(0)): the split coldft_mix + colidft kernels
+int g_colfuse = -1;
+bool colfuse_on() {
+  if (g_colfuse < 0) {
+    const char* e = getenv("BLINDNO_COLFUSE");
+    g_colfuse = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_colfuse != 0;
+}
+
+BLINDNO_API int blindno_set_colfuse(int on) {
+  const int prev = colfuse_on() ? 1 : 0;
+  g_colfuse = on ? 1 : 0;
+  return prev;
+}
+
 BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, float* Y, float* Z,
                                   const float* FB, const float* GB, int Gw, int64_t wtgs, int Bn,
                                   int Ci, int Co, int P1, int m1, int m2, int P2, int dir,
@@ -820,6 +1015,32 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const int64_t npairs = (int64_t)Bn * m2;
   if (npairs * (cin > cout ? cin : cout) * (P1 > K1p ? P1 : K1p) >= INT32_MAX)
     return (int)hipErrorInvalidValue;
+  const int HB = (P1 + 15) / 16;
+  hipStream_t st = (hipStream_t)stream;
+  // the fused pass: fp32 mix, Cin and Cout equal (G pairs fill the same 16 rows on both sides),
+  // at most 64 kept rows, at most 10 row blocks per K chunk
+  const int KSf = Jt >= 4 ? 1 : 4 / Jt;          // K chunks so that the 4 waves have units
+  if (colfuse_on() && !h16 && Ci == Co && Ci <= 16 && K1p <= 64 && (HB + KSf - 1) / KSf <= 10) {
+    const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
+    const int G = 16 / cin;
+    const int KS = KSf;
+    const int HBc = (HB + KS - 1) / KS;
+    const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
+    const dim3 g((unsigned)cdiv(npairs, G));
+#define CF_(D_, H_)                                                                           \
+  colfuse_kernel<D_, H_><<<g, 256, 0, st>>>((const float2*)At, (const float2*)Wt,             \
+                                            (const f32x4*)FB, (const f32x4*)GB, (float2*)Xs,   \
+                                            (float2*)Z, (int)npairs, Ci, Co, P1, m1, m2, P2, G, \
+                                            KS, vec, Bg, wtgs, tiled)
+#define CFD_(H_) do { if (dir == 0) CF_(0, H_); else CF_(1, H_); } while (0)
+    if (HBc <= 3) CFD_(3);
+    else if (HBc <= 5) CFD_(5);
+    else if (HBc <= 10) CFD_(10);
+    else return (int)hipErrorInvalidValue;
+#undef CFD_
+#undef CF_
+    return (int)hipGetLastError();
+  }
   // pairs per workgroup: enough 16-row tiles for the four waves, tiles filled
   int G = 1;
   while (((G * cin + 15) / 16) * Jt < COLPASS_WAVE_TILES && G * cin < 64) ++G;
@@ -828,7 +1049,6 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const size_t sh = sizeof(float2) * (size_t)G * cin * (K1p + 1);
   if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
   const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
-  hipStream_t st = (hipStream_t)stream;
   const dim3 g1((unsigned)cdiv(npairs, G));
   const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
   // full operand prefetch when the launch is too small to hide latency with waves

@@ -502,3 +502,41 @@ def test_head_lift_fwd_and_input_grad_vs_fp64(N, G):
     d64 = dx0.double().cpu()[:, :, :N, :N]
     dref = sum(torch.einsum("nchw,cj->nhwj", d64[gi * Bg:(gi + 1) * Bg], w64[gi]) for gi in range(G))
     assert rel_l2(d_in.double().cpu().numpy(), dref.numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("Bn,C,m,P,Gw", [(208, 4, 12, 160, 1), (8, 12, 32, 160, 2), (4, 12, 32, 160, 1),
+                                         (8, 4, 12, 320, 1), (37, 3, 16, 150, 1), (6, 8, 20, 96, 1),
+                                         (5, 16, 8, 40, 1)])
+def test_fused_column_pass_matches_split(Bn, C, m, P, Gw):
+    """The fused column pass (blindno_set_colfuse(1): column DFT, mix and column inverse in one
+    workgroup, the spectrum in LDS) vs the split coldft_mix + colidft kernels on the same inputs,
+    both directions: the saved spectrum Xs and the row coefficients Z (plain or the wide row
+    inverse's tiled layout) agree to fp32 rounding (the fused kernel sums the column DFT in up to
+    4 row chunks).  Cases: FNO_input at config C, the grouped heads, one head, FNO_input at 320
+    rows (config E), odd widths / ragged row blocks, 16 channels."""
+    import ctypes
+    from blindno import ops
+    from blindno._lib import call, ptr, query, stream_ptr
+    g = torch.Generator(device="cuda").manual_seed(Bn + C + m)
+    K1 = ops.kept_rows_count(m, P)
+    K1p = 16 * ((K1 + 15) // 16)
+    At = torch.randn(Bn, m, C, P, 2, device="cuda", generator=g)
+    Wt = torch.randn(Gw, m, K1, C, C, 2, device="cuda", generator=g) * 0.2
+    FB, GB = ops.twiddle_cols(P, m, At.device)
+    wtgs = m * K1 * C * C * 2 if Gw > 1 else 0
+    res = {}
+    for fused in (0, 1):
+        prev = query("blindno_set_colfuse", fused)
+        for d in (0, 1):
+            Xs = torch.full((Bn, m, C, K1, 2), float("nan"), device="cuda")
+            Y = torch.empty(Bn, m, C, K1p, 2, device="cuda")
+            Z = torch.full((Bn, P, m, C, 2), float("nan"), device="cuda")
+            call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(Xs), ptr(Y), ptr(Z), ptr(FB), ptr(GB), Gw,
+                 ctypes.c_int64(wtgs), Bn, C, C, P, m, m, P, d, stream_ptr())
+            res[(fused, d)] = (Xs, Z)
+        query("blindno_set_colfuse", prev)
+    torch.cuda.synchronize()
+    for d in (0, 1):
+        for a, b in zip(res[(1, d)], res[(0, d)]):
+            assert torch.isfinite(a).all()
+            assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-6, d

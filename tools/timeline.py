@@ -19,13 +19,15 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     back = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
-                 r.get("Queue_Id", "")) for r in rows)
+                 r.get("Queue_Id", ""), r.get("Grid_Size", ""), r.get("Workgroup_Size", ""),
+                 r.get("VGPR_Count", r.get("Arch_VGPR_Count", ""))) for r in rows)
     adams = [i for i, e in enumerate(ev) if e[2].startswith("adam")]
     a0, a1 = adams[-1 - back], adams[-back]
     t0 = ev[a0 + 1][0]
     busy = 0
     for e in ev[a0 + 1:a1 + 1]:
-        print(f"{(e[0] - t0) / 1e3:8.1f} {(e[1] - e[0]) / 1e3:7.1f} q{e[3]} {e[2][:64]}")
+        wg = int(e[4]) // max(1, int(e[5])) if e[4] and e[5] else ""
+        print(f"{(e[0] - t0) / 1e3:8.1f} {(e[1] - e[0]) / 1e3:7.1f} q{e[3]} wg={wg:<6} v{e[6]:<4} {e[2][:64]}")
         busy += e[1] - e[0]
     print(f"step {(ev[a1][1] - t0) / 1e3:.1f} us, kernel-busy sum {busy / 1e3:.1f} us")
 
