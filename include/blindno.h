@@ -167,6 +167,12 @@ int blindno_mix1d(const float* At, const float* Wt, float* Xs, float* Z, int Bn,
 int blindno_rowidft_epi(const float* Z, const float* x, const float* wc, const float* bc,
                         float* z, const float* tb, int Bn, int C, int P1, int P2, int m2,
                         int act, blindno_stream_t stream);
+/* blindno_rowidft_epi writing z on the output crop h < oN1, w < oN2 only (the FNO_input body's
+ * last layer, whose one reader -- the projection, FNOModules.py:234 -- reads nothing else; the
+ * rest of z is left unwritten). */
+int blindno_rowidft_epi_crop(const float* Z, const float* x, const float* wc, const float* bc,
+                             float* z, const float* tb, int Bn, int C, int P1, int P2, int m2,
+                             int act, int oN1, int oN2, blindno_stream_t stream);
 
 /* Adjoint of rowidft_epi w.r.t. its input field:
  *   dx[n,i,h,w] = sum_k Re(G[n,h,k,i] e^{+2pi i k w/P2}) + sum_o Wc[o,i] dz[n,o,h,w]

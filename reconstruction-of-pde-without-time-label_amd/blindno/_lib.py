@@ -34,6 +34,7 @@ SIGNATURES = {
     "blindno_mix_wgrad_part": "pppiiiiiiis",
     "blindno_mix1d": "ppppiiiiiis",
     "blindno_rowidft_epi": "ppppppiiiiiis",
+    "blindno_rowidft_epi_crop": "pppppp" + "iiiiiiii" + "s",
     "blindno_rowidft_bwd": "pppppppiiiiiis",
     "blindno_rowidft_bwd_crop": "pppppppiiiiiiiis",
     "blindno_rowidft_bwd_rd": "pppppppiiiiiiiipps",

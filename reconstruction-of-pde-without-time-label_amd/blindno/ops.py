@@ -1013,7 +1013,11 @@ class BagEncoderFn(torch.autograd.Function):
             else:
                 Xk, Z = spec_forward(zs[-1], 1, Wt, sh, At=At_next)
                 if last:
-                    z = k_rowidft_epi(Z, zs[-1], cw, cb, Bn, C, P1, P2, meta.m2, 1)
+                    # the projection reads the output on its crop only: write nothing else
+                    z = _empty(Bn, C, P1, P2, like=X)
+                    call("blindno_rowidft_epi_crop", ptr(Z), ptr(zs[-1]), ptr(cw), ptr(cb), ptr(z),
+                         ptr(twiddle_rowinv(P2, meta.m2, X.device)), Bn, C, P1, P2, meta.m2, 1, Ho, Wo,
+                         stream_ptr())
                 else:
                     z, At_next = k_rowidft_epi_rd(Z, zs[-1], cw, cb, Bn, C, P1, P2, meta.m2, 1, 1)
             Xs.append(Xk)

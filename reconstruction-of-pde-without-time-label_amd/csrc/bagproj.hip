@@ -299,38 +299,48 @@ __global__ __launch_bounds__(256) void bagproj_bwd_kernel(
 #pragma unroll
   for (int j = 0; j < kJ; ++j) acc[j] = (float4){0.f, 0.f, 0.f, 0.f};
   float gsum = 0.f;
-  const int cs = (tid >> 4) & 3, ls = tid >> 6;
+  // four consecutive 16-point tiles per step: the dz = lw ghat v stream then covers 64
+  // consecutive points per wave instruction (256-B runs of one channel plane; a 16-point tile
+  // gave 64-B runs), wave w taking channel w over every snapshot
+  const int cw = tid >> 6, p64 = tid & 63;
   const unsigned ntiles = (g.npts + 15) / 16;
-  for (unsigned tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const unsigned f = tile * 16 + (unsigned)c16;
-    const bool ok = f < g.npts;
-    const float gh = ok ? gs[f] : 0.f;
-    const float4* st = reinterpret_cast<const float4*>(stats) + (size_t)tile * kTileF4 + tid;
-    float4 sv[kJ];
+  const unsigned ntg = (ntiles + 3) / 4;
+  for (unsigned tg = blockIdx.x; tg < ntg; tg += gridDim.x) {
+    {
+      const unsigned f = tg * 64 + (unsigned)p64;
+      if (f < g.npts && cw < C) {
+        const float gh = gs[f];
+        const unsigned bo = g.base(f) + (unsigned)cw * g.HW;
+        const unsigned ls = (unsigned)C * g.HW;
+        int l = 0;
+        for (; l + 3 < U; l += 4) {                 // four loads in flight per thread
+          float vv[4];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) sv[j] = st[256 * j];
-    if (tid < 16) gsum += gh;
-    if (ok && cs < C) {
-      const unsigned bo = g.base(f) + (unsigned)cs * g.HW;
-      int l = ls;
-      for (; l + 12 < U; l += 16) {                // four loads in flight per thread
-        float vv[4];
+          for (int i = 0; i < 4; ++i) vv[i] = v[bo + (unsigned)(l + i) * ls];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) vv[i] = v[bo + (unsigned)((l + 4 * i) * C) * g.HW];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dz[bo + (unsigned)((l + 4 * i) * C) * g.HW] = slw[l + 4 * i] * gh * vv[i];
-      }
-      for (; l < U; l += 4) {
-        const unsigned o = bo + (unsigned)(l * C) * g.HW;
-        dz[o] = slw[l] * gh * v[o];
+          for (int i = 0; i < 4; ++i) dz[bo + (unsigned)(l + i) * ls] = slw[l + i] * gh * vv[i];
+        }
+        for (; l < U; ++l) dz[bo + (unsigned)l * ls] = slw[l] * gh * v[bo + (unsigned)l * ls];
       }
     }
+#pragma unroll 1
+    for (int t4 = 0; t4 < 4; ++t4) {
+      const unsigned tile = tg * 4 + (unsigned)t4;
+      if (tile >= ntiles) break;
+      const unsigned f = tile * 16 + (unsigned)c16;
+      const float gh = f < g.npts ? gs[f] : 0.f;
+      const float4* st = reinterpret_cast<const float4*>(stats) + (size_t)tile * kTileF4 + tid;
+      float4 sv[kJ];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      acc[j].x = fmaf(gh, sv[j].x, acc[j].x);
-      acc[j].y = fmaf(gh, sv[j].y, acc[j].y);
-      acc[j].z = fmaf(gh, sv[j].z, acc[j].z);
-      acc[j].w = fmaf(gh, sv[j].w, acc[j].w);
+      for (int j = 0; j < kJ; ++j) sv[j] = st[256 * j];
+      if (tid < 16) gsum += gh;
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        acc[j].x = fmaf(gh, sv[j].x, acc[j].x);
+        acc[j].y = fmaf(gh, sv[j].y, acc[j].y);
+        acc[j].z = fmaf(gh, sv[j].z, acc[j].z);
+        acc[j].w = fmaf(gh, sv[j].w, acc[j].w);
+      }
     }
   }
   // sum over the 16 points (lanes c16) in a fixed butterfly order

@@ -16,6 +16,7 @@
 // image in MFMA lane order (twiddle_rowinv, staged once per workgroup in LDS).
 #include "common.h"
 #include "blindno.h"
+#include "gelu_pk.h"
 #include "kernels.h"
 
 using namespace blindno;
@@ -465,6 +466,64 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
 // 4 s + g) is permuted into this order while it is staged.
 // MODE / ACT / WG / LIFT as rowinv_mfma_kernel; RD: 0 none, 1 next row DFT of the field, 2 of
 // GELU(field).  S = m2 / 2 (m2 % 4 == 0, m2 <= 16); P1 % 16 == 0, P2 % 32 == 0.
+// the epilogue GELUs of the transposed kernel on packed fp32 pairs (gelu_pk.h: the same A&S
+// evaluation, two values per v_pk instruction)
+#ifndef ROWFUSE_PKGELU
+#define ROWFUSE_PKGELU 0
+#endif
+__device__ __forceinline__ f32x4 gelu4(f32x4 x) {
+#if ROWFUSE_PKGELU
+  using namespace blindno::gelu_pk;
+  f32x4 y;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const f32x2 v = {x[2 * i], x[2 * i + 1]};
+    f32x2 e;
+    const f32x2 cdf = norm_cdf_pair(v * splat2(kK), e);
+    const f32x2 g = v * cdf;
+    y[2 * i] = g.x;
+    y[2 * i + 1] = g.y;
+  }
+  return y;
+#else
+  return (f32x4){gelu_f(x[0]), gelu_f(x[1]), gelu_f(x[2]), gelu_f(x[3])};
+#endif
+}
+// GELU and GELU' of four values (the adjoint's input activation and its derivative)
+__device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
+#if ROWFUSE_PKGELU
+  using namespace blindno::gelu_pk;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const f32x2 v = {x[2 * i], x[2 * i + 1]};
+    const f32x2 hk = v * splat2(kK);
+    f32x2 ep;
+    const f32x2 cdf = norm_cdf_pair_pdf(hk, ep);
+    const f32x2 gv = v * cdf;
+    const f32x2 dv = pk_fma(hk, ep, cdf);          // Phi + h phi(h)
+    a[2 * i] = gv.x;
+    a[2 * i + 1] = gv.y;
+    dg[2 * i] = dv.x;
+    dg[2 * i + 1] = dv.y;
+  }
+#else
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float ar, dr;
+    gelu_both(x[r], ar, dr);
+    a[r] = ar;
+    dg[r] = dr;
+  }
+#endif
+}
+// timing experiments only (wrong results): RF_GELU(x) = x drops the epilogue GELUs, RF_NORD
+// the next layer's row-DFT MFMAs
+#ifndef RF_GELU
+#define RF_GELU(x) gelu4(x)
+#endif
+#ifndef RF_NORD
+#define RF_NORD 0
+#endif
 #ifndef ROWFUSE_BLOCKS
 #define ROWFUSE_BLOCKS 512
 #endif
@@ -517,10 +576,14 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
   const int c16 = lane & 15, g = lane >> 4;
-  const int HB = P1 >> 4;
+  // MODE 0 without the next row DFT: the output is written on its crop h < dN1, w < dN2 only
+  // (the encoder's last layer, read by the projection on the crop alone): whole 16-row blocks and
+  // 16 NH-column steps past the crop are skipped
+  constexpr bool OCROP = MODE == 0 && RD == 0;
+  const int HB = OCROP ? (dN1 + 15) >> 4 : P1 >> 4;
   const int nitems = Bn * HB;
   const int HW = P1 * P2;                           // field < 2^31 elements (launcher)
-  const int NS = NT / NH;                           // steps per row block
+  const int NS = OCROP ? (dN2 + 16 * NH - 1) / (16 * NH) : NT / NH;   // steps per row block
   constexpr bool has_wc = HW_;
   float W[C][C], bv[C], w0[C][3], b0[C];
 #pragma unroll
@@ -659,10 +722,14 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
         if (MODE == 0) {
           f32x4 xin[C];
 #pragma unroll
-          for (int c = 0; c < C; ++c)
+          for (int c = 0; c < C; ++c) {
+            if (LIFT) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              xin[c][r] = LIFT ? x0(c, r) : (ACT ? gelu_f(cur.a[c][hf][r]) : cur.a[c][hf][r]);
+              for (int r = 0; r < 4; ++r) xin[c][r] = x0(c, r);
+            } else {
+              xin[c] = ACT ? RF_GELU(cur.a[c][hf]) : cur.a[c][hf];
+            }
+          }
 #pragma unroll
           for (int o = 0; o < C; ++o) {
             f32x4 y = d[o];
@@ -676,10 +743,7 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
               }
             }
             *reinterpret_cast<f32x4*>(out + fbase + o * HW + w) = y;
-            if (RD) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) ya[o][r] = RD == 2 ? gelu_f(y[r]) : y[r];
-            }
+            if (RD) ya[o] = RD == 2 ? RF_GELU(y) : y;
           }
         } else {
           if (WG) {
@@ -691,6 +755,8 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
 #pragma unroll
           for (int c = 0; c < C; ++c) {
             f32x4 dg = d[c];
+            f32x4 a4 = zero4, dg4 = zero4;
+            if (!LIFT && ACT) gelu_both4(cur.s[c][hf], a4, dg4);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float v = dg[r];
@@ -702,9 +768,8 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
               if (LIFT) {
                 ain = x0(c, r);
               } else if (ACT) {
-                float dgl;
-                gelu_both(cur.s[c][hf][r], ain, dgl);
-                v *= dgl;
+                ain = a4[r];
+                v *= dg4[r];
               } else {
                 ain = cur.s[c][hf][r];
               }
@@ -728,7 +793,7 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
             if (RD) ya[c] = dg;
           }
         }
-        if (RD) {
+        if (RD && !RF_NORD) {
           // next layer's row DFT, transposed: A = its twiddles (lane: column k' = 16 nt + c16;
           // K = w = 16 kb + 4 kq + s of rowdft's image), B = the field values this lane holds
           const int kb = (16 * NH * st + 4 * NH * g + 4 * hf) >> 4, kq = (NH * g + hf) & 3;
@@ -945,9 +1010,15 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       // P2 = 160 (the encoder at 128^2), forward: the step loop fully unrolled (the adjoint's
       // larger operand set and in-pass weight-gradient sums spill when unrolled: runtime loop)
       const bool p160 = P2 == 160 && MODE == 0;
+      // the output crop (MODE 0, no next row DFT): 128 of the 160 columns, 4 steps
+      const bool crop128 = MODE == 0 && !rd.At && dN2 == 128;
 #define RF(RD_, S_)                                                                            \
   do {                                                                                         \
-    if (wc && p160)                                                                            \
+    if (wc && p160 && crop128 && RD_ == 0)                                                     \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, true, MODE == 0 ? 128 / (16 * NHm) : 0> \
+          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+                                      dN2, rd);                                                \
+    else if (wc && p160 && (dN2 == P2 || RD_ != 0))                                            \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, true, MODE == 0 ? 160 / (16 * NHm) : 0> \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd);                                                \
@@ -1033,6 +1104,28 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
 }
 
 }  // namespace
+
+// The encoder's last layer: the row inverse + epilogue written on the output crop h < oN1,
+// w < oN2 only (its one reader, the projection, reads nothing else); the rest of z is left
+// unwritten.  Other shapes take the full-field kernels.
+BLINDNO_API int blindno_rowidft_epi_crop(const float* Z, const float* x, const float* wc,
+                                         const float* bc, float* z, const float* tb, int Bn,
+                                         int C, int P1, int P2, int m2, int act, int oN1, int oN2,
+                                         void* stream) {
+  if (oN1 < 1 || oN1 > P1 || oN2 < 1 || oN2 > P2) return (int)hipErrorInvalidValue;
+  RowinvGeom g = rowinv_geom(Bn, C, P1, P2, m2);
+  if (rowfuse_shape(Bn, C, P1, P2, m2)) {
+    const int items = Bn * ((oN1 + 15) / 16);
+    const int b = (items + kW - 1) / kW;
+    g.blocks = b < ROWFUSE_BLOCKS ? b : ROWFUSE_BLOCKS;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (act)
+    return rowinv_launch<0, 1, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, g.blocks, Bn, C, P1, P2,
+                                  m2, st, BagLift{}, 1, 0, oN1, oN2);
+  return rowinv_launch<0, 0, 0>(Z, x, nullptr, wc, bc, z, tb, nullptr, g.blocks, Bn, C, P1, P2, m2,
+                                st, BagLift{}, 1, 0, oN1, oN2);
+}
 
 BLINDNO_API int blindno_rowidft_epi_g(const float* Z, const float* x, const float* wc,
                                       const float* bc, float* z, const float* tb, int G,

@@ -169,3 +169,24 @@ def test_rowfuse_lift_variants_match_general_kernel(fuse):
          rel_l2(p1.cpu().numpy(), p0.cpu().numpy()))
     print(f"rowfuse lift vs general kernel: z {e[0]:.2e} At {e[1]:.2e} partial sums {e[2]:.2e}")
     assert e[0] <= 2e-6 and e[1] <= 2e-6 and e[2] <= 2e-6
+
+
+@pytest.mark.parametrize("act,oN1,oN2,Bn_", [(1, 128, 128, 6), (0, 128, 128, 6), (1, 100, 96, 5), (1, 160, 160, 3)])
+def test_output_crop_matches_full_field(fuse, act, oN1, oN2, Bn_):
+    """blindno_rowidft_epi_crop (the encoder's last layer written on the projection's crop only)
+    vs blindno_rowidft_epi: the crop h < oN1, w < oN2 is identical to the bit (same kernel code per
+    element; only whole row blocks and column steps past the crop are skipped); 128 x 128 is the
+    fully unrolled 4-step instance, 100 x 96 the runtime-step one, 160 x 160 no crop."""
+    from blindno import ops
+    from blindno._lib import call, ptr, stream_ptr
+    g = torch.Generator(device="cuda").manual_seed(act + oN1 + oN2)
+    Z = torch.randn(Bn_, P, m, C, 2, device="cuda", generator=g) * 0.1
+    x = torch.randn(Bn_, C, P, P, device="cuda", generator=g)
+    cw = torch.randn(C, C, 1, 1, device="cuda", generator=g) * 0.3
+    cb = torch.randn(C, device="cuda", generator=g) * 0.1
+    full = ops.k_rowidft_epi(Z, x, cw, cb, Bn_, C, P, P, m, act)
+    crop = torch.full_like(full, float("nan"))
+    call("blindno_rowidft_epi_crop", ptr(Z), ptr(x), ptr(cw), ptr(cb), ptr(crop),
+         ptr(ops.twiddle_rowinv(P, m, Z.device)), Bn_, C, P, P, m, act, oN1, oN2, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(crop[:, :, :oN1, :oN2], full[:, :, :oN1, :oN2])
