@@ -469,7 +469,7 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
 // the epilogue GELUs of the transposed kernel on packed fp32 pairs (gelu_pk.h: the same A&S
 // evaluation, two values per v_pk instruction)
 #ifndef ROWFUSE_PKGELU
-#define ROWFUSE_PKGELU 0
+#define ROWFUSE_PKGELU 1
 #endif
 __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
 #if ROWFUSE_PKGELU
@@ -546,6 +546,9 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 #endif
 #ifndef ROWFUSE_NH1
 #define ROWFUSE_NH1 1
+#endif
+#ifndef ROWFUSE_NH0_NORD
+#define ROWFUSE_NH0_NORD 2
 #endif
 // HW: the layer has its 1x1 conv (wc != NULL) -- a compile-time flag: a runtime test around each
 // operand load made hipcc branch around the loads and count their waits conservatively.
@@ -825,9 +828,10 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
         __builtin_amdgcn_sched_barrier(0);
         step(st, buf[st & 1]);
       }
-    } else if (MODE == 1 && !ROWFUSE_PF1) {
+    } else if (MODE == 1 && !(ROWFUSE_PF1 && RD == 0)) {
       // the adjoint without operand prefetch (its operand set is twice the forward's; the
-      // registers buy occupancy instead)
+      // registers buy occupancy instead): always with the next row DFT in the pass (one wave
+      // per SIMD with the prefetch buffers, two without: bwd_rd_crop 115 -> 108 us, r04g)
       for (int st = 0; st < NS; ++st) {
         if (st > 0) load(st, buf[0]);
         step(st, buf[0]);
@@ -1006,7 +1010,10 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       const size_t red = sizeof(float) * (size_t)kW * (C * C + C + 4 * C);
       if (shf < red) shf = red;
       if (shf > 160 * 1024) return (int)hipErrorInvalidValue;
-      constexpr int NHm = MODE == 0 ? ROWFUSE_NH0 : ROWFUSE_NH1;
+      // column tiles per step: 2 in the forward (ROWFUSE_NH0; without the next row DFT
+      // ROWFUSE_NH0_NORD: 1 tile gives 4 waves per SIMD instead of 2 -- 124 vs 176 VGPRs -- but
+      // the step measured 0.5 % slower, r04h), 1 in the adjoint
+#define NHX(RD_) (MODE == 0 ? ((RD_) == 0 ? ROWFUSE_NH0_NORD : ROWFUSE_NH0) : ROWFUSE_NH1)
       // P2 = 160 (the encoder at 128^2), forward: the step loop fully unrolled (the adjoint's
       // larger operand set and in-pass weight-gradient sums spill when unrolled: runtime loop)
       const bool p160 = P2 == 160 && MODE == 0;
@@ -1015,19 +1022,21 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
 #define RF(RD_, S_)                                                                            \
   do {                                                                                         \
     if (wc && p160 && crop128 && RD_ == 0)                                                     \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, true, MODE == 0 ? 128 / (16 * NHm) : 0> \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true,                             \
+                     MODE == 0 ? 128 / (16 * NHX(RD_)) : 0>                                    \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd);                                                \
     else if (wc && p160 && (dN2 == P2 || RD_ != 0))                                            \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, true, MODE == 0 ? 160 / (16 * NHm) : 0> \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true,                             \
+                     MODE == 0 ? 160 / (16 * NHX(RD_)) : 0>                                    \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd);                                                \
     else if (wc)                                                                               \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, true>                                  \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true>                             \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd);                                                \
     else                                                                                       \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHm, false>                                 \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), false>                            \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd);                                                \
   } while (0)
@@ -1038,6 +1047,7 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       else RF_S(1);
 #undef RF_S
 #undef RF
+#undef NHX
       return (int)hipGetLastError();
     }
   }
