@@ -559,7 +559,9 @@ def parity_check_nio(model, graphed, opt, xb, yb, grid, T, seed):
     test_config_d_graphed_niofp2d_nc_128) and the count of branches an unconditioned fp64 forward
     takes differently is reported (bar 1e-5 of all).  Pass: GPU vs fp64 fields 1e-5 and every
     gradient 1e-4 (conv biases ahead of batch-statistics BatchNorm, whose true gradient is 0,
-    excluded), GPU vs the reference's fp32 fields 1e-5, flips within the bar."""
+    excluded), dL/dbasis (the trunk's upstream gradient) vs fp64 1e-5, GPU vs the reference's fp32
+    fields 1e-5, flips within the bar.  The full-chain errors of the worst gradients are reported beside
+    the reference fp32 step's own."""
     import blindno
     from oracle import cpu_ref, fno_ref
     from blindno.train import DataParallel, GraphedBagStep
@@ -573,12 +575,18 @@ def parity_check_nio(model, graphed, opt, xb, yb, grid, T, seed):
              "convblock4_2", "convblock7_1", "convblock7_2", "convblock7_3")
     hooks = [getattr(model.branch, n).register_forward_hook(lambda mod, i, o: rec.append(o.detach() > 0))
              for n in names]
+    # the trunk's upstream gradient dL/dbasis as the replay computes it (a copy captured into the
+    # graph, like the branch masks)
+    rec_db = []
+    hooks.append(model.trunk.register_full_backward_hook(
+        lambda mod, gi, go: rec_db.append(go[0].detach().clone())))
     gs = GraphedBagStep(model, blindno.mse_loss, opt, DataParallel(opt), xb, yb, grid)
     key = gs.replay(idx)
     torch.cuda.synchronize()
     for h in hooks:
         h.remove()
     masks = rec[-10:]
+    dbasis_gpu = rec_db[-1].clone()
     out_gpu, loss_gpu = gs.out[key].clone(), gs.loss[key].clone()
     pnames = {id(q): k for k, q in model.named_parameters()}
     grads_gpu = {pnames[id(prm)]: opt.grad[off:off + sz].detach().clone()
@@ -598,9 +606,19 @@ def parity_check_nio(model, graphed, opt, xb, yb, grid, T, seed):
     flips = sum(int((a != b).sum()) for a, b in zip(masks, own))
     total = sum(a.numel() for a in masks)
     del own
-    out64 = cpu_ref.niofp2d_fft(p64, xb.double(), grid.double(), idx=list(idx), heads=heads, branch_masks=masks)
+    taps = {}
+    out64 = cpu_ref.niofp2d_fft(p64, xb.double(), grid.double(), idx=list(idx), heads=heads, branch_masks=masks,
+                                taps=taps)
     loss64 = ((out64 - yb.double()) ** 2).mean()
     loss64.backward()
+    dbasis64 = taps.pop("basis").grad.detach()
+    # the trunk as a stage as well: dL/dbasis vs fp64, and the trunk's gradients vs the fp64 trunk
+    # given the replay's dL/dbasis.  Its BatchNorm1d over the 16384 grid points sees a nearly
+    # constant upstream gradient (rank B = 4): fp32 batch sums there cost 1e-3 of the trunk's
+    # gradients (torch's GPU BatchNorm too; its CPU one sums in fp64), csrc/batchnorm.hip sums in fp64
+    pt = {k[len("trunk."):]: v.detach().clone().requires_grad_(True) for k, v in p64.items()
+          if k.startswith("trunk.")}
+    cpu_ref._ffn(pt, grid.double().reshape(-1, 2), 3).backward(dbasis_gpu.double())
 
     def rel(a, b):
         a, b = a.double().cpu(), b.double().cpu()
@@ -611,8 +629,14 @@ def parity_check_nio(model, graphed, opt, xb, yb, grid, T, seed):
 
     skip = ("layers.0.bias",)
     keys = [k for k in grads_gpu if not k.endswith(skip)]
-    gw, gk = max((rel(grads_gpu[k].view(p64[k].shape), p64[k].grad), k) for k in keys)
-    rw, rk = max((rel(p32[k].grad, p64[k].grad), k) for k in keys)
+    eg = {k: rel(grads_gpu[k].view(p64[k].shape), p64[k].grad) for k in keys}
+    er = {k: rel(p32[k].grad, p64[k].grad) for k in keys}
+    es = {k: rel(grads_gpu[k].view(p64[k].shape), pt[k[len("trunk."):]].grad) for k in keys
+          if k.startswith("trunk.")}
+    e_db = rel(dbasis_gpu, dbasis64)
+    gw, gk = max((v, k) for k, v in eg.items())
+    rw, rk = max((v, k) for k, v in er.items())
+    top = sorted(keys, key=lambda k: -eg[k])[:6]
     gpu64, gpu32, ref64 = fields(out_gpu, out64.detach()), fields(out_gpu, out32.detach()), \
         fields(out32.detach(), out64.detach())
     fmt = lambda d: {k: float(f"{v:.3e}") for k, v in d.items()}
@@ -626,11 +650,16 @@ def parity_check_nio(model, graphed, opt, xb, yb, grid, T, seed):
                                loss=float(f"{abs(float(loss_gpu) - float(loss64)) / abs(float(loss64)):.3e}")),
            "ref_fp32_vs_fp64": dict(fmt(ref64), grad_max=float(f"{rw:.3e}"), grad_worst=rk,
                                     note="the fp32 reference takes its own LeakyReLU branches"),
+           "grads_worst": {k: {"gpu": float(f"{eg[k]:.3e}"), "ref_fp32": float(f"{er[k]:.3e}")}
+                                      for k in top},
+           "trunk_stage": {"dbasis": float(f"{e_db:.3e}"),
+                           "grad_max": float(f"{max(es.values()):.3e}"),
+                           "note": "trunk gradients vs the fp64 trunk given the replay's dL/dbasis"},
            "branch_flips": {"count": int(flips), "of": int(total), "bar": "1e-5 of all"},
            "grads_excluded": "conv biases ahead of batch-statistics BatchNorm (true gradient 0)",
            "tolerance": {"fields": 1e-5, "grads": 1e-4}}
     res["pass"] = bool(gpu64["fwd"] <= 1e-5 and max(gpu64["Fx"], gpu64["Fy"]) <= 1e-5 and gw <= 1e-4
-                       and gpu32["fwd"] <= 1e-5 and flips <= 1e-5 * total)
+                       and e_db <= 1e-5 and gpu32["fwd"] <= 1e-5 and flips <= 1e-5 * total)
     return res
 
 

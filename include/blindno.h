@@ -474,9 +474,10 @@ int blindno_conv_wgrad_g(const float* dz, const float* x, float* partial, int nc
  * nn.BatchNorm2d + nn.LeakyReLU(inplace) pair of each block).  z (Npad, C, HW) NCHW, batch =
  * rows [0, N); rows [N, Npad) of y / dz are written 0.  training != 0: batch statistics
  * (biased variance), running_mean/var updated with momentum (unbiased variance) when non-NULL;
- * training == 0: running statistics.  save (C, 4) = mean, invstd, gamma invstd,
- * beta - mean gamma invstd (written by the forward, read by the backward).  partial: scratch of
- * C * blindno_bn_act_nslices(N, C, HW) * 2 floats; coef (C, 3) scratch of the backward.
+ * training == 0: running statistics.  save (C, 4) = mean, invstd, gamma invstd, beta
+ * (y = act(gamma invstd (z - mean) + beta); written by the forward, read by the backward).
+ * partial: 8-B aligned scratch of C * blindno_bn_act_nslices(N, C, HW) * 4 floats (2 fp64 sums
+ * per slice: the statistics accumulate in fp64); coef (C, 3) scratch of the backward.
  * gamma/beta may be NULL (affine=False); dgamma/dbeta may be NULL. */
 int blindno_bn_act_nslices(int N, int C, int HW);
 int blindno_bn_act_fwd(const float* z, const float* gamma, const float* beta, float* run_mean,

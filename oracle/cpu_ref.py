@@ -187,7 +187,8 @@ def _ffn(p, x, n_hidden_layers):
 def niofp2d_fft(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
                 idx: Optional[Sequence[int]] = None, n_hidden_layers: int = 3,
                 heads: Sequence[str] = ("fno_drift", "fno_diffusion"),
-                branch_masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
+                branch_masks: Optional[Sequence[torch.Tensor]] = None,
+                taps: Optional[dict] = None) -> torch.Tensor:
     """NIOFP2D.forward, 2d_FPE/NIOModules.py:47-83 (NC heads fno_Fx/fno_Fy:
     2d_Non_conservative_FPE/NIOModules.py:46-82): the Encoder2D branch on every drawn snapshot,
     the FFN trunk on the grid points, DeepOnetNoBiasOrg ``(w @ basis^T + b0) / sqrt(p)``
@@ -197,6 +198,9 @@ def niofp2d_fft(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
     B, L, nx, ny = x.shape
     w = encoder2d_conv(sub_params(p, "branch"), x.unsqueeze(2), branch_masks)
     basis = _ffn(sub_params(p, "trunk"), grid.reshape(-1, 2), n_hidden_layers)
+    if taps is not None and basis.requires_grad:
+        basis.retain_grad()          # dL/dbasis: the trunk's upstream gradient (bench.py parity)
+        taps["basis"] = basis
     u = ((w @ basis.T + p["deeponet.b0"]) / basis.shape[-1] ** 0.5).view(B, L, nx, ny)
     gcf = grid.permute(2, 0, 1).unsqueeze(0).expand(B, 2, nx, ny)
     h = _bag_mean(u, gcf, p["fc0.weight"], p["fc0.bias"])

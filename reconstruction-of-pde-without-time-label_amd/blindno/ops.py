@@ -34,6 +34,10 @@ MIX_F16 = False
 # of recomputing fc1 / GELU / GELU' per snapshot point.  False: the per-snapshot projection
 # kernels (csrc/project.hip) and the bag-mean kernel, as before.
 BAG_STATS = True
+# the bag-statistics projection keeps 3 KB per (bag, crop point) plus v (the last layer's field
+# size) from forward to backward: ~190 MB at config C, ~800 MB at config E (256^2, B = 4).
+# Above this budget the per-snapshot projection runs instead (same results).
+BAG_STATS_MAX_BYTES = 4 << 30
 
 
 def set_mix_precision(name: str) -> None:
@@ -1029,11 +1033,15 @@ class BagEncoderFn(torch.autograd.Function):
         width = bw.shape[0]
         h = _empty(B, S, width, like=X)
         ctx.bag = None
-        if BAG_STATS and Hd == 128 and Cout == 1 and L <= 1024:
+        nstats = query("blindno_project_bag_stats_floats", B, Ho, Wo) if Hd == 128 else 0
+        if (BAG_STATS and Hd == 128 and Cout == 1 and L <= 1024
+                and 4 * (nstats + Bn * C * P1 * P2) <= BAG_STATS_MAX_BYTES):
             # projection + bag mean at bag level: the backward becomes a reduction of the
-            # statistics the forward leaves (csrc/bagproj.hip)
+            # statistics the forward leaves (csrc/bagproj.hip).  stats and v are fresh buffers
+            # only this forward writes and only this backward reads (never handed to the caller),
+            # so they ride on ctx without save_for_backward's version check
             ubar = _empty(B, S, like=X)
-            stats = _empty(query("blindno_project_bag_stats_floats", B, Ho, Wo), like=X)
+            stats = _empty(nstats, like=X)
             v = _empty(Bn, C, P1, P2, like=X)
             call("blindno_project_bag_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b),
                  ptr(lw), ptr(ubar), ptr(stats), ptr(v), B, L, C, P1, P2, Ho, Wo, Hd, stream_ptr())
@@ -1078,11 +1086,10 @@ class BagEncoderFn(torch.autograd.Function):
         crop = (Ho, Wo) if n >= 2 else None
         dz = _empty(Bn, C, P1, P2, like=gh) if crop else torch.zeros(Bn, C, P1, P2, dtype=F32, device=gh.device)
         np_p = Hd * C + Hd + Cout * Hd + Cout
-        nchunk = query("blindno_project_bwd_nchunk", Bn, Ho, Wo)
+        nchunk = query("blindno_project_bag_bwd_nchunk" if bag is not None else "blindno_project_bwd_nchunk",
+                       B if bag is not None else Bn, Ho, Wo)
         partial = _empty(nchunk, np_p, like=gh)
         if bag is not None:
-            nchunk = query("blindno_project_bag_bwd_nchunk", B, Ho, Wo)
-            partial = _empty(nchunk, np_p, like=gh)
             call("blindno_project_bag_bwd", ptr(bag[0]), ptr(sgr), ptr(fc2w), ptr(lw), ptr(bag[1]),
                  ptr(dz), ptr(partial), nchunk, B, L, C, P1, P2, Ho, Wo, Hd, stream_ptr())
         elif lw is not None:
@@ -1435,7 +1442,7 @@ class BNActFn(torch.autograd.Function):
             bn.num_batches_tracked.add_(1)
             mom = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
         S = query("blindno_bn_act_nslices", n, C, HW)
-        partial = torch.empty(C * S * 2, device=z.device, dtype=F32)
+        partial = torch.empty(C * S * 4, device=z.device, dtype=F32)   # C S 2 fp64 sums
         save = torch.empty(C, 4, device=z.device, dtype=F32)
         y = torch.empty_like(z)
         rm = bn.running_mean if (track or not use_batch) else None
@@ -1455,7 +1462,7 @@ class BNActFn(torch.autograd.Function):
         dz = torch.empty_like(z)
         dgamma = torch.empty(C, device=z.device, dtype=F32) if gamma is not None and ctx.needs_input_grad[1] else None
         dbeta = torch.empty(C, device=z.device, dtype=F32) if ctx.needs_input_grad[2] else None
-        partial = torch.empty(C * S * 2, device=z.device, dtype=F32)
+        partial = torch.empty(C * S * 4, device=z.device, dtype=F32)   # C S 2 fp64 sums
         coef = torch.empty(C, 3, device=z.device, dtype=F32)
         call("blindno_bn_act_bwd", ptr(dy), ptr(z), ptr(gamma), ptr(save), ptr(dz), ptr(dgamma), ptr(dbeta),
              ptr(partial), ptr(coef), n, Npad, C, HW, slope, use_batch, stream_ptr())

@@ -12,7 +12,12 @@
 // Eval mode normalises with the running statistics.  Per-channel statistics are two-level
 // reductions in a fixed order (deterministic): S slices per channel write partial sums,
 // one finalize thread per channel combines them.  The sums are shifted by the channel's first
-// element (z[0, c, 0]) so sum/sum-of-squares keep their precision when |mean| >> std.
+// element (z[0, c, 0]) so sum/sum-of-squares keep their precision when |mean| >> std, and are
+// accumulated in fp64 (as torch's CPU BatchNorm does): the backward's mean of the upstream
+// gradient must be exact to fp32 rounding when that gradient is nearly constant over the batch
+// -- the NIO trunk's BatchNorm1d over 16384 grid points fed a rank-B gradient, where fp32 sums
+// left 7e-4 of gradient error upstream of the layer (tools/diag_trunk_graph.py; torch's GPU
+// BatchNorm, fp32 sums, measured the same 7e-4, its CPU one 4e-6).
 //
 // HBM traffic per element: forward 2 reads + 1 write (stats pass, apply pass), backward
 // 4 reads + 1 write (dy and z twice; nothing but z and the per-channel coefficients is saved).
@@ -35,13 +40,14 @@ constexpr int kSave = 4;
 
 __device__ __forceinline__ float leaky(float v, float slope) { return v > 0.f ? v : v * slope; }
 
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  v = wave_sum(v);
+__device__ __forceinline__ double block_sum(double v, double* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0) red[wave] = v;
   __syncthreads();
-  float s = 0.f;
+  double s = 0.0;
 #pragma unroll
   for (int w = 0; w < kBnThreads / 64; ++w) s += red[w];
   return s;
@@ -50,12 +56,12 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // partial[(c S + s) 2 + {0, 1}] = sums of (z - shift) and (z - shift)^2 over slice s of channel c
 template <bool VEC>
 __global__ __launch_bounds__(kBnThreads) void bn_stats_kernel(const float* __restrict__ z,
-                                                              float* __restrict__ partial, int N,
+                                                              double* __restrict__ partial, int N,
                                                               int C, int HW) {
-  __shared__ float red[kBnThreads / 64];
+  __shared__ double red[kBnThreads / 64];
   const int c = blockIdx.y, S = gridDim.x, s = blockIdx.x;
   const float shift = z[(int64_t)c * HW];
-  float s1 = 0.f, s2 = 0.f;
+  double s1 = 0.0, s2 = 0.0;
   if (VEC) {
     const int HW4 = HW >> 2;
     const int64_t M4 = (int64_t)N * HW4;
@@ -63,18 +69,18 @@ __global__ __launch_bounds__(kBnThreads) void bn_stats_kernel(const float* __res
       const int64_t n = e / HW4;
       const int q4 = (int)(e - n * HW4);
       const float4 v = *reinterpret_cast<const float4*>(z + (n * C + c) * HW + 4 * q4);
-      const float a = v.x - shift, b = v.y - shift, d = v.z - shift, f = v.w - shift;
+      const double a = v.x - shift, b = v.y - shift, d = v.z - shift, f = v.w - shift;
       s1 += (a + b) + (d + f);
-      s2 = fmaf(a, a, s2); s2 = fmaf(b, b, s2); s2 = fmaf(d, d, s2); s2 = fmaf(f, f, s2);
+      s2 = fma(a, a, s2); s2 = fma(b, b, s2); s2 = fma(d, d, s2); s2 = fma(f, f, s2);
     }
   } else {
     const int64_t M = (int64_t)N * HW;
     for (int64_t e = (int64_t)s * kBnThreads + threadIdx.x; e < M; e += (int64_t)S * kBnThreads) {
       const int64_t n = e / HW;
       const int q = (int)(e - n * HW);
-      const float a = z[(n * C + c) * HW + q] - shift;
+      const double a = z[(n * C + c) * HW + q] - shift;
       s1 += a;
-      s2 = fmaf(a, a, s2);
+      s2 = fma(a, a, s2);
     }
   }
   s1 = block_sum(s1, red);
@@ -85,7 +91,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_stats_kernel(const float* __res
   }
 }
 
-__global__ void bn_finalize_kernel(const float* __restrict__ z, const float* __restrict__ partial,
+__global__ void bn_finalize_kernel(const float* __restrict__ z, const double* __restrict__ partial,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ run_mean, float* __restrict__ run_var,
                                    float* __restrict__ save, int S, int N, int C, int HW, float eps,
@@ -95,15 +101,15 @@ __global__ void bn_finalize_kernel(const float* __restrict__ z, const float* __r
   float mean, invstd;
   if (training) {
     const double M = (double)N * HW;
-    float s1 = 0.f, s2 = 0.f;
+    double s1 = 0.0, s2 = 0.0;
     for (int s = 0; s < S; ++s) {
       s1 += partial[((int64_t)c * S + s) * 2 + 0];
       s2 += partial[((int64_t)c * S + s) * 2 + 1];
     }
     const float shift = z[(int64_t)c * HW];
-    const float m1 = (float)(s1 / M);                       // mean of (z - shift)
-    const float var = fmaxf((float)(s2 / M) - m1 * m1, 0.f); // biased
-    mean = shift + m1;
+    const double m1 = s1 / M;                                    // mean of (z - shift)
+    const float var = (float)fmax(s2 / M - m1 * m1, 0.0);       // biased
+    mean = (float)(shift + m1);
     invstd = 1.0f / sqrtf(var + eps);
     if (run_mean) {
       const float unbiased = M > 1.0 ? (float)(var * (M / (M - 1.0))) : var;
@@ -161,17 +167,17 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const float* __res
 template <bool VEC>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_stats_kernel(
     const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ save,
-    float* __restrict__ partial, int N, int C, int HW, float slope) {
-  __shared__ float red[kBnThreads / 64];
+    double* __restrict__ partial, int N, int C, int HW, float slope) {
+  __shared__ double red[kBnThreads / 64];
   const int c = blockIdx.y, S = gridDim.x, s = blockIdx.x;
   const float mean = save[c * kSave + 0], invstd = save[c * kSave + 1];
   const float a = save[c * kSave + 2], b = save[c * kSave + 3];
-  float sg = 0.f, sgx = 0.f;
+  double sg = 0.0, sgx = 0.0;
   auto acc = [&](float zv, float dv) {
     const float zc = zv - mean;
     const float g = fmaf(a, zc, b) > 0.f ? dv : dv * slope;
-    sg += g;
-    sgx = fmaf(g, zc * invstd, sgx);
+    sg += (double)g;
+    sgx = fma((double)g, (double)(zc * invstd), sgx);
   };
   if (VEC) {
     const int HW4 = HW >> 2;
@@ -201,20 +207,20 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_stats_kernel(
 
 // dgamma = sum g xhat, dbeta = sum g; coef[c] = (k1 = gamma invstd, mean g, mean g xhat)
 // (train mode; eval mode has no batch-statistics terms: mean terms 0)
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial,
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ partial,
                                        const float* __restrict__ gamma,
                                        const float* __restrict__ save, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ coef, int S,
                                        int N, int C, int HW, int training) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float sg = 0.f, sgx = 0.f;
+  double sg = 0.0, sgx = 0.0;
   for (int s = 0; s < S; ++s) {
     sg += partial[((int64_t)c * S + s) * 2 + 0];
     sgx += partial[((int64_t)c * S + s) * 2 + 1];
   }
-  if (dgamma) dgamma[c] = sgx;
-  if (dbeta) dbeta[c] = sg;
+  if (dgamma) dgamma[c] = (float)sgx;
+  if (dbeta) dbeta[c] = (float)sg;
   const double M = (double)N * HW;
   coef[c * 3 + 0] = (gamma ? gamma[c] : 1.0f) * save[c * kSave + 1];
   coef[c * 3 + 1] = training ? (float)(sg / M) : 0.f;
@@ -296,11 +302,14 @@ BLINDNO_API int blindno_bn_act_fwd(const float* z, const float* gamma, const flo
   hipStream_t st = (hipStream_t)stream;
   const bool vec = (HW & 3) == 0;
   const int S = bn_slices(N, HW);
+  // partial holds C S 2 doubles (8-B aligned)
+  double* pd = reinterpret_cast<double*>(partial);
   if (training) {
-    if (vec) bn_stats_kernel<true><<<dim3(S, C), kBnThreads, 0, st>>>(z, partial, N, C, HW);
-    else bn_stats_kernel<false><<<dim3(S, C), kBnThreads, 0, st>>>(z, partial, N, C, HW);
+    if (((uintptr_t)partial & 7) != 0) return (int)hipErrorInvalidValue;
+    if (vec) bn_stats_kernel<true><<<dim3(S, C), kBnThreads, 0, st>>>(z, pd, N, C, HW);
+    else bn_stats_kernel<false><<<dim3(S, C), kBnThreads, 0, st>>>(z, pd, N, C, HW);
   }
-  bn_finalize_kernel<<<cdiv(C, 64), 64, 0, st>>>(z, partial, gamma, beta, run_mean, run_var, save,
+  bn_finalize_kernel<<<cdiv(C, 64), 64, 0, st>>>(z, pd, gamma, beta, run_mean, run_var, save,
                                                 S, N, C, HW, eps, momentum, training);
   const int64_t total = (int64_t)Npad * C * HW;
   if (vec) bn_apply_kernel<true><<<apply_grid(total, true), kBnThreads, 0, st>>>(z, save, y, N, Npad, C, HW, slope);
@@ -317,9 +326,11 @@ BLINDNO_API int blindno_bn_act_bwd(const float* dy, const float* z, const float*
   hipStream_t st = (hipStream_t)stream;
   const bool vec = (HW & 3) == 0;
   const int S = bn_slices(N, HW);
-  if (vec) bn_bwd_stats_kernel<true><<<dim3(S, C), kBnThreads, 0, st>>>(dy, z, save, partial, N, C, HW, slope);
-  else bn_bwd_stats_kernel<false><<<dim3(S, C), kBnThreads, 0, st>>>(dy, z, save, partial, N, C, HW, slope);
-  bn_bwd_finalize_kernel<<<cdiv(C, 64), 64, 0, st>>>(partial, gamma, save, dgamma, dbeta, coef, S, N,
+  if (((uintptr_t)partial & 7) != 0) return (int)hipErrorInvalidValue;
+  double* pd = reinterpret_cast<double*>(partial);
+  if (vec) bn_bwd_stats_kernel<true><<<dim3(S, C), kBnThreads, 0, st>>>(dy, z, save, pd, N, C, HW, slope);
+  else bn_bwd_stats_kernel<false><<<dim3(S, C), kBnThreads, 0, st>>>(dy, z, save, pd, N, C, HW, slope);
+  bn_bwd_finalize_kernel<<<cdiv(C, 64), 64, 0, st>>>(pd, gamma, save, dgamma, dbeta, coef, S, N,
                                                     C, HW, training);
   const int64_t total = (int64_t)Npad * C * HW;
   if (vec) bn_bwd_apply_kernel<true><<<apply_grid(total, true), kBnThreads, 0, st>>>(dy, z, save, coef, dz, N, Npad, C, HW, slope);

@@ -568,7 +568,9 @@ bool use_tm(int mode, const ConvArgs& g) {
 template <int MODE>
 void launch_igemm(dim3 g3, int M, int Ncol, const float* pa, const float* pb, const float* bias,
                   float* out, const ConvArgs& g, hipStream_t st) {
-  if (use_tm(MODE, g)) return launch_igemm_t<MODE, true>(g3, M, Ncol, pa, pb, bias, out, g, st);
+  // BWD_W's vector loads read dy (pa) as f32x4: a C host may hand an offset pointer
+  const bool aligned = MODE != BWD_W || ((uintptr_t)pa & 15) == 0;
+  if (aligned && use_tm(MODE, g)) return launch_igemm_t<MODE, true>(g3, M, Ncol, pa, pb, bias, out, g, st);
   launch_igemm_t<MODE, false>(g3, M, Ncol, pa, pb, bias, out, g, st);
 }
 

@@ -937,18 +937,9 @@ bool rowfuse_shape(int Bn, int C, int P1, int P2, int m2) {
          2 * m2 <= P2 && Bn > 0 && (int64_t)Bn * C * P1 * P2 < INT32_MAX;
 }
 
-RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
+// the general kernel's geometry (rowinv_mfma_kernel)
+RowinvGeom rowinv_geom_general(int Bn, int C, int P1, int P2, int m2) {
   RowinvGeom g;
-  if (rowfuse_shape(Bn, C, P1, P2, m2)) {
-    // whole 16-row blocks per work item, one per wave; partials are per workgroup
-    g.TPW = P2 / 16;
-    g.nitems = Bn * (P1 / 16);
-    const int b = (g.nitems + kW - 1) / kW;
-    g.blocks = b < ROWFUSE_BLOCKS ? b : ROWFUSE_BLOCKS;
-    g.ldsb = false;
-    g.lds = 0;
-    return g;
-  }
   const int KS = (m2 + 1) / 2, NT = (P2 + 15) / 16;
   const int NG = (C + 3) / 4;
   const int64_t base = (int64_t)((Bn * P1 + 3) / 4) * NG;
@@ -972,6 +963,19 @@ RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   return g;
 }
 
+RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
+  if (!rowfuse_shape(Bn, C, P1, P2, m2)) return rowinv_geom_general(Bn, C, P1, P2, m2);
+  // whole 16-row blocks per work item, one per wave; partials are per workgroup
+  RowinvGeom g;
+  g.TPW = P2 / 16;
+  g.nitems = Bn * (P1 / 16);
+  const int b = (g.nitems + kW - 1) / kW;
+  g.blocks = b < ROWFUSE_BLOCKS ? b : ROWFUSE_BLOCKS;
+  g.ldsb = false;
+  g.lds = 0;
+  return g;
+}
+
 template <int MODE, int ACT, int WG, int LIFT = 0>
 int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
                   const float* bc, float* out, const float* TB, float* partial, int nblocks,
@@ -988,13 +992,6 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
   if (WG && C > 4) return (int)hipErrorInvalidValue;
   const int64_t zel = (int64_t)Bn * P1 * m2 * C * 2, fel = (int64_t)Bn * C * P1 * P2;
   if (zel >= INT32_MAX || fel >= ((int64_t)1 << 40)) return (int)hipErrorInvalidValue;
-  RowinvGeom g = rowinv_geom(Bn, C, P1, P2, m2);
-  size_t sh = g.lds;
-  if (WG) {
-    const size_t need = sizeof(float) * (size_t)kW * (C * C + C + (LIFT ? 4 * C : 0));
-    if (need > sh) sh = need;
-  }
-  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
   const int cm = C <= 4 ? 4 : (C <= 8 ? 8 : (C <= 16 ? 16 : 32));
   const int ks = (m2 + 1) / 2;
   if (ks > 24) return (int)hipErrorInvalidValue;               // m2 <= 48
@@ -1051,6 +1048,16 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       return (int)hipGetLastError();
     }
   }
+  // the general kernel's own geometry also where the shape suits rowfuse but a launch-time gate
+  // (G, alignment, crop width) sent it here; nblocks stays the caller's (it sized the partials,
+  // and the persistent general kernel strides its items over any grid)
+  const RowinvGeom g = rowinv_geom_general(Bn, C, P1, P2, m2);
+  size_t sh = g.lds;
+  if (WG) {
+    const size_t need = sizeof(float) * (size_t)kW * (C * C + C + (LIFT ? 4 * C : 0));
+    if (need > sh) sh = need;
+  }
+  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
   if constexpr (!WG && !LIFT) {
     // wide fields with the spectrum in A-tile order (rowinv_tile_layout; full-field dz only)
     if (rowinv_tile_layout(Bn, C, P1, P2, m2) && dN1 == P1 && dN2 == P2) {

@@ -306,6 +306,42 @@ def test_ffn_trunk_native_matches_fp64():
                 assert int(b) == int(b64[k]) == it + 1, k
 
 
+def test_ffn_trunk_nearly_constant_upstream_gradient():
+    """The trunk as config D trains it: its upstream gradient dL/dbasis is rank B = 4 over the
+    16384 grid points and nearly constant, so the BatchNorm1d backward subtracts a batch mean that
+    all but cancels the gradient.  The batch sums must then be exact to fp32 rounding (csrc/
+    batchnorm.hip sums in fp64, like torch's CPU BatchNorm): fp32 sums left ~1e-3 of error in every
+    gradient upstream of the layer (torch's GPU BatchNorm prints its own error here for context)."""
+    import copy
+    from blindno.deeponet import FFN
+    torch.manual_seed(5)
+    f = FFN(2, 25, 3, 100, "leaky_relu", 0.0).cuda().train()
+    ref = copy.deepcopy(f).double()
+    gx, gy = torch.meshgrid(torch.linspace(0, 1, 128), torch.linspace(0, 1, 128), indexing="ij")
+    grid = torch.stack([gx, gy], -1).reshape(-1, 2).cuda()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    cot = (torch.randn(1, 25, device="cuda", generator=g)
+           + 1e-3 * torch.randn(grid.shape[0], 25, device="cuda", generator=g))
+    y = f(grid)
+    f.zero_grad()
+    y.backward(cot)
+    ref.zero_grad()
+    ref(grid.double()).backward(cot.double())
+    tg = copy.deepcopy(f)
+    tg.zero_grad()
+    tg._native_ok = lambda x: False           # torch's fp32 GPU ops, for context
+    tg(grid).backward(cot)
+    p64, pt = dict(ref.named_parameters()), dict(tg.named_parameters())
+    worst = 0.0
+    for k, p in f.named_parameters():
+        e = rel_l2(p.grad.cpu().numpy(), p64[k].grad.cpu().numpy())
+        et = rel_l2(pt[k].grad.cpu().numpy(), p64[k].grad.cpu().numpy())
+        print(f"  {k:24s} native {e:.2e}  torch-gpu fp32 {et:.2e}")
+        worst = max(worst, e)
+        assert e <= 1e-4, k
+    print(f"  worst {worst:.2e}")
+
+
 @pytest.mark.parametrize("B,L,S,weighted", [(4, 75, 16384, False), (2, 51, 80, True), (3, 1, 6400, False)])
 def test_deeponet_bag_matches_fp64(B, L, S, weighted):
     """ops.DeepONetBagFn (DeepOnetNoBiasOrg + the bag mean that reads it, csrc/deeponet.hip) vs

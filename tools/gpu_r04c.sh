@@ -8,3 +8,5 @@ timeout -k 10 500 python -u bench.py --config D --no-cpu --steps 10 --warmup 3 >
 cut -c1-300 gpurun_out/bench_${TAG}_D.json
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -5 gpurun_out/bench_$TAG.err; exit 1; }
 cut -c1-300 gpurun_out/bench_$TAG.json
+BLINDNO_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 2 --no-cpu --no-parity > gpurun_out/bench_${TAG}_n2gloo.json 2> gpurun_out/bench_${TAG}_n2gloo.err || { tail -5 gpurun_out/bench_${TAG}_n2gloo.err; exit 1; }
+python3 -c "import json;d=json.loads(open('gpurun_out/bench_${TAG}_n2gloo.json').read().strip().splitlines()[-1]);print({k:d['dist'][k] for k in ('params_identical_across_ranks','params_max_abs_diff_vs_rank0','bag_ids_per_rank')})"
