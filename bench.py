@@ -356,6 +356,14 @@ def main():
                 res["roofline"]["valu_issue_util_source"] = (
                     "PMC SQ_INSTS_VALU / _TRANS_F32 / _MFMA, GRBM_GUI_ACTIVE clock, kbench Bn=300: " +
                     rec["source"])
+            pb = os.path.join(ROOT, "profiles", "pmc_benched_step.json")
+            if res["roofline"] and a.config == "C" and os.path.exists(pb):
+                # the same utilisation over the benched step's own dispatches (graph replays,
+                # drawn bag sizes; tools/pmc_bench.sh + tools/pmc_bench.py)
+                sb = json.load(open(pb))
+                if "valu_issue_util" in sb:
+                    res["roofline"]["valu_issue_util_benched_step"] = sb["valu_issue_util"]
+                    res["roofline"]["valu_issue_util_benched_step_source"] = sb.get("source")
             if a.config in ("C", "E"):
                 res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
         if world == 1 and a.config in ("A", "B", "C", "D", "E"):

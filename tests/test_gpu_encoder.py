@@ -309,37 +309,41 @@ def test_ffn_trunk_native_matches_fp64():
 def test_ffn_trunk_nearly_constant_upstream_gradient():
     """The trunk as config D trains it: its upstream gradient dL/dbasis is rank B = 4 over the
     16384 grid points and nearly constant, so the BatchNorm1d backward subtracts a batch mean that
-    all but cancels the gradient.  The batch sums must then be exact to fp32 rounding (csrc/
-    batchnorm.hip sums in fp64, like torch's CPU BatchNorm): fp32 sums left ~1e-3 of error in every
-    gradient upstream of the layer (torch's GPU BatchNorm prints its own error here for context)."""
+    all but cancels the gradient, and every fp32 evaluation carries an error floor of eps times
+    the cancellation ratio.  Bar: the reference's own fp32 execution (torch on the CPU, whose
+    BatchNorm sums in fp64 like csrc/batchnorm.hip) sets the floor; the native trunk stays within
+    3x of it (or 1e-4).  torch's GPU BatchNorm (fp32 sums) is printed for context: what fp32 batch
+    sums cost here (config D's trunk gradients: 1.4e-3 before the fp64 sums, bench parity leg)."""
     import copy
     from blindno.deeponet import FFN
     torch.manual_seed(5)
     f = FFN(2, 25, 3, 100, "leaky_relu", 0.0).cuda().train()
     ref = copy.deepcopy(f).double()
+    cpu = copy.deepcopy(f).cpu()
     gx, gy = torch.meshgrid(torch.linspace(0, 1, 128), torch.linspace(0, 1, 128), indexing="ij")
     grid = torch.stack([gx, gy], -1).reshape(-1, 2).cuda()
     g = torch.Generator(device="cuda").manual_seed(6)
     cot = (torch.randn(1, 25, device="cuda", generator=g)
-           + 1e-3 * torch.randn(grid.shape[0], 25, device="cuda", generator=g))
+           + 1e-2 * torch.randn(grid.shape[0], 25, device="cuda", generator=g))
     y = f(grid)
     f.zero_grad()
     y.backward(cot)
     ref.zero_grad()
     ref(grid.double()).backward(cot.double())
+    cpu.zero_grad()
+    cpu(grid.cpu()).backward(cot.cpu())
     tg = copy.deepcopy(f)
     tg.zero_grad()
     tg._native_ok = lambda x: False           # torch's fp32 GPU ops, for context
     tg(grid).backward(cot)
-    p64, pt = dict(ref.named_parameters()), dict(tg.named_parameters())
-    worst = 0.0
+    p64, pc, pt = dict(ref.named_parameters()), dict(cpu.named_parameters()), dict(tg.named_parameters())
     for k, p in f.named_parameters():
-        e = rel_l2(p.grad.cpu().numpy(), p64[k].grad.cpu().numpy())
-        et = rel_l2(pt[k].grad.cpu().numpy(), p64[k].grad.cpu().numpy())
-        print(f"  {k:24s} native {e:.2e}  torch-gpu fp32 {et:.2e}")
-        worst = max(worst, e)
-        assert e <= 1e-4, k
-    print(f"  worst {worst:.2e}")
+        want = p64[k].grad.cpu().numpy()
+        e = rel_l2(p.grad.cpu().numpy(), want)
+        ec = rel_l2(pc[k].grad.numpy(), want)
+        et = rel_l2(pt[k].grad.cpu().numpy(), want)
+        print(f"  {k:24s} native {e:.2e}  cpu fp32 {ec:.2e}  torch-gpu fp32 {et:.2e}")
+        assert e <= max(1e-4, 3.0 * ec), k
 
 
 @pytest.mark.parametrize("B,L,S,weighted", [(4, 75, 16384, False), (2, 51, 80, True), (3, 1, 6400, False)])

@@ -36,6 +36,7 @@ KERNELS = {
     "blindno_project_fwd": r"project_fwd_mfma_kernel<4,",
     "blindno_rowdft": r"rowdft_mfma_kernel<",
     "blindno_rowidft_epi": r"rowfuse_kernel<0, 1, 0, 0, 0,",
+    "colfuse (blindno_colpass, FNO_input)": r"colfuse_kernel<0,",
     "blindno_rowidft_epi_rd": r"rowfuse_kernel<0, 1, 0, 0, 2,",
     "blindno_rowidft_bwd": r"rowfuse_kernel<1, 1, 1, 0, 0,",
     "blindno_rowidft_bwd_rd_crop": r"rowfuse_kernel<1, 1, 1, 0, 1,",
