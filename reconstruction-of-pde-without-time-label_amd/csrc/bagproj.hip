@@ -40,8 +40,11 @@ constexpr int kHd = 128;            // fc1 = Linear(width, 128)
 constexpr int kNStat = 6;           // A, S, Q_0..Q_3
 constexpr int kTileF4 = (kHd / 16) * kNStat * 64;   // float4 slots per 16-point tile: 3072
 constexpr int kMaxU = 1024;
+#ifndef BAGPROJ_QUAD
+#define BAGPROJ_QUAD 1
+#endif
 #ifndef BAGPROJ_FWD_WAVES
-#define BAGPROJ_FWD_WAVES 2
+#define BAGPROJ_FWD_WAVES 3
 #endif
 
 // point f of the flattened (bag, crop point) space -> offset of (bag b, snapshot 0, channel 0,
@@ -191,15 +194,35 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
         const float az = zs[buf][l][c16][g4];
         const f32x2 wl = splat2(slw[l0 + l]);
         f32x2 vp[4];
+#if BAGPROJ_QUAD
+        // both tiles' pre-activations first, then the four pairs' GELU / GELU' in lockstep
+        f32x2 hq[4], sq[4], eq[4];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
           f32x4 d = {bb[tt][0], bb[tt][1], bb[tt][2], bb[tt][3]};
           d = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[tt], az, d, 0, 0, 0);
+          hq[2 * tt] = (f32x2){d[0], d[1]};
+          hq[2 * tt + 1] = (f32x2){d[2], d[3]};
+        }
+        norm_cdf_quad_pdf_centered(hq, sq, eq);
+#endif
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+#if !BAGPROJ_QUAD
+          f32x4 d = {bb[tt][0], bb[tt][1], bb[tt][2], bb[tt][3]};
+          d = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[tt], az, d, 0, 0, 0);
           const f32x2 h[2] = {{d[0], d[1]}, {d[2], d[3]}};
+#else
+          const f32x2 h[2] = {hq[2 * tt], hq[2 * tt + 1]};
+#endif
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
+#if BAGPROJ_QUAD
+            const f32x2 ep = eq[2 * tt + i], sg = sq[2 * tt + i];
+#else
             f32x2 ep;
             const f32x2 sg = norm_cdf_pair_pdf_centered(h[i], ep);   // Phi - 1/2
+#endif
             const f32x2 gd = pk_fma(h[i], ep, sg);                  // GELU' - 1/2
             A[tt][i] = pk_fma(wl, h[i] * sg, A[tt][i]);             // lw k h (Phi - 1/2)
             S[tt][i] = pk_fma(wl, gd, S[tt][i]);

@@ -77,5 +77,38 @@ __device__ __forceinline__ f32x2 norm_cdf_pair_pdf_centered(f32x2 hk, f32x2& ep)
   return (f32x2){copysignf(m.x, hk.x), copysignf(m.y, hk.y)};
 }
 
+// norm_cdf_pair_pdf_centered on four pairs in lockstep: every step of the evaluation is issued
+// for the four pairs before the next step, so consecutive packed ops are independent (a packed
+// op reading the previous VALU result costs a wait state on gfx950: the one-pair chain carried
+// an s_nop between each Horner step)
+__device__ __forceinline__ void norm_cdf_quad_pdf_centered(const f32x2 (&hk)[4], f32x2 (&s)[4],
+                                                           f32x2 (&ep)[4]) {
+  f32x2 t[4], q[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    t[j] = (f32x2){__builtin_amdgcn_rcpf(fmaf(fabsf(hk[j].x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk[j].y), kT, 1.0f))};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2 ea = pk_fma(-hk[j], hk[j], splat2(kLog2Kp));
+    ep[j] = (f32x2){__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q[j] = pk_fma(t[j], splat2(1.129831073415752f), splat2(-1.5468324069611348f));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q[j] = pk_fma(t[j], q[j], splat2(1.513048048260859f));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q[j] = pk_fma(t[j], q[j], splat2(-0.3028373926078324f));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q[j] = pk_fma(t[j], q[j], splat2(0.27125769625911544f));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q[j] = -(q[j] * t[j]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2 m = pk_fma(q[j], ep[j], splat2(0.5f));         // 1/2 - half
+    s[j] = (f32x2){copysignf(m.x, hk[j].x), copysignf(m.y, hk[j].y)};
+  }
+}
+
 }  // namespace gelu_pk
 }  // namespace blindno

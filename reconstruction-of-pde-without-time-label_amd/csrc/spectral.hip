@@ -482,8 +482,10 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
 //   3. column inverse Z = Y conj(F) on the matrix cores, the 4 waves over the P1 / 16 row tiles.
 // Same twiddle images (FB, GB) and the same summation order within each K chunk as the split
 // kernels; Xs (the saved spectrum) is written as before, Y is not.
-template <int DIR, int HBC>
-__global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__ At,
+// NW waves per workgroup: 8 for the small head launches (one (sample, mode) pair of 12 channels
+// per workgroup and only Bn m2 of them: with 4 waves the chip runs one wave per SIMD)
+template <int DIR, int HBC, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restrict__ At,
                                                       const float2* __restrict__ Wt,
                                                       const f32x4* __restrict__ FB,
                                                       const f32x4* __restrict__ GB,
@@ -493,8 +495,10 @@ __global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__
                                                       int KS, int vec, int Bg, int64_t wtgs,
                                                       int tiled) {
   constexpr int kLd = 65;                          // LDS row stride (float2) for K1p <= 64
-  // DFT partials, chunk kc in columns [kc K1p, (kc + 1) K1p) (KS K1p <= 64), then Y
-  __shared__ float2 sP[16][kLd];
+  constexpr int kLdP = 16 * NW + 1;                 // DFT partials: KS K1p <= 16 NW
+  constexpr int kT = 64 * NW;
+  // DFT partials, chunk kc in columns [kc K1p, (kc + 1) K1p), then Y
+  __shared__ float2 sP[16][kLdP];
   __shared__ float2 sX[16][kLd];
   const int K1 = kept_rows_count(m1, P1);
   const int Jt = (K1 + 15) >> 4, K1p = Jt * 16;
@@ -514,7 +518,7 @@ __global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__
   {
     const bool rok = r16 < rows;
     const float2* ar = At + ((int64_t)q0 * Cin + (rok ? r16 : 0)) * P1;
-    for (int u = wave; u < Jt * KS; u += 4) {
+    for (int u = wave; u < Jt * KS; u += NW) {
       const int jt = u % Jt, kc = u / Jt;
       const int hb0 = kc * HBc;
       const int nhb = min(HBc, HB - hb0);
@@ -540,7 +544,7 @@ __global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__
   }
   __syncthreads();
   // chunk sum in order, the adjoint's c_k / (P1 P2) scale, the saved spectrum
-  for (int e = threadIdx.x; e < 16 * K1p; e += 256) {
+  for (int e = threadIdx.x; e < 16 * K1p; e += kT) {
     const int row = e / K1p, j = e - row * K1p;
     float2 v = sP[row][j];
     for (int kc = 1; kc < KS; ++kc) {
@@ -561,7 +565,7 @@ __global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__
   __syncthreads();
 
   // ---- 2. the mix: Y[p o][j] into sP (rows >= orows and columns >= K1 zero)
-  for (int e = threadIdx.x; e < 16 * K1p; e += 256) {
+  for (int e = threadIdx.x; e < 16 * K1p; e += kT) {
     const int o = e % Cout;                       // output channel fastest: contiguous weights
     const int t = e / Cout;
     const int j = t % K1p, p = t / K1p;
@@ -596,7 +600,7 @@ __global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__
     sP[orow][j] = make_float2(re, im);
   }
   // rows past G Cout (e.g. 12-channel pairs) are zero: the inverse's A operand reads all 16
-  for (int e = threadIdx.x; e < 16 * K1p; e += 256) {
+  for (int e = threadIdx.x; e < 16 * K1p; e += kT) {
     const int row = e / K1p;
     if (row >= min(16, (16 / Cout) * Cout)) sP[row][e - row * K1p] = make_float2(0.f, 0.f);
   }
@@ -605,7 +609,7 @@ __global__ __launch_bounds__(256) void colfuse_kernel(const float2* __restrict__
   // ---- 3. column inverse: D[orow][h] = sum_j Y[orow][j] conj F[h][j], h tiles over the waves
   const int Ht = HB;
   const int R = m2 * Cout;
-  for (int ht = wave; ht < Ht; ht += 4) {
+  for (int ht = wave; ht < Ht; ht += NW) {
     const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
     f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
     // every j block's twiddles in flight before the first MFMA (Jt <= 4)
@@ -991,6 +995,16 @@ bool colfuse_on() {
   return g_colfuse != 0;
 }
 
+// colfuse workgroup size: 0 = by launch size (default), 4 or 8 waves forced (BLINDNO_COLFUSE_WAVES)
+int g_colfuse_waves = -1;
+int colfuse_waves() {
+  if (g_colfuse_waves < 0) {
+    const char* e = getenv("BLINDNO_COLFUSE_WAVES");
+    g_colfuse_waves = e ? atoi(e) : 0;
+  }
+  return g_colfuse_waves;
+}
+
 BLINDNO_API int blindno_set_colfuse(int on) {
   const int prev = colfuse_on() ? 1 : 0;
   g_colfuse = on ? 1 : 0;
@@ -1019,25 +1033,30 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   hipStream_t st = (hipStream_t)stream;
   // the fused pass: fp32 mix, Cin and Cout equal (G pairs fill the same 16 rows on both sides),
   // at most 64 kept rows, at most 10 row blocks per K chunk
-  const int KSf = Jt >= 4 ? 1 : 4 / Jt;          // K chunks so that the 4 waves have units
+  // workgroups of 8 waves when the launch has fewer than two workgroups per CU (the heads)
+  const int G16 = 16 / cin;
+  const int NWf = (colfuse_waves() == 8 || (colfuse_waves() == 0 && cdiv(npairs, G16 > 0 ? G16 : 1) < 512)) ? 8 : 4;
+  const int KSf = Jt >= NWf ? 1 : NWf / Jt;      // K chunks so that the waves have units
   if (colfuse_on() && !h16 && Ci == Co && Ci <= 16 && K1p <= 64 && (HB + KSf - 1) / KSf <= 10) {
     const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
-    const int G = 16 / cin;
+    const int G = G16;
     const int KS = KSf;
     const int HBc = (HB + KS - 1) / KS;
     const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
     const dim3 g((unsigned)cdiv(npairs, G));
-#define CF_(D_, H_)                                                                           \
-  colfuse_kernel<D_, H_><<<g, 256, 0, st>>>((const float2*)At, (const float2*)Wt,             \
-                                            (const f32x4*)FB, (const f32x4*)GB, (float2*)Xs,   \
-                                            (float2*)Z, (int)npairs, Ci, Co, P1, m1, m2, P2, G, \
-                                            KS, vec, Bg, wtgs, tiled)
-#define CFD_(H_) do { if (dir == 0) CF_(0, H_); else CF_(1, H_); } while (0)
+#define CF_(D_, H_, W_)                                                                          \
+  colfuse_kernel<D_, H_, W_><<<g, 64 * W_, 0, st>>>((const float2*)At, (const float2*)Wt,        \
+                                                    (const f32x4*)FB, (const f32x4*)GB,          \
+                                                    (float2*)Xs, (float2*)Z, (int)npairs, Ci, Co, \
+                                                    P1, m1, m2, P2, G, KS, vec, Bg, wtgs, tiled)
+#define CFW_(H_, W_) do { if (dir == 0) CF_(0, H_, W_); else CF_(1, H_, W_); } while (0)
+#define CFD_(H_) do { if (NWf == 8) CFW_(H_, 8); else CFW_(H_, 4); } while (0)
     if (HBc <= 3) CFD_(3);
     else if (HBc <= 5) CFD_(5);
     else if (HBc <= 10) CFD_(10);
     else return (int)hipErrorInvalidValue;
 #undef CFD_
+#undef CFW_
 #undef CF_
     return (int)hipGetLastError();
   }
