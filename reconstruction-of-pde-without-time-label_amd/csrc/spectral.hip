@@ -484,7 +484,8 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
 // kernels; Xs (the saved spectrum) is written as before, Y is not.
 // NW waves per workgroup: 8 for the small head launches (one (sample, mode) pair of 12 channels
 // per workgroup and only Bn m2 of them: with 4 waves the chip runs one wave per SIMD)
-template <int DIR, int HBC, int NW = 4>
+// H16: the fp16-operand mix of coldft_mix (config E), block-scaled over this workgroup's rows
+template <int DIR, int HBC, int NW = 4, bool H16 = false>
 __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restrict__ At,
                                                       const float2* __restrict__ Wt,
                                                       const f32x4* __restrict__ FB,
@@ -564,6 +565,30 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
   }
   __syncthreads();
 
+  // H16: block scale 2^e with max |component| * 2^e in [2^14, 2^15) over the spectra rows
+  float hs = 1.0f, hinv = 1.0f;
+  if constexpr (H16) {
+    __shared__ float smax[NW];
+    float mx = 0.f;
+    for (int e = threadIdx.x; e < rows * K1p; e += kT) {
+      const float2 v = sX[e / K1p][e % K1p];
+      mx = fmaxf(mx, fmaxf(fabsf(v.x), fabsf(v.y)));
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    if (lane == 0) smax[wave] = mx;
+    __syncthreads();
+    mx = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mx = fmaxf(mx, smax[w]);
+    if (mx > 0.f && mx < 3.0e38f) {
+      int ex;
+      frexpf(mx, &ex);
+      hs = ldexpf(1.0f, 15 - ex);
+      hinv = ldexpf(1.0f, ex - 15);
+    }
+  }
+
   // ---- 2. the mix: Y[p o][j] into sP (rows >= orows and columns >= K1 zero)
   for (int e = threadIdx.x; e < 16 * K1p; e += kT) {
     const int o = e % Cout;                       // output channel fastest: contiguous weights
@@ -579,16 +604,35 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
                               : Wt;
       const float2* wj = wg + ((int64_t)k * K1 + j) * Ci * Co;
       const float2* xp = &sX[p * Cin][j];
+      if constexpr (H16) {
 #pragma unroll 4
-      for (int c = 0; c < Cin; ++c) {
-        const float2 a = xp[c * kLd];
-        const float2 w = DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
-        if (DIR == 0) {
-          re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
-          im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
-        } else {                                    // conj(w) * a
-          re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
-          im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+        for (int c = 0; c < Cin; ++c) {
+          const float2 a = xp[c * kLd];
+          const f16x2 ah = {(_Float16)(a.x * hs), (_Float16)(a.y * hs)};
+          const float2 w = DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
+          const _Float16 wr = (_Float16)w.x, wi = (_Float16)w.y;
+          if (DIR == 0) {
+            re = __builtin_amdgcn_fdot2(ah, (f16x2){wr, (_Float16)(-wi)}, re, false);
+            im = __builtin_amdgcn_fdot2(ah, (f16x2){wi, wr}, im, false);
+          } else {
+            re = __builtin_amdgcn_fdot2(ah, (f16x2){wr, wi}, re, false);
+            im = __builtin_amdgcn_fdot2(ah, (f16x2){(_Float16)(-wi), wr}, im, false);
+          }
+        }
+        re *= hinv;
+        im *= hinv;
+      } else {
+#pragma unroll 4
+        for (int c = 0; c < Cin; ++c) {
+          const float2 a = xp[c * kLd];
+          const float2 w = DIR == 0 ? wj[c * Co + o] : wj[o * Co + c];
+          if (DIR == 0) {
+            re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
+            im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
+          } else {                                    // conj(w) * a
+            re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
+            im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+          }
         }
       }
       if (DIR == 0) {
@@ -995,6 +1039,16 @@ bool colfuse_on() {
   return g_colfuse != 0;
 }
 
+// the fused pass also for the fp16-operand mix (config E); BLINDNO_COLFUSE16=0: the split kernels
+int g_colfuse16 = -1;
+bool colfuse16_on() {
+  if (g_colfuse16 < 0) {
+    const char* e = getenv("BLINDNO_COLFUSE16");
+    g_colfuse16 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_colfuse16 != 0;
+}
+
 // colfuse workgroup size: 0 = by launch size (default), 4 or 8 waves forced (BLINDNO_COLFUSE_WAVES)
 int g_colfuse_waves = -1;
 int colfuse_waves() {
@@ -1037,18 +1091,21 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   const int G16 = 16 / cin;
   const int NWf = (colfuse_waves() == 8 || (colfuse_waves() == 0 && cdiv(npairs, G16 > 0 ? G16 : 1) < 512)) ? 8 : 4;
   const int KSf = Jt >= NWf ? 1 : NWf / Jt;      // K chunks so that the waves have units
-  if (colfuse_on() && !h16 && Ci == Co && Ci <= 16 && K1p <= 64 && (HB + KSf - 1) / KSf <= 10) {
+  if (colfuse_on() && (!h16 || colfuse16_on()) && Ci == Co && Ci <= 16 && K1p <= 64 &&
+      (HB + KSf - 1) / KSf <= 10) {
     const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
     const int G = G16;
     const int KS = KSf;
     const int HBc = (HB + KS - 1) / KS;
     const int vec = (P1 % 2 == 0) && ((((uintptr_t)At) & 15) == 0);
     const dim3 g((unsigned)cdiv(npairs, G));
-#define CF_(D_, H_, W_)                                                                          \
-  colfuse_kernel<D_, H_, W_><<<g, 64 * W_, 0, st>>>((const float2*)At, (const float2*)Wt,        \
-                                                    (const f32x4*)FB, (const f32x4*)GB,          \
-                                                    (float2*)Xs, (float2*)Z, (int)npairs, Ci, Co, \
-                                                    P1, m1, m2, P2, G, KS, vec, Bg, wtgs, tiled)
+#define CF16_(D_, H_, W_, F_)                                                                   \
+  colfuse_kernel<D_, H_, W_, F_><<<g, 64 * W_, 0, st>>>((const float2*)At, (const float2*)Wt,    \
+                                                        (const f32x4*)FB, (const f32x4*)GB,      \
+                                                        (float2*)Xs, (float2*)Z, (int)npairs, Ci, \
+                                                        Co, P1, m1, m2, P2, G, KS, vec, Bg, wtgs, \
+                                                        tiled)
+#define CF_(D_, H_, W_) do { if (h16) CF16_(D_, H_, W_, true); else CF16_(D_, H_, W_, false); } while (0)
 #define CFW_(H_, W_) do { if (dir == 0) CF_(0, H_, W_); else CF_(1, H_, W_); } while (0)
 #define CFD_(H_) do { if (NWf == 8) CFW_(H_, 8); else CFW_(H_, 4); } while (0)
     if (HBc <= 3) CFD_(3);
@@ -1058,6 +1115,7 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
 #undef CFD_
 #undef CFW_
 #undef CF_
+#undef CF16_
     return (int)hipGetLastError();
   }
   // pairs per workgroup: enough 16-row tiles for the four waves, tiles filled

@@ -540,3 +540,43 @@ def test_fused_column_pass_matches_split(Bn, C, m, P, Gw):
         for a, b in zip(res[(1, d)], res[(0, d)]):
             assert torch.isfinite(a).all()
             assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-6, d
+
+
+@pytest.mark.parametrize("Bn,C,m,P,Gw", [(300, 4, 12, 320, 1), (8, 12, 32, 320, 2), (40, 4, 12, 160, 1)])
+def test_fused_column_pass_fp16_mix(Bn, C, m, P, Gw):
+    """The fused column pass with the fp16-operand mix (config E: dir bit 1; the spectra block-
+    scaled per workgroup) vs the fp32 mix on the same inputs, both directions, next to the split
+    kernels' fp16 mix: the fused kernel scales over its own 16 rows (the split one over its G
+    pairs), so the two fp16 results differ at fp16 rounding; each stays within 2e-3 of the fp32
+    mix and the fused one no worse than 1.5x the split one (+1e-4)."""
+    import ctypes
+    from blindno import ops
+    from blindno._lib import call, ptr, query, stream_ptr
+    g = torch.Generator(device="cuda").manual_seed(Bn + C + m + 7)
+    K1 = ops.kept_rows_count(m, P)
+    K1p = 16 * ((K1 + 15) // 16)
+    At = torch.randn(Bn, m, C, P, 2, device="cuda", generator=g)
+    Wt = torch.randn(Gw, m, K1, C, C, 2, device="cuda", generator=g) * 0.2
+    FB, GB = ops.twiddle_cols(P, m, At.device)
+    wtgs = m * K1 * C * C * 2 if Gw > 1 else 0
+    res = {}
+    for fused in (0, 1):
+        prev = query("blindno_set_colfuse", fused)
+        for d in (0, 1):
+            for h in (0, 2):
+                Xs = torch.full((Bn, m, C, K1, 2), float("nan"), device="cuda")
+                Y = torch.empty(Bn, m, C, K1p, 2, device="cuda")
+                Z = torch.full((Bn, P, m, C, 2), float("nan"), device="cuda")
+                call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(Xs), ptr(Y), ptr(Z), ptr(FB), ptr(GB), Gw,
+                     ctypes.c_int64(wtgs), Bn, C, C, P, m, m, P, d | h, stream_ptr())
+                res[(fused, d, h)] = Z
+        query("blindno_set_colfuse", prev)
+    torch.cuda.synchronize()
+    for d in (0, 1):
+        ref = res[(1, d, 0)].cpu().numpy()
+        e_f = rel_l2(res[(1, d, 2)].cpu().numpy(), ref)
+        e_s = rel_l2(res[(0, d, 2)].cpu().numpy(), ref)
+        print(f"  dir {d}: fp16 mix vs fp32, fused {e_f:.2e}, split {e_s:.2e}")
+        assert torch.isfinite(res[(1, d, 2)]).all()
+        assert e_f <= 2e-3 and e_s <= 2e-3, (d, e_f, e_s)
+        assert e_f <= 1.5 * e_s + 1e-4, (d, e_f, e_s)
