@@ -195,8 +195,6 @@ def main():
             graphed.capture(L)
         torch.cuda.synchronize()
 
-    X2, Y2 = X.view(X.shape[0], -1), Y.view(Y.shape[0], -1)
-    xb2, yb2 = xb.view(B, -1), yb.view(B, -1)
     hostp = {"batch_select": 0.0, "draw": 0.0, "step": 0.0, "n": 0}
 
     n_loss = [0]             # steps whose loss went into loss_acc (the kernel-timer steps do not)
@@ -205,10 +203,8 @@ def main():
         t0_ = time.perf_counter()
         j = (i * B) % (n_local - B + 1)
         ids = order[j:j + B]
-        # 2D views: torch's vectorised row gather for both (Y's (N, N, 2) rows otherwise take
-        # the small-index kernel, 5.6 us for 0.5 MB)
-        torch.index_select(X2, 0, ids, out=xb2)
-        torch.index_select(Y2, 0, ids, out=yb2)
+        torch.index_select(X, 0, ids, out=xb)
+        torch.index_select(Y, 0, ids, out=yb)
         if graphed is not None and not eager:
             t1_ = time.perf_counter()
             idx = (draw_distinct if a.config == "C_attn" else blindno.draw_bag)(T)[1]
