@@ -129,7 +129,7 @@ def main():
     import blindno
     from blindno import timing
     from blindno.nio import draw_bag_distinct as draw_distinct
-    from blindno.train import (DataParallel, FlatAdam, GraphedBagStep, grid1d, grid2d,
+    from blindno.train import (BatchSelect, DataParallel, FlatAdam, GraphedBagStep, grid1d, grid2d,
                                shard_bag_ids, synthetic_bags)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,6 +195,8 @@ def main():
             graphed.capture(L)
         torch.cuda.synchronize()
 
+    # the batch (bags and targets of the drawn ids) in one blindno_gather_batch launch
+    select = BatchSelect([X, Y], [xb, yb])
     hostp = {"batch_select": 0.0, "draw": 0.0, "step": 0.0, "n": 0}
 
     n_loss = [0]             # steps whose loss went into loss_acc (the kernel-timer steps do not)
@@ -203,8 +205,7 @@ def main():
         t0_ = time.perf_counter()
         j = (i * B) % (n_local - B + 1)
         ids = order[j:j + B]
-        torch.index_select(X, 0, ids, out=xb)
-        torch.index_select(Y, 0, ids, out=yb)
+        select(ids)
         if graphed is not None and not eager:
             t1_ = time.perf_counter()
             idx = (draw_distinct if a.config == "C_attn" else blindno.draw_bag)(T)[1]

@@ -390,6 +390,11 @@ int blindno_rowsq(const float* a, const float* b, double* out, int rows, int n, 
  * copy (the reference's DDP bucket flatten, 2d_FPE/train_fno.py:121,143). */
 int blindno_gather_flat(const void* const* srcs, const int64_t* offs, const int64_t* ns, int nseg,
                         float* dst, blindno_stream_t stream);
+/* Batch select: dsts[i][b] = srcs[i][ids[b]] (rows of rows[i] floats) for nseg <= 4 tensors in
+ * one launch; srcs / dsts / rows are HOST arrays, ids a DEVICE int64 array of B row indices
+ * (bench.py: the bags X and targets Y of the step's batch). */
+int blindno_gather_batch(const void* const* srcs, void* const* dsts, const int64_t* rows, int nseg,
+                         const int64_t* ids, int B, blindno_stream_t stream);
 int blindno_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1,
                  float beta2, float eps, float step_size, float bc2s, float gscale,
                  blindno_stream_t stream);

@@ -84,6 +84,7 @@ SIGNATURES = {
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",
     "blindno_gather_flat": "pppips",
+    "blindno_gather_batch": "pppipis",
     "blindno_reduce_partials_multi": "ppppis",
     "blindno_unpack_w2d_multi": "ppppis",
     "blindno_pack_w2d_multi": "ppppis",

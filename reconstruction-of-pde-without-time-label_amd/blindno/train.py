@@ -462,6 +462,33 @@ class GraphedBagStep:
         return L
 
 
+class BatchSelect:
+    """The training loop's batch select (2d_FPE/train_fno.py:113-116: the DataLoader's batch)
+    from HBM-resident tensors: ``dsts[i][b] = srcs[i][ids[b]]`` for every pair in one
+    blindno_gather_batch launch (ids: a device int64 slice of the epoch permutation)."""
+
+    def __init__(self, srcs, dsts):
+        if not 1 <= len(srcs) == len(dsts) <= 4:
+            raise ValueError("BatchSelect: 1..4 (src, dst) pairs")
+        for s_, d_ in zip(srcs, dsts):
+            if not (s_.is_contiguous() and d_.is_contiguous() and s_.dtype == d_.dtype == torch.float32
+                    and s_.shape[1:] == d_.shape[1:]):
+                raise ValueError("BatchSelect: contiguous fp32 tensors with matching row shapes")
+        self.B = dsts[0].shape[0]
+        self._keep = (list(srcs), list(dsts))
+        n = len(srcs)
+        self._srcs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+        self._dsts = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dsts])
+        self._rows = (ctypes.c_int64 * n)(*[t[0].numel() for t in srcs])
+        self._n = n
+
+    def __call__(self, ids: torch.Tensor):
+        if ids.dtype != torch.int64 or not ids.is_contiguous() or ids.numel() != self.B:
+            raise ValueError("BatchSelect: ids must be a contiguous int64 tensor of the batch size")
+        call("blindno_gather_batch", self._srcs, self._dsts, self._rows, self._n, ptr(ids), self.B,
+             stream_ptr())
+
+
 def shard_bag_ids(n_bags: int, per_rank_batch: int, rank: int, world: int):
     """Bag-keyed data-parallel sharding (the reference's accelerate sampler
     splits one dataset over the processes): rank r of ``world`` owns the global bags

@@ -1254,6 +1254,57 @@ BLINDNO_API int blindno_gather_flat(const void* const* srcs, const int64_t* offs
   return (int)hipGetLastError();
 }
 
+// Batch select of the training loop (the DataLoader's batch, 2d_FPE/train_fno.py:113-116): rows
+// ids[b] of up to kBatchSegs row-major tensors (bags X (n, T N1 N2), targets Y (n, N1 N2 C)) into
+// their batch buffers, in ONE launch: blockIdx.y = (segment, batch row), 16-B copies when the
+// rows are 16-B aligned.  ids are device int64 (the epoch's permutation slice).
+constexpr int kBatchSegs = 4;
+struct BatchSegs {
+  const float* src[kBatchSegs];
+  float* dst[kBatchSegs];
+  int64_t row[kBatchSegs];   // floats per row
+  int nseg, vec;
+};
+
+__global__ __launch_bounds__(kBlock) void gather_batch_kernel(BatchSegs sg, const int64_t* __restrict__ ids,
+                                                              int B) {
+  const int sb = blockIdx.y, seg = sb / B, b = sb - seg * B;
+  const int64_t row = sg.row[seg];
+  const float* __restrict__ src = sg.src[seg] + ids[b] * row;
+  float* __restrict__ dst = sg.dst[seg] + (int64_t)b * row;
+  if (sg.vec) {
+    const int64_t n4 = row >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
+      reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < row; i += (int64_t)gridDim.x * kBlock)
+      dst[i] = src[i];
+  }
+}
+
+BLINDNO_API int blindno_gather_batch(const void* const* srcs, void* const* dsts, const int64_t* rows,
+                                     int nseg, const int64_t* ids, int B, void* stream) {
+  if (nseg < 1 || nseg > kBatchSegs || B < 1 || !ids) return (int)hipErrorInvalidValue;
+  BatchSegs sg{};
+  sg.nseg = nseg;
+  sg.vec = 1;
+  int64_t maxrow = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (!srcs[i] || !dsts[i] || rows[i] < 1) return (int)hipErrorInvalidValue;
+    sg.src[i] = (const float*)srcs[i];
+    sg.dst[i] = (float*)dsts[i];
+    sg.row[i] = rows[i];
+    if ((rows[i] & 3) || ((uintptr_t)srcs[i] & 15) || ((uintptr_t)dsts[i] & 15)) sg.vec = 0;
+    if (rows[i] > maxrow) maxrow = rows[i];
+  }
+  const int64_t items = sg.vec ? maxrow / 4 : maxrow;
+  int64_t gx = (items + kBlock * 4 - 1) / (kBlock * 4);        // ~4 elements per thread
+  if (gx < 1) gx = 1;
+  if (gx > 4096) gx = 4096;
+  gather_batch_kernel<<<dim3((unsigned)gx, (unsigned)(nseg * B)), kBlock, 0, (hipStream_t)stream>>>(sg, ids, B);
+  return (int)hipGetLastError();
+}
+
 BLINDNO_API int blindno_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1,
                              float beta2, float eps, float step_size, float bc2s, float gscale,
                              void* stream) {

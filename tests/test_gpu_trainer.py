@@ -125,3 +125,21 @@ def test_trainer_nio_2d(tmp_path):
     sd = torch.load(os.path.join(out, ckpts[0]), weights_only=True)
     m = exp.model(61, "cuda")
     m.load_state_dict(sd)
+
+
+@pytest.mark.parametrize("shape", [(7, 13, 16, 16), (5, 3, 9)])
+def test_batch_select_matches_index_select(shape):
+    """train.BatchSelect (blindno_gather_batch: the bags and targets of the step's batch in one
+    launch) is bit-identical to torch.index_select for the aligned (16-B) and unaligned row
+    paths, with repeated and out-of-order ids."""
+    from blindno.train import BatchSelect
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.randn(*shape, device="cuda", generator=g)
+    Y = torch.randn(shape[0], 6, 2, device="cuda", generator=g)
+    ids = torch.tensor([4, 0, 4, shape[0] - 1], dtype=torch.int64, device="cuda")
+    xb = torch.full((4,) + tuple(shape[1:]), float("nan"), device="cuda")
+    yb = torch.full((4, 6, 2), float("nan"), device="cuda")
+    BatchSelect([X, Y], [xb, yb])(ids)
+    torch.cuda.synchronize()
+    assert torch.equal(xb, torch.index_select(X, 0, ids))
+    assert torch.equal(yb, torch.index_select(Y, 0, ids))
