@@ -45,6 +45,13 @@ constexpr int kFwdNP4 = PROJ_FWD_NP4;
 #endif
 constexpr int kBwdNP4 = PROJ_BWD_NP4;
 // hidden-tile loop unroll of the backward (1: rolled)
+// CK >= 8 (the heads' 12 channels), T16: dz = (W1 w2)^T dH on the matrix cores -- dH staged
+// through a wave-private LDS tile into the B layout (hidden x points), 4 v_mfma_f32_16x16x4f32 per
+// hidden tile into one accumulator -- instead of 2 CK packed FMAs per hidden tile and a
+// reduce-scatter of 4 CK values over the 16 hidden lanes per point tile
+#ifndef PB_DZMFMA
+#define PB_DZMFMA 1
+#endif
 #ifndef PB_TUNROLL
 #define PB_TUNROLL 1
 #endif
@@ -255,6 +262,7 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
   __shared__ f32x4 sgw1[kWaves][kNT][64];
   __shared__ float sgb1[kWaves][kNT][64];
   __shared__ float sgw2[kWaves][kNT][COM][64];     // dW2 accumulators (lane = hidden c16)
+  __shared__ float sdh[PB_DZMFMA && CK >= 8 ? kWaves : 1][16 * 17];   // dH transpose tiles
   stage_weights<CK, COM>(sw, w1, b1, w2, C, Cout, 1.0f);
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
@@ -341,11 +349,13 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
         for (int c = 0; c < COM; ++c) gb2[c] += (gv[np][0][c] + gv[np][1][c]) + (gv[np][2][c] + gv[np][3][c]);
       }
     }
-    float dzp[NP][NV];
+    constexpr bool kDzM = PB_DZMFMA && CK >= 8 && NP == 1 && T16;
+    float dzp[kDzM ? 1 : NP][kDzM ? 1 : NV];
 #pragma unroll
-    for (int np = 0; np < NP; ++np)
+    for (int np = 0; np < (kDzM ? 1 : NP); ++np)
 #pragma unroll
-      for (int e = 0; e < NV; ++e) dzp[np][e] = 0.f;
+      for (int e = 0; e < (kDzM ? 1 : NV); ++e) dzp[np][e] = 0.f;
+    f32x4 dzacc = {0.f, 0.f, 0.f, 0.f};            // kDzM: D[channel 4 g4 + r][point c16]
 #pragma unroll PB_TUNROLL
     for (int t = 0; t < kNT; ++t) {
       const int j = 16 * t + c16;
@@ -398,15 +408,32 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
         const f32x2 dh01 = da01 * pk_fma(h01, ep01, cdf01);
         const f32x2 dh23 = da23 * pk_fma(h23, ep23, cdf23);
         const float dh[4] = {dh01.x, dh01.y, dh23.x, dh23.y};
+        if constexpr (kDzM) {
+          // dH (points 4 g4 + r, hidden c16) -> wave-private LDS [hidden][point] -> B operands
+          // (hidden 4 g4 + r, point c16); A = row c16 (channel) of (W1 w2)^T
+          float* sd = sdh[wave];
 #pragma unroll
-        for (int i = 0; i < CK; ++i) {                                 // k dz (scaled at the store)
-          const f32x2 wi = {wr[i], wr[i]};
-          f32x2 p01 = {dzp[np][i * 4 + 0], dzp[np][i * 4 + 1]};
-          f32x2 p23 = {dzp[np][i * 4 + 2], dzp[np][i * 4 + 3]};
-          p01 = __builtin_elementwise_fma(dh01, wi, p01);
-          p23 = __builtin_elementwise_fma(dh23, wi, p23);
-          dzp[np][i * 4 + 0] = p01.x; dzp[np][i * 4 + 1] = p01.y;
-          dzp[np][i * 4 + 2] = p23.x; dzp[np][i * 4 + 3] = p23.y;
+          for (int r = 0; r < 4; ++r) sd[c16 * 17 + 4 * g4 + r] = dh[r];
+          float bv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[r] = sd[(4 * g4 + r) * 17 + c16];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int jr = 16 * t + 4 * g4 + r;
+            const float a = c16 < C ? sw.w1[jr][c16] * (kFoldW2 ? sw.w2[0][jr] : 1.0f) : 0.f;
+            dzacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[r], dzacc, 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < CK; ++i) {                               // k dz (scaled at the store)
+            const f32x2 wi = {wr[i], wr[i]};
+            f32x2 p01 = {dzp[np][i * 4 + 0], dzp[np][i * 4 + 1]};
+            f32x2 p23 = {dzp[np][i * 4 + 2], dzp[np][i * 4 + 3]};
+            p01 = __builtin_elementwise_fma(dh01, wi, p01);
+            p23 = __builtin_elementwise_fma(dh23, wi, p23);
+            dzp[np][i * 4 + 0] = p01.x; dzp[np][i * 4 + 1] = p01.y;
+            dzp[np][i * 4 + 2] = p23.x; dzp[np][i * 4 + 3] = p23.y;
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -420,10 +447,24 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
 #pragma unroll
       for (int c = 0; c < COM; ++c) sgw2[wave][t][c][lane] = gw2[c].x + gw2[c].y;
     }
+    if constexpr (kDzM) {
+      // lane (g4, c16): channels 4 g4 + r of point c16 of the tile (one sample row: T16)
+      const unsigned tile = grp;
+      if (tile < ntiles) {
+        unsigned n0, q0;
+        const unsigned zo0 = pm.zoff(pbase + tile * 16u, n0, q0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ch = 4 * g4 + r;
+          if (ch < C) dz[zo0 + (unsigned)c16 + (unsigned)ch * (unsigned)pm.HW] = kInvK * dzacc[r];
+        }
+      }
+      continue;
+    }
     // reduce-scatter dzp over the 16 hidden lanes: lane keeps value index e = 16 m + c16,
     // i.e. channel 4 m + (c16 >> 2), point 4 g4 + (c16 & 3)
 #pragma unroll
-    for (int np = 0; np < NP; ++np) {
+    for (int np = 0; np < (kDzM ? 1 : NP); ++np) {
 #pragma unroll
       for (int s = 8; s >= 1; s >>= 1) {
         const bool up = (c16 & s) != 0;
