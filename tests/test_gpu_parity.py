@@ -321,8 +321,11 @@ def test_bag_stats_projection_matches_per_snapshot(N, B, dedup):
     grid = torch.tensor(np.stack([gx, gy], 2)).cuda()
     idx = np.random.RandomState(3).choice(60, 57)
     res = []
-    for bag_stats in (True, False):
+    budget = ops.BAG_STATS_MAX_BYTES
+    # third run: bag statistics on but over the byte budget -> the per-snapshot path, identically
+    for bag_stats, max_bytes in ((True, budget), (False, budget), (True, 0)):
         ops.BAG_STATS = bag_stats
+        ops.BAG_STATS_MAX_BYTES = max_bytes
         nio.DEDUP_BAGS = dedup
         try:
             m.zero_grad()
@@ -331,7 +334,10 @@ def test_bag_stats_projection_matches_per_snapshot(N, B, dedup):
             res.append((out.detach().cpu().numpy(), [p.grad.cpu().numpy() for p in m.FNO_input.parameters()]))
         finally:
             ops.BAG_STATS = True
+            ops.BAG_STATS_MAX_BYTES = budget
             nio.DEDUP_BAGS = True
+    assert np.array_equal(res[2][0], res[1][0])
+    assert all(np.array_equal(a, b) for a, b in zip(res[2][1], res[1][1]))
     e_out = rel_l2(res[0][0], res[1][0])
     e_g = [rel_l2(a, b) for a, b in zip(res[0][1], res[1][1])]
     print(f"bag-level vs per-snapshot projection: out {e_out:.2e}, FNO_input grads max {max(e_g):.2e}")
