@@ -762,6 +762,24 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
     return out, (small, x0, Xs, Wts, zs)
 
 
+# The grouped heads' projection backward writes dz on the Ho x Wo crop only and its readers need
+# zeros on the padding: one persistent buffer per shape whose padding is zeroed once (no fill
+# kernel per step).  Created outside stream capture (GraphedBagStep's eager warm-up) so a graph
+# references ordinary pool memory, never its own pool; a miss during capture falls back to a
+# captured fill.  Only the single-chain grouped path uses it (the forked heads run two streams).
+_DZ_PAD = {}
+
+
+def _padded_grad_buffer(shape, device):
+    key = (tuple(shape), str(device))
+    t = _DZ_PAD.get(key)
+    if t is None:
+        t = torch.zeros(shape, dtype=F32, device=device)
+        if not torch.cuda.is_current_stream_capturing():
+            _DZ_PAD[key] = t
+    return t
+
+
 def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
     """Adjoint of fno_forward_grouped: (d_inp summed over the heads, [grads of head g])."""
     G = len(prms)
@@ -777,7 +795,7 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
     grads = [[None] * len(p) for p in prms]
     off_fc1 = 2 + 4 * n
     # projection
-    dz = torch.zeros(Bn, C, P1, P2, dtype=F32, device=inp.device)
+    dz = _padded_grad_buffer((Bn, C, P1, P2), inp.device)
     np_p = Hd * C + Hd + Cout * Hd + Cout
     nchunk = query("blindno_project_bwd_nchunk", Bg, Ho, Wo)
     partial = _empty(nchunk, G, np_p, like=inp)
