@@ -172,13 +172,19 @@ def encoder2d_conv(p: Dict[str, torch.Tensor], x: torch.Tensor,
     return _lin(h.flatten(1).view(B, L, -1), p, "linear")
 
 
-def _ffn(p, x, n_hidden_layers):
+def _ffn(p, x, n_hidden_layers, masks=None):
     """FFN.forward, 2d_FPE/DeepONetModules.py:155-185 (leaky_relu 0.01, dropout 0, train-mode
-    BatchNorm1d)."""
+    BatchNorm1d).  ``masks``: the LeakyReLU branches (pre-activation > 0) to take, one per
+    activation -- an fp64 arbiter evaluated on the branches an fp32 run took."""
     F = torch.nn.functional
-    h = F.leaky_relu(_lin(x, p, "input_layer"), 0.01)
+
+    def act(z, i):
+        if masks is None:
+            return F.leaky_relu(z, 0.01)
+        return torch.where(masks[i].to(z.device), z, 0.01 * z)
+    h = act(_lin(x, p, "input_layer"), 0)
     for k in range(n_hidden_layers - 1):
-        h = F.leaky_relu(_lin(h, p, f"hidden_layers.{k}"), 0.01)
+        h = act(_lin(h, p, f"hidden_layers.{k}"), k + 1)
         h = F.batch_norm(h, None, None, p[f"batch_layers.{k}.weight"], p[f"batch_layers.{k}.bias"],
                          training=True, eps=1e-5)
     return _lin(h, p, "output_layer")
@@ -188,7 +194,8 @@ def niofp2d_fft(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
                 idx: Optional[Sequence[int]] = None, n_hidden_layers: int = 3,
                 heads: Sequence[str] = ("fno_drift", "fno_diffusion"),
                 branch_masks: Optional[Sequence[torch.Tensor]] = None,
-                taps: Optional[dict] = None) -> torch.Tensor:
+                taps: Optional[dict] = None,
+                trunk_masks: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
     """NIOFP2D.forward, 2d_FPE/NIOModules.py:47-83 (NC heads fno_Fx/fno_Fy:
     2d_Non_conservative_FPE/NIOModules.py:46-82): the Encoder2D branch on every drawn snapshot,
     the FFN trunk on the grid points, DeepOnetNoBiasOrg ``(w @ basis^T + b0) / sqrt(p)``
@@ -197,7 +204,7 @@ def niofp2d_fft(p: Dict[str, torch.Tensor], x: torch.Tensor, grid: torch.Tensor,
         x = x[:, torch.as_tensor(list(idx), device=x.device)]
     B, L, nx, ny = x.shape
     w = encoder2d_conv(sub_params(p, "branch"), x.unsqueeze(2), branch_masks)
-    basis = _ffn(sub_params(p, "trunk"), grid.reshape(-1, 2), n_hidden_layers)
+    basis = _ffn(sub_params(p, "trunk"), grid.reshape(-1, 2), n_hidden_layers, trunk_masks)
     if taps is not None and basis.requires_grad:
         basis.retain_grad()          # dL/dbasis: the trunk's upstream gradient (bench.py parity)
         taps["basis"] = basis

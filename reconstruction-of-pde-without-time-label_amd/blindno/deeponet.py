@@ -108,9 +108,17 @@ class _FFNBase(nn.Module):
         from . import ops
         slope = self.activation.negative_slope
         F = torch.nn.functional
-        x = F.leaky_relu(ops.linear(x, self.input_layer.weight, self.input_layer.bias), slope)
+        # record_branches: a list receives each LeakyReLU's branch mask (pre-activation > 0),
+        # for an fp64 arbiter that takes the same branches (bench.py's config-D parity leg)
+        rec = getattr(self, "record_branches", None)
+
+        def act(z):
+            if rec is not None:
+                rec.append(z.detach() > 0)
+            return F.leaky_relu(z, slope)
+        x = act(ops.linear(x, self.input_layer.weight, self.input_layer.bias))
         for l, b in zip(self.hidden_layers, self.batch_layers):
-            x = F.leaky_relu(ops.linear(x, l.weight, l.bias), slope)
+            x = act(ops.linear(x, l.weight, l.bias))
             x = ops.BNActFn.apply(x, b.weight, b.bias, b, x.shape[0], 1.0)
         return ops.linear(x, self.output_layer.weight, self.output_layer.bias)
 
