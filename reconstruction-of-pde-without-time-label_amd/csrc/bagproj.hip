@@ -67,7 +67,10 @@ struct BagGeom {
 //     multiply), zbar summed by the staging threads, w2 re-read at the statistics write:
 //     no per-snapshot register moves and 20 fewer live VGPRs;
 //   * double-buffered 8-snapshot chunks: one barrier per chunk instead of three per 16.
-constexpr int kSC2 = 8;
+#ifndef BAGPROJ_SC
+#define BAGPROJ_SC 8
+#endif
+constexpr int kSC2 = BAGPROJ_SC;        // snapshots per staged chunk (a multiple of 4)
 
 __device__ __forceinline__ float swap_sum32(float a, float b) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
