@@ -265,6 +265,52 @@ int blindno_rowidft_bwd_lift(const float* G, const float* dz, const float* X, co
                              const float* tb, float* partial, int B, int T, int L, int N1, int N2,
                              int C, int P1, int P2, int m2, blindno_stream_t stream);
 
+/* --- The column pass folded into the row kernels (FNO_input: C = 4, m1 = m2 = 12 -> K1 = 24
+ *     kept rows; csrc/colspec.h).  Replaces blindno_colpass between the row kernels of
+ *     SpectralConv2d.forward (2d_FPE/FNOModules.py:156-178) in the FNO_input layer chain
+ *     (FNOModules.py:226-232): only the K1 x m2 column spectrum crosses kernels.
+ * part: per (sample, 16-row block) column-DFT partials, blindno_colspec_nchunk(Cp, m2) chunks of
+ *   64 lanes x 2 floats each (layout: colspec.h); tab: Tab[P1][2 K1] = (cos, sin)(2 pi r_j h / P1)
+ *   (blindno.ops.twiddle_colspec); Y / Xsave (Bn, m2, C, K1) complex.
+ * blindno_colspec_ok: 1 when a layer of this shape takes the folded path. */
+int blindno_colspec_ok(int Bn, int C, int P1, int P2, int m1, int m2);
+int blindno_colspec_nchunk(int C, int m2);
+/* row DFT of f(x) (GELU when act) on the N1v x N2v valid region + column-DFT partials */
+int blindno_rowdft_cd(const float* x, float* part, const float* Tp, const float* tab, int Bn, int C,
+                      int P1, int P2, int m2, int act, int N1v, int N2v, blindno_stream_t stream);
+/* the same for the bag's snapshots X[b][idx[l]] (one channel; sample n = b L + l) */
+int blindno_rowdft_bag_lift_cd(const float* X, const int* idx, float* part, const float* Tp,
+                               const float* tab, int B, int T, int L, int N1, int N2, int P1,
+                               int P2, int m2, blindno_stream_t stream);
+/* partials of nbv blocks summed in block order -> Xsave (dir 0: X; dir 1: G = c_k/(P1 P2) X) and
+ * Y (dir 0: c_k/(P1 P2) sum_c X W; dir 1: sum_o conj(W) G), as blindno_colpass forms them.
+ * Lift (w0 != NULL, dir 0, Cp = 1): X[c] = w0[c,0] U + w0[c,1] Dg2[0] + w0[c,2] Dg2[1] +
+ * b0[c] Dg2[2].  Wt NULL: Xsave only. */
+int blindno_colmix(const float* part, int nbv, const float* Wt, float* Xsave, float* Y, int Bn, int C,
+                   int Cp, int P1, int P2, int m1, int m2, int dir, const float* w0, const float* b0,
+                   const float* Dg2, blindno_stream_t stream);
+/* row inverses with Z built from Y (ZY) and, with part != NULL, the next row DFT as column-DFT
+ * partials (CD): counterparts of blindno_rowidft_epi(_crop / _rd), _epi_lift_rd, _bwd_rd /
+ * _bwd_crop and _bwd_lift.  Tp: the next row DFT's image (blindno_rowdft's). */
+int blindno_rowidft_epi_zc(const float* Y, const float* x, const float* wc, const float* bc, float* z,
+                           const float* tb, const float* tab, float* part, const float* Tp, int Bn,
+                           int C, int P1, int P2, int m1, int m2, int act, int act_next, int oN1,
+                           int oN2, blindno_stream_t stream);
+int blindno_rowidft_epi_lift_zc(const float* Y, const float* X, const int* idx, const float* grid,
+                                const float* w0, const float* b0, const float* wc, const float* bc,
+                                float* z, const float* tb, const float* tab, float* part,
+                                const float* Tp, int B, int T, int L, int N1, int N2, int C, int P1,
+                                int P2, int m1, int m2, int act_next, blindno_stream_t stream);
+int blindno_rowidft_bwd_zc(const float* Y, const float* dz, const float* wc, const float* xsrc,
+                           float* dx, const float* tb, const float* tab, float* part,
+                           const float* Tp, float* partial, int Bn, int C, int P1, int P2, int m1,
+                           int m2, int act, int dN1, int dN2, blindno_stream_t stream);
+int blindno_rowidft_bwd_lift_zc(const float* Y, const float* dz, const float* X, const int* idx,
+                                const float* grid, const float* w0, const float* b0,
+                                const float* wc, const float* tb, const float* tab, float* partial,
+                                int B, int T, int L, int N1, int N2, int C, int P1, int P2, int m1,
+                                int m2, blindno_stream_t stream);
+
 /* 1x1-conv weight/bias gradient partials (for C > 8): partial[nchunk][C*C + C] with
  * dWc[o,i] = sum dz[n,o,.] f(x[n,i,.]),  dbc[o] = sum dz[n,o,.];
  * nchunk must equal blindno_conv_wgrad_nchunk(Bn, P1, P2). */
@@ -332,7 +378,8 @@ int blindno_bagmean_bwd(const float* dy, const float* w, float* s, int B, int S,
  *   wbar[b,k] = sum_l lw_l w[b,l,k];  ubar[b,p] = (wbar[b] . basis[p] + b0 sum_l lw_l) * scale
  * (scale = 1/sqrt(P)); wbar (B, P) is saved for the backward.  Backward from g = dL/dubar
  * (B, S): dw (B, L, P), dbasis (S, P), db0 (1, NULL: none); partial: nblk * (B P + 1) floats,
- * nblk = blindno_deeponet_bag_nblk(S).  B <= 64, P <= 64, L <= 1024. */
+ * nblk = blindno_deeponet_bag_nblk(S).  P <= 64; any B (the backward runs bag chunks of 64
+ * in stream order, dbasis / db0 summed over the chunks in that order). */
 int blindno_deeponet_bag_nblk(int S);
 int blindno_deeponet_bag_fwd(const float* w, const float* basis, const float* b0, const float* lw,
                              float* wbar, float* ubar, int B, int L, int S, int P, float scale,
@@ -391,10 +438,12 @@ int blindno_rowsq(const float* a, const float* b, double* out, int rows, int n, 
 int blindno_gather_flat(const void* const* srcs, const int64_t* offs, const int64_t* ns, int nseg,
                         float* dst, blindno_stream_t stream);
 /* Batch select: dsts[i][b] = srcs[i][ids[b]] (rows of rows[i] floats) for nseg <= 4 tensors in
- * one launch; srcs / dsts / rows are HOST arrays, ids a DEVICE int64 array of B row indices
- * (bench.py: the bags X and targets Y of the step's batch). */
-int blindno_gather_batch(const void* const* srcs, void* const* dsts, const int64_t* rows, int nseg,
-                         const int64_t* ids, int B, blindno_stream_t stream);
+ * one launch; srcs / dsts / rows / nsrc (row count of each source) are HOST arrays, ids a DEVICE
+ * int64 array of B row indices (bench.py: the bags X and targets Y of the step's batch).  An id
+ * outside [0, nsrc[i]) fills its batch row of dsts[i] with NaN (no out-of-bounds read). */
+int blindno_gather_batch(const void* const* srcs, void* const* dsts, const int64_t* rows,
+                         const int64_t* nsrc, int nseg, const int64_t* ids, int B,
+                         blindno_stream_t stream);
 int blindno_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1,
                  float beta2, float eps, float step_size, float bc2s, float gscale,
                  blindno_stream_t stream);

@@ -30,6 +30,15 @@ SIGNATURES = {
     "blindno_rowidft_epi_lift": "ppppppppppiiiiiiiiis",
     "blindno_rowidft_bwd_lift": "ppppppppppiiiiiiiiis",
     "blindno_colpass": "pppppppiiiiiiiis",
+    "blindno_colspec_ok": "iiiiii",
+    "blindno_colspec_nchunk": "ii",
+    "blindno_rowdft_cd": "ppppiiiiiiiis",
+    "blindno_rowdft_bag_lift_cd": "pppppiiiiiiiis",
+    "blindno_colmix": "pipppiiiiiiiippps",
+    "blindno_rowidft_epi_zc": "ppppppppp" + "iiiiiiiiii" + "s",
+    "blindno_rowidft_epi_lift_zc": "ppppppppppppp" + "iiiiiiiiiii" + "s",
+    "blindno_rowidft_bwd_zc": "pppppppppp" + "iiiiiiiii" + "s",
+    "blindno_rowidft_bwd_lift_zc": "ppppppppppp" + "iiiiiiiiii" + "s",
     "blindno_mix_wgrad": "ppppiiiiiis",
     "blindno_mix_wgrad_part": "pppiiiiiiis",
     "blindno_mix1d": "ppppiiiiiis",
@@ -84,7 +93,7 @@ SIGNATURES = {
     "blindno_bn_act_fwd": "ppppppppiiiifffis",
     "blindno_bn_act_bwd": "pppppppppiiiifis",
     "blindno_gather_flat": "pppips",
-    "blindno_gather_batch": "pppipis",
+    "blindno_gather_batch": "ppppipis",
     "blindno_reduce_partials_multi": "ppppis",
     "blindno_unpack_w2d_multi": "ppppis",
     "blindno_pack_w2d_multi": "ppppis",

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -38,6 +39,13 @@ BAG_STATS = True
 # size) from forward to backward: ~190 MB at config C, ~800 MB at config E (256^2, B = 4).
 # Above this budget the per-snapshot projection runs instead (same results).
 BAG_STATS_MAX_BYTES = 4 << 30
+
+# The column pass of the snapshot encoder's spectral layers folded into the row kernels around
+# it (csrc/colspec.h: column-DFT partials written by the kernel that forms the row spectrum, the
+# mix on the partials, the row coefficients rebuilt from the mixed spectrum in the next row
+# inverse's prologue): FNO_input at C = 4, m1 = m2 = 12 with the fp32 mix.  False: the fused
+# column pass (blindno_colpass) between the row kernels, as before.
+COLSPEC = os.environ.get("BLINDNO_COLSPEC", "1") != "0"
 
 
 def set_mix_precision(name: str) -> None:
@@ -165,6 +173,29 @@ def twiddle_cols(P1: int, m1: int, device):
         t = (cv(FB), cv(GB))
         _TWC[key] = t
     return t
+
+
+_TWS = {}
+
+
+def twiddle_colspec(P1: int, m1: int, device) -> torch.Tensor:
+    """Tab[h][2 j + p] = (cos, sin)(2 pi r_j h / P1) for the kept rows r_j (csrc/colspec.h):
+    the column DFT's F (= cos - i sin) and the column inverse's conj(F); built in double."""
+    dev = torch.device(device)
+    key = (P1, m1, dev.index)
+    t = _TWS.get(key)
+    if t is None:
+        r = torch.tensor(kept_rows(m1, P1), dtype=torch.int64)
+        h = torch.arange(P1, dtype=torch.int64)
+        ph = ((h[:, None] * r[None, :]) % P1).to(torch.float64) * (2.0 * torch.pi / P1)
+        t = torch.stack([torch.cos(ph), torch.sin(ph)], -1).reshape(P1, -1).to(F32).to(dev).contiguous()
+        _TWS[key] = t
+    return t
+
+
+def colspec_ok(Bn, C, P1, P2, m1, m2) -> bool:
+    """The folded column pass applies (blindno_colspec_ok; fp32 mix only)."""
+    return COLSPEC and not MIX_F16 and bool(query("blindno_colspec_ok", Bn, C, P1, P2, m1, m2))
 
 
 def require_device(*ts):
@@ -973,6 +1004,63 @@ def _grid_planes(grid, N1, N2, P1, P2, m2):
     return Dg
 
 
+_DG2_CACHE = {}
+
+
+def _grid_spec2(grid, N1, N2, P1, P2, m1, m2):
+    """Column spectra Dg2 (m2, 3, K1) complex of the grid / bias planes gx, gy, 1 on the crop
+    (the 2D counterpart of _grid_planes, for the folded column pass: the encoder's first-layer
+    spectrum is W0[:,0] U + W0[:,1] Dg2[0] + W0[:,2] Dg2[1] + b0 Dg2[2]); cached like Dg."""
+    key = (grid.device, grid.data_ptr(), grid._version, N1, N2, P1, P2, m1, m2)
+    hit = _DG2_CACHE.get(key)
+    if hit is not None:
+        return hit[-1]
+    capturing = torch.cuda.is_current_stream_capturing()
+    w = torch.tensor([[1.0, 0.0], [0.0, 1.0], [0.0, 0.0]], dtype=F32, device=grid.device)
+    b = torch.tensor([0.0, 0.0, 1.0], dtype=F32, device=grid.device)
+    g0 = _empty(1, 3, P1, P2, like=grid)
+    call("blindno_lift_fwd", ptr(_c(grid)), ptr(w), ptr(b), ptr(g0), 1, N1, N2, 2, 3, P1, P2,
+         stream_ptr())
+    nb = P1 // 16
+    part = _empty(nb * query("blindno_colspec_nchunk", 3, m2) * 128, like=grid)
+    call("blindno_rowdft_cd", ptr(g0), ptr(part), ptr(twiddle_mfma(P2, m2, grid.device)),
+         ptr(twiddle_colspec(P1, m1, grid.device)), 1, 3, P1, P2, m2, 0, P1, P2, stream_ptr())
+    K1 = kept_rows_count(m1, P1)
+    Dg2 = _empty(1, m2, 3, K1, 2, like=grid)
+    call("blindno_colmix", ptr(part), nb, None, ptr(Dg2), None, 1, 3, 3, P1, P2, m1, m2, 0, None, None,
+         None, stream_ptr())
+    if not capturing:
+        if len(_DG2_CACHE) > 16:
+            _DG2_CACHE.clear()
+        _DG2_CACHE[key] = (grid, Dg2)
+    return Dg2
+
+
+class _ColSpec:
+    """Launch helpers of the folded column pass for one encoder geometry (csrc/colspec.h)."""
+
+    def __init__(self, Bn, C, P1, P2, m1, m2, device):
+        self.Bn, self.C, self.P1, self.P2, self.m1, self.m2 = Bn, C, P1, P2, m1, m2
+        self.K1 = kept_rows_count(m1, P1)
+        self.nb = P1 // 16
+        self.tab = twiddle_colspec(P1, m1, device)
+        self.Tp = twiddle_mfma(P2, m2, device)
+        self.tb = twiddle_rowinv(P2, m2, device)
+
+    def part(self, Cp, like):
+        return _empty(self.Bn * self.nb * query("blindno_colspec_nchunk", Cp, self.m2) * 128, like=like)
+
+    def mix(self, part, nbv, Wt, direction, Cp=None, lift=None):
+        """(Xsave, Y) of the summed partials: direction 0 (X, Y = mix) or 1 (G, conj mix)."""
+        Xs = _empty(self.Bn, self.m2, self.C, self.K1, 2, like=part)
+        Y = _empty(self.Bn, self.m2, self.C, self.K1, 2, like=part)
+        w0, b0, Dg2 = lift if lift is not None else (None, None, None)
+        call("blindno_colmix", ptr(part), nbv, ptr(Wt), ptr(Xs), ptr(Y), self.Bn, self.C,
+             Cp or self.C, self.P1, self.P2, self.m1, self.m2, direction, ptr(w0), ptr(b0), ptr(Dg2),
+             stream_ptr())
+        return Xs, Y
+
+
 class BagEncoderFn(torch.autograd.Function):
     """The snapshot-bag encoder of NIOFP2D_FNO as ONE autograd node (2d_FPE/NIOModules.py:
     548-575): FNO_input (an FNO2d of input [u, gx, gy]) on every snapshot of the bag, then the
@@ -1005,14 +1093,49 @@ class BagEncoderFn(torch.autograd.Function):
         if C > 4 or meta.dim != 2 or n < 1:
             raise BlindnoError("BagEncoderFn: needs a 2D FNO of width <= 4")
         fc0w, fc0b = prm[0], prm[1]
-        Dg = _grid_planes(grid, N1, N2, P1, P2, meta.m2)
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         Xs, Wts, zs = [], [], []
         Wts_all = pack_w2d_many([(prm[2 + 4 * k], prm[3 + 4 * k]) for k in range(n)], P1)
+        cs = _ColSpec(Bn, C, P1, P2, meta.m1, meta.m2, X.device) \
+            if colspec_ok(Bn, C, P1, P2, meta.m1, meta.m2) else None
+        ctx.cs = cs
+        if cs is not None:
+            # the column pass folded into the row kernels: per layer, the kernel that forms the
+            # row spectrum leaves its column-DFT partials, blindno_colmix forms Xs and the mixed Y,
+            # and the row inverse rebuilds its row coefficients from Y
+            Dg2 = _grid_spec2(grid, N1, N2, P1, P2, meta.m1, meta.m2)
+            part = cs.part(1, X)
+            call("blindno_rowdft_bag_lift_cd", ptr(X), ptr(idx_t), ptr(part), ptr(cs.Tp), ptr(cs.tab), B, T,
+                 L, N1, N2, P1, P2, meta.m2, stream_ptr())
+            nbv = (N1 + 15) // 16
+            for k in range(n):
+                off = 2 + k * 4
+                cw, cb = prm[off + 2], prm[off + 3]
+                Wt = Wts_all[k]
+                last = k == n - 1
+                Xk, Y = cs.mix(part, nbv, Wt, 0, Cp=1 if k == 0 else C,
+                               lift=(fc0w, fc0b, Dg2) if k == 0 else None)
+                z = _empty(Bn, C, P1, P2, like=X)
+                part = None if last else cs.part(C, X)
+                if k == 0:
+                    call("blindno_rowidft_epi_lift_zc", ptr(Y), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),
+                         ptr(fc0b), ptr(cw), ptr(cb), ptr(z), ptr(cs.tb), ptr(cs.tab), ptr(part), ptr(cs.Tp),
+                         B, T, L, N1, N2, C, P1, P2, meta.m1, meta.m2, 1, stream_ptr())
+                else:
+                    # the last layer is read by the projection on its crop only
+                    oN1, oN2 = (Ho, Wo) if last else (P1, P2)
+                    call("blindno_rowidft_epi_zc", ptr(Y), ptr(zs[-1]), ptr(cw), ptr(cb), ptr(z), ptr(cs.tb),
+                         ptr(cs.tab), ptr(part), ptr(cs.Tp), Bn, C, P1, P2, meta.m1, meta.m2, 1, 1, oN1, oN2,
+                         stream_ptr())
+                nbv = P1 // 16
+                Xs.append(Xk)
+                Wts.append(Wt)
+                zs.append(z)
+        Dg = _grid_planes(grid, N1, N2, P1, P2, meta.m2) if cs is None else None
         # each row inverse but the last also takes the next layer's row DFT of GELU(z) in its
         # pass (the field is not read back for it)
         At_next = None
-        for k in range(n):
+        for k in range(n if cs is None else 0):
             off = 2 + k * 4
             w1, w2, cw, cb = prm[off:off + 4]
             Wt = Wts_all[k]
@@ -1124,8 +1247,51 @@ class BagEncoderFn(torch.autograd.Function):
         grads[off_fc1 + 3] = gp[o:o + Cout]
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         fc0w, fc0b = prm[0], prm[1]
+        cs = ctx.cs
+        ctx.cs = None
+        if cs is not None:
+            # the folded column pass (forward above): the last layer's adjoint starts from the
+            # row DFT + column-DFT partials of dz on its crop; each adjoint row inverse rebuilds
+            # its row coefficients from the conj-mixed spectrum and leaves the previous layer's
+            # partials; the weight gradient reads the saved spectra as before
+            part = cs.part(C, gh)
+            valid = crop or (P1, P2)
+            call("blindno_rowdft_cd", ptr(dz), ptr(part), ptr(cs.Tp), ptr(cs.tab), Bn, C, P1, P2, meta.m2, 0,
+                 valid[0], valid[1], stream_ptr())
+            nbv = (valid[0] + 15) // 16
+            for k in reversed(range(n)):
+                off = 2 + 4 * k
+                w1, w2, cw, cb = prm[off:off + 4]
+                G, Yb = cs.mix(part, nbv, Wts[k], 1)
+                dWt = k_mix_wgrad(Xs[k], G, Bn, C, C, sh.K1, meta.m2, deferrable=True)
+                grads[off], grads[off + 1] = unpack_weights(dWt, (w1, w2), P1, 2)
+                dv = crop if (k == n - 1 and crop) else (P1, P2)
+                if k > 0:
+                    nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, meta.m2)
+                    pw = _empty(nchunk, C * C + C, like=gh)
+                    dx = _empty(Bn, C, P1, P2, like=gh)
+                    part = cs.part(C, gh)
+                    call("blindno_rowidft_bwd_zc", ptr(Yb), ptr(dz), ptr(cw), ptr(zs[k - 1]), ptr(dx), ptr(cs.tb),
+                         ptr(cs.tab), ptr(part), ptr(cs.Tp), ptr(pw), Bn, C, P1, P2, meta.m1, meta.m2, 1,
+                         dv[0], dv[1], stream_ptr())
+                    g = reduce_partials(pw, nchunk, C * C + C)
+                    grads[off + 2], grads[off + 3] = g[:C * C].view_as(cw), g[C * C:]
+                    dz = dx
+                    nbv = P1 // 16
+                else:
+                    nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, meta.m2)
+                    npl = C * C + C + 4 * C
+                    pl = _empty(nchunk, npl, like=gh)
+                    call("blindno_rowidft_bwd_lift_zc", ptr(Yb), ptr(dz), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),
+                         ptr(fc0b), ptr(cw), ptr(cs.tb), ptr(cs.tab), ptr(pl), B, T, L, N1, N2, C, P1, P2,
+                         meta.m1, meta.m2, stream_ptr())
+                    g = reduce_partials(pl, nchunk, npl)
+                    grads[off + 2] = g[:C * C].view_as(cw)
+                    grads[off + 3] = g[C * C:C * C + C]
+                    grads[0] = g[C * C + C:C * C + 4 * C].view(C, 3)
+                    grads[1] = g[C * C + 4 * C:]
         At_dz = None          # row DFT of dz taken by the later layer's adjoint pass
-        for k in reversed(range(n)):
+        for k in reversed(range(n if cs is None else 0)):
             off = 2 + 4 * k
             w1, w2, cw, cb = prm[off:off + 4]
             valid = crop if k == n - 1 else None
@@ -1209,6 +1375,9 @@ class DeepONetBagFn(torch.autograd.Function):
         S = basis.shape[0]
         if basis.shape[1] != P:
             raise BlindnoError(f"deeponet: branch {tuple(w.shape)} / trunk {tuple(basis.shape)} mismatch")
+        if P > 64:
+            raise BlindnoError(f"deeponet: at most 64 basis functions (n_basis = 25 in every reference "
+                               f"script), got {P}")
         scale = 1.0 / math.sqrt(P)
         wbar = _empty(B, P, like=w)
         ubar = _empty(B, S, like=w)

@@ -480,13 +480,16 @@ class BatchSelect:
         self._srcs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
         self._dsts = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dsts])
         self._rows = (ctypes.c_int64 * n)(*[t[0].numel() for t in srcs])
+        self._nsrc = (ctypes.c_int64 * n)(*[t.shape[0] for t in srcs])
         self._n = n
 
     def __call__(self, ids: torch.Tensor):
         if ids.dtype != torch.int64 or not ids.is_contiguous() or ids.numel() != self.B:
             raise ValueError("BatchSelect: ids must be a contiguous int64 tensor of the batch size")
-        call("blindno_gather_batch", self._srcs, self._dsts, self._rows, self._n, ptr(ids), self.B,
-             stream_ptr())
+        # an id outside a source's rows fills that batch row with NaN on the device (checking
+        # the range here would cost a device->host sync per step)
+        call("blindno_gather_batch", self._srcs, self._dsts, self._rows, self._nsrc, self._n, ptr(ids),
+             self.B, stream_ptr())
 
 
 def shard_bag_ids(n_bags: int, per_rank_batch: int, rank: int, world: int):

@@ -1,0 +1,145 @@
+// The column pass of a 2D spectral layer folded into the row kernels that surround it
+// (FNO_input of the snapshot encoder: C = 4 channels, m1 = 12 -> K1 = 24 kept frequency rows,
+// m2 = 12 column modes; 2d_FPE/FNOModules.py:156-178, 226-232).
+//
+// The separate column pass (colfuse_kernel) read the row spectrum At and wrote the row
+// coefficients Z of every layer: 2 x 18 MB round trips plus a launch per layer at config C.
+// Here only the K1 x m2 column spectrum crosses kernels:
+//   * CD ("column DFT"): the row kernel that produces At (the row DFT, or the row inverse that
+//     takes the next layer's row DFT in its pass) also takes At's column DFT over its own
+//     16-row block, Xs_blk[k][c][j] = sum_{h in blk} At[h][k][c] F[h][j] (F = e^{-2 pi i r_j h / P1}),
+//     and writes it as a per-block partial (fixed layout, below);
+//   * colmix (colspec.hip): sums the P1 / 16 block partials of a sample in block order (fixed
+//     order, deterministic), forms the saved spectrum Xs and the mixed spectrum Y as the column
+//     pass did (Y = c_k / (P1 P2) sum_c Xs W, or the adjoint's conj(W) mix);
+//   * ZY ("Z from Y"): the next row inverse rebuilds the row coefficients of its 16 rows,
+//     Z[h][k][c] = sum_j Y[k][c][j] conj(F[h][j]), on the matrix cores in its prologue (72
+//     v_mfma_f32_16x16x4f32 per 16-row block), straight into its B-operand registers.
+// Both folded GEMMs use one twiddle table Tab[h][2 j + p] = (p ? sin : cos)(2 pi r_j h / P1),
+// staged in LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace blindno {
+
+typedef float cs_f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCsK1 = 24;                  // kept frequency rows (m1 = 12)
+constexpr int kCsMT2 = 2 * kCsK1 / 16;     // 16-row M tiles of the column DFT (rows (j, p))
+constexpr int kCsKQ = kCsK1 / 4;           // complex Y values per lane and k in the ZY GEMM
+
+struct SpecCol {
+  const float* Y;     // ZY: Y[n][k][c][j] (complex, j < K1) from colmix; nullptr: read Z
+  float* part;        // CD: per-block partials (layout below); nullptr: write At instead
+  const float* tab;   // Tab[h][2 K1] (global; staged in LDS by the kernel)
+  int nblk;           // CD: 16-row blocks per sample in the partial buffer (P1 / 16)
+};
+
+// Partials of one (sample n, 16-row block b): NCH = C NNT MT2 chunks of 64 lanes x float2,
+//   part[((n nblk + b) NCH + ch) 128 + 2 lane + e],  ch = (c NNT + nt) MT2 + mt2,
+// lane = 16 g + c16 holding Xs_part[k][c][j] component q, with
+//   k = 8 nt + (c16 >> 1), q = c16 & 1 (0: Re, 1: Im), j = 8 mt2 + 2 g + e.
+// (NNT = ceil(2 m2 / 16) column tiles of the row spectrum; columns k >= m2 hold zeros.)
+__host__ __device__ __forceinline__ int colspec_nchunk(int C, int m2) {
+  return C * ((2 * m2 + 15) / 16) * kCsMT2;
+}
+
+// swap with the neighbouring lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2]
+__device__ __forceinline__ float cs_swap1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
+// CD epilogue of one channel: acc[nt] = At[h0 + 4 g + r][k' = 16 nt + c16] (the row spectrum of
+// the block in the MFMA D layout, k' = 2 k + Re/Im), sTab the LDS twiddle table.  Writes the
+// channel's NNT MT2 chunks at dst (= part + ((n nblk + b) NCH + c NNT MT2) 128).
+//   Out[(j, p)][k'] = sum_h F_p[j][h] At[h][k'],  F_0 = cos, F_1 = sin  (A = Tab, B = acc)
+//   Xs_re = Out[(j,0)][re] + Out[(j,1)][im],  Xs_im = Out[(j,0)][im] - Out[(j,1)][re]
+// rows m = 2 j + p of tile mt2 hold (j = 8 mt2 + 2 g + (r >> 1), p = r & 1) in a lane's D, and
+// the Re / Im columns of one mode sit in neighbouring lanes: one DPP swap per pair.
+template <int NNT>
+__device__ __forceinline__ void cd_store(const cs_f32x4 (&acc)[NNT], const float* __restrict__ sTab,
+                                         int h0, int lane, float* __restrict__ dst) {
+  const int c16 = lane & 15, g = lane >> 4;
+  float ft[kCsMT2][4];
+#pragma unroll
+  for (int mt = 0; mt < kCsMT2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ft[mt][r] = sTab[(h0 + 4 * g + r) * (2 * kCsK1) + 16 * mt + c16];
+  const float sg = (lane & 1) ? -1.0f : 1.0f;
+#pragma unroll
+  for (int nt = 0; nt < NNT; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < kCsMT2; ++mt) {
+      cs_f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o = __builtin_amdgcn_mfma_f32_16x16x4f32(ft[mt][r], acc[nt][r], o, 0, 0, 0);
+      const float p1 = cs_swap1(o[1]), p3 = cs_swap1(o[3]);
+      float2 v;
+      v.x = fmaf(sg, p1, o[0]);
+      v.y = fmaf(sg, p3, o[2]);
+      *reinterpret_cast<float2*>(dst + (nt * kCsMT2 + mt) * 128 + 2 * lane) = v;
+    }
+}
+
+// ZY prologue: the row coefficients of rows h0 .. h0 + 15 of sample n, as the transposed row
+// inverse's B operand zb[c][sp] = Z[h0 + c16][kk = S g + sp][c] (kk = 2 k + Re/Im).
+//   D[(kk, c)][h] = sum_{(j, q)} A[(kk, c)][(j, q)] B[(j, q)][h]
+//   A: Re rows (Y_re, -Y_im), Im rows (Y_im, Y_re);  B[(j, q)][h] = Tab[h][2 j + q]
+// M rows m = 16 mt + 4 g' + r' <-> (kk = S g' + mt, c = r'), so a lane's D of tile mt is
+// zb[r][mt]; K index (j, q) = 2 j + q = (K1 / 2) g + s over the K1 / 2 steps s (each lane group
+// streams K1 / 4 consecutive complex Y values of one (k, c)).
+// (split in two so that the caller can issue its own first loads between them: zy_fetch
+// issues the Y loads and the twiddle reads, zy_mfma consumes them)
+template <int S, int C>
+struct ZyOperands {
+  float bt[kCsK1 / 2];
+  float yv[S / 2][2 * kCsKQ];
+};
+
+template <int S, int C>
+__device__ __forceinline__ void zy_fetch(const float* __restrict__ Y, const float* __restrict__ sTab,
+                                         int n, int m2, int h0, int lane, ZyOperands<S, C>& op) {
+  static_assert(C == 4 && S % 2 == 0, "zy_fetch: C = 4, even S");
+  const int c16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < S / 2; ++i) {
+    const int k = (S / 2) * (c16 >> 2) + i;
+    const cs_f32x4* yp = reinterpret_cast<const cs_f32x4*>(
+        Y + ((((int64_t)n * m2 + k) * C + (c16 & 3)) * kCsK1 + kCsKQ * g) * 2);
+#pragma unroll
+    for (int q = 0; q < kCsKQ / 2; ++q) {
+      const cs_f32x4 v = yp[q];
+      op.yv[i][4 * q] = v.x; op.yv[i][4 * q + 1] = v.y; op.yv[i][4 * q + 2] = v.z; op.yv[i][4 * q + 3] = v.w;
+    }
+  }
+  const cs_f32x4* tr = reinterpret_cast<const cs_f32x4*>(sTab + (h0 + c16) * (2 * kCsK1) + (kCsK1 / 2) * g);
+#pragma unroll
+  for (int q = 0; q < kCsK1 / 8; ++q) {
+    const cs_f32x4 v = tr[q];
+    op.bt[4 * q] = v.x; op.bt[4 * q + 1] = v.y; op.bt[4 * q + 2] = v.z; op.bt[4 * q + 3] = v.w;
+  }
+}
+
+template <int S, int C>
+__device__ __forceinline__ void zy_mfma(const ZyOperands<S, C>& op, float (&zb)[C][S]) {
+  cs_f32x4 za[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) za[i] = (cs_f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < S / 2; ++i)
+#pragma unroll
+    for (int s = 0; s < kCsK1 / 2; ++s) {
+      const float yr = op.yv[i][2 * (s >> 1)], yi = op.yv[i][2 * (s >> 1) + 1];
+      const float are = (s & 1) ? -yi : yr;
+      const float aim = (s & 1) ? yr : yi;
+      za[2 * i] = __builtin_amdgcn_mfma_f32_16x16x4f32(are, op.bt[s], za[2 * i], 0, 0, 0);
+      za[2 * i + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim, op.bt[s], za[2 * i + 1], 0, 0, 0);
+    }
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int sp = 0; sp < S; ++sp) zb[c][sp] = za[sp][c];
+}
+
+}  // namespace blindno

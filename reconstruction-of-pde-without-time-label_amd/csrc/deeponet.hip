@@ -13,6 +13,8 @@
 //     dwbar[b, k]  = scale sum_p g[b, p] basis[p, k],   dw[b, l, k] = lw_l dwbar[b, k],
 //     db0          = scale sum_{b, p} g[b, p] sum_l lw_l.
 // The two reductions over p are per-workgroup partials summed in a fixed order (no atomics).
+// More than kMaxB bags run as bag chunks of kMaxB in stream order: dbasis and db0 of a later
+// chunk are added to the earlier chunks' (fixed chunk order, deterministic).
 #include "common.h"
 #include "blindno.h"
 
@@ -22,8 +24,7 @@ namespace {
 
 constexpr int kPts = 256;          // grid points per workgroup
 constexpr int kMaxP = 64;          // basis functions (n_basis = 25 in every reference script)
-constexpr int kMaxB = 64;          // bags per launch
-constexpr int kMaxL = 1024;
+constexpr int kMaxB = 64;          // bags per backward launch (LDS: 148.7 KB at B = P = 64)
 
 // ubar[b, p] for the kPts points of this workgroup and bag blockIdx.y
 __global__ __launch_bounds__(kPts) void deeponet_bag_fwd_kernel(
@@ -63,7 +64,8 @@ __global__ __launch_bounds__(kPts) void deeponet_bag_fwd_kernel(
 //     partial[blk][b P + k] = scale sum_{p in blk} g[b, p] basis[p, k],  partial[blk][B P] = scale sum g
 __global__ __launch_bounds__(kPts) void deeponet_bag_bwd_kernel(
     const float* __restrict__ g, const float* __restrict__ basis, const float* __restrict__ wbar,
-    float* __restrict__ dbasis, float* __restrict__ partial, int B, int S, int P, float scale) {
+    float* __restrict__ dbasis, float* __restrict__ partial, int B, int S, int P, float scale,
+    int accumulate) {
   // dynamic LDS: sg [B][kPts + 1] (g scaled), sb [kPts][P + 1] (basis rows), sw [B][P] (wbar)
   extern __shared__ float lds[];
   float* sg = lds;
@@ -84,7 +86,8 @@ __global__ __launch_bounds__(kPts) void deeponet_bag_bwd_kernel(
     const int q = e / P, k = e - q * P;
     float acc = 0.f;
     for (int b = 0; b < B; ++b) acc = fmaf(sg[b * (kPts + 1) + q], sw[b * P + k], acc);
-    dbasis[(size_t)(p0 + q) * P + k] = acc;
+    float* o = dbasis + (size_t)(p0 + q) * P + k;
+    *o = accumulate ? *o + acc : acc;
   }
   // partials: one (b, k) pair (or the b0 sum) per thread, points in order
   const int npair = B * P + 1;
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(kPts) void deeponet_bag_bwd_kernel(
 // fixed-order sum of the partials; dw[b, l, k] = lw_l dwbar[b, k], db0 = sum g * sum_l lw_l
 __global__ __launch_bounds__(256) void deeponet_bag_finish_kernel(
     const float* __restrict__ partial, const float* __restrict__ lw, float* __restrict__ dw,
-    float* __restrict__ db0, int nblk, int B, int L, int P) {
+    float* __restrict__ db0, int nblk, int B, int L, int P, int accumulate) {
   __shared__ float sd[kMaxB * kMaxP + 1];
   const int npair = B * P + 1;
   for (int e = threadIdx.x; e < npair; e += blockDim.x) {
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256) void deeponet_bag_finish_kernel(
       lsum = 0.f;
       for (int l = 0; l < L; ++l) lsum += lw[l];
     }
-    db0[0] = sd[B * P] * lsum;
+    db0[0] = accumulate ? db0[0] + sd[B * P] * lsum : sd[B * P] * lsum;
   }
   const float inv = 1.0f / (float)L;
   const int n = B * L * P;
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(256) void deeponet_bag_finish_kernel(
 }
 
 bool dims_ok(int B, int L, int S, int P) {
-  return B >= 1 && B <= kMaxB && L >= 1 && L <= kMaxL && S >= 1 && P >= 1 && P <= kMaxP;
+  return B >= 1 && L >= 1 && S >= 1 && P >= 1 && P <= kMaxP;
 }
 
 }  // namespace
@@ -155,10 +158,15 @@ BLINDNO_API int blindno_deeponet_bag_bwd(const float* g, const float* basis, con
   if (!dims_ok(B, L, S, P) || !g || !basis || !wbar || !dw || !dbasis || !partial ||
       nblk != blindno_deeponet_bag_nblk(S))
     return (int)hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * ((size_t)B * (kPts + 1) + (size_t)kPts * (P + 1) + (size_t)B * P);
-  deeponet_bag_bwd_kernel<<<nblk, kPts, lds, (hipStream_t)stream>>>(g, basis, wbar, dbasis, partial,
-                                                                    B, S, P, scale);
-  deeponet_bag_finish_kernel<<<1, 256, 0, (hipStream_t)stream>>>(partial, lw, dw, db0, nblk, B, L,
-                                                                 P);
+  // bag chunks of <= kMaxB in stream order; each reuses the partial buffer (sized for B bags)
+  for (int c0 = 0; c0 < B; c0 += kMaxB) {
+    const int bc = B - c0 < kMaxB ? B - c0 : kMaxB;
+    const size_t lds =
+        sizeof(float) * ((size_t)bc * (kPts + 1) + (size_t)kPts * (P + 1) + (size_t)bc * P);
+    deeponet_bag_bwd_kernel<<<nblk, kPts, lds, (hipStream_t)stream>>>(
+        g + (size_t)c0 * S, basis, wbar + (size_t)c0 * P, dbasis, partial, bc, S, P, scale, c0 > 0);
+    deeponet_bag_finish_kernel<<<1, 256, 0, (hipStream_t)stream>>>(
+        partial, lw, dw + (size_t)c0 * L * P, db0, nblk, bc, L, P, c0 > 0);
+  }
   return (int)hipGetLastError();
 }

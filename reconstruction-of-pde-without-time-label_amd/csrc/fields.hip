@@ -1257,21 +1257,29 @@ BLINDNO_API int blindno_gather_flat(const void* const* srcs, const int64_t* offs
 // Batch select of the training loop (the DataLoader's batch, 2d_FPE/train_fno.py:113-116): rows
 // ids[b] of up to kBatchSegs row-major tensors (bags X (n, T N1 N2), targets Y (n, N1 N2 C)) into
 // their batch buffers, in ONE launch: blockIdx.y = (segment, batch row), 16-B copies when the
-// rows are 16-B aligned.  ids are device int64 (the epoch's permutation slice).
+// rows are 16-B aligned.  ids are device int64 (the epoch's permutation slice); an id outside
+// [0, n) of its source fills that batch row with NaN (the step's loss turns NaN) instead of
+// reading past the tensor.
 constexpr int kBatchSegs = 4;
 struct BatchSegs {
   const float* src[kBatchSegs];
   float* dst[kBatchSegs];
   int64_t row[kBatchSegs];   // floats per row
+  int64_t n[kBatchSegs];     // rows of each source
   int nseg, vec;
 };
 
 __global__ __launch_bounds__(kBlock) void gather_batch_kernel(BatchSegs sg, const int64_t* __restrict__ ids,
                                                               int B) {
   const int sb = blockIdx.y, seg = sb / B, b = sb - seg * B;
-  const int64_t row = sg.row[seg];
-  const float* __restrict__ src = sg.src[seg] + ids[b] * row;
+  const int64_t row = sg.row[seg], id = ids[b];
+  const float* __restrict__ src = sg.src[seg] + id * row;
   float* __restrict__ dst = sg.dst[seg] + (int64_t)b * row;
+  if (id < 0 || id >= sg.n[seg]) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < row; i += (int64_t)gridDim.x * kBlock)
+      dst[i] = __builtin_nanf("");
+    return;
+  }
   if (sg.vec) {
     const int64_t n4 = row >> 2;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock)
@@ -1283,14 +1291,16 @@ __global__ __launch_bounds__(kBlock) void gather_batch_kernel(BatchSegs sg, cons
 }
 
 BLINDNO_API int blindno_gather_batch(const void* const* srcs, void* const* dsts, const int64_t* rows,
-                                     int nseg, const int64_t* ids, int B, void* stream) {
-  if (nseg < 1 || nseg > kBatchSegs || B < 1 || !ids) return (int)hipErrorInvalidValue;
+                                     const int64_t* nsrc, int nseg, const int64_t* ids, int B,
+                                     void* stream) {
+  if (nseg < 1 || nseg > kBatchSegs || B < 1 || !ids || !nsrc) return (int)hipErrorInvalidValue;
   BatchSegs sg{};
   sg.nseg = nseg;
   sg.vec = 1;
   int64_t maxrow = 0;
   for (int i = 0; i < nseg; ++i) {
-    if (!srcs[i] || !dsts[i] || rows[i] < 1) return (int)hipErrorInvalidValue;
+    if (!srcs[i] || !dsts[i] || rows[i] < 1 || nsrc[i] < 1) return (int)hipErrorInvalidValue;
+    sg.n[i] = nsrc[i];
     sg.src[i] = (const float*)srcs[i];
     sg.dst[i] = (float*)dsts[i];
     sg.row[i] = rows[i];

@@ -414,9 +414,16 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
           float* sd = sdh[wave];
 #pragma unroll
           for (int r = 0; r < 4; ++r) sd[c16 * 17 + 4 * g4 + r] = dh[r];
+          // the tile is shared by the wave's lanes: order the writes before the cross-lane
+          // reads, and the reads before the next point tile's writes (LDS ops of one wave
+          // complete in order; the barrier keeps the compiler from moving them across)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           float bv[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) bv[r] = sd[(4 * g4 + r) * 17 + c16];
+          __builtin_amdgcn_wave_barrier();
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int jr = 16 * t + 4 * g4 + r;

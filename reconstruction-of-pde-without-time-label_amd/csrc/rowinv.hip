@@ -18,6 +18,7 @@
 #include "blindno.h"
 #include "gelu_pk.h"
 #include "kernels.h"
+#include "colspec.h"
 
 using namespace blindno;
 
@@ -553,20 +554,28 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 // HW: the layer has its 1x1 conv (wc != NULL) -- a compile-time flag: a runtime test around each
 // operand load made hipcc branch around the loads and count their waits conservatively.
 // NSC: steps per row block as a compile-time constant (P2 / (16 NH)), 0 = a runtime loop.
-template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH, bool HW_ = true, int NSC = 0>
+// ZY / CD (colspec.h): the row coefficients built from the mixed column spectrum sc.Y in the
+// prologue of each 16-row block instead of read as Z; the next row DFT taken in the opposite
+// orientation (D = f(y) T: rows on the M side) and its column DFT over the block written as
+// partials to sc.part instead of At.
+template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH, bool HW_ = true, int NSC = 0,
+          bool ZY = false, bool CD = false>
 __global__ __launch_bounds__(256) void rowfuse_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int P1, int P2,
-    BagLift bl, int dN1, int dN2, RowDftNext rd) {
+    BagLift bl, int dN1, int dN2, RowDftNext rd, SpecCol sc) {
   constexpr int C = 4;
   constexpr int m2 = 2 * S;
   constexpr int NNT = (4 * S + 15) / 16;          // 16-column tiles of the next row DFT
   constexpr int Npad = 16 * NNT;
+  static_assert(!CD || RD, "CD takes the column DFT of the next row DFT");
   const int NT = P2 >> 4;                           // MFMA column tiles (NT % NH == 0)
   extern __shared__ float lds[];
   float* sA = lds;                                  // [NT][64 lanes][S]
   float* sT = lds + NT * 64 * S;                    // RD: [NT][4][Npad][4] (rowdft's image)
+  float* sTab = sT + (RD ? NT * 16 * Npad : 0);     // ZY / CD: [P1][2 K1]
+  if (ZY || CD) stage_to_lds(sTab, sc.tab, P1 * 2 * kCsK1);
   for (int e = threadIdx.x; e < NT * 64 * S; e += blockDim.x) {
     const int t = e / (64 * S), rem = e - t * (64 * S);
     const int ln = rem / S, sp = rem - ln * S;
@@ -617,12 +626,18 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
   };
   f32x4 znext[S];
   const int item0 = blockIdx.x * kW + wave;
-  if (ROWFUSE_ZPRE) load_z(item0, znext);
+  if (ROWFUSE_ZPRE && !ZY) load_z(item0, znext);
   for (int item = item0; item < nitems; item += gridDim.x * kW) {
     const int n = item / HB;
-    const int h = ((item - n * HB) << 4) + c16;
+    const int h0 = (item - n * HB) << 4;
+    const int h = h0 + c16;
     float zb[C][S];
-    {
+    // ZY: the Y loads go out first; the row coefficients are formed after the first field
+    // loads are issued (below), so their latencies overlap
+    ZyOperands<ZY ? S : 2, C> zop;
+    if constexpr (ZY) {
+      zy_fetch<S, C>(sc.Y, sTab, n, m2, h0, lane, zop);
+    } else {
       f32x4 zcur[S];
       if (ROWFUSE_ZPRE) {
 #pragma unroll
@@ -806,8 +821,12 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
 #pragma unroll
             for (int c = 0; c < C; ++c)
 #pragma unroll
-              for (int s = 0; s < 4; ++s)
-                racc[c][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[s], ya[c][s], racc[c][nt], 0, 0, 0);
+              for (int s = 0; s < 4; ++s) {
+                if constexpr (CD)       // D[h][k']: the block's rows on the M side
+                  racc[c][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[c][s], tb[s], racc[c][nt], 0, 0, 0);
+                else                    // D[k'][h]
+                  racc[c][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tb[s], ya[c][s], racc[c][nt], 0, 0, 0);
+              }
           }
         }
       }
@@ -819,7 +838,8 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
     // sinks the loads next to their first use)
     Ops buf[2];
     load(0, buf[0]);
-    if (ROWFUSE_ZPRE) load_z(item + gridDim.x * kW, znext);   // after this item's first loads
+    if constexpr (ZY) zy_mfma<S, C>(zop, zb);
+    if (ROWFUSE_ZPRE && !ZY) load_z(item + gridDim.x * kW, znext);   // after this item's first loads
     if constexpr (NSC > 0) {
       // the step count is a compile-time constant: straight-line steps, the waits counted exactly
 #pragma unroll
@@ -848,7 +868,12 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
         }
       }
     }
-    if (RD) {
+    if constexpr (CD) {
+      const int nch = colspec_nchunk(C, m2);
+      float* dst = sc.part + ((int64_t)(n * sc.nblk + (h0 >> 4)) * nch) * 128;
+#pragma unroll
+      for (int c = 0; c < C; ++c) cd_store<NNT>(racc[c], sTab, h0, lane, dst + c * NNT * kCsMT2 * 128);
+    } else if (RD) {
       // lane: row h, spectrum columns k' = 16 nt + 4 g + r -> modes 8 nt + 2 g + r/2 (Re, Im)
 #pragma unroll
       for (int c = 0; c < C; ++c)
@@ -976,12 +1001,15 @@ RowinvGeom rowinv_geom(int Bn, int C, int P1, int P2, int m2) {
   return g;
 }
 
-template <int MODE, int ACT, int WG, int LIFT = 0>
+// ZC: the column pass folded in (colspec.h; sc.Y for ZY, sc.part for CD with the next row
+// DFT): the transposed C = 4 kernel only, m2 = 12, with the 1x1 conv; no fallback
+template <int MODE, int ACT, int WG, int LIFT = 0, bool ZC = false>
 int rowinv_launch(const float* Z, const float* xs, const float* dz, const float* wc,
                   const float* bc, float* out, const float* TB, float* partial, int nblocks,
                   int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{},
                   int G = 1, int64_t wgs = 0, int dN1 = 0, int dN2 = 0,
-                  RowDftNext rd = RowDftNext{nullptr, nullptr, 0, 0}) {
+                  RowDftNext rd = RowDftNext{nullptr, nullptr, 0, 0},
+                  SpecCol sc = SpecCol{nullptr, nullptr, nullptr, 0}) {
   if (dN1 <= 0) dN1 = P1;
   if (dN2 <= 0) dN2 = P2;
   if (dN1 > P1 || dN2 > P2) return (int)hipErrorInvalidValue;
@@ -999,11 +1027,16 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
     // the transposed C = 4 kernel: 16-B field accesses need aligned bases and a crop width
     // (dz's valid region, the snapshot) in whole float4s
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    const bool rd_ok = !rd.At || rd.Npad == 16 * ((2 * m2 + 15) / 16);
+    const bool rd_ok = (!rd.At && !(ZC && sc.part)) || rd.Npad == 16 * ((2 * m2 + 15) / 16);
+    const bool zc_ok = !ZC || (m2 == 12 && wc && sc.tab && al(sc.Y) && al(sc.tab) &&
+                              (!sc.part || (rd.Tp && sc.nblk == P1 / 16)) && (sc.Y || sc.part));
+    if (ZC && !(rowfuse_shape(Bn, C, P1, P2, m2) && zc_ok)) return (int)hipErrorInvalidValue;
     if (rowfuse_shape(Bn, C, P1, P2, m2) && G == 1 && al(Z) && al(xs) && al(dz) && al(out) &&
-        dN2 % 4 == 0 && rd_ok && (!LIFT || (bl.N2 % 4 == 0 && al(bl.X) && al(bl.grid)))) {
+        dN2 % 4 == 0 && rd_ok && zc_ok && (!LIFT || (bl.N2 % 4 == 0 && al(bl.X) && al(bl.grid)))) {
       const int NT = P2 / 16, S = m2 / 2;
-      size_t shf = sizeof(float) * ((size_t)NT * 64 * S + (rd.At ? (size_t)NT * 16 * rd.Npad : 0));
+      const bool rdx = rd.At || (ZC && sc.part);          // the next row DFT taken in the pass
+      size_t shf = sizeof(float) * ((size_t)NT * 64 * S + (rdx ? (size_t)NT * 16 * rd.Npad : 0) +
+                                    (ZC ? (size_t)P1 * 2 * kCsK1 : 0));
       const size_t red = sizeof(float) * (size_t)kW * (C * C + C + 4 * C);
       if (shf < red) shf = red;
       if (shf > 160 * 1024) return (int)hipErrorInvalidValue;
@@ -1016,34 +1049,43 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       const bool p160 = P2 == 160 && MODE == 0;
       // the output crop (MODE 0, no next row DFT): 128 of the 160 columns, 4 steps
       const bool crop128 = MODE == 0 && !rd.At && dN2 == 128;
-#define RF(RD_, S_)                                                                            \
+#define RFX(RD_, S_, ZY_, CD_)                                                                 \
   do {                                                                                         \
     if (wc && p160 && crop128 && RD_ == 0)                                                     \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true,                             \
-                     MODE == 0 ? 128 / (16 * NHX(RD_)) : 0>                                    \
+                     MODE == 0 ? 128 / (16 * NHX(RD_)) : 0, ZY_, CD_>                          \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
-                                      dN2, rd);                                                \
+                                      dN2, rd, sc);                                            \
     else if (wc && p160 && (dN2 == P2 || RD_ != 0))                                            \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true,                             \
-                     MODE == 0 ? 160 / (16 * NHX(RD_)) : 0>                                    \
+                     MODE == 0 ? 160 / (16 * NHX(RD_)) : 0, ZY_, CD_>                          \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
-                                      dN2, rd);                                                \
+                                      dN2, rd, sc);                                            \
     else if (wc)                                                                               \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true>                             \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true, 0, ZY_, CD_>                \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
-                                      dN2, rd);                                                \
-    else                                                                                       \
+                                      dN2, rd, sc);                                            \
+    else if (!ZY_)                                                                             \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), false>                            \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
-                                      dN2, rd);                                                \
+                                      dN2, rd, sc);                                            \
   } while (0)
+#define RF(RD_, S_) RFX(RD_, S_, false, false)
 #define RF_S(RD_) \
   do { if (S == 2) RF(RD_, 2); else if (S == 4) RF(RD_, 4); else if (S == 6) RF(RD_, 6); else RF(RD_, 8); } while (0)
-      if (!rd.At) RF_S(0);
-      else if (rd.act) RF_S(2);
-      else RF_S(1);
+      if constexpr (ZC) {
+        // ZY always; CD with the next row DFT (act: of GELU(field)); m2 = 12 (zc_ok)
+        if (!sc.part) RFX(0, 6, true, false);
+        else if (rd.act) RFX(2, 6, true, true);
+        else RFX(1, 6, true, true);
+      } else {
+        if (!rd.At) RF_S(0);
+        else if (rd.act) RF_S(2);
+        else RF_S(1);
+      }
 #undef RF_S
 #undef RF
+#undef RFX
 #undef NHX
       return (int)hipGetLastError();
     }
@@ -1309,4 +1351,115 @@ BLINDNO_API int blindno_rowidft_bwd_lift(const float* G, const float* dz, const 
   const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
   return rowinv_launch<1, 0, 1, 1>(G, nullptr, dz, wc, nullptr, nullptr, tb, partial,
                                    nb, Bn, C, P1, P2, m2, (hipStream_t)stream, bl);
+}
+
+// ------------------------------------------------------------ folded column pass (colspec.h)
+// The row kernels of FNO_input with the column pass folded in: Y (Bn, m2, C, K1) complex from
+// blindno_colmix replaces Z; part (Bn, P1 / 16, NCH, 64, 2) receives the column-DFT partials of
+// the next row spectrum (blindno_colspec_nchunk) instead of At; tab = Tab[P1][2 K1]
+// (blindno.ops.twiddle_colspec).  Shapes: blindno_colspec_ok.
+namespace {
+SpecCol spec_col(const float* Y, float* part, const float* tab, int P1) {
+  return SpecCol{Y, part, tab, P1 / 16};
+}
+}  // namespace
+
+BLINDNO_API int blindno_colspec_ok(int Bn, int C, int P1, int P2, int m1, int m2) {
+  return (rowfuse_shape(Bn, C, P1, P2, m2) && m2 == 12 && m1 == 12 && kept_rows_count(m1, P1) == kCsK1 &&
+          (int64_t)P1 * 2 * kCsK1 * 4 <= 64 * 1024) ? 1 : 0;
+}
+
+BLINDNO_API int blindno_colspec_nchunk(int C, int m2) { return colspec_nchunk(C, m2); }
+
+// blindno_rowidft_epi (+ crop oN1 x oN2 when part is NULL) with Z built from Y; part != NULL:
+// also the next layer's row DFT of f(z) (f = GELU when act_next) as column-DFT partials
+BLINDNO_API int blindno_rowidft_epi_zc(const float* Y, const float* x, const float* wc,
+                                       const float* bc, float* z, const float* tb,
+                                       const float* tab, float* part, const float* Tp, int Bn,
+                                       int C, int P1, int P2, int m1, int m2, int act, int act_next,
+                                       int oN1, int oN2, void* stream) {
+  if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !tab || (part && !Tp) ||
+      oN1 < 1 || oN1 > P1 || oN2 < 1 || oN2 > P2 || (part && (oN1 != P1 || oN2 != P2)))
+    return (int)hipErrorInvalidValue;
+  const int items = Bn * (((part ? P1 : oN1) + 15) / 16);
+  const int b = (items + kW - 1) / kW;
+  const int nb = b < ROWFUSE_BLOCKS ? b : ROWFUSE_BLOCKS;
+  hipStream_t st = (hipStream_t)stream;
+  const RowDftNext rd{nullptr, part ? Tp : nullptr, ((2 * m2 + 15) / 16) * 16, act_next};
+  const SpecCol sc = spec_col(Y, part, tab, P1);
+  if (act)
+    return rowinv_launch<0, 1, 0, 0, true>(nullptr, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1,
+                                           P2, m2, st, BagLift{}, 1, 0, oN1, oN2, rd, sc);
+  return rowinv_launch<0, 0, 0, 0, true>(nullptr, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1,
+                                         P2, m2, st, BagLift{}, 1, 0, oN1, oN2, rd, sc);
+}
+
+// blindno_rowidft_epi_lift(_rd) with Z built from Y and, with part != NULL, the next row DFT of
+// GELU(z) (act_next) or z as column-DFT partials
+BLINDNO_API int blindno_rowidft_epi_lift_zc(const float* Y, const float* X, const int* idx,
+                                            const float* grid, const float* w0, const float* b0,
+                                            const float* wc, const float* bc, float* z,
+                                            const float* tb, const float* tab, float* part,
+                                            const float* Tp, int B, int T, int L, int N1, int N2,
+                                            int C, int P1, int P2, int m1, int m2, int act_next,
+                                            void* stream) {
+  const int Bn = B * L;
+  if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !tab || (part && !Tp) || !wc || !bc ||
+      N1 > P1 || N2 > P2)
+    return (int)hipErrorInvalidValue;
+  const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  const RowDftNext rd{nullptr, part ? Tp : nullptr, ((2 * m2 + 15) / 16) * 16, act_next};
+  return rowinv_launch<0, 0, 0, 1, true>(nullptr, nullptr, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C,
+                                         P1, P2, m2, (hipStream_t)stream, bl, 1, 0, 0, 0, rd,
+                                         spec_col(Y, part, tab, P1));
+}
+
+// blindno_rowidft_bwd_rd / _crop with Z built from Y; part != NULL: the row DFT of dx as
+// column-DFT partials (the previous layer's adjoint); partial: the 1x1-conv weight-gradient
+// partials (blindno_rowidft_bwd_nchunk, C <= 4) or NULL
+BLINDNO_API int blindno_rowidft_bwd_zc(const float* Y, const float* dz, const float* wc,
+                                       const float* xsrc, float* dx, const float* tb,
+                                       const float* tab, float* part, const float* Tp,
+                                       float* partial, int Bn, int C, int P1, int P2, int m1,
+                                       int m2, int act, int dN1, int dN2, void* stream) {
+  if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !tab || (part && !Tp) || dN1 < 1 ||
+      dN1 > P1 || dN2 < 1 || dN2 > P2 || !wc)
+    return (int)hipErrorInvalidValue;
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  hipStream_t st = (hipStream_t)stream;
+  const BagLift nb0{};
+  const RowDftNext rd{nullptr, part ? Tp : nullptr, ((2 * m2 + 15) / 16) * 16, 0};
+  const SpecCol sc = spec_col(Y, part, tab, P1);
+  if (partial) {
+    if (act)
+      return rowinv_launch<1, 1, 1, 0, true>(nullptr, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C,
+                                             P1, P2, m2, st, nb0, 1, 0, dN1, dN2, rd, sc);
+    return rowinv_launch<1, 0, 1, 0, true>(nullptr, xsrc, dz, wc, nullptr, dx, tb, partial, nb, Bn, C,
+                                           P1, P2, m2, st, nb0, 1, 0, dN1, dN2, rd, sc);
+  }
+  if (act)
+    return rowinv_launch<1, 1, 0, 0, true>(nullptr, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C,
+                                           P1, P2, m2, st, nb0, 1, 0, dN1, dN2, rd, sc);
+  return rowinv_launch<1, 0, 0, 0, true>(nullptr, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1,
+                                         P2, m2, st, nb0, 1, 0, dN1, dN2, rd, sc);
+}
+
+// blindno_rowidft_bwd_lift with Z built from Y
+BLINDNO_API int blindno_rowidft_bwd_lift_zc(const float* Y, const float* dz, const float* X,
+                                            const int* idx, const float* grid, const float* w0,
+                                            const float* b0, const float* wc, const float* tb,
+                                            const float* tab, float* partial, int B, int T, int L,
+                                            int N1, int N2, int C, int P1, int P2, int m1, int m2,
+                                            void* stream) {
+  const int Bn = B * L;
+  if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !tab || !wc || !partial || N1 > P1 ||
+      N2 > P2)
+    return (int)hipErrorInvalidValue;
+  const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
+  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  return rowinv_launch<1, 0, 1, 1, true>(nullptr, nullptr, dz, wc, nullptr, nullptr, tb, partial, nb, Bn,
+                                         C, P1, P2, m2, (hipStream_t)stream, bl, 1, 0, 0, 0,
+                                         RowDftNext{nullptr, nullptr, 0, 0},
+                                         spec_col(Y, nullptr, tab, P1));
 }

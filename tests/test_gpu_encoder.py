@@ -346,11 +346,14 @@ def test_ffn_trunk_nearly_constant_upstream_gradient():
         assert e <= max(1e-4, 3.0 * ec), k
 
 
-@pytest.mark.parametrize("B,L,S,weighted", [(4, 75, 16384, False), (2, 51, 80, True), (3, 1, 6400, False)])
+@pytest.mark.parametrize("B,L,S,weighted", [(4, 75, 16384, False), (2, 51, 80, True), (3, 1, 6400, False),
+                                             (130, 7, 600, True), (2, 1500, 300, False)])
 def test_deeponet_bag_matches_fp64(B, L, S, weighted):
     """ops.DeepONetBagFn (DeepOnetNoBiasOrg + the bag mean that reads it, csrc/deeponet.hip) vs
     the reference composition in fp64: mean_l ((w basis^T + b0) / sqrt(P)), with 1/L or
-    multiplicity weights; ubar and the gradients of w, basis and b0."""
+    multiplicity weights; ubar and the gradients of w, basis and b0.  B = 130 runs the backward
+    as three bag chunks (64 + 64 + 2, dbasis / db0 summed over them); L = 1500 is past the old
+    1024-snapshot bound."""
     from blindno import ops
     torch.manual_seed(B * L + S)
     P = 25

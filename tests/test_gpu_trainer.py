@@ -143,3 +143,10 @@ def test_batch_select_matches_index_select(shape):
     torch.cuda.synchronize()
     assert torch.equal(xb, torch.index_select(X, 0, ids))
     assert torch.equal(yb, torch.index_select(Y, 0, ids))
+    # an id past the source's rows (or negative) fills its batch row with NaN, the others intact
+    bad = torch.tensor([1, shape[0], 2, -1], dtype=torch.int64, device="cuda")
+    BatchSelect([X, Y], [xb, yb])(bad)
+    torch.cuda.synchronize()
+    assert torch.equal(xb[0], X[1]) and torch.equal(xb[2], X[2]) and torch.equal(yb[2], Y[2])
+    assert bool(torch.isnan(xb[1]).all()) and bool(torch.isnan(xb[3]).all())
+    assert bool(torch.isnan(yb[1]).all()) and bool(torch.isnan(yb[3]).all())

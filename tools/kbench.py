@@ -49,7 +49,9 @@ def main():
         res.append((name, us, nbytes / (us * 1e-6) / 1e9))
         print(f"{name:40s} {us:9.1f} us  {nbytes / (us * 1e-6) / 1e9:8.0f} GB/s", flush=True)
 
-    for tag, Bn, C, m, Cout in (("input", 300, 4, 12, 1), ("head", 4, 12, 32, 1), ("head2", 8, 12, 32, 1)):
+    # "u52": the encoder at the step's mean bag size (4 bags x ~52 distinct snapshots)
+    for tag, Bn, C, m, Cout in (("input", 300, 4, 12, 1), ("u52", 208, 4, 12, 1), ("head", 4, 12, 32, 1),
+                                ("head2", 8, 12, 32, 1)):
         P, N = 160, 128
         z = torch.randn(Bn, C, P, P, device=dev)
         w1 = torch.randn(128, C, device=dev) * 0.3
@@ -57,7 +59,7 @@ def main():
         w2 = torch.randn(Cout, 128, device=dev) * 0.1
         b2 = torch.randn(Cout, device=dev)
         out = torch.empty(Bn, N, N, Cout, device=dev)
-        div = 75 if tag == "input" else 1          # the encoder's bag-mean gradient: one field per bag
+        div = {"input": 75, "u52": 52}.get(tag, 1)  # the encoder's bag-mean gradient: one field per bag
         dout = torch.randn(Bn // div, N, N, Cout, device=dev)
         dz = torch.zeros_like(z)
         nch = query("blindno_project_bwd_nchunk", Bn, N, N)
@@ -129,9 +131,39 @@ def main():
                 return ops.k_rowidft_epi_rd(Zl, z, cw, cb, Bn, C, P, P, m, 1, 1)
             # SURVEY 8d's algorithmic bytes of one layer: read x, write y, the weights
             case(f"layer_colpass+epi_rd[{tag}]", layer, 2 * fld + 16 * C * C * m * m)
+            if ops.colspec_ok(Bn, C, P, P, m, m):
+                # the column pass folded into the row kernels (csrc/colspec.h)
+                cs = ops._ColSpec(Bn, C, P, P, m, m, dev)
+                p_in, p_out = cs.part(C, z), cs.part(C, z)
+                zo = torch.empty_like(z)
+                cd = lambda: call("blindno_rowdft_cd", ptr(z), ptr(p_in), ptr(cs.Tp), ptr(cs.tab), Bn, C, P, P, m, 1,
+                                  P, P, stream_ptr())
+                cd()
+                pb = 4 * p_in.numel()
+                case(f"rowdft_cd[{tag}]", cd, fld + pb)
+                case(f"colmix[{tag}]", lambda: cs.mix(p_in, cs.nb, Wt, 0), pb + 2 * 8 * Bn * m * C * 24)
+                _, Yc = cs.mix(p_in, cs.nb, Wt, 0)
+                epi_zc = lambda: call("blindno_rowidft_epi_zc", ptr(Yc), ptr(z), ptr(cw), ptr(cb), ptr(zo), ptr(cs.tb),
+                                      ptr(cs.tab), ptr(p_out), ptr(cs.Tp), Bn, C, P, P, m, m, 1, 1, P, P, stream_ptr())
+                case(f"rowidft_epi_zc[{tag}]", epi_zc, 2 * fld + pb)
+                case(f"rowidft_epi_zy[{tag}]",
+                     lambda: call("blindno_rowidft_epi_zc", ptr(Yc), ptr(z), ptr(cw), ptr(cb), ptr(zo), ptr(cs.tb),
+                                  ptr(cs.tab), None, None, Bn, C, P, P, m, m, 1, 0, P, P, stream_ptr()), 2 * fld)
+
+                def layer_f():
+                    cs.mix(p_in, cs.nb, Wt, 0)
+                    epi_zc()
+                case(f"layer_colmix+epi_zc[{tag}]", layer_f, 2 * fld + 16 * C * C * m * m)
+                nch = query("blindno_rowidft_bwd_nchunk", Bn, C, P, P, m)
+                pw = torch.empty(nch, C * C + C, device=dev)
+                case(f"rowidft_bwd_zc_crop[{tag}]",
+                     lambda: call("blindno_rowidft_bwd_zc", ptr(Yc), ptr(z), ptr(cw), ptr(z), ptr(zo), ptr(cs.tb),
+                                  ptr(cs.tab), ptr(p_out), ptr(cs.Tp), ptr(pw), Bn, C, P, P, m, m, 1, N, N,
+                                  stream_ptr()),
+                     fld * (2 + (N * N) / (P * P)) + pb)
         if C > 4:
             case(f"conv_wgrad[{tag}]", lambda: ops.k_conv_wgrad(z, z, Bn, C, P, P, 1), 2 * fld)
-        inp = torch.randn(Bn, N, N, 3 if tag == "input" else C, device=dev)
+        inp = torch.randn(Bn, N, N, 3 if C == 4 else C, device=dev)
         fc0w = torch.randn(C, inp.shape[-1], device=dev)
         fc0b = torch.randn(C, device=dev)
         x0 = torch.empty(Bn, C, P, P, device=dev)
