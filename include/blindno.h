@@ -275,6 +275,8 @@ int blindno_rowidft_bwd_lift(const float* G, const float* dz, const float* X, co
  * blindno_colspec_ok: 1 when a layer of this shape takes the folded path. */
 int blindno_colspec_ok(int Bn, int C, int P1, int P2, int m1, int m2);
 int blindno_colspec_nchunk(int C, int m2);
+/* rows of the weight-gradient partials of blindno_rowidft_bwd_zc / _bwd_lift_zc */
+int blindno_colspec_bwd_nchunk(int Bn, int P1);
 /* row DFT of f(x) (GELU when act) on the N1v x N2v valid region + column-DFT partials */
 int blindno_rowdft_cd(const float* x, float* part, const float* Tp, const float* tab, int Bn, int C,
                       int P1, int P2, int m2, int act, int N1v, int N2v, blindno_stream_t stream);

@@ -32,6 +32,7 @@ SIGNATURES = {
     "blindno_colpass": "pppppppiiiiiiiis",
     "blindno_colspec_ok": "iiiiii",
     "blindno_colspec_nchunk": "ii",
+    "blindno_colspec_bwd_nchunk": "ii",
     "blindno_rowdft_cd": "ppppiiiiiiiis",
     "blindno_rowdft_bag_lift_cd": "pppppiiiiiiiis",
     "blindno_colmix": "pipppiiiiiiiippps",

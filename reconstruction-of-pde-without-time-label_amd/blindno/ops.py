@@ -180,7 +180,8 @@ _TWS = {}
 
 def twiddle_colspec(P1: int, m1: int, device) -> torch.Tensor:
     """Tab[h][2 j + p] = (cos, sin)(2 pi r_j h / P1) for the kept rows r_j (csrc/colspec.h):
-    the column DFT's F (= cos - i sin) and the column inverse's conj(F); built in double."""
+    the column DFT's F (= cos - i sin) and the column inverse's conj(F); followed by the same
+    values as TabT[h / 4][2 j + p][h % 4] (the column DFT's lane order); built in double."""
     dev = torch.device(device)
     key = (P1, m1, dev.index)
     t = _TWS.get(key)
@@ -188,7 +189,9 @@ def twiddle_colspec(P1: int, m1: int, device) -> torch.Tensor:
         r = torch.tensor(kept_rows(m1, P1), dtype=torch.int64)
         h = torch.arange(P1, dtype=torch.int64)
         ph = ((h[:, None] * r[None, :]) % P1).to(torch.float64) * (2.0 * torch.pi / P1)
-        t = torch.stack([torch.cos(ph), torch.sin(ph)], -1).reshape(P1, -1).to(F32).to(dev).contiguous()
+        tab = torch.stack([torch.cos(ph), torch.sin(ph)], -1).reshape(P1, -1)
+        tabT = tab.view(P1 // 4, 4, -1).permute(0, 2, 1)
+        t = torch.cat([tab.reshape(-1), tabT.reshape(-1)]).to(F32).to(dev).contiguous()
         _TWS[key] = t
     return t
 
@@ -1267,7 +1270,7 @@ class BagEncoderFn(torch.autograd.Function):
                 grads[off], grads[off + 1] = unpack_weights(dWt, (w1, w2), P1, 2)
                 dv = crop if (k == n - 1 and crop) else (P1, P2)
                 if k > 0:
-                    nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, meta.m2)
+                    nchunk = query("blindno_colspec_bwd_nchunk", Bn, P1)
                     pw = _empty(nchunk, C * C + C, like=gh)
                     dx = _empty(Bn, C, P1, P2, like=gh)
                     part = cs.part(C, gh)
@@ -1279,7 +1282,7 @@ class BagEncoderFn(torch.autograd.Function):
                     dz = dx
                     nbv = P1 // 16
                 else:
-                    nchunk = query("blindno_rowidft_bwd_nchunk", Bn, C, P1, P2, meta.m2)
+                    nchunk = query("blindno_colspec_bwd_nchunk", Bn, P1)
                     npl = C * C + C + 4 * C
                     pl = _empty(nchunk, npl, like=gh)
                     call("blindno_rowidft_bwd_lift_zc", ptr(Yb), ptr(dz), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),

@@ -15,8 +15,10 @@
 //   * ZY ("Z from Y"): the next row inverse rebuilds the row coefficients of its 16 rows,
 //     Z[h][k][c] = sum_j Y[k][c][j] conj(F[h][j]), on the matrix cores in its prologue (72
 //     v_mfma_f32_16x16x4f32 per 16-row block), straight into its B-operand registers.
-// Both folded GEMMs use one twiddle table Tab[h][2 j + p] = (p ? sin : cos)(2 pi r_j h / P1),
-// staged in LDS.
+// Both folded GEMMs read the twiddles (cos, sin)(2 pi r_j h / P1) of their 16 rows straight from
+// global memory (L2-resident, 30 KB per layout at P1 = 160), in two layouts: Tab[h][2 j + p] for
+// ZY (a lane streams one row) and TabT[h / 4][2 j + p][h % 4] for CD (a lane takes four rows of
+// one (j, p)).  No LDS staging: it kept two workgroups per CU at most.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -32,8 +34,10 @@ constexpr int kCsKQ = kCsK1 / 4;           // complex Y values per lane and k in
 struct SpecCol {
   const float* Y;     // ZY: Y[n][k][c][j] (complex, j < K1) from colmix; nullptr: read Z
   float* part;        // CD: per-block partials (layout below); nullptr: write At instead
-  const float* tab;   // Tab[h][2 K1] (global; staged in LDS by the kernel)
+  const float* tab;   // Tab[h][2 K1]
+  const float* tabT;  // TabT[h / 4][2 K1][4]
   int nblk;           // CD: 16-row blocks per sample in the partial buffer (P1 / 16)
+  int w3;             // launch choice: the 3-wave register budget (rowinv.hip, MODE 0)
 };
 
 // Partials of one (sample n, 16-row block b): NCH = C NNT MT2 chunks of 64 lanes x float2,
@@ -51,21 +55,20 @@ __device__ __forceinline__ float cs_swap1(float v) {
 }
 
 // CD epilogue of one channel: acc[nt] = At[h0 + 4 g + r][k' = 16 nt + c16] (the row spectrum of
-// the block in the MFMA D layout, k' = 2 k + Re/Im), sTab the LDS twiddle table.  Writes the
+// the block in the MFMA D layout, k' = 2 k + Re/Im), tabT the twiddle table.  Writes the
 // channel's NNT MT2 chunks at dst (= part + ((n nblk + b) NCH + c NNT MT2) 128).
 //   Out[(j, p)][k'] = sum_h F_p[j][h] At[h][k'],  F_0 = cos, F_1 = sin  (A = Tab, B = acc)
 //   Xs_re = Out[(j,0)][re] + Out[(j,1)][im],  Xs_im = Out[(j,0)][im] - Out[(j,1)][re]
 // rows m = 2 j + p of tile mt2 hold (j = 8 mt2 + 2 g + (r >> 1), p = r & 1) in a lane's D, and
 // the Re / Im columns of one mode sit in neighbouring lanes: one DPP swap per pair.
 template <int NNT>
-__device__ __forceinline__ void cd_store(const cs_f32x4 (&acc)[NNT], const float* __restrict__ sTab,
+__device__ __forceinline__ void cd_store(const cs_f32x4 (&acc)[NNT], const float* __restrict__ tabT,
                                          int h0, int lane, float* __restrict__ dst) {
   const int c16 = lane & 15, g = lane >> 4;
-  float ft[kCsMT2][4];
+  cs_f32x4 ft[kCsMT2];
 #pragma unroll
   for (int mt = 0; mt < kCsMT2; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ft[mt][r] = sTab[(h0 + 4 * g + r) * (2 * kCsK1) + 16 * mt + c16];
+    ft[mt] = *reinterpret_cast<const cs_f32x4*>(tabT + (((h0 >> 2) + g) * (2 * kCsK1) + 16 * mt + c16) * 4);
   const float sg = (lane & 1) ? -1.0f : 1.0f;
 #pragma unroll
   for (int nt = 0; nt < NNT; ++nt)
@@ -98,7 +101,7 @@ struct ZyOperands {
 };
 
 template <int S, int C>
-__device__ __forceinline__ void zy_fetch(const float* __restrict__ Y, const float* __restrict__ sTab,
+__device__ __forceinline__ void zy_fetch(const float* __restrict__ Y, const float* __restrict__ tab,
                                          int n, int m2, int h0, int lane, ZyOperands<S, C>& op) {
   static_assert(C == 4 && S % 2 == 0, "zy_fetch: C = 4, even S");
   const int c16 = lane & 15, g = lane >> 4;
@@ -113,7 +116,7 @@ __device__ __forceinline__ void zy_fetch(const float* __restrict__ Y, const floa
       op.yv[i][4 * q] = v.x; op.yv[i][4 * q + 1] = v.y; op.yv[i][4 * q + 2] = v.z; op.yv[i][4 * q + 3] = v.w;
     }
   }
-  const cs_f32x4* tr = reinterpret_cast<const cs_f32x4*>(sTab + (h0 + c16) * (2 * kCsK1) + (kCsK1 / 2) * g);
+  const cs_f32x4* tr = reinterpret_cast<const cs_f32x4*>(tab + (h0 + c16) * (2 * kCsK1) + (kCsK1 / 2) * g);
 #pragma unroll
   for (int q = 0; q < kCsK1 / 8; ++q) {
     const cs_f32x4 v = tr[q];

@@ -38,10 +38,9 @@ __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
   constexpr int Npad = 16 * NNT;
   extern __shared__ float lds[];
   float* sT = lds;                                 // [KB][4][Npad][4]
-  float* sTab = lds + KB * 16 * Npad;              // [P1][2 K1]
   stage_to_lds(sT, Tp, KB * 16 * Npad);
-  stage_to_lds(sTab, tab, P1 * 2 * kCsK1);
   __syncthreads();
+  const float* tabT = tab + P1 * 2 * kCsK1;        // TabT (colspec.h), after Tab
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
   const int r16 = lane & 15, kq = lane >> 4;
@@ -95,7 +94,7 @@ __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
       }
     }
     float* dst = part + (((int64_t)n * nb + b) * nch + c * NNT * kCsMT2) * 128;
-    cd_store<NNT>(acc, sTab, h0, lane, dst);
+    cd_store<NNT>(acc, tabT, h0, lane, dst);
   }
 }
 
@@ -215,8 +214,7 @@ __global__ __launch_bounds__(kMixThreads) void colmix_kernel(
 
 bool cd_geom_ok(int Bn, int C, int P1, int P2, int m2) {
   return Bn > 0 && C > 0 && C <= 16 && P1 % 16 == 0 && P1 <= 512 && P2 > 0 && m2 > 0 &&
-         m2 <= 16 && 2 * m2 <= P2 && (int64_t)Bn * C * P1 * P2 < INT32_MAX &&
-         (int64_t)P1 * 2 * kCsK1 * 4 <= 64 * 1024;
+         m2 <= 16 && 2 * m2 <= P2 && (int64_t)Bn * C * P1 * P2 < INT32_MAX;
 }
 
 template <bool LIFT>
@@ -225,7 +223,7 @@ int rowdft_cd_launch(const float* x, const int* idx, float* part, const float* T
                      int N2v, int T, int L, hipStream_t st) {
   const int KB = (P2 + 15) / 16, NNT = (2 * m2 + 15) / 16, Npad = 16 * NNT;
   const int nbv = (N1v + 15) / 16;
-  const size_t sh = sizeof(float) * ((size_t)KB * 16 * Npad + (size_t)P1 * 2 * kCsK1);
+  const size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
   if (sh > 160 * 1024 || NNT > 2) return (int)hipErrorInvalidValue;
   const int64_t items = (int64_t)Bn * C * nbv;
   const int64_t b = (items + kCdWaves - 1) / kCdWaves;

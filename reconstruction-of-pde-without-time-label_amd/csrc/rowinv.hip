@@ -551,6 +551,7 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 #ifndef ROWFUSE_NH0_NORD
 #define ROWFUSE_NH0_NORD 2
 #endif
+
 // HW: the layer has its 1x1 conv (wc != NULL) -- a compile-time flag: a runtime test around each
 // operand load made hipcc branch around the loads and count their waits conservatively.
 // NSC: steps per row block as a compile-time constant (P2 / (16 NH)), 0 = a runtime loop.
@@ -558,9 +559,15 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 // prologue of each 16-row block instead of read as Z; the next row DFT taken in the opposite
 // orientation (D = f(y) T: rows on the M side) and its column DFT over the block written as
 // partials to sc.part instead of At.
+// ZW: waves per SIMD the registers are budgeted for (0: unconstrained, two at most for the
+// kernels with the next row DFT).  The persistent grid of 4-wave workgroups at 2 waves per SIMD
+// holds 2048 16-row work items at once; beyond that the rest ran as a second round (Bn = 208
+// snapshots = 2080 items: 75 us, where 2000 items took 56).  The MODE 0 ZY / CD kernels take a
+// 3-wave budget (one column tile per step) when their items fit 3072 slots but not 2048
 template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH, bool HW_ = true, int NSC = 0,
-          bool ZY = false, bool CD = false>
-__global__ __launch_bounds__(256) void rowfuse_kernel(
+          bool ZY = false, bool CD = false, int ZW = 0>
+__global__ __launch_bounds__(256, ZW > 0 ? ZW : 1)
+void rowfuse_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, float* __restrict__ partial, int Bn, int P1, int P2,
@@ -574,8 +581,7 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
   extern __shared__ float lds[];
   float* sA = lds;                                  // [NT][64 lanes][S]
   float* sT = lds + NT * 64 * S;                    // RD: [NT][4][Npad][4] (rowdft's image)
-  float* sTab = sT + (RD ? NT * 16 * Npad : 0);     // ZY / CD: [P1][2 K1]
-  if (ZY || CD) stage_to_lds(sTab, sc.tab, P1 * 2 * kCsK1);
+
   for (int e = threadIdx.x; e < NT * 64 * S; e += blockDim.x) {
     const int t = e / (64 * S), rem = e - t * (64 * S);
     const int ln = rem / S, sp = rem - ln * S;
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
     // loads are issued (below), so their latencies overlap
     ZyOperands<ZY ? S : 2, C> zop;
     if constexpr (ZY) {
-      zy_fetch<S, C>(sc.Y, sTab, n, m2, h0, lane, zop);
+      zy_fetch<S, C>(sc.Y, sc.tab, n, m2, h0, lane, zop);
     } else {
       f32x4 zcur[S];
       if (ROWFUSE_ZPRE) {
@@ -872,7 +878,7 @@ __global__ __launch_bounds__(256) void rowfuse_kernel(
       const int nch = colspec_nchunk(C, m2);
       float* dst = sc.part + ((int64_t)(n * sc.nblk + (h0 >> 4)) * nch) * 128;
 #pragma unroll
-      for (int c = 0; c < C; ++c) cd_store<NNT>(racc[c], sTab, h0, lane, dst + c * NNT * kCsMT2 * 128);
+      for (int c = 0; c < C; ++c) cd_store<NNT>(racc[c], sc.tabT, h0, lane, dst + c * NNT * kCsMT2 * 128);
     } else if (RD) {
       // lane: row h, spectrum columns k' = 16 nt + 4 g + r -> modes 8 nt + 2 g + r/2 (Re, Im)
 #pragma unroll
@@ -1009,7 +1015,7 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
                   int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{},
                   int G = 1, int64_t wgs = 0, int dN1 = 0, int dN2 = 0,
                   RowDftNext rd = RowDftNext{nullptr, nullptr, 0, 0},
-                  SpecCol sc = SpecCol{nullptr, nullptr, nullptr, 0}) {
+                  SpecCol sc = SpecCol{nullptr, nullptr, nullptr, nullptr, 0, 0}) {
   if (dN1 <= 0) dN1 = P1;
   if (dN2 <= 0) dN2 = P2;
   if (dN1 > P1 || dN2 > P2) return (int)hipErrorInvalidValue;
@@ -1028,15 +1034,14 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
     // (dz's valid region, the snapshot) in whole float4s
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     const bool rd_ok = (!rd.At && !(ZC && sc.part)) || rd.Npad == 16 * ((2 * m2 + 15) / 16);
-    const bool zc_ok = !ZC || (m2 == 12 && wc && sc.tab && al(sc.Y) && al(sc.tab) &&
+    const bool zc_ok = !ZC || (m2 == 12 && wc && sc.tab && sc.tabT && al(sc.Y) && al(sc.tab) && al(sc.tabT) &&
                               (!sc.part || (rd.Tp && sc.nblk == P1 / 16)) && (sc.Y || sc.part));
     if (ZC && !(rowfuse_shape(Bn, C, P1, P2, m2) && zc_ok)) return (int)hipErrorInvalidValue;
     if (rowfuse_shape(Bn, C, P1, P2, m2) && G == 1 && al(Z) && al(xs) && al(dz) && al(out) &&
         dN2 % 4 == 0 && rd_ok && zc_ok && (!LIFT || (bl.N2 % 4 == 0 && al(bl.X) && al(bl.grid)))) {
       const int NT = P2 / 16, S = m2 / 2;
       const bool rdx = rd.At || (ZC && sc.part);          // the next row DFT taken in the pass
-      size_t shf = sizeof(float) * ((size_t)NT * 64 * S + (rdx ? (size_t)NT * 16 * rd.Npad : 0) +
-                                    (ZC ? (size_t)P1 * 2 * kCsK1 : 0));
+      size_t shf = sizeof(float) * ((size_t)NT * 64 * S + (rdx ? (size_t)NT * 16 * rd.Npad : 0));
       const size_t red = sizeof(float) * (size_t)kW * (C * C + C + 4 * C);
       if (shf < red) shf = red;
       if (shf > 160 * 1024) return (int)hipErrorInvalidValue;
@@ -1049,35 +1054,43 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
       const bool p160 = P2 == 160 && MODE == 0;
       // the output crop (MODE 0, no next row DFT): 128 of the 160 columns, 4 steps
       const bool crop128 = MODE == 0 && !rd.At && dN2 == 128;
-#define RFX(RD_, S_, ZY_, CD_)                                                                 \
+#define RFG(RD_, S_, ZY_, CD_, NH_, ZW_)                                                       \
   do {                                                                                         \
     if (wc && p160 && crop128 && RD_ == 0)                                                     \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true,                             \
-                     MODE == 0 ? 128 / (16 * NHX(RD_)) : 0, ZY_, CD_>                          \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, true, MODE == 0 ? 128 / (16 * NH_) : 0, \
+                     ZY_, CD_, ZW_>                                                            \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
     else if (wc && p160 && (dN2 == P2 || RD_ != 0))                                            \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true,                             \
-                     MODE == 0 ? 160 / (16 * NHX(RD_)) : 0, ZY_, CD_>                          \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, true, MODE == 0 ? 160 / (16 * NH_) : 0, \
+                     ZY_, CD_, ZW_>                                                            \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
     else if (wc)                                                                               \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), true, 0, ZY_, CD_>                \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, true, 0, ZY_, CD_, ZW_>                \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
     else if (!ZY_)                                                                             \
-      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NHX(RD_), false>                            \
+      rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, false>                                 \
           <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
   } while (0)
+#define RFX(RD_, S_, ZY_, CD_) RFG(RD_, S_, ZY_, CD_, NHX(RD_), 0)
 #define RF(RD_, S_) RFX(RD_, S_, false, false)
 #define RF_S(RD_) \
   do { if (S == 2) RF(RD_, 2); else if (S == 4) RF(RD_, 4); else if (S == 6) RF(RD_, 6); else RF(RD_, 8); } while (0)
       if constexpr (ZC) {
-        // ZY always; CD with the next row DFT (act: of GELU(field)); m2 = 12 (zc_ok)
-        if (!sc.part) RFX(0, 6, true, false);
-        else if (rd.act) RFX(2, 6, true, true);
-        else RFX(1, 6, true, true);
+        // ZY always; CD with the next row DFT (act: of GELU(field)); m2 = 12 (zc_ok); the 3-wave
+        // budget (sc.w3: one column tile per step in the forward) chosen by the caller
+        if (MODE == 0 && sc.w3) {
+          if (!sc.part) RFG(0, 6, true, false, ROWFUSE_NH0_NORD, 3);
+          else if (rd.act) RFG(2, 6, true, true, 1, 3);
+          else RFG(1, 6, true, true, 1, 3);
+        } else {
+          if (!sc.part) RFX(0, 6, true, false);
+          else if (rd.act) RFX(2, 6, true, true);
+          else RFX(1, 6, true, true);
+        }
       } else {
         if (!rd.At) RF_S(0);
         else if (rd.act) RF_S(2);
@@ -1086,6 +1099,7 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
 #undef RF_S
 #undef RF
 #undef RFX
+#undef RFG
 #undef NHX
       return (int)hipGetLastError();
     }
@@ -1359,17 +1373,40 @@ BLINDNO_API int blindno_rowidft_bwd_lift(const float* G, const float* dz, const 
 // the next row spectrum (blindno_colspec_nchunk) instead of At; tab = Tab[P1][2 K1]
 // (blindno.ops.twiddle_colspec).  Shapes: blindno_colspec_ok.
 namespace {
-SpecCol spec_col(const float* Y, float* part, const float* tab, int P1) {
-  return SpecCol{Y, part, tab, P1 / 16};
+SpecCol spec_col(const float* Y, float* part, const float* tab, int P1, int w3 = 0) {
+  // tab: Tab (P1 x 2 K1) followed by TabT (the same values, P1 / 4 x 2 K1 x 4)
+  return SpecCol{Y, part, tab, tab ? tab + (size_t)P1 * 2 * kCsK1 : nullptr, P1 / 16, w3};
 }
 }  // namespace
 
+// persistent grid of the MODE 0 ZY / CD kernels: 4-wave workgroups filling ROWFUSE_ZC_WAVES0
+// waves per SIMD (256 CUs x 4 SIMDs)
+int zc_blocks(int items, int waves) {
+  const int cap = waves > 2 ? 256 * waves : ROWFUSE_BLOCKS;
+  const int b = (items + kW - 1) / kW;
+  return b < cap ? b : cap;
+}
+// the MODE 0 kernels: the 3-wave budget for item counts in (ROWFUSE_ZC3_MIN, ROWFUSE_ZC3_MAX]
+// (measured: 2000 items 55.6 -> 51.9 us, 2080 items 74.7 -> 69.8 us, 3000 items 89.9 -> 102.8 us)
+#ifndef ROWFUSE_ZC3_MIN
+#define ROWFUSE_ZC3_MIN 0
+#endif
+#ifndef ROWFUSE_ZC3_MAX
+#define ROWFUSE_ZC3_MAX 2600
+#endif
+bool zc_w3(int items) { return items > ROWFUSE_ZC3_MIN && items <= ROWFUSE_ZC3_MAX; }
+int zc_blocks0(int items) { return zc_blocks(items, zc_w3(items) ? 3 : 2); }
+int zc_blocks1(int items) { return zc_blocks(items, 2); }
+
 BLINDNO_API int blindno_colspec_ok(int Bn, int C, int P1, int P2, int m1, int m2) {
   return (rowfuse_shape(Bn, C, P1, P2, m2) && m2 == 12 && m1 == 12 && kept_rows_count(m1, P1) == kCsK1 &&
-          (int64_t)P1 * 2 * kCsK1 * 4 <= 64 * 1024) ? 1 : 0;
+          P1 % 16 == 0) ? 1 : 0;
 }
 
 BLINDNO_API int blindno_colspec_nchunk(int C, int m2) { return colspec_nchunk(C, m2); }
+
+// weight-gradient partial rows of blindno_rowidft_bwd_zc / _bwd_lift_zc (one per workgroup)
+BLINDNO_API int blindno_colspec_bwd_nchunk(int Bn, int P1) { return zc_blocks1(Bn * (P1 / 16)); }
 
 // blindno_rowidft_epi (+ crop oN1 x oN2 when part is NULL) with Z built from Y; part != NULL:
 // also the next layer's row DFT of f(z) (f = GELU when act_next) as column-DFT partials
@@ -1382,11 +1419,10 @@ BLINDNO_API int blindno_rowidft_epi_zc(const float* Y, const float* x, const flo
       oN1 < 1 || oN1 > P1 || oN2 < 1 || oN2 > P2 || (part && (oN1 != P1 || oN2 != P2)))
     return (int)hipErrorInvalidValue;
   const int items = Bn * (((part ? P1 : oN1) + 15) / 16);
-  const int b = (items + kW - 1) / kW;
-  const int nb = b < ROWFUSE_BLOCKS ? b : ROWFUSE_BLOCKS;
+  const int nb = zc_blocks0(items);
   hipStream_t st = (hipStream_t)stream;
   const RowDftNext rd{nullptr, part ? Tp : nullptr, ((2 * m2 + 15) / 16) * 16, act_next};
-  const SpecCol sc = spec_col(Y, part, tab, P1);
+  const SpecCol sc = spec_col(Y, part, tab, P1, zc_w3(items));
   if (act)
     return rowinv_launch<0, 1, 0, 0, true>(nullptr, x, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C, P1,
                                            P2, m2, st, BagLift{}, 1, 0, oN1, oN2, rd, sc);
@@ -1408,11 +1444,12 @@ BLINDNO_API int blindno_rowidft_epi_lift_zc(const float* Y, const float* X, cons
       N1 > P1 || N2 > P2)
     return (int)hipErrorInvalidValue;
   const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
-  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  const int items = Bn * (P1 / 16);
+  const int nb = zc_blocks0(items);
   const RowDftNext rd{nullptr, part ? Tp : nullptr, ((2 * m2 + 15) / 16) * 16, act_next};
   return rowinv_launch<0, 0, 0, 1, true>(nullptr, nullptr, nullptr, wc, bc, z, tb, nullptr, nb, Bn, C,
                                          P1, P2, m2, (hipStream_t)stream, bl, 1, 0, 0, 0, rd,
-                                         spec_col(Y, part, tab, P1));
+                                         spec_col(Y, part, tab, P1, zc_w3(items)));
 }
 
 // blindno_rowidft_bwd_rd / _crop with Z built from Y; part != NULL: the row DFT of dx as
@@ -1426,7 +1463,7 @@ BLINDNO_API int blindno_rowidft_bwd_zc(const float* Y, const float* dz, const fl
   if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !tab || (part && !Tp) || dN1 < 1 ||
       dN1 > P1 || dN2 < 1 || dN2 > P2 || !wc)
     return (int)hipErrorInvalidValue;
-  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  const int nb = zc_blocks1(Bn * (P1 / 16));
   hipStream_t st = (hipStream_t)stream;
   const BagLift nb0{};
   const RowDftNext rd{nullptr, part ? Tp : nullptr, ((2 * m2 + 15) / 16) * 16, 0};
@@ -1457,7 +1494,7 @@ BLINDNO_API int blindno_rowidft_bwd_lift_zc(const float* Y, const float* dz, con
       N2 > P2)
     return (int)hipErrorInvalidValue;
   const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
-  const int nb = rowinv_geom(Bn, C, P1, P2, m2).blocks;
+  const int nb = zc_blocks1(Bn * (P1 / 16));
   return rowinv_launch<1, 0, 1, 1, true>(nullptr, nullptr, dz, wc, nullptr, nullptr, tb, partial, nb, Bn,
                                          C, P1, P2, m2, (hipStream_t)stream, bl, 1, 0, 0, 0,
                                          RowDftNext{nullptr, nullptr, 0, 0},

@@ -11,6 +11,8 @@
 #   kbench:REGEX      tools/kbench.py REGEX (per-kernel timing at Bn = 300)
 #   ab:VARS[:REGEX]   A/B of library variants (variants/<v>/libblindno.so, comma separated)
 #                     against the in-tree library: 3 alternations of the config-C bench
+#   abenv:VAR=a,b     the config-C bench under VAR=a, VAR=b, ... (3 alternations), e.g.
+#                     abenv:BLINDNO_COLSPEC=1,0
 #   pmc:KERNEL        PMC counters over the benched step for KERNEL (tools/pmc_bench.sh)
 #   pmck:REGEX        PMC HBM traffic of kbench kernels (tools/pmc_kbench.sh -> pmc_traffic)
 # Index of the round-by-round evidence these produce: DESIGN.md section 8.
@@ -67,6 +69,15 @@ for step in "$@"; do
             || exit 1
         done
       done 2>&1 | tee gpurun_out/ab_$TAG.txt ;;
+    abenv)
+      var=${arg%%=*}; vals=${arg#*=}
+      for rep in 1 2 3; do
+        for val in ${vals//,/ }; do
+          env $var=$val timeout -k 10 300 python -u bench.py --no-cpu --no-parity 2>/dev/null | python3 -c \
+            "import json,sys;d=json.loads(sys.stdin.read().strip().splitlines()[-1]);r=d.get('roofline_spectral',{});print('$var=$val bench', d['value'], d['ms_per_step'], 'spectral', r.get('frac'), r.get('ms_per_layer'))" \
+            || exit 1
+        done
+      done 2>&1 | tee gpurun_out/abenv_$TAG.txt ;;
     pmc)
       bash tools/pmc_bench.sh $TAG "$arg" C || exit 1
       python3 tools/pmc_bench.py gpurun_out/pmcb_$TAG "$arg" 8 > gpurun_out/pmc_bench_$TAG.json

@@ -50,8 +50,11 @@ def main():
         print(f"{name:40s} {us:9.1f} us  {nbytes / (us * 1e-6) / 1e9:8.0f} GB/s", flush=True)
 
     # "u52": the encoder at the step's mean bag size (4 bags x ~52 distinct snapshots)
-    for tag, Bn, C, m, Cout in (("input", 300, 4, 12, 1), ("u52", 208, 4, 12, 1), ("head", 4, 12, 32, 1),
-                                ("head2", 8, 12, 32, 1)):
+    # "u50": 200 snapshots, 2000 16-row items (< the 2048 resident waves of the row kernels)
+    # KBENCH_BN=160,240: further encoder-shaped sizes ("bn160", ...)
+    extra = [(f"bn{b}", int(b), 4, 12, 1) for b in os.environ.get("KBENCH_BN", "").split(",") if b]
+    for tag, Bn, C, m, Cout in [("input", 300, 4, 12, 1), ("u52", 208, 4, 12, 1), ("u50", 200, 4, 12, 1),
+                                *extra, ("head", 4, 12, 32, 1), ("head2", 8, 12, 32, 1)]:
         P, N = 160, 128
         z = torch.randn(Bn, C, P, P, device=dev)
         w1 = torch.randn(128, C, device=dev) * 0.3
@@ -59,7 +62,7 @@ def main():
         w2 = torch.randn(Cout, 128, device=dev) * 0.1
         b2 = torch.randn(Cout, device=dev)
         out = torch.empty(Bn, N, N, Cout, device=dev)
-        div = {"input": 75, "u52": 52}.get(tag, 1)  # the encoder's bag-mean gradient: one field per bag
+        div = {"input": 75, "u52": 52, "u50": 50}.get(tag, 1 if C > 4 else Bn // 4)  # the encoder's bag-mean gradient: one field per bag
         dout = torch.randn(Bn // div, N, N, Cout, device=dev)
         dz = torch.zeros_like(z)
         nch = query("blindno_project_bwd_nchunk", Bn, N, N)
@@ -154,7 +157,7 @@ def main():
                     cs.mix(p_in, cs.nb, Wt, 0)
                     epi_zc()
                 case(f"layer_colmix+epi_zc[{tag}]", layer_f, 2 * fld + 16 * C * C * m * m)
-                nch = query("blindno_rowidft_bwd_nchunk", Bn, C, P, P, m)
+                nch = query("blindno_colspec_bwd_nchunk", Bn, P)
                 pw = torch.empty(nch, C * C + C, device=dev)
                 case(f"rowidft_bwd_zc_crop[{tag}]",
                      lambda: call("blindno_rowidft_bwd_zc", ptr(Yc), ptr(z), ptr(cw), ptr(z), ptr(zo), ptr(cs.tb),
