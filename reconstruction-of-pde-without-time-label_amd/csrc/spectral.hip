@@ -288,6 +288,9 @@ constexpr int kFullHB = 10;
 #ifndef COLMIX_C12
 #define COLMIX_C12 1
 #endif
+#ifndef COLFUSE_C12
+#define COLFUSE_C12 1
+#endif
 // H16 (config E, blindno.ops.set_mix_precision("fp16")): the channel mix takes fp16 operands
 // with fp32 accumulation -- each complex multiply-add is two v_dot2c_f32_f16 (packed fp16
 // pairs, exact products, fp32 sum).  The column spectra are block-scaled first: the workgroup's
@@ -590,6 +593,58 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
   }
 
   // ---- 2. the mix: Y[p o][j] into sP (rows >= orows and columns >= K1 zero)
+  // the 12-channel heads (one pair per workgroup, 16 K1p = 1024 outputs, 2 per thread at 8
+  // waves): every weight load of the thread's outputs issued before the first multiply (with
+  // the generic 4-unrolled loop each output waited on three L2 round trips in turn); same
+  // summation order
+  if (COLFUSE_C12 && !H16 && Cin == 12 && Cout == 12 && 16 * K1p <= 2 * kT && np == 1) {
+    constexpr int kC = 12;
+    float2 wv[2][kC];
+    int jv[2], ov[2];
+    bool live[2];
+    const int k = q0 % m2;
+    const float2* wg = wtgs ? reinterpret_cast<const float2*>(
+                                  reinterpret_cast<const float*>(Wt) + (q0 / m2 / Bg) * wtgs)
+                            : Wt;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + i * kT;
+      ov[i] = e % kC;
+      const int t = e / kC;
+      jv[i] = t % K1p;
+      live[i] = e < 16 * K1p && t < K1p && jv[i] < K1;      // p == 0 (one pair)
+      const float2* wj = wg + ((int64_t)k * K1 + (live[i] ? jv[i] : 0)) * kC * kC;
+#pragma unroll
+      for (int c = 0; c < kC; ++c) wv[i][c] = DIR == 0 ? wj[c * kC + ov[i]] : wj[ov[i] * kC + c];
+    }
+    const float sc = DIR == 0 ? c2r_weight(k, P2) * inv : 1.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + i * kT;
+      if (e >= 16 * K1p) continue;
+      const int t = e / kC;
+      if (t >= K1p) continue;                        // rows >= 12 are zeroed below
+      float re = 0.f, im = 0.f;
+      if (live[i]) {
+        const float2* xp = &sX[0][jv[i]];
+#pragma unroll
+        for (int c = 0; c < kC; ++c) {
+          const float2 a = xp[c * kLd];
+          const float2 w = wv[i][c];
+          if (DIR == 0) {
+            re = fmaf(a.x, w.x, fmaf(-a.y, w.y, re));
+            im = fmaf(a.x, w.y, fmaf(a.y, w.x, im));
+          } else {
+            re = fmaf(w.x, a.x, fmaf(w.y, a.y, re));
+            im = fmaf(w.x, a.y, fmaf(-w.y, a.x, im));
+          }
+        }
+        re *= sc;
+        im *= sc;
+      }
+      sP[ov[i]][jv[i]] = make_float2(re, im);
+    }
+  } else
   for (int e = threadIdx.x; e < 16 * K1p; e += kT) {
     const int o = e % Cout;                       // output channel fastest: contiguous weights
     const int t = e / Cout;

@@ -35,11 +35,16 @@ KERNELS = {
     "blindno_project_bwd": r"project_bwd_mfma_kernel<4,",
     "blindno_project_fwd": r"project_fwd_mfma_kernel<4,",
     "blindno_rowdft": r"rowdft_mfma_kernel<",
-    "blindno_rowidft_epi": r"rowfuse_kernel<0, 1, 0, 0, 0,",
+    "blindno_rowidft_epi": r"rowfuse_kernel<0, 1, 0, 0, 0, .*false, false",
     "colfuse (blindno_colpass, FNO_input)": r"colfuse_kernel<0,",
-    "blindno_rowidft_epi_rd": r"rowfuse_kernel<0, 1, 0, 0, 2,",
-    "blindno_rowidft_bwd": r"rowfuse_kernel<1, 1, 1, 0, 0,",
-    "blindno_rowidft_bwd_rd_crop": r"rowfuse_kernel<1, 1, 1, 0, 1,",
+    "blindno_rowidft_epi_rd": r"rowfuse_kernel<0, 1, 0, 0, 2, .*false, false",
+    "blindno_rowidft_bwd": r"rowfuse_kernel<1, 1, 1, 0, 0, .*false, false",
+    "blindno_rowidft_bwd_rd_crop": r"rowfuse_kernel<1, 1, 1, 0, 1, .*false, false",
+    # the column pass folded into the row kernels (csrc/colspec.h)
+    "blindno_colmix": r"colmix_kernel<0, false>",
+    "blindno_rowidft_epi_zc": r"rowfuse_kernel<0, 1, 0, 0, 2, .*true, true",
+    "blindno_rowdft_cd": r"rowdft_cd_kernel<2, true, false>",
+    "blindno_rowidft_bwd_zc_crop": r"rowfuse_kernel<1, 1, 1, 0, 1, .*true, true",
     "coldft_mix (blindno_colpass)": r"coldft_mix_kernel<0,",
     "colidft (blindno_colpass)": r"colidft_kernel",
 }
