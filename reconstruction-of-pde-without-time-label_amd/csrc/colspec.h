@@ -40,30 +40,44 @@ struct SpecCol {
   int w3;             // launch choice: the 3-wave register budget (rowinv.hip, MODE 0)
 };
 
-// Partials of one (sample n, 16-row block b): NCH = C NNT MT2 chunks of 64 lanes x float2,
-//   part[((n nblk + b) NCH + ch) 128 + 2 lane + e],  ch = (c NNT + nt) MT2 + mt2,
-// lane = 16 g + c16 holding Xs_part[k][c][j] component q, with
-//   k = 8 nt + (c16 >> 1), q = c16 & 1 (0: Re, 1: Im), j = 8 mt2 + 2 g + e.
-// (NNT = ceil(2 m2 / 16) column tiles of the row spectrum; columns k >= m2 hold zeros.)
-__host__ __device__ __forceinline__ int colspec_nchunk(int C, int m2) {
-  return C * ((2 * m2 + 15) / 16) * kCsMT2;
+// Partials of one (sample n, 16-row block b): NCH chunks of 64 lanes x float2,
+//   part[((n nblk + b) NCH + ch) 128 + 2 lane + e],
+// lane = 16 g + c16 holding Xs_part[k][c][j] component q = c16 & 1 (0: Re, 1: Im),
+// j = 8 mt2 + 2 g + e.  The row spectrum's NNT = ceil(2 m2 / 16) column tiles: NF full ones,
+//   ch = (c NF + nt) MT2 + mt2,              k = 8 nt + (c16 >> 1),
+// and, when 2 m2 % 16 == 8 (m2 = 12: columns 16..23 of the second tile), a half tile whose 8
+// live columns of channels 2p and 2p + 1 share one chunk (a quarter less partial traffic):
+//   ch = (C NF + p) MT2 + mt2,  c = 2 p + (c16 >> 3),  k = 8 (NNT - 1) + ((c16 & 7) >> 1).
+struct ColspecGeom {
+  int NNT, NF, half, nch;
+};
+__host__ __device__ __forceinline__ ColspecGeom colspec_geom(int C, int m2) {
+  ColspecGeom g;
+  g.NNT = (2 * m2 + 15) / 16;
+  g.half = (2 * m2) % 16 == 8 ? 1 : 0;
+  g.NF = g.NNT - g.half;
+  g.nch = (C * g.NF + (g.half ? (C + 1) / 2 : 0)) * kCsMT2;
+  return g;
 }
+__host__ __device__ __forceinline__ int colspec_nchunk(int C, int m2) { return colspec_geom(C, m2).nch; }
 
 // swap with the neighbouring lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2]
 __device__ __forceinline__ float cs_swap1(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
 }
 
-// CD epilogue of one channel: acc[nt] = At[h0 + 4 g + r][k' = 16 nt + c16] (the row spectrum of
+// CD epilogue of channel c: acc[nt] = At[h0 + 4 g + r][k' = 16 nt + c16] (the row spectrum of
 // the block in the MFMA D layout, k' = 2 k + Re/Im), tabT the twiddle table.  Writes the
-// channel's NNT MT2 chunks at dst (= part + ((n nblk + b) NCH + c NNT MT2) 128).
+// channel's chunks of the block at blk = part + (n nblk + b) NCH 128 (layout above; in the half
+// tile only lanes c16 < 8 store, at lane + 8 for odd channels).
 //   Out[(j, p)][k'] = sum_h F_p[j][h] At[h][k'],  F_0 = cos, F_1 = sin  (A = Tab, B = acc)
 //   Xs_re = Out[(j,0)][re] + Out[(j,1)][im],  Xs_im = Out[(j,0)][im] - Out[(j,1)][re]
 // rows m = 2 j + p of tile mt2 hold (j = 8 mt2 + 2 g + (r >> 1), p = r & 1) in a lane's D, and
 // the Re / Im columns of one mode sit in neighbouring lanes: one DPP swap per pair.
 template <int NNT>
 __device__ __forceinline__ void cd_store(const cs_f32x4 (&acc)[NNT], const float* __restrict__ tabT,
-                                         int h0, int lane, float* __restrict__ dst) {
+                                         int h0, int lane, float* __restrict__ blk, int c, int C,
+                                         int m2) {
   const int c16 = lane & 15, g = lane >> 4;
   cs_f32x4 ft[kCsMT2];
 #pragma unroll
@@ -81,7 +95,13 @@ __device__ __forceinline__ void cd_store(const cs_f32x4 (&acc)[NNT], const float
       float2 v;
       v.x = fmaf(sg, p1, o[0]);
       v.y = fmaf(sg, p3, o[2]);
-      *reinterpret_cast<float2*>(dst + (nt * kCsMT2 + mt) * 128 + 2 * lane) = v;
+      const ColspecGeom cg = colspec_geom(C, m2);
+      if (nt < cg.NF) {
+        *reinterpret_cast<float2*>(blk + ((c * cg.NF + nt) * kCsMT2 + mt) * 128 + 2 * lane) = v;
+      } else if (c16 < 8) {
+        const int ln = (c & 1) ? lane + 8 : lane;
+        *reinterpret_cast<float2*>(blk + ((C * cg.NF + (c >> 1)) * kCsMT2 + mt) * 128 + 2 * ln) = v;
+      }
     }
 }
 

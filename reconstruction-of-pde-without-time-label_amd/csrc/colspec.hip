@@ -93,8 +93,8 @@ __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
         for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bt[s], acc[t], 0, 0, 0);
       }
     }
-    float* dst = part + (((int64_t)n * nb + b) * nch + c * NNT * kCsMT2) * 128;
-    cd_store<NNT>(acc, tabT, h0, lane, dst);
+    float* blk = part + ((int64_t)n * nb + b) * nch * 128;
+    cd_store<NNT>(acc, tabT, h0, lane, blk, c, C, m2);
   }
 }
 
@@ -123,11 +123,11 @@ __global__ __launch_bounds__(kMixThreads) void colmix_kernel(
   float2* sW = sX + (LIFT ? m2 * C * kMixJ : 0);   // [m2][kMixJ][C][C]: the weight slice
   const int n = blockIdx.x / kCsMT2, mt = blockIdx.x - n * kCsMT2;
   const int j0 = kMixJ * mt;
-  const int NNT = (2 * m2 + 15) / 16;
-  const int nch = colspec_nchunk(Cp, m2);
+  const ColspecGeom cg = colspec_geom(Cp, m2);
+  const int nch = cg.nch;
   const int nb = P1 >> 4;
   // one float4 (lanes 2 lp, 2 lp + 1 of chunk (cn, mt)) per thread and block
-  const int npos = Cp * NNT * 32;
+  const int npos = (nch / kCsMT2) * 32;
   if (Wt) {
     const int nw = m2 * kMixJ * C * C;
     for (int e = threadIdx.x; e < nw; e += kMixThreads) {
@@ -147,10 +147,17 @@ __global__ __launch_bounds__(kMixThreads) void colmix_kernel(
 #pragma unroll
     for (int b = 1; b < kMixMaxB; ++b)
       if (b < nbv) acc += v[b];
-    const int nt = cn % NNT, c = cn / NNT;
     const int ln = 2 * lp, c16 = ln & 15, g = ln >> 4;
-    const int k = 8 * nt + (c16 >> 1), jl = 2 * g;
-    if (k < m2) {
+    int c, k;
+    if (cn < Cp * cg.NF) {
+      c = cn / cg.NF;
+      k = 8 * (cn % cg.NF) + (c16 >> 1);
+    } else {                                       // the half tile of channels 2p, 2p + 1
+      c = 2 * (cn - Cp * cg.NF) + (c16 >> 3);
+      k = 8 * cg.NF + ((c16 & 7) >> 1);
+    }
+    const int jl = 2 * g;
+    if (k < m2 && c < Cp) {
       float2* d = sP + ((int64_t)k * Cp + c) * kMixJ + jl;
       d[0] = make_float2(acc.x, acc.z);
       d[1] = make_float2(acc.y, acc.w);

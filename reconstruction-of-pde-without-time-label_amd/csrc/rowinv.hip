@@ -876,9 +876,9 @@ void rowfuse_kernel(
     }
     if constexpr (CD) {
       const int nch = colspec_nchunk(C, m2);
-      float* dst = sc.part + ((int64_t)(n * sc.nblk + (h0 >> 4)) * nch) * 128;
+      float* blk = sc.part + ((int64_t)(n * sc.nblk + (h0 >> 4)) * nch) * 128;
 #pragma unroll
-      for (int c = 0; c < C; ++c) cd_store<NNT>(racc[c], sc.tabT, h0, lane, dst + c * NNT * kCsMT2 * 128);
+      for (int c = 0; c < C; ++c) cd_store<NNT>(racc[c], sc.tabT, h0, lane, blk, c, C, m2);
     } else if (RD) {
       // lane: row h, spectrum columns k' = 16 nt + 4 g + r -> modes 8 nt + 2 g + r/2 (Re, Im)
 #pragma unroll
