@@ -708,9 +708,11 @@ class FNOFn(torch.autograd.Function):
 
 # ---------------------------------------------------------------------------- grouped heads
 # Two FNO2d heads on the same input run as ONE chain of launches over 2 B samples: every
-# kernel selects the weights of the sample's head (blindno_*_g entry points).  The heads'
-# small weights (fc0, 1x1 convs, fc1/fc2) are packed into one buffer per step (one copy
-# kernel), the spectral weights into one packed Wt per layer.
+# kernel selects the weights of the sample's head (blindno_*_g entry points): head g's copy of a
+# small weight (fc0, 1x1 convs, fc1/fc2) at base + g S.  When the heads' parameters sit at one
+# fixed distance in memory (FlatAdam's flat buffer: both heads' parameter lists have the same
+# layout) the kernels read them in place; otherwise they are packed into one buffer per step
+# (one copy kernel).  The spectral weights go into one packed Wt per layer.
 
 
 def _small_params(prm, n, nw):
@@ -750,6 +752,34 @@ def _sub(buf, off):
     return buf[off:] if off else buf
 
 
+HEAD_WEIGHTS_IN_PLACE = os.environ.get("BLINDNO_HEAD_INPLACE", "1") != "0"
+
+
+class _GroupWeights:
+    """The grouped heads' small weights: ``p(i)`` = the device pointer of head 0's tensor i,
+    head g's at + g * S floats."""
+
+    def __init__(self, smalls):
+        d = None
+        direct = all(t.is_contiguous() and t.dtype == F32 for sm in smalls for t in sm)
+        for g in range(1, len(smalls)):
+            for a, b in zip(smalls[0], smalls[g]):
+                diff = b.data_ptr() - a.data_ptr()
+                if diff % (4 * g) or (d is not None and diff != g * d):
+                    direct = False
+                    break
+                d = diff // g
+        if direct and d and HEAD_WEIGHTS_IN_PLACE:
+            self.base, self.buf, self.S = list(smalls[0]), None, d // 4
+        else:
+            self.offs, self.S = _offsets(smalls[0])
+            self.buf = torch.cat([t.reshape(-1) for sm in smalls for t in sm])
+            self.base = None
+
+    def p(self, i):
+        return ptr(self.base[i]) if self.base is not None else ptr(_sub(self.buf, self.offs[i]))
+
+
 def fno_forward_grouped(meta: FNOMeta, inp, prms):
     """Both heads' FNO2d forward in one chain; returns (out (Bg, Ho, Wo, G*Cout), saved)."""
     G = len(prms)
@@ -757,10 +787,10 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
     Bn = G * Bg
     C, n = meta.width, meta.n_layers
     smalls = [_small_params(p, n, 2) for p in prms]
-    offs, S = _offsets(smalls[0])
-    small = torch.cat([t.reshape(-1) for sm in smalls for t in sm])
+    small = _GroupWeights(smalls)
+    S = small.S
     x0 = _empty(Bn, C, P1, P2, like=inp)
-    call("blindno_lift_fwd_g", ptr(inp), ptr(_sub(small, offs[0])), ptr(_sub(small, offs[1])), ptr(x0),
+    call("blindno_lift_fwd_g", ptr(inp), small.p(0), small.p(1), ptr(x0),
          G, S, Bn, N1, N2, Cin, C, P1, P2, stream_ptr())
     K1 = kept_rows_count(meta.m1, P1)
     K1p = 16 * ((K1 + 15) // 16)
@@ -780,8 +810,8 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
         call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(X), ptr(Y), ptr(Z), ptr(FB), ptr(GB), G,
              Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, _mixdir(0), stream_ptr())
         z = _empty(Bn, C, P1, P2, like=inp)
-        call("blindno_rowidft_epi_g", ptr(Z), ptr(src), ptr(_sub(small, offs[2 + 2 * k])),
-             ptr(_sub(small, offs[3 + 2 * k])), ptr(z), ptr(twiddle_rowinv(P2, meta.m2, inp.device)),
+        call("blindno_rowidft_epi_g", ptr(Z), ptr(src), small.p(2 + 2 * k),
+             small.p(3 + 2 * k), ptr(z), ptr(twiddle_rowinv(P2, meta.m2, inp.device)),
              G, S, Bn, C, P1, P2, meta.m2, act, stream_ptr())
         Xs.append(X)
         Wts.append(Wt)
@@ -790,8 +820,8 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
     o1 = 2 + 2 * n
     Hd, Cout = smalls[0][o1].shape[0], smalls[0][o1 + 2].shape[0]
     out = _empty(Bg, Ho, Wo, G * Cout, like=inp)
-    call("blindno_project_fwd_g", ptr(zs[-1]), ptr(_sub(small, offs[o1])), ptr(_sub(small, offs[o1 + 1])),
-         ptr(_sub(small, offs[o1 + 2])), ptr(_sub(small, offs[o1 + 3])), ptr(out), G, S, Bn, C, P1, P2,
+    call("blindno_project_fwd_g", ptr(zs[-1]), small.p(o1), small.p(o1 + 1),
+         small.p(o1 + 2), small.p(o1 + 3), ptr(out), G, S, Bn, C, P1, P2,
          Ho, Wo, Hd, Cout, G * Cout, 0, stream_ptr())
     return out, (small, x0, Xs, Wts, zs)
 
@@ -822,7 +852,7 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
     C, n = meta.width, meta.n_layers
     small, x0, Xs, Wts, zs = saved
     smalls = [_small_params(p, n, 2) for p in prms]
-    offs, S = _offsets(smalls[0])
+    S = small.S
     o1 = 2 + 2 * n
     Hd, Cout = smalls[0][o1].shape[0], smalls[0][o1 + 2].shape[0]
     gout = _c(gout)
@@ -833,8 +863,8 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
     np_p = Hd * C + Hd + Cout * Hd + Cout
     nchunk = query("blindno_project_bwd_nchunk", Bg, Ho, Wo)
     partial = _empty(nchunk, G, np_p, like=inp)
-    call("blindno_project_bwd_g", ptr(zs[-1]), ptr(_sub(small, offs[o1])), ptr(_sub(small, offs[o1 + 1])),
-         ptr(_sub(small, offs[o1 + 2])), ptr(gout), ptr(dz), ptr(partial), nchunk, G, S, Bn, C, P1, P2,
+    call("blindno_project_bwd_g", ptr(zs[-1]), small.p(o1), small.p(o1 + 1),
+         small.p(o1 + 2), ptr(gout), ptr(dz), ptr(partial), nchunk, G, S, Bn, C, P1, P2,
          Ho, Wo, Hd, Cout, G * Cout, 0, stream_ptr())
     gp = reduce_partials(partial, nchunk, G * np_p).view(G, np_p)
     for g in range(G):
@@ -879,14 +909,14 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
             grads[g][off + 2] = gc[g, :C * C].view_as(prms[g][off + 2])
             grads[g][off + 3] = gc[g, C * C:]
         dz_new = _empty(Bn, C, P1, P2, like=inp)
-        call("blindno_rowidft_bwd_g", ptr(GZ), ptr(dz), ptr(_sub(small, offs[2 + 2 * k])), ptr(src),
+        call("blindno_rowidft_bwd_g", ptr(GZ), ptr(dz), small.p(2 + 2 * k), ptr(src),
              ptr(dz_new), ptr(tb), G, S, Bn, C, P1, P2, meta.m2, act, stream_ptr())
         dz = dz_new
     np_l = C * Cin + C
     nchunk = query("blindno_lift_bwd_nchunk", Bg, N1, N2)
     partial = _empty(nchunk, G, np_l, like=inp)
     d_inp = torch.empty_like(inp) if need_inp_grad else None
-    call("blindno_lift_bwd_g", ptr(dz), ptr(inp), ptr(small), ptr(d_inp), ptr(partial), nchunk, G, S,
+    call("blindno_lift_bwd_g", ptr(dz), ptr(inp), small.p(0), ptr(d_inp), ptr(partial), nchunk, G, S,
          Bn, N1, N2, Cin, C, P1, P2, stream_ptr())
     gl = reduce_partials(partial, nchunk, G * np_l).view(G, np_l)
     for g in range(G):
