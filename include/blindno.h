@@ -92,7 +92,9 @@ int blindno_project_bwd_w(const float* z, const float* w1, const float* b1, cons
  *   stats (blindno_project_bag_stats_floats(B, Ho, Wo) floats): per 16-point tile the bag-level
  *         sums A = sum lw GELU(h), S = sum lw GELU'(h), Q = sum lw GELU'(h) z^T,
  *   v (B U, C, P1, P2) on the crop: W1^T (w2 * GELU'(h)) per snapshot point.
- * Backward: gs (B, Ho Wo) = the gradient of ubar; writes dz = lw_l gs v on the crop and
+ * Backward: gs (B, Ho Wo) = the gradient of ubar; writes dz = lw_l gs v on the crop (dz NULL:
+ * not written, v not read -- the consumers form it on load, blindno_rowdft_cd_bag /
+ * blindno_rowidft_bwd_zc_bag) and
  * per-workgroup partials [dW1 (Hd*C) | db1 (Hd) | dW2 (Hd) | db2] into partial[nchunk][...],
  * nchunk = blindno_project_bag_bwd_nchunk(B, Ho, Wo) (any value >= 1). */
 int64_t blindno_project_bag_stats_floats(int B, int Ho, int Wo);
@@ -307,6 +309,18 @@ int blindno_rowidft_bwd_zc(const float* Y, const float* dz, const float* wc, con
                            float* dx, const float* tb, const float* tab, float* part,
                            const float* Tp, float* partial, int Bn, int C, int P1, int P2, int m1,
                            int m2, int act, int dN1, int dN2, blindno_stream_t stream);
+/* the encoder's last layer with dz = lw_l ghat v formed on load (v from blindno_project_bag_fwd,
+ * ghat (B, Ho Wo) the bag-level gradient, lw (U) or NULL for 1 / U; Bn = B U; the projection
+ * backward then writes no dz): counterparts of blindno_rowdft_cd (crop Ho x Wo, act 0) and of
+ * blindno_rowidft_bwd_zc with the weight-gradient and column-DFT partials */
+int blindno_rowdft_cd_bag(const float* v, const float* ghat, const float* lw, int U, float* part,
+                          const float* Tp, const float* tab, int Bn, int C, int P1, int P2, int m2,
+                          int Ho, int Wo, blindno_stream_t stream);
+int blindno_rowidft_bwd_zc_bag(const float* Y, const float* v, const float* ghat, const float* lw,
+                               int U, const float* wc, const float* xsrc, float* dx, const float* tb,
+                               const float* tab, float* part, const float* Tp, float* partial,
+                               int Bn, int C, int P1, int P2, int m1, int m2, int act, int Ho, int Wo,
+                               blindno_stream_t stream);
 int blindno_rowidft_bwd_lift_zc(const float* Y, const float* dz, const float* X, const int* idx,
                                 const float* grid, const float* w0, const float* b0,
                                 const float* wc, const float* tb, const float* tab, float* partial,

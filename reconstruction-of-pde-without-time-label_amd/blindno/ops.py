@@ -46,6 +46,9 @@ BAG_STATS_MAX_BYTES = 4 << 30
 # inverse's prologue): FNO_input at C = 4, m1 = m2 = 12 with the fp32 mix.  False: the fused
 # column pass (blindno_colpass) between the row kernels, as before.
 COLSPEC = os.environ.get("BLINDNO_COLSPEC", "1") != "0"
+# ... with the bag-level projection, the last layer's gradient dz = lw_l ghat v formed on load by
+# its readers instead of written by the projection backward (BLINDNO_BAGDZ=0: written)
+BAG_DZ_ON_LOAD = os.environ.get("BLINDNO_BAGDZ", "1") != "0"
 
 
 def set_mix_precision(name: str) -> None:
@@ -1258,7 +1261,14 @@ class BagEncoderFn(torch.autograd.Function):
         # consumers (the last layer's row DFT and row-inverse adjoint) read just that region, so
         # the padding (36% of the field at 128^2) is never zero-filled (88 MB at config C)
         crop = (Ho, Wo) if n >= 2 else None
-        dz = _empty(Bn, C, P1, P2, like=gh) if crop else torch.zeros(Bn, C, P1, P2, dtype=F32, device=gh.device)
+        cs = ctx.cs
+        ctx.cs = None
+        # the folded column pass with the bag-level projection: dz = lw_l ghat v is formed on load
+        # by its two readers (the last layer's row DFT and row-inverse adjoint), so the projection
+        # backward neither writes dz nor reads v (a field write and read less per step)
+        bagdz = cs is not None and bag is not None and crop is not None and BAG_DZ_ON_LOAD
+        dz = None if bagdz else (_empty(Bn, C, P1, P2, like=gh) if crop else
+                                 torch.zeros(Bn, C, P1, P2, dtype=F32, device=gh.device))
         np_p = Hd * C + Hd + Cout * Hd + Cout
         nchunk = query("blindno_project_bag_bwd_nchunk" if bag is not None else "blindno_project_bwd_nchunk",
                        B if bag is not None else Bn, Ho, Wo)
@@ -1280,8 +1290,6 @@ class BagEncoderFn(torch.autograd.Function):
         grads[off_fc1 + 3] = gp[o:o + Cout]
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         fc0w, fc0b = prm[0], prm[1]
-        cs = ctx.cs
-        ctx.cs = None
         if cs is not None:
             # the folded column pass (forward above): the last layer's adjoint starts from the
             # row DFT + column-DFT partials of dz on its crop; each adjoint row inverse rebuilds
@@ -1289,8 +1297,12 @@ class BagEncoderFn(torch.autograd.Function):
             # partials; the weight gradient reads the saved spectra as before
             part = cs.part(C, gh)
             valid = crop or (P1, P2)
-            call("blindno_rowdft_cd", ptr(dz), ptr(part), ptr(cs.Tp), ptr(cs.tab), Bn, C, P1, P2, meta.m2, 0,
-                 valid[0], valid[1], stream_ptr())
+            if bagdz:
+                call("blindno_rowdft_cd_bag", ptr(bag[1]), ptr(sgr), ptr(lw), L, ptr(part), ptr(cs.Tp),
+                     ptr(cs.tab), Bn, C, P1, P2, meta.m2, Ho, Wo, stream_ptr())
+            else:
+                call("blindno_rowdft_cd", ptr(dz), ptr(part), ptr(cs.Tp), ptr(cs.tab), Bn, C, P1, P2, meta.m2,
+                     0, valid[0], valid[1], stream_ptr())
             nbv = (valid[0] + 15) // 16
             for k in reversed(range(n)):
                 off = 2 + 4 * k
@@ -1304,9 +1316,14 @@ class BagEncoderFn(torch.autograd.Function):
                     pw = _empty(nchunk, C * C + C, like=gh)
                     dx = _empty(Bn, C, P1, P2, like=gh)
                     part = cs.part(C, gh)
-                    call("blindno_rowidft_bwd_zc", ptr(Yb), ptr(dz), ptr(cw), ptr(zs[k - 1]), ptr(dx), ptr(cs.tb),
-                         ptr(cs.tab), ptr(part), ptr(cs.Tp), ptr(pw), Bn, C, P1, P2, meta.m1, meta.m2, 1,
-                         dv[0], dv[1], stream_ptr())
+                    if bagdz and k == n - 1:
+                        call("blindno_rowidft_bwd_zc_bag", ptr(Yb), ptr(bag[1]), ptr(sgr), ptr(lw), L, ptr(cw),
+                             ptr(zs[k - 1]), ptr(dx), ptr(cs.tb), ptr(cs.tab), ptr(part), ptr(cs.Tp), ptr(pw),
+                             Bn, C, P1, P2, meta.m1, meta.m2, 1, Ho, Wo, stream_ptr())
+                    else:
+                        call("blindno_rowidft_bwd_zc", ptr(Yb), ptr(dz), ptr(cw), ptr(zs[k - 1]), ptr(dx),
+                             ptr(cs.tb), ptr(cs.tab), ptr(part), ptr(cs.Tp), ptr(pw), Bn, C, P1, P2, meta.m1,
+                             meta.m2, 1, dv[0], dv[1], stream_ptr())
                     g = reduce_partials(pw, nchunk, C * C + C)
                     grads[off + 2], grads[off + 3] = g[:C * C].view_as(cw), g[C * C:]
                     dz = dx

@@ -332,7 +332,8 @@ __global__ __launch_bounds__(256) void bagproj_bwd_kernel(
   const unsigned ntiles = (g.npts + 15) / 16;
   const unsigned ntg = (ntiles + 3) / 4;
   for (unsigned tg = blockIdx.x; tg < ntg; tg += gridDim.x) {
-    {
+    if (dz) {
+      // (dz NULL: the consumers form dz = lw ghat v on load, csrc/colspec.h BagDz)
       const unsigned f = tg * 64 + (unsigned)p64;
       if (f < g.npts && cw < C) {
         const float gh = gs[f];
@@ -461,7 +462,7 @@ BLINDNO_API int blindno_project_bag_bwd(const float* stats, const float* gs, con
                                         float* partial, int nchunk, int B, int U, int C, int P1,
                                         int P2, int Ho, int Wo, int Hd, void* stream) {
   BagGeom g;
-  if (!bag_geom(B, U, C, P1, P2, Ho, Wo, Hd, g) || !stats || !gs || !v || !dz || !partial ||
+  if (!bag_geom(B, U, C, P1, P2, Ho, Wo, Hd, g) || !stats || !gs || (dz && !v) || !partial ||
       nchunk < 1)
     return (int)hipErrorInvalidValue;
   bagproj_bwd_kernel<<<nchunk, 256, 0, (hipStream_t)stream>>>(stats, gs, w2, lw, v, dz, partial, g);

@@ -38,7 +38,19 @@ struct SpecCol {
   const float* tabT;  // TabT[h / 4][2 K1][4]
   int nblk;           // CD: 16-row blocks per sample in the partial buffer (P1 / 16)
   int w3;             // launch choice: the 3-wave register budget (rowinv.hip, MODE 0)
+  // the bag-mean gradient of the encoder's last layer formed on load (BagDz, below): the
+  // adjoint's dz argument is then the bag projection's v
+  const float* dzg;   // ghat (B, S): the bag-level upstream gradient, S = Ho Wo
+  const float* dzl;   // lw (U) multiplicity weights, NULL: 1 / U
+  int dzU, dzWo, dzS;
 };
+
+// dz of the encoder's last layer (csrc/bagproj.hip): dz[b U + l][c][h][w] = lw_l ghat[b][h Wo + w]
+// v[b U + l][c][h][w] on the Ho x Wo crop.  Its consumers form it on load from v instead of the
+// projection backward writing it (one field write and read less per step).
+__device__ __forceinline__ float bagdz_scale(const float* lw, int U, int l) {
+  return lw ? lw[l] : 1.0f / (float)U;
+}
 
 // Partials of one (sample n, 16-row block b): NCH chunks of 64 lanes x float2,
 //   part[((n nblk + b) NCH + ch) 128 + 2 lane + e],

@@ -30,11 +30,14 @@ constexpr int kCdWaves = 4;
 // the D layout is At[h0 + 4 g + r][k' = 16 nt + c16] -- what cd_store takes.
 // LIFT: the rows are the bag's snapshots X[b][idx[l]] (one channel, zero past N1 x N2); otherwise
 // x[n][c][h][w], read on the valid region N1v x N2v (zero elsewhere), GELU'd first when act.
-template <int NNT, bool ALIGNED, bool LIFT>
+// BDZ: x is the bag projection's v and the rows are dz = lw_l ghat v (the encoder's last-layer
+// gradient formed on load, colspec.h BagDz): ghat (B, N1v N2v), lw (L = U snapshots per bag)
+template <int NNT, bool ALIGNED, bool LIFT, bool BDZ = false>
 __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
     const float* __restrict__ x, const int* __restrict__ idx, float* __restrict__ part,
     const float* __restrict__ Tp, const float* __restrict__ tab, int Bn, int C, int P1, int P2,
-    int m2, int KB, int nbv, int N1v, int N2v, int act, int T, int L) {
+    int m2, int KB, int nbv, int N1v, int N2v, int act, int T, int L,
+    const float* __restrict__ ghat = nullptr, const float* __restrict__ lw = nullptr) {
   constexpr int Npad = 16 * NNT;
   extern __shared__ float lds[];
   float* sT = lds;                                 // [KB][4][Npad][4]
@@ -54,6 +57,13 @@ __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
     const int h0 = b << 4, h = h0 + r16;
     const bool rok = h < N1v;
     const float* xr;
+    const float* gr = ghat;                        // BDZ: this row of ghat
+    float lwl = 0.f;
+    if constexpr (BDZ) {
+      const int bb = n / L, l = n - bb * L;
+      gr = ghat + ((int64_t)bb * N1v + (rok ? h : 0)) * N2v;
+      lwl = bagdz_scale(lw, L, l);
+    }
     if constexpr (LIFT) {
       const int bb = n / L, l = n - bb * L;
       xr = x + (((int64_t)bb * T + (rok ? idx[l] : 0)) * N1v + (rok ? h : 0)) * N2v;
@@ -68,9 +78,17 @@ __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
       if (ALIGNED && w0 + 3 < N2v) {
         const float4 v = rok ? *reinterpret_cast<const float4*>(xr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
         a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+        if constexpr (BDZ) {
+          const float4 gv = rok ? *reinterpret_cast<const float4*>(gr + w0) : make_float4(0.f, 0.f, 0.f, 0.f);
+          a[0] *= gv.x * lwl; a[1] *= gv.y * lwl; a[2] *= gv.z * lwl; a[3] *= gv.w * lwl;
+        }
       } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) a[s] = (rok && w0 + s < N2v) ? xr[w0 + s] : 0.f;
+        for (int s = 0; s < 4; ++s) {
+          const bool ok = rok && w0 + s < N2v;
+          a[s] = ok ? xr[w0 + s] : 0.f;
+          if constexpr (BDZ) a[s] = ok ? a[s] * (gr[w0 + s] * lwl) : 0.f;
+        }
       }
     };
     const int KBv = (N2v + 15) >> 4;              // K blocks past the valid columns are zero
@@ -224,10 +242,11 @@ bool cd_geom_ok(int Bn, int C, int P1, int P2, int m2) {
          m2 <= 16 && 2 * m2 <= P2 && (int64_t)Bn * C * P1 * P2 < INT32_MAX;
 }
 
-template <bool LIFT>
+template <bool LIFT, bool BDZ = false>
 int rowdft_cd_launch(const float* x, const int* idx, float* part, const float* Tp,
                      const float* tab, int Bn, int C, int P1, int P2, int m2, int act, int N1v,
-                     int N2v, int T, int L, hipStream_t st) {
+                     int N2v, int T, int L, hipStream_t st, const float* ghat = nullptr,
+                     const float* lw = nullptr) {
   const int KB = (P2 + 15) / 16, NNT = (2 * m2 + 15) / 16, Npad = 16 * NNT;
   const int nbv = (N1v + 15) / 16;
   const size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
@@ -235,10 +254,11 @@ int rowdft_cd_launch(const float* x, const int* idx, float* part, const float* T
   const int64_t items = (int64_t)Bn * C * nbv;
   const int64_t b = (items + kCdWaves - 1) / kCdWaves;
   const int blocks = (int)(b < COLSPEC_RD_BLOCKS ? b : COLSPEC_RD_BLOCKS);
-  const bool aligned = N2v % 4 == 0 && (LIFT || P2 % 4 == 0) && (((uintptr_t)x) & 15) == 0;
+  const bool aligned = N2v % 4 == 0 && (LIFT || P2 % 4 == 0) && (((uintptr_t)x) & 15) == 0 &&
+                       (((uintptr_t)ghat) & 15) == 0;
 #define CDK(NNT_, AL_)                                                                         \
-  rowdft_cd_kernel<NNT_, AL_, LIFT><<<blocks, 64 * kCdWaves, sh, st>>>(                        \
-      x, idx, part, Tp, tab, Bn, C, P1, P2, m2, KB, nbv, N1v, N2v, act, T, L)
+  rowdft_cd_kernel<NNT_, AL_, LIFT, BDZ><<<blocks, 64 * kCdWaves, sh, st>>>(                   \
+      x, idx, part, Tp, tab, Bn, C, P1, P2, m2, KB, nbv, N1v, N2v, act, T, L, ghat, lw)
   if (NNT == 1) {
     if (aligned) CDK(1, true); else CDK(1, false);
   } else {
@@ -262,6 +282,18 @@ BLINDNO_API int blindno_rowdft_cd(const float* x, float* part, const float* Tp, 
     return (int)hipErrorInvalidValue;
   return rowdft_cd_launch<false>(x, nullptr, part, Tp, tab, Bn, C, P1, P2, m2, act, N1v, N2v, 0, 1,
                                  (hipStream_t)stream);
+}
+
+// blindno_rowdft_cd of the encoder's last-layer gradient dz = lw_l ghat v formed on load (v from
+// blindno_project_bag_fwd, ghat (B, Ho Wo), lw (U, NULL: 1 / U); Bn = B U; act 0; crop Ho x Wo)
+BLINDNO_API int blindno_rowdft_cd_bag(const float* v, const float* ghat, const float* lw, int U,
+                                      float* part, const float* Tp, const float* tab, int Bn, int C,
+                                      int P1, int P2, int m2, int Ho, int Wo, void* stream) {
+  if (!v || !ghat || !part || !Tp || !tab || U < 1 || Bn % U || !cd_geom_ok(Bn, C, P1, P2, m2) ||
+      Ho < 1 || Ho > P1 || Wo < 1 || Wo > P2)
+    return (int)hipErrorInvalidValue;
+  return rowdft_cd_launch<false, true>(v, nullptr, part, Tp, tab, Bn, C, P1, P2, m2, 0, Ho, Wo, 0, U,
+                                       (hipStream_t)stream, ghat, lw);
 }
 
 // The snapshot encoder's first stage: row DFT + column-DFT partials of the bag's snapshots

@@ -564,8 +564,9 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 // holds 2048 16-row work items at once; beyond that the rest ran as a second round (Bn = 208
 // snapshots = 2080 items: 75 us, where 2000 items took 56).  The MODE 0 ZY / CD kernels take a
 // 3-wave budget (one column tile per step) when their items fit 3072 slots but not 2048
+// DZB (MODE 1): dz = lw_l ghat v formed on load (SpecCol.dzg / dzl; the dz argument is v)
 template <int MODE, int ACT, int WG, int LIFT, int RD, int S, int NH, bool HW_ = true, int NSC = 0,
-          bool ZY = false, bool CD = false, int ZW = 0>
+          bool ZY = false, bool CD = false, int ZW = 0, bool DZB = false>
 __global__ __launch_bounds__(256, ZW > 0 ? ZW : 1)
 void rowfuse_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
@@ -672,6 +673,14 @@ void rowfuse_kernel(
       grow = bl.grid + (int64_t)h * bl.N2 * 2;
     }
     const bool drow = MODE == 0 || h < dN1;
+    // DZB: this item's ghat row and lw_l (dz = lw_l ghat v on the dN1 x dN2 crop)
+    const float* dzrow = sc.dzg;
+    float dzlw = 0.f;
+    if constexpr (DZB) {
+      const int b = n / sc.dzU, l = n - b * sc.dzU;
+      dzrow = sc.dzg + (int64_t)b * sc.dzS + (int64_t)(drow ? h : 0) * sc.dzWo;
+      dzlw = bagdz_scale(sc.dzl, sc.dzU, l);
+    }
     // field operands of one step: 16-B loads from clamped offsets, then selects
     struct Ops {
       f32x4 a[C][NH];      // MODE 0: layer input x; MODE 1: dz of every output channel
@@ -683,6 +692,12 @@ void rowfuse_kernel(
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
         const int w = 16 * NH * st + 4 * NH * g + 4 * hf;
+        f32x4 gsc = zero4;                           // DZB: lw_l ghat of the lane's 4 points
+        if constexpr (DZB && MODE == 1) {
+          const bool ok = drow && w < dN2;
+          const f32x4 gv = *reinterpret_cast<const f32x4*>(dzrow + (ok ? w : 0));
+          gsc = ok ? gv * dzlw : zero4;
+        }
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           o.a[c][hf] = zero4;
@@ -691,7 +706,8 @@ void rowfuse_kernel(
           if (MODE == 1 && has_wc) {
             const bool ok = drow && w < dN2;
             const f32x4 v = *reinterpret_cast<const f32x4*>(dz + (ok ? fbase + c * HW + w : 0));
-            o.a[c][hf] = ok ? v : zero4;
+            if constexpr (DZB) o.a[c][hf] = ok ? v * gsc : zero4;
+            else o.a[c][hf] = ok ? v : zero4;
           }
           if (MODE == 1 && !LIFT && (ACT || WG))
             o.s[c][hf] = *reinterpret_cast<const f32x4*>(xs + fbase + c * HW + w);
@@ -1015,7 +1031,7 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
                   int Bn, int C, int P1, int P2, int m2, hipStream_t st, BagLift bl = BagLift{},
                   int G = 1, int64_t wgs = 0, int dN1 = 0, int dN2 = 0,
                   RowDftNext rd = RowDftNext{nullptr, nullptr, 0, 0},
-                  SpecCol sc = SpecCol{nullptr, nullptr, nullptr, nullptr, 0, 0}) {
+                  SpecCol sc = SpecCol{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, 0}) {
   if (dN1 <= 0) dN1 = P1;
   if (dN2 <= 0) dN2 = P2;
   if (dN1 > P1 || dN2 > P2) return (int)hipErrorInvalidValue;
@@ -1086,6 +1102,17 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
           if (!sc.part) RFG(0, 6, true, false, ROWFUSE_NH0_NORD, 3);
           else if (rd.act) RFG(2, 6, true, true, 1, 3);
           else RFG(1, 6, true, true, 1, 3);
+        } else if (sc.dzg) {
+          // the encoder's last-layer adjoint with dz formed on load (MODE 1 with its weight
+          // gradient and the previous layer's partials; no NSC unroll in MODE 1)
+          if constexpr (MODE == 1 && WG == 1 && LIFT == 0) {
+            if (!sc.part || rd.act || !wc) return (int)hipErrorInvalidValue;
+            rowfuse_kernel<MODE, ACT, WG, LIFT, 1, 6, ROWFUSE_NH1, true, 0, true, true, 0, true>
+                <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1,
+                                            dN2, rd, sc);
+          } else {
+            return (int)hipErrorInvalidValue;
+          }
         } else {
           if (!sc.part) RFX(0, 6, true, false);
           else if (rd.act) RFX(2, 6, true, true);
@@ -1375,7 +1402,8 @@ BLINDNO_API int blindno_rowidft_bwd_lift(const float* G, const float* dz, const 
 namespace {
 SpecCol spec_col(const float* Y, float* part, const float* tab, int P1, int w3 = 0) {
   // tab: Tab (P1 x 2 K1) followed by TabT (the same values, P1 / 4 x 2 K1 x 4)
-  return SpecCol{Y, part, tab, tab ? tab + (size_t)P1 * 2 * kCsK1 : nullptr, P1 / 16, w3};
+  return SpecCol{Y, part, tab, tab ? tab + (size_t)P1 * 2 * kCsK1 : nullptr, P1 / 16, w3,
+                 nullptr, nullptr, 0, 0, 0};
 }
 }  // namespace
 
@@ -1480,6 +1508,34 @@ BLINDNO_API int blindno_rowidft_bwd_zc(const float* Y, const float* dz, const fl
                                            P1, P2, m2, st, nb0, 1, 0, dN1, dN2, rd, sc);
   return rowinv_launch<1, 0, 0, 0, true>(nullptr, xsrc, dz, wc, nullptr, dx, tb, nullptr, nb, Bn, C, P1,
                                          P2, m2, st, nb0, 1, 0, dN1, dN2, rd, sc);
+}
+
+// blindno_rowidft_bwd_zc (with the 1x1-conv weight-gradient partials and the previous layer's
+// column-DFT partials) for the encoder's last layer, whose dz = lw_l ghat v is formed on load:
+// v (Bn, C, P1, P2) from blindno_project_bag_fwd, ghat (B, Ho Wo), lw (U, NULL: 1 / U), Bn = B U
+BLINDNO_API int blindno_rowidft_bwd_zc_bag(const float* Y, const float* v, const float* ghat,
+                                           const float* lw, int U, const float* wc,
+                                           const float* xsrc, float* dx, const float* tb,
+                                           const float* tab, float* part, const float* Tp,
+                                           float* partial, int Bn, int C, int P1, int P2, int m1,
+                                           int m2, int act, int Ho, int Wo, void* stream) {
+  if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !v || !ghat || U < 1 || Bn % U || !tab ||
+      !part || !Tp || !partial || !wc || Ho < 1 || Ho > P1 || Wo < 1 || Wo > P2 || Wo % 4)
+    return (int)hipErrorInvalidValue;
+  const int nb = zc_blocks1(Bn * (P1 / 16));
+  hipStream_t st = (hipStream_t)stream;
+  const RowDftNext rd{nullptr, Tp, ((2 * m2 + 15) / 16) * 16, 0};
+  SpecCol sc = spec_col(Y, part, tab, P1);
+  sc.dzg = ghat;
+  sc.dzl = lw;
+  sc.dzU = U;
+  sc.dzWo = Wo;
+  sc.dzS = Ho * Wo;
+  if (act)
+    return rowinv_launch<1, 1, 1, 0, true>(nullptr, xsrc, v, wc, nullptr, dx, tb, partial, nb, Bn, C, P1,
+                                           P2, m2, st, BagLift{}, 1, 0, Ho, Wo, rd, sc);
+  return rowinv_launch<1, 0, 1, 0, true>(nullptr, xsrc, v, wc, nullptr, dx, tb, partial, nb, Bn, C, P1,
+                                         P2, m2, st, BagLift{}, 1, 0, Ho, Wo, rd, sc);
 }
 
 // blindno_rowidft_bwd_lift with Z built from Y
