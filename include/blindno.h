@@ -538,6 +538,18 @@ int blindno_rowidft_bwd_g(const float* Gs, const float* dz, const float* wc, con
                           int P2, int m2, int act, blindno_stream_t stream);
 int blindno_conv_wgrad_g(const float* dz, const float* x, float* partial, int nchunk, int G,
                          int Bn, int C, int P1, int P2, int act, blindno_stream_t stream);
+/* One layer of the grouped heads' backward in a single launch (the adjoint of FNOModules.py:
+ * 226-232 per layer; three independent, latency-bound steps at the heads' size):
+ *   At = blindno_rowdft(dz, act 0), the conv_wgrad_g partials of (dz, GELU^act(src)) and, when
+ *   Xs != NULL, mix_wgrad_g(Xs, Gs) -> dWt (the layer processed before, Ci = Co = C), all with
+ *   the grids of their own launches (bit-identical results).  cnchunk =
+ *   blindno_conv_wgrad_nchunk(Bn / G, P1, P2), mnsplit = blindno_mix_wgrad_nsplit(Bn / G, ...).
+ *   Shapes: blindno_rowdft_wgrad_ok (the conv gradient's matrix-core form, 5 <= C <= 15). */
+int blindno_rowdft_wgrad_ok(int Bn, int C, int P1, int P2, int m2);
+int blindno_rowdft_wgrad_g(const float* dz, const float* src, float* At, const float* Tp,
+                           float* cpartial, int cnchunk, int act, const float* Xs,
+                           const float* Gs, float* dWt, float* mpartial, int mnsplit, int K1,
+                           int G, int Bn, int C, int P1, int P2, int m2, blindno_stream_t stream);
 
 /* ---- NIO encoder ConvBlock normalisation: BatchNorm2d fused with LeakyReLU
  * (2d_FPE/Baselines.py:40-52 ConvBlock = Conv -> BatchNorm2d -> LeakyReLU(slope); replaces the

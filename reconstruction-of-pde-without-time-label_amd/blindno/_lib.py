@@ -84,6 +84,8 @@ SIGNATURES = {
     "blindno_rowidft_epi_g": "ppppppiliiiiiis",
     "blindno_rowidft_bwd_g": "ppppppiliiiiiis",
     "blindno_conv_wgrad_g": "pppiiiiiiis",
+    "blindno_rowdft_wgrad_ok": "iiiii",
+    "blindno_rowdft_wgrad_g": "pppppiippppiiiiiiiis",
     "blindno_bagmean_fwd_w": "pppppp" + "iiiii" + "s",
     "blindno_project_bwd_w": "pppppppp" + "i" + "iiiiiiiiiii" + "s",
     "blindno_project_bag_stats_floats": "iii",

@@ -49,6 +49,9 @@ COLSPEC = os.environ.get("BLINDNO_COLSPEC", "1") != "0"
 # ... with the bag-level projection, the last layer's gradient dz = lw_l ghat v formed on load by
 # its readers instead of written by the projection backward (BLINDNO_BAGDZ=0: written)
 BAG_DZ_ON_LOAD = os.environ.get("BLINDNO_BAGDZ", "1") != "0"
+# the grouped heads' backward: row DFT + conv gradient + the previous layer's mix gradient in
+# one launch per layer (BLINDNO_HEADBWD_MERGED=0: three launches)
+HEAD_BWD_MERGED = os.environ.get("BLINDNO_HEADBWD_MERGED", "1") != "0"
 
 
 def set_mix_precision(name: str) -> None:
@@ -881,32 +884,65 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
     FB, GB = twiddle_cols(P1, meta.m1, inp.device)
     tb = twiddle_rowinv(P2, meta.m2, inp.device)
     np_c = C * C + C
+    ns = query("blindno_mix_wgrad_nsplit", Bg, C, C, K1, meta.m2)
+    nch = query("blindno_conv_wgrad_nchunk", Bg, P1, P2)
+    # one launch per layer for the row DFT of dz, the conv gradient and the previous layer's
+    # spectral weight gradient (blindno_rowdft_wgrad_g); the last layer's mix gradient after
+    # the loop
+    merged = HEAD_BWD_MERGED and query("blindno_rowdft_wgrad_ok", Bn, C, P1, P2, meta.m2) == 1
+    pending = None                  # (layer, Xs, Gs) whose mix gradient is not launched yet
+
+    def mix_buffers():
+        dWt = _empty(G, meta.m2, K1, C, C, 2, like=inp)
+        part = _empty(ns, G, meta.m2 * K1 * C * C * 2, like=inp) if ns > 1 else None
+        return dWt, part
+
+    def mix_grads(kk, dWt):
+        o = 2 + 4 * kk
+        if _DEFER is not None:
+            dws = [d for g in range(G) for d in unpack_w2d(dWt[g], prms[g][o], P1)]
+        else:
+            dws = [torch.empty_like(prms[g][o]) for g in range(G) for _ in range(2)]
+            call("blindno_unpack_w2d_2", ptr(dWt), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), C,
+                 C, meta.m1, meta.m2, P1, stream_ptr())
+        for g in range(G):
+            grads[g][o], grads[g][o + 1] = dws[2 * g], dws[2 * g + 1]
+
+    def mix_launch(kk, Xk, Gk):
+        dWt, part = mix_buffers()
+        call("blindno_mix_wgrad_g", ptr(Xk), ptr(Gk), ptr(dWt), ptr(part) if part is not None else None,
+             ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
+        mix_grads(kk, dWt)
+
     for k in reversed(range(n)):
         off = 2 + 4 * k
         src, act = (x0, 0) if k == 0 else (zs[k - 1], 1)
         Wt = Wts[k]
-        At = k_rowdft(dz, Bn, C, P1, P2, meta.m2, 0)
+        pc = _empty(nch, G, np_c, like=inp)
+        if merged:
+            At = _empty(Bn, meta.m2, C, P1, 2, like=inp)
+            mx = (None, None, None, None)
+            if pending is not None:
+                dWt, part = mix_buffers()
+                mx = (pending[1], pending[2], dWt, part)
+            call("blindno_rowdft_wgrad_g", ptr(dz), ptr(src), ptr(At), ptr(twiddle_mfma(P2, meta.m2, inp.device)),
+                 ptr(pc), nch, act, *[ptr(t) if t is not None else None for t in mx], ns, K1, G, Bn, C,
+                 P1, P2, meta.m2, stream_ptr())
+            if pending is not None:
+                mix_grads(pending[0], dWt)
+        else:
+            At = k_rowdft(dz, Bn, C, P1, P2, meta.m2, 0)
         Gs = _empty(Bn, meta.m2, C, K1, 2, like=inp)
         Y = _empty(Bn, meta.m2, C, K1p, 2, like=inp)
         GZ = _empty(Bn, P1, meta.m2, C, 2, like=inp)
         call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(Gs), ptr(Y), ptr(GZ), ptr(FB), ptr(GB), G,
              Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, _mixdir(1), stream_ptr())
-        dWt = _empty(G, meta.m2, K1, C, C, 2, like=inp)
-        ns = query("blindno_mix_wgrad_nsplit", Bg, C, C, K1, meta.m2)
-        part = _empty(ns, G, meta.m2 * K1 * C * C * 2, like=inp) if ns > 1 else None
-        call("blindno_mix_wgrad_g", ptr(Xs[k]), ptr(Gs), ptr(dWt), ptr(part) if part is not None else None,
-             ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
-        if _DEFER is not None:
-            dws = [d for g in range(G) for d in unpack_w2d(dWt[g], prms[g][off], P1)]
+        if merged:
+            pending = (k, Xs[k], Gs)
         else:
-            dws = [torch.empty_like(prms[g][off]) for g in range(G) for _ in range(2)]
-            call("blindno_unpack_w2d_2", ptr(dWt), ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), C,
-                 C, meta.m1, meta.m2, P1, stream_ptr())
-        for g in range(G):
-            grads[g][off], grads[g][off + 1] = dws[2 * g], dws[2 * g + 1]
-        nch = query("blindno_conv_wgrad_nchunk", Bg, P1, P2)
-        pc = _empty(nch, G, np_c, like=inp)
-        call("blindno_conv_wgrad_g", ptr(dz), ptr(src), ptr(pc), nch, G, Bn, C, P1, P2, act, stream_ptr())
+            mix_launch(k, Xs[k], Gs)
+            call("blindno_conv_wgrad_g", ptr(dz), ptr(src), ptr(pc), nch, G, Bn, C, P1, P2, act,
+                 stream_ptr())
         gc = reduce_partials(pc, nch, G * np_c).view(G, np_c)
         for g in range(G):
             grads[g][off + 2] = gc[g, :C * C].view_as(prms[g][off + 2])
@@ -915,6 +951,8 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         call("blindno_rowidft_bwd_g", ptr(GZ), ptr(dz), small.p(2 + 2 * k), ptr(src),
              ptr(dz_new), ptr(tb), G, S, Bn, C, P1, P2, meta.m2, act, stream_ptr())
         dz = dz_new
+    if pending is not None:
+        mix_launch(*pending)
     np_l = C * Cin + C
     nchunk = query("blindno_lift_bwd_nchunk", Bg, N1, N2)
     partial = _empty(nchunk, G, np_l, like=inp)

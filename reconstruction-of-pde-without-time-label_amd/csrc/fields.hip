@@ -14,6 +14,7 @@
 #include "common.h"
 #include "blindno.h"
 #include "kernels.h"
+#include "wgrad.h"
 
 using namespace blindno;
 
@@ -406,70 +407,13 @@ __global__ __launch_bounds__(256) void lift_bwd_w_mfma_kernel(const float* __res
   }
 }
 
-// 1x1-conv weight / bias gradient of the wide fields (the C = 12 heads) on the matrix cores:
-// dWc[o][i] = sum_p dz[o][p] f(x)[i][p] is a C x C GEMM over the points (K), 16 points per
-// four v_mfma_f32_16x16x4f32: lane (c16, g4) loads float4 dz[o = c16][p0 + 4 g4 ..] (A) and
-// f(x)[i = c16][p0 + 4 g4 ..] (B), component s feeding step s (the same point order for both
-// operands), and column C of B is 1.0 so D[o][C] accumulates the bias gradient.  The VALU
-// kernel above staged both fields in LDS and spent ~2 C^2 LDS reads per point.  Waves add
-// their 16 x 16 blocks in wave order; partial[blockIdx.x][g][C*C + C] as conv_wgrad_kernel.
 template <int ACT>
 __global__ __launch_bounds__(256) void conv_wgrad_mfma_kernel(const float* __restrict__ dz,
                                                               const float* __restrict__ x,
                                                               float* __restrict__ partial, int C,
                                                               int HW, int Bg) {
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  __shared__ f32x4 sacc[4][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int c16 = lane & 15, g4 = lane >> 4;
-  const int grp = blockIdx.y;
-  const int64_t gofs = (int64_t)grp * Bg * C * HW;
-  dz += gofs;
-  x += gofs;
-  const int cpn = (HW + 15) >> 4;                  // 16-point chunks per sample
-  const int64_t nch = (int64_t)Bg * cpn;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const bool vec = (HW & 3) == 0;
-  for (int64_t ch = (int64_t)blockIdx.x * 4 + wave; ch < nch; ch += (int64_t)gridDim.x * 4) {
-    const int n = (int)(ch / cpn);
-    const int p = (int)(ch - (int64_t)n * cpn) * 16 + 4 * g4;
-    float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
-    if (c16 < C) {
-      const float* dr = dz + ((int64_t)n * C + c16) * HW;
-      const float* xr = x + ((int64_t)n * C + c16) * HW;
-      if (vec && p + 3 < HW) {
-        const float4 va = *reinterpret_cast<const float4*>(dr + p);
-        const float4 vb = *reinterpret_cast<const float4*>(xr + p);
-        a[0] = va.x; a[1] = va.y; a[2] = va.z; a[3] = va.w;
-        b[0] = vb.x; b[1] = vb.y; b[2] = vb.z; b[3] = vb.w;
-      } else {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          if (p + s < HW) { a[s] = dr[p + s]; b[s] = xr[p + s]; }
-      }
-      if (ACT) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) b[s] = gelu_f(b[s]);
-      }
-    } else if (c16 == C) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) b[s] = p + s < HW ? 1.0f : 0.f;   // bias column
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
-  }
-  sacc[wave][lane] = acc;
-  __syncthreads();
-  // D[o = 4 g4 + r][i = c16] at lane (g4, c16), reg r
-  const int np = C * C + C;
-  float* pp = partial + ((int64_t)blockIdx.x * gridDim.y + grp) * np;
-  for (int e = threadIdx.x; e < np; e += blockDim.x) {
-    const int o = e < C * C ? e / C : e - C * C;
-    const int i = e < C * C ? e - (e / C) * C : C;
-    const int ln = 16 * (o >> 2) + i, r = o & 3;
-    pp[e] = ((sacc[0][ln][r] + sacc[1][ln][r]) + sacc[2][ln][r]) + sacc[3][ln][r];
-  }
+  conv_wgrad_mfma_block<ACT>(dz, x, partial, C, HW, Bg, blockIdx.x, gridDim.x, blockIdx.y,
+                             gridDim.y);
 }
 
 // out[p] = sum_c partial[c][p], deterministic.  A workgroup owns PB <= 64 consecutive
@@ -997,7 +941,7 @@ BLINDNO_API int blindno_conv_wgrad_g(const float* dz, const float* x, float* par
   const int64_t ntiles = (int64_t)Bg * tpn;
   const size_t sh = sizeof(float) * 2 * (size_t)C * (TP + 1);
   const dim3 grid(nchunk, G);
-  if (CONV_WGRAD_MFMA && C >= 5 && C <= 15 && HW < INT32_MAX / 16) {
+  if (CONV_WGRAD_MFMA && conv_wgrad_mfma_ok(C, HW)) {
     if (act)
       conv_wgrad_mfma_kernel<1><<<grid, 256, 0, (hipStream_t)stream>>>(dz, x, partial, C, (int)HW, Bg);
     else

@@ -11,6 +11,7 @@
 #include "common.h"
 #include "blindno.h"
 #include "kernels.h"
+#include "wgrad.h"
 
 using namespace blindno;
 
@@ -48,13 +49,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // STAGE: the twiddle image is staged in LDS by every workgroup; otherwise the B operands are
 // read from the global image (L1/L2-resident) -- when each wave runs about one work item the
 // staging is as many bytes as the wave's own x rows and costs a full latency up front.
+// (the body takes its workgroup index bx of gx explicitly: rowdft_wgrad_kernel below hosts it
+// beside other work in one launch)
 template <int NT, int ALIGNED, bool STAGE>
-__global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
-                                                          float* __restrict__ At,
-                                                          const float* __restrict__ Tp,
-                                                          int nrows, int C, int P1, int P2,
-                                                          int m2, int KB, int Npad, int ntile_groups,
-                                                          int act, int N1v, int N2v) {
+__device__ __forceinline__ void rowdft_mfma_block(const float* __restrict__ x,
+                                                  float* __restrict__ At,
+                                                  const float* __restrict__ Tp, int nrows, int C,
+                                                  int P1, int P2, int m2, int KB, int Npad,
+                                                  int ntile_groups, int act, int N1v, int N2v,
+                                                  int bx, int gx) {
   extern __shared__ float smT[];                 // [KB][4][Npad][4]
   if constexpr (STAGE) {
     const int nT = KB * 16 * Npad;
@@ -67,7 +70,7 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
   const int r16 = lane & 15, kq = lane >> 4;
   const int nrt = (nrows + 15) >> 4;
   const int64_t nwork = (int64_t)nrt * ntile_groups;
-  for (int64_t wk = (int64_t)blockIdx.x * 4 + wave; wk < nwork; wk += (int64_t)gridDim.x * 4) {
+  for (int64_t wk = (int64_t)bx * 4 + wave; wk < nwork; wk += (int64_t)gx * 4) {
     const int rt = (int)(wk / ntile_groups);
     const int tg = (int)(wk % ntile_groups);
     const int t0 = tg * NT;                       // first 16-column tile of this wave
@@ -127,6 +130,17 @@ __global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restric
       }
     }
   }
+}
+
+template <int NT, int ALIGNED, bool STAGE>
+__global__ __launch_bounds__(256) void rowdft_mfma_kernel(const float* __restrict__ x,
+                                                          float* __restrict__ At,
+                                                          const float* __restrict__ Tp,
+                                                          int nrows, int C, int P1, int P2,
+                                                          int m2, int KB, int Npad, int ntile_groups,
+                                                          int act, int N1v, int N2v) {
+  rowdft_mfma_block<NT, ALIGNED, STAGE>(x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, ntile_groups,
+                                        act, N1v, N2v, blockIdx.x, gridDim.x);
 }
 
 // Row DFT of the first FNO layer of the snapshot encoder with the lift folded in.  The lifted
@@ -812,20 +826,21 @@ __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__
 }
 
 // dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]
-__global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restrict__ X,
-                                                           const float2* __restrict__ G,
-                                                           float2* __restrict__ out, int Bn,
-                                                           int Ci, int Co, int K1, int m2) {
-  // blockIdx.y = sample slice: out[y][idx] = sum over this slice's samples (partials when
-  // gridDim.y > 1, reduced in fixed order afterwards)
-  // blockIdx.z = weight group: its Bn / gridDim.z samples only; out[(y G + g)][idx]
+// workgroup (bx, by, bz) of (gx, gy, gz), kBlock threads:
+//   by = sample slice: out[y][idx] = sum over this slice's samples (partials when gy > 1,
+//   reduced in fixed order afterwards)
+//   bz = weight group: its Bn / gz samples only; out[(y G + g)][idx]
+__device__ __forceinline__ void mix_wgrad_block(const float2* __restrict__ X,
+                                                const float2* __restrict__ G,
+                                                float2* __restrict__ out, int Bn, int Ci, int Co,
+                                                int K1, int m2, int bx, int by, int bz, int gx,
+                                                int gy, int gz) {
   const int total = m2 * K1 * Ci * Co;
-  const int Bg = Bn / gridDim.z, grp = blockIdx.z;
-  const int ns = (Bg + gridDim.y - 1) / gridDim.y;
-  const int n0 = grp * Bg + blockIdx.y * ns, n1 = min(grp * Bg + Bg, n0 + ns);
+  const int Bg = Bn / gz, grp = bz;
+  const int ns = (Bg + gy - 1) / gy;
+  const int n0 = grp * Bg + by * ns, n1 = min(grp * Bg + Bg, n0 + ns);
   const int sX = m2 * Ci * K1, sG = m2 * Co * K1;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += gridDim.x * blockDim.x) {
+  for (int idx = bx * kBlock + threadIdx.x; idx < total; idx += gx * kBlock) {
     const int o = idx % Co;
     int t = idx / Co;
     const int i = t % Ci;
@@ -847,8 +862,62 @@ __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restr
       re = fma((double)a.x, (double)g.x, fma((double)a.y, (double)g.y, re));
       im = fma((double)a.x, (double)g.y, fma(-(double)a.y, (double)g.x, im));
     }
-    out[((int64_t)blockIdx.y * gridDim.z + grp) * total + idx] = make_float2((float)re, (float)im);
+    out[((int64_t)by * gz + grp) * total + idx] = make_float2((float)re, (float)im);
   }
+}
+
+__global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restrict__ X,
+                                                           const float2* __restrict__ G,
+                                                           float2* __restrict__ out, int Bn,
+                                                           int Ci, int Co, int K1, int m2) {
+  mix_wgrad_block(X, G, out, Bn, Ci, Co, K1, m2, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x,
+                  gridDim.y, gridDim.z);
+}
+
+// The heads' backward, one layer (reverse order k = n-1 .. 0): the row DFT of dz_k, the 1x1-conv
+// weight gradient of (dz_k, f(x_k)) and the spectral weight gradient of layer k + 1 (whose
+// column pass has just run) are independent of each other, and each is a few-microsecond,
+// latency-bound launch at the heads' size (Bn = 8 at config C).  One launch hosts all three:
+// workgroups [0, nbr) run the row DFT, the next nchunk G the conv gradient, the rest the mix
+// gradient (nbm = 0: none), each with the grid coordinates of its own launch, so the results
+// are bit-identical to the three separate launches.
+struct ConvWgradJob {
+  const float* dz;
+  const float* x;
+  float* partial;
+  int C, HW, Bg, nchunk, G;
+};
+struct MixWgradJob {
+  const float2* X;
+  const float2* Gs;
+  float2* out;
+  int Bn, Ci, Co, K1, m2, gx, gy, gz;
+};
+
+template <int NT, int ALIGNED, int ACT>
+__global__ __launch_bounds__(256) void rowdft_wgrad_kernel(const float* __restrict__ x,
+                                                           float* __restrict__ At,
+                                                           const float* __restrict__ Tp,
+                                                           int nrows, int C, int P1, int P2,
+                                                           int m2, int KB, int Npad,
+                                                           int ntile_groups, int nbr,
+                                                           ConvWgradJob cw, MixWgradJob mw) {
+  int b = blockIdx.x;
+  if (b < nbr) {
+    rowdft_mfma_block<NT, ALIGNED, false>(x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, ntile_groups,
+                                          0, P1, P2, b, nbr);
+    return;
+  }
+  b -= nbr;
+  const int nbc = cw.nchunk * cw.G;
+  if (b < nbc) {
+    conv_wgrad_mfma_block<ACT>(cw.dz, cw.x, cw.partial, cw.C, cw.HW, cw.Bg, b % cw.nchunk,
+                               cw.nchunk, b / cw.nchunk, cw.G);
+    return;
+  }
+  b -= nbc;
+  mix_wgrad_block(mw.X, mw.Gs, mw.out, mw.Bn, mw.Ci, mw.Co, mw.K1, mw.m2, b % mw.gx,
+                  (b / mw.gx) % mw.gy, b / (mw.gx * mw.gy), mw.gx, mw.gy, mw.gz);
 }
 
 // ------------------------------------------------------------------------------ 1D mode mix
@@ -980,46 +1049,62 @@ __global__ void pack_w1d_kernel(const float2* __restrict__ src, float2* __restri
 
 }  // namespace
 
-BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, int Bn, int C,
-                                    int P1, int P2, int m2, int act, int N1v, int N2v,
-                                    void* stream) {
+// launch shape of the row DFT over (Bn C P1) rows, columns < N2v live
+struct RowdftPlan {
+  int nrows, KB, Npad, nt, groups, blocks;
+  int64_t nwork;
+  size_t sh;
+  bool aligned, stage;
+};
+static int rowdft_plan(const float* x, int Bn, int C, int P1, int P2, int m2, int N1v, int N2v,
+                       RowdftPlan& p) {
   if (Bn <= 0 || C <= 0 || P1 <= 0 || P2 <= 0 || m2 <= 0 || m2 > P2 / 2 + 1 || N1v < 1 ||
       N1v > P1 || N2v < 1 || N2v > P2)
     return (int)hipErrorInvalidValue;
   const int64_t nrows64 = (int64_t)Bn * C * P1;
   if (nrows64 > INT32_MAX) return (int)hipErrorInvalidValue;
-  const int nrows = (int)nrows64;
-  const int KB = (N2v + 15) / 16;                 // K blocks past the valid columns are zero
-  const int Npad = ((2 * m2 + 15) / 16) * 16;
-  const int ntiles = Npad / 16;
-  const size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
-  if (sh > 160 * 1024) return (int)hipErrorInvalidValue;
+  p.nrows = (int)nrows64;
+  p.KB = (N2v + 15) / 16;                         // K blocks past the valid columns are zero
+  p.Npad = ((2 * m2 + 15) / 16) * 16;
+  const int ntiles = p.Npad / 16;
+  p.sh = sizeof(float) * (size_t)p.KB * 16 * p.Npad;
+  if (p.sh > 160 * 1024) return (int)hipErrorInvalidValue;
   // tiles per wave: all of them when there are many row tiles, else split for parallelism
-  const int nrt = (nrows + 15) / 16;
+  const int nrt = (p.nrows + 15) / 16;
   int nt = ntiles;
   if (nt > 4) nt = 4;
   while (nt > 1 && (int64_t)nrt * ((ntiles + nt - 1) / nt) < ROWDFT_MIN_WORK) nt >>= 1;
   while (ntiles % nt) --nt;
-  const int groups = ntiles / nt;
-  const int64_t nwork = (int64_t)nrt * groups;
-  const int blocks = (int)((nwork + 3) / 4 < ROWDFT_MAX_BLOCKS ? (nwork + 3) / 4 : ROWDFT_MAX_BLOCKS);
-  const bool aligned = (P2 % 4) == 0 && (((uintptr_t)x) & 15) == 0;
-  hipStream_t st = (hipStream_t)stream;
+  p.nt = nt;
+  p.groups = ntiles / nt;
+  p.nwork = (int64_t)nrt * p.groups;
+  p.blocks = (int)((p.nwork + 3) / 4 < ROWDFT_MAX_BLOCKS ? (p.nwork + 3) / 4 : ROWDFT_MAX_BLOCKS);
+  p.aligned = (P2 % 4) == 0 && (((uintptr_t)x) & 15) == 0;
   // stage the twiddle image only when the waves reuse it (>= ROWDFT_STAGE_ITEMS work items
   // per wave)
-  const bool stage = nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * blocks;
+  p.stage = p.nwork >= (int64_t)ROWDFT_STAGE_ITEMS * 4 * p.blocks;
+  return 0;
+}
+
+BLINDNO_API int blindno_rowdft_crop(const float* x, float* At, const float* Tp, int Bn, int C,
+                                    int P1, int P2, int m2, int act, int N1v, int N2v,
+                                    void* stream) {
+  RowdftPlan p;
+  const int e = rowdft_plan(x, Bn, C, P1, P2, m2, N1v, N2v, p);
+  if (e) return e;
+  hipStream_t st = (hipStream_t)stream;
 #define RD(NT_, AL_)                                                                        \
   do {                                                                                      \
-    if (stage)                                                                              \
-      rowdft_mfma_kernel<NT_, AL_, true><<<blocks, 256, sh, st>>>(                          \
-          x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
+    if (p.stage)                                                                            \
+      rowdft_mfma_kernel<NT_, AL_, true><<<p.blocks, 256, p.sh, st>>>(                      \
+          x, At, Tp, p.nrows, C, P1, P2, m2, p.KB, p.Npad, p.groups, act, N1v, N2v);        \
     else                                                                                    \
-      rowdft_mfma_kernel<NT_, AL_, false><<<blocks, 256, 0, st>>>(                          \
-          x, At, Tp, nrows, C, P1, P2, m2, KB, Npad, groups, act, N1v, N2v);                \
+      rowdft_mfma_kernel<NT_, AL_, false><<<p.blocks, 256, 0, st>>>(                        \
+          x, At, Tp, p.nrows, C, P1, P2, m2, p.KB, p.Npad, p.groups, act, N1v, N2v);        \
   } while (0)
 #define RD_AL(NT_) \
-  if (aligned) RD(NT_, 1); else RD(NT_, 0);
-  switch (nt) {
+  if (p.aligned) RD(NT_, 1); else RD(NT_, 0);
+  switch (p.nt) {
     case 1: RD_AL(1) break;
     case 2: RD_AL(2) break;
     case 3: RD_AL(3) break;
@@ -1235,6 +1320,65 @@ BLINDNO_API int blindno_mix_wgrad_part(const float* X, const float* G, float* pa
   mix_wgrad_kernel<<<g, kBlock, 0, (hipStream_t)stream>>>((const float2*)X, (const float2*)G,
                                                           (float2*)partial, Bn, Ci, Co, K1, m2);
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_rowdft_wgrad_ok(int Bn, int C, int P1, int P2, int m2) {
+  RowdftPlan p;
+  return conv_wgrad_mfma_ok(C, (int64_t)P1 * P2) &&
+                 rowdft_plan(nullptr, Bn, C, P1, P2, m2, P1, P2, p) == 0
+             ? 1
+             : 0;
+}
+
+// One layer of the heads' backward in one launch (rowdft_wgrad_kernel): At = rowDFT(dz) as
+// blindno_rowdft, the conv gradient partials of (dz, f(src)) as blindno_conv_wgrad_g and, when
+// Xs != NULL, the previous layer's spectral weight gradient as blindno_mix_wgrad_g.
+BLINDNO_API int blindno_rowdft_wgrad_g(const float* dz, const float* src, float* At,
+                                       const float* Tp, float* cpartial, int cnchunk, int act,
+                                       const float* Xs, const float* Gs, float* dWt,
+                                       float* mpartial, int mnsplit, int K1, int G, int Bn, int C,
+                                       int P1, int P2, int m2, void* stream) {
+  if (G < 1 || Bn % G || !dz || !src || !At || !Tp || !cpartial) return (int)hipErrorInvalidValue;
+  const int Bg = Bn / G;
+  const int64_t HW = (int64_t)P1 * P2;
+  if (!conv_wgrad_mfma_ok(C, HW) || cnchunk != blindno_conv_wgrad_nchunk(Bg, P1, P2))
+    return (int)hipErrorInvalidValue;
+  RowdftPlan p;
+  int e = rowdft_plan(dz, Bn, C, P1, P2, m2, P1, P2, p);
+  if (e) return e;
+  MixWgradJob mw{(const float2*)Xs, (const float2*)Gs, nullptr, Bn, C, C, K1, m2, 1, 1, G};
+  int64_t nbm = 0;
+  const int64_t total = (int64_t)m2 * K1 * C * C;
+  if (Xs) {
+    if (!Gs || !dWt || K1 < 1 || total >= INT32_MAX / 2 || mnsplit < 1 ||
+        (mnsplit > 1 && !mpartial))
+      return (int)hipErrorInvalidValue;
+    mw.out = (float2*)(mnsplit > 1 ? mpartial : dWt);
+    mw.gx = (int)cdiv(total, kBlock);
+    mw.gy = mnsplit;
+    nbm = (int64_t)mw.gx * mw.gy * G;
+  }
+  const ConvWgradJob cw{dz, src, cpartial, C, (int)HW, Bg, cnchunk, G};
+  const int64_t nb = p.blocks + (int64_t)cnchunk * G + nbm;
+  if (nb >= INT32_MAX) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+#define RW(NT_, AL_, A_)                                                                      \
+  rowdft_wgrad_kernel<NT_, AL_, A_><<<(unsigned)nb, 256, 0, st>>>(                            \
+      dz, At, Tp, p.nrows, C, P1, P2, m2, p.KB, p.Npad, p.groups, p.blocks, cw, mw)
+#define RW_A(NT_, AL_) do { if (act) RW(NT_, AL_, 1); else RW(NT_, AL_, 0); } while (0)
+#define RW_AL(NT_) do { if (p.aligned) RW_A(NT_, 1); else RW_A(NT_, 0); } while (0)
+  switch (p.nt) {
+    case 1: RW_AL(1); break;
+    case 2: RW_AL(2); break;
+    case 3: RW_AL(3); break;
+    default: RW_AL(4); break;
+  }
+#undef RW_AL
+#undef RW_A
+#undef RW
+  e = (int)hipGetLastError();
+  if (e || !Xs || mnsplit == 1) return e;
+  return blindno_reduce_partials(mpartial, dWt, mnsplit, (int)(2 * total * G), stream);
 }
 
 BLINDNO_API int blindno_mix_wgrad_g(const float* X, const float* G, float* dWt, float* partial,

@@ -273,6 +273,41 @@ def test_head_pair_grouped_matches_separate_heads(width, modes, N, B):
     assert rel_l2(gh.cpu().numpy(), h.grad.cpu().numpy()) <= 1e-6
 
 
+@pytest.mark.parametrize("width,modes,N,B", [(12, 16, 64, 3), (12, 32, 128, 4), (6, 5, 16, 2)])
+def test_head_backward_merged_launch_bit_identical(width, modes, N, B):
+    """The grouped heads' backward with the row DFT, the conv gradient and the previous layer's
+    mix gradient in one launch per layer (blindno_rowdft_wgrad_g) against the three separate
+    launches: every gradient bit-identical (each job keeps its own grid and summation order).
+    (6, 5, 16, 2): C = 6 < the 12 of the heads, still the conv gradient's matrix-core form."""
+    from blindno import FNO2d, ops
+    from blindno.fno import fno_params
+    torch.manual_seed(22)
+    heads = [FNO2d(modes, width, 3, width, 1).cuda() for _ in range(2)]
+    h = torch.randn(B, N, N, width, device="cuda", requires_grad=True)
+    side = torch.cuda.Stream()
+    p0, p1 = fno_params(heads[0], 2), fno_params(heads[1], 2)
+    meta = heads[0].meta(width)
+    Pm = ops._fno_geometry(h, meta)[4:6]
+    assert ops.query("blindno_rowdft_wgrad_ok", 2 * B, width, Pm[0], Pm[1], meta.m2) == 1
+    res = {}
+    prev = ops.HEAD_BWD_MERGED
+    try:
+        for merged in (False, True):
+            ops.HEAD_BWD_MERGED = merged
+            for p in p0 + p1:
+                p.grad = None
+            h.grad = None
+            out = ops.HeadPairFn.apply(meta, heads[1].meta(width), len(p0), side, h, *p0, *p1)
+            cot = torch.randn(out.shape, generator=torch.Generator().manual_seed(5)).cuda()
+            (out * cot).sum().backward()
+            torch.cuda.synchronize()
+            res[merged] = [p.grad.clone() for p in p0 + p1] + [h.grad.clone()]
+    finally:
+        ops.HEAD_BWD_MERGED = prev
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("dim", [2, 1])
 def test_dedup_bag_matches_full_bag(dim):
     """A with-replacement bag run once per distinct snapshot (multiplicity weights in the bag
