@@ -150,6 +150,12 @@ int blindno_mix_wgrad(const float* X, const float* G, float* dWt, float* partial
  * (complex); the caller reduces them (blindno_reduce_partials(_multi), 2 m2 K1 Ci Co Gw floats). */
 int blindno_mix_wgrad_part(const float* X, const float* G, float* partial, int nsplit, int Gw,
                            int Bn, int Ci, int Co, int K1, int m2, blindno_stream_t stream);
+/* Several blindno_mix_wgrad_g / _part launches in one (the deferred spectral weight gradients
+ * of a backward pass: the heads' layers and the encoder's; bit-identical results): job q reads
+ * X[q], G[q] and writes out[q] -- dWt (Gw, m2, K1, Ci, Co) when nsplit == 1, else the
+ * nsplit x Gw partials for the caller to reduce; shp[7 q ..] = (Bn, Ci, Co, K1, m2, nsplit, Gw). */
+int blindno_mix_wgrad_multi(const void* const* X, const void* const* G, void* const* out,
+                            const int* shp, int njobs, blindno_stream_t stream);
 
 /* 1D mode mix (compl_mul1d + DC halving, 1d_FPE/FNOModules.py:43-58).  At (Bn,m,C,1).
  * dir 0 (forward):  Xs = At with X[.,0] *= 0.5 (saved); Z[n][0][k][o] = c_k/P2 sum_i Xs W.
@@ -344,6 +350,13 @@ int blindno_reduce_partials(const float* partial, float* out, int nchunk, int np
 int blindno_reduce_partials_multi(const void* const* partials, void* const* outs,
                                   const int* nchunks, const int* nps, int nseg,
                                   blindno_stream_t stream);
+/* The same with pieces: segment i stores only parameters [e0s[i], e1s[i]) of its reduction, at
+ * outs[i][p - e0s[i]] (each summed exactly as in the whole reduction), so the parameter
+ * gradients of one reduction can land straight in an optimizer's flat gradient buffer
+ * (blindno.ops._Deferred.redirect).  e0s / e1s NULL: whole reductions. */
+int blindno_reduce_partials_pieces(const void* const* partials, void* const* outs,
+                                   const int* nchunks, const int* nps, const int* e0s,
+                                   const int* e1s, int nseg, blindno_stream_t stream);
 
 /* Pack reference-layout 2D weights (Ci,Co,m1,m2,2) x2 into Wt (m2,K1,Ci,Co) complex. */
 int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, int Ci, int Co, int m1,
@@ -436,6 +449,11 @@ int blindno_mse_finish(const float* partial, int nblk, int64_t n, float* loss,
  * launch instead of a separate add); acc may be NULL. */
 int blindno_mse_finish_acc(const float* partial, int nblk, int64_t n, float* loss, float* acc,
                            blindno_stream_t stream);
+/* blindno_mse (no gradient) + blindno_mse_finish_acc in ONE launch (bit-identical): the
+ * workgroup that finishes last sums the partials.  counter: one unsigned in device memory,
+ * zero before the first call; every call leaves it zero again. */
+int blindno_mse_fwd(const float* p, const float* t, float* partial, int64_t n, int nblk,
+                    float* loss, float* acc, unsigned* counter, blindno_stream_t stream);
 
 /* Per-row sums of squares in fp64 for relative-L2 metrics (2d_FPE/train_fno.py:160-163,
  * eval_fno.py:124-128, 2d_Non_conservative_FPE/compute_time_error.py:321-333).

@@ -44,6 +44,7 @@ SIGNATURES = {
     "blindno_rowidft_bwd_zc_bag": "pppp" + "i" + "pppppppp" + "iiiiiiiii" + "s",
     "blindno_mix_wgrad": "ppppiiiiiis",
     "blindno_mix_wgrad_part": "pppiiiiiiis",
+    "blindno_mix_wgrad_multi": "ppppis",
     "blindno_mix1d": "ppppiiiiiis",
     "blindno_rowidft_epi": "ppppppiiiiiis",
     "blindno_rowidft_epi_crop": "pppppp" + "iiiiiiii" + "s",
@@ -63,6 +64,7 @@ SIGNATURES = {
     "blindno_mse": "pppplips",
     "blindno_mse_finish": "pilps",
     "blindno_mse_finish_acc": "pilpps",
+    "blindno_mse_fwd": "ppplippps",
     "blindno_rowsq": "pppiiiiiis",
     "blindno_adam": "pppplffffffs",
     "blindno_gpe_solve": "ppppddiiipppiiis",
@@ -100,6 +102,7 @@ SIGNATURES = {
     "blindno_gather_flat": "pppips",
     "blindno_gather_batch": "ppppipis",
     "blindno_reduce_partials_multi": "ppppis",
+    "blindno_reduce_partials_pieces": "ppppppis",
     "blindno_unpack_w2d_multi": "ppppis",
     "blindno_pack_w2d_multi": "ppppis",
     "blindno_fp_propagate": "pppiiiiiids",

@@ -226,30 +226,94 @@ def _empty(*shape, like):
     return torch.empty(*shape, dtype=F32, device=like.device)
 
 
-# Deferred weight-gradient finalisation.  Inside ``deferred_reductions()`` the partial-sum
-# reductions and the spectral-weight unpacks of a backward pass are only recorded; the returned
-# gradient tensors are filled by two batched launches (blindno_reduce_partials_multi,
-# blindno_unpack_w2d_multi) when the context exits -- 10 + 5 small latency-bound launches per
-# config-C step become 2, with bit-identical results.  The recorded sources stay referenced
-# until the flush is enqueued, so the allocator cannot hand their memory to later kernels.
-# Only for callers that read no returned gradient before the exit (GraphedBagStep: the
-# gradients are consumed by the flat gather after backward, and are None before it).
+# Deferred weight-gradient finalisation.  Inside ``deferred_reductions()`` the spectral weight
+# gradients (the mix GEMMs over the samples), the partial-sum reductions and the spectral-weight
+# unpacks of a backward pass are only recorded; the returned gradient tensors are filled by
+# three batched launches (blindno_mix_wgrad_multi, blindno_reduce_partials_pieces,
+# blindno_unpack_w2d_multi) when the context exits -- 5 + 10 + 5 small latency-bound launches
+# per config-C step become 3, with bit-identical results.  ``redirect`` (before the exit) makes
+# those launches store parameter gradients straight into an optimizer's flat gradient buffer,
+# so no gather copy follows.  The recorded sources stay referenced until the flush is enqueued,
+# so the allocator cannot hand their memory to later kernels.  Only for callers that read no
+# returned gradient before the exit (GraphedBagStep: the gradients are consumed by the
+# optimizer after backward, and are None before it).
 _DEFER = None
 
 
 class _Deferred:
     def __init__(self):
-        self.red = []      # (partial, out, nchunk, np)
-        self.unp = []      # (dWt slice, dw1, dw2, (Ci, Co, m1, m2, P1), base of dw1 / dw2)
+        self.mix = []      # (X, G, out, (Bn, Ci, Co, K1, m2, nsplit, Gw)): spectral weight gradients
+        self.red = []      # [partial, out, nchunk, np, pieces]; pieces: [(e0, e1, dst)] (redirect)
+        self.unp = []      # [dWt slice, dw1, dw2, (Ci, Co, m1, m2, P1), base of dw1 / dw2]
+
+    def redirect(self, pairs):
+        """Have the flushed kernels store gradients straight into their final buffers: for
+        every (param, dst) pair -- dst a float32 tensor of the parameter's real size, e.g. a
+        view of an optimizer's flat gradient buffer -- whose ``.grad`` is one of the recorded
+        unpack outputs or a slice of a recorded reduction's output, that gradient is written
+        at dst instead (a piece of the reduction: the same summation order, bit-identical) and
+        ``.grad`` is re-pointed to dst.  Called after backward, before the flush.  Returns the
+        redirected parameters."""
+        done = []
+        for p, dst in pairs:
+            g = p.grad
+            if g is None:
+                continue
+            gr = torch.view_as_real(g) if g.is_complex() else g
+            if gr.dtype != F32 or not gr.is_contiguous() or dst.numel() != gr.numel():
+                continue
+            gp, n = gr.data_ptr(), gr.numel()
+            hit = False
+            for u in self.unp:
+                for k in (1, 2):
+                    if u[k].data_ptr() == gp and u[k].numel() == n:
+                        u[k] = dst.view(u[k].shape)
+                        hit = True
+                        break
+                if hit:
+                    break
+            if not hit:
+                for r in self.red:
+                    op, on = r[1].data_ptr(), r[1].numel()
+                    if op <= gp and gp + 4 * n <= op + 4 * on and (gp - op) % 4 == 0:
+                        e0 = (gp - op) // 4
+                        if all(e1 <= e0 or e0 + n <= a for a, e1, _ in r[4]):
+                            r[4].append((e0, e0 + n, dst))
+                            hit = True
+                        break
+            if hit:
+                v = dst.view(gr.shape)
+                p.grad = torch.view_as_complex(v) if g.is_complex() else v
+                done.append(p)
+        return done
 
     def flush(self):
+        if self.mix:
+            n = len(self.mix)
+            xs = (ctypes.c_void_p * n)(*[m[0].data_ptr() for m in self.mix])
+            gs = (ctypes.c_void_p * n)(*[m[1].data_ptr() for m in self.mix])
+            os_ = (ctypes.c_void_p * n)(*[m[2].data_ptr() for m in self.mix])
+            shp = (ctypes.c_int * (7 * n))(*[v for m in self.mix for v in m[3]])
+            call("blindno_mix_wgrad_multi", xs, gs, os_, shp, n, stream_ptr())
         if self.red:
-            n = len(self.red)
-            srcs = (ctypes.c_void_p * n)(*[r[0].data_ptr() for r in self.red])
-            outs = (ctypes.c_void_p * n)(*[r[1].data_ptr() for r in self.red])
-            ncs = (ctypes.c_int * n)(*[r[2] for r in self.red])
-            nps = (ctypes.c_int * n)(*[r[3] for r in self.red])
-            call("blindno_reduce_partials_multi", srcs, outs, ncs, nps, n, stream_ptr())
+            segs = []          # (partial, dst address, nchunk, np, e0, e1)
+            for partial, out, nchunk, np_, pieces in self.red:
+                pos = 0
+                for e0, e1, dst in sorted(pieces, key=lambda t: t[0]):
+                    if e0 > pos:
+                        segs.append((partial, out.data_ptr() + 4 * pos, nchunk, np_, pos, e0))
+                    segs.append((partial, dst.data_ptr(), nchunk, np_, e0, e1))
+                    pos = e1
+                if pos < np_:
+                    segs.append((partial, out.data_ptr() + 4 * pos, nchunk, np_, pos, np_))
+            n = len(segs)
+            srcs = (ctypes.c_void_p * n)(*[t[0].data_ptr() for t in segs])
+            outs = (ctypes.c_void_p * n)(*[t[1] for t in segs])
+            ncs = (ctypes.c_int * n)(*[t[2] for t in segs])
+            nps = (ctypes.c_int * n)(*[t[3] for t in segs])
+            e0s = (ctypes.c_int * n)(*[t[4] for t in segs])
+            e1s = (ctypes.c_int * n)(*[t[5] for t in segs])
+            call("blindno_reduce_partials_pieces", srcs, outs, ncs, nps, e0s, e1s, n, stream_ptr())
         if self.unp:
             n = len(self.unp)
             srcs = (ctypes.c_void_p * n)(*[u[0].data_ptr() for u in self.unp])
@@ -257,7 +321,7 @@ class _Deferred:
             d2 = (ctypes.c_void_p * n)(*[u[2].data_ptr() for u in self.unp])
             shp = (ctypes.c_int * (5 * n))(*[v for u in self.unp for v in u[3]])
             call("blindno_unpack_w2d_multi", srcs, d1, d2, shp, n, stream_ptr())
-        self.red, self.unp = [], []
+        self.mix, self.red, self.unp = [], [], []
 
 
 @contextlib.contextmanager
@@ -265,7 +329,7 @@ def deferred_reductions():
     global _DEFER
     prev, _DEFER = _DEFER, _Deferred()
     try:
-        yield
+        yield _DEFER
         _DEFER.flush()
     finally:
         _DEFER = prev
@@ -286,7 +350,7 @@ def immediate_reductions():
 def reduce_partials(partial: torch.Tensor, nchunk: int, np_: int) -> torch.Tensor:
     out = _empty(np_, like=partial)
     if _DEFER is not None:
-        _DEFER.red.append((partial, out, int(nchunk), int(np_)))
+        _DEFER.red.append([partial, out, int(nchunk), int(np_), []])
         return out
     call("blindno_reduce_partials", ptr(partial), ptr(out), nchunk, np_, stream_ptr())
     return out
@@ -301,7 +365,7 @@ def unpack_w2d(dWt: torch.Tensor, like: torch.Tensor, P1: int):
     Ci, Co, m1, m2 = like.shape[:4]
     if _DEFER is not None:
         base = torch.empty((2,) + tuple(like.shape), dtype=like.dtype, device=like.device)
-        _DEFER.unp.append((dWt, base[0], base[1], (Ci, Co, m1, m2, P1), base))
+        _DEFER.unp.append([dWt, base[0], base[1], (Ci, Co, m1, m2, P1), base])
         return base[0], base[1]
     # two separate tensors (torch custom ops may not return aliasing outputs)
     dw1, dw2 = torch.empty_like(like), torch.empty_like(like)
@@ -344,12 +408,16 @@ def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2, deferrable=False):
     reader of dWt is itself deferred (the 2D unpack), so under deferred_reductions() the
     sample-split reduction may join the batched finalisation."""
     ns = query("blindno_mix_wgrad_nsplit", Bn, Ci, Co, K1, m2)
-    if _DEFER is not None and deferrable and ns > 1:
-        # partials now, their reduction with the batched finalisation (before the unpack)
-        part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X)
-        call("blindno_mix_wgrad_part", ptr(X), ptr(G), ptr(part), ns, 1, Bn, Ci, Co, K1, m2,
-             stream_ptr())
-        return reduce_partials(part, ns, m2 * K1 * Ci * Co * 2).view(m2, K1, Ci, Co, 2)
+    if _DEFER is not None and deferrable:
+        # the mix gradient itself joins the batched finalisation (one launch for every layer's,
+        # before the reductions and the unpack)
+        if ns > 1:
+            part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X)
+            _DEFER.mix.append((X, G, part, (Bn, Ci, Co, K1, m2, ns, 1)))
+            return reduce_partials(part, ns, m2 * K1 * Ci * Co * 2).view(m2, K1, Ci, Co, 2)
+        dWt = _empty(m2, K1, Ci, Co, 2, like=X)
+        _DEFER.mix.append((X, G, dWt, (Bn, Ci, Co, K1, m2, 1, 1)))
+        return dWt
     dWt = _empty(m2, K1, Ci, Co, 2, like=X)
     part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X) if ns > 1 else None
     call("blindno_mix_wgrad", ptr(X), ptr(G), ptr(dWt), ptr(part) if part is not None else None, ns,
@@ -908,10 +976,18 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         for g in range(G):
             grads[g][o], grads[g][o + 1] = dws[2 * g], dws[2 * g + 1]
 
+    # under deferred_reductions() the mix gradients join the batched finalisation instead
+    defer_mix = _DEFER is not None
+
     def mix_launch(kk, Xk, Gk):
         dWt, part = mix_buffers()
-        call("blindno_mix_wgrad_g", ptr(Xk), ptr(Gk), ptr(dWt), ptr(part) if part is not None else None,
-             ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
+        if defer_mix:
+            _DEFER.mix.append((Xk, Gk, part if ns > 1 else dWt, (Bn, C, C, K1, meta.m2, ns, G)))
+            if ns > 1:
+                _DEFER.red.append([part, dWt, ns, dWt.numel(), []])
+        else:
+            call("blindno_mix_wgrad_g", ptr(Xk), ptr(Gk), ptr(dWt), ptr(part) if part is not None else None,
+                 ns, G, Bn, C, C, K1, meta.m2, stream_ptr())
         mix_grads(kk, dWt)
 
     for k in reversed(range(n)):
@@ -937,12 +1013,13 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         GZ = _empty(Bn, P1, meta.m2, C, 2, like=inp)
         call("blindno_colpass_g", ptr(At), ptr(Wt), ptr(Gs), ptr(Y), ptr(GZ), ptr(FB), ptr(GB), G,
              Wt[0].numel(), Bn, C, C, P1, meta.m1, meta.m2, P2, _mixdir(1), stream_ptr())
-        if merged:
+        if merged and not defer_mix:
             pending = (k, Xs[k], Gs)
         else:
             mix_launch(k, Xs[k], Gs)
-            call("blindno_conv_wgrad_g", ptr(dz), ptr(src), ptr(pc), nch, G, Bn, C, P1, P2, act,
-                 stream_ptr())
+            if not merged:
+                call("blindno_conv_wgrad_g", ptr(dz), ptr(src), ptr(pc), nch, G, Bn, C, P1, P2, act,
+                     stream_ptr())
         gc = reduce_partials(pc, nch, G * np_c).view(G, np_c)
         for g in range(G):
             grads[g][off + 2] = gc[g, :C * C].view_as(prms[g][off + 2])
@@ -1549,6 +1626,21 @@ def _mse_blocks(n):
     return max(1, min(1024, (n + 1023) // 1024))
 
 
+_MSE_COUNTER = {}
+
+
+def _mse_counter(dev):
+    """The fused MSE forward's completion counter (one per device, zero between launches;
+    created outside stream capture by the eager warm-up, so graphs reference ordinary memory)."""
+    key = str(dev)
+    c = _MSE_COUNTER.get(key)
+    if c is None:
+        c = torch.zeros(1, dtype=torch.int32, device=dev)
+        if not torch.cuda.is_current_stream_capturing():
+            _MSE_COUNTER[key] = c
+    return c
+
+
 class MSEFn(torch.autograd.Function):
     """nn.MSELoss() (mean reduction) with a fused gradient kernel."""
 
@@ -1559,11 +1651,11 @@ class MSEFn(torch.autograd.Function):
         n = pred.numel()
         nblk = _mse_blocks(n)
         partial = _empty(nblk, like=pred)
-        call("blindno_mse", ptr(pred), ptr(target), ptr(partial), None, n, nblk, None,
-             stream_ptr())
         loss = _empty((), like=pred)
-        # acc (float32 scalar, optional): the loss is also added to it in the same launch
-        call("blindno_mse_finish_acc", ptr(partial), nblk, n, ptr(loss), ptr(acc), stream_ptr())
+        # acc (float32 scalar, optional): the loss is also added to it in the same launch; the
+        # partials and their sum in one launch (the last workgroup to finish sums them)
+        call("blindno_mse_fwd", ptr(pred), ptr(target), ptr(partial), n, nblk, ptr(loss), ptr(acc),
+             ptr(_mse_counter(pred.device)), stream_ptr())
         ctx.save_for_backward(pred, target)
         return loss
 

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import time
 from typing import Iterable, List, Optional
 
@@ -25,6 +26,11 @@ import torch.distributed as dist
 
 from . import ops
 from ._lib import call, ptr, stream_ptr
+
+
+# the graphed step's deferred finalisation writes the gradients straight into the flat buffer
+# (BLINDNO_REDIRECT=0: into their own tensors, then one gather copy)
+REDIRECT_GRADS = os.environ.get("BLINDNO_REDIRECT", "1") != "0"
 
 
 def _real(t: torch.Tensor) -> torch.Tensor:
@@ -80,12 +86,19 @@ class FlatAdam:
         zero)."""
         sel = range(len(self.params)) if subset is None else \
             [i for i, p in enumerate(self.params) if any(p is q for q in subset)]
-        gs = []
+        gs, keep = [], []
         for i in sel:
             p = self.params[i]
             if p.grad is None:
                 raise RuntimeError("FlatAdam: a trained parameter received no gradient")
-            gs.append(_real(p.grad).reshape(-1))
+            g = _real(p.grad).reshape(-1)
+            if g.data_ptr() == self._gviews[i].data_ptr():
+                continue                   # already in place (ops._Deferred.redirect)
+            gs.append(g)
+            keep.append(i)
+        sel = keep
+        if not gs:
+            return self.grad
         if self.grad.is_cuda and all(g.is_contiguous() for g in gs):
             # one blindno_gather_flat launch (segments as kernel arguments; graph-capturable)
             srcs = (ctypes.c_void_p * len(gs))(*[g.data_ptr() for g in gs])
@@ -95,6 +108,13 @@ class FlatAdam:
         else:
             torch._foreach_copy_([self._gviews[i] for i in sel], gs)
         return self.grad
+
+    def grad_targets(self, subset=None):
+        """(parameter, its view of the flat gradient buffer) pairs, for the deferred
+        finalisation to write the gradients in place (ops._Deferred.redirect)."""
+        sel = range(len(self.params)) if subset is None else \
+            [i for i, p in enumerate(self.params) if any(p is q for q in subset)]
+        return [(self.params[i], self._gviews[i]) for i in sel]
 
     def span(self, subset):
         """[lo, hi) of the flat buffer holding ``subset`` (must be contiguous in it)."""
@@ -249,8 +269,10 @@ class GraphedBagStep:
         bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
         out = self.model(self.x, self.grid, bag_idx=bag)
         loss, add = self._loss(out, accumulate)
-        with ops.deferred_reductions():               # one batched gradient finalisation
+        with ops.deferred_reductions() as fin:        # one batched gradient finalisation,
             loss.backward(self._one)
+            if REDIRECT_GRADS:                        # storing into the flat buffer
+                fin.redirect(self.opt.grad_targets())
         self.opt.gather_grads()
         if add:
             self.loss_acc.add_(loss.detach())
@@ -264,8 +286,10 @@ class GraphedBagStep:
         hd = h.detach().requires_grad_(True)
         out = self.model.forward_heads(hd)
         loss, add = self._loss(out, accumulate)
-        with ops.deferred_reductions():
+        with ops.deferred_reductions() as fin:
             loss.backward(self._one)
+            if REDIRECT_GRADS:
+                fin.redirect(self.opt.grad_targets(self.head_params))
         self.opt.gather_grads(self.head_params)
         if add:
             self.loss_acc.add_(loss.detach())
@@ -273,8 +297,10 @@ class GraphedBagStep:
 
     def _body_b(self, h, hd):
         """Graph B: the encoder's backward from the heads' input gradient, and its gather."""
-        with ops.deferred_reductions():
+        with ops.deferred_reductions() as fin:
             h.backward(hd.grad)
+            if REDIRECT_GRADS:
+                fin.redirect(self.opt.grad_targets(self.enc_params))
         self.opt.gather_grads(self.enc_params)
 
     def _buffers(self):

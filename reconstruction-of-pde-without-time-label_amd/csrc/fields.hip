@@ -177,10 +177,12 @@ __global__ __launch_bounds__(kBlock) void lift_fwd_wide_kernel(
   }
 }
 
+// (workgroup bx of gx explicit: lift_bwd_both_kernel hosts it beside the weight gradient)
 template <int CIN, int CM>
-__global__ __launch_bounds__(kBlock) void lift_bwd_in_wide_kernel(
+__device__ __forceinline__ void lift_bwd_in_wide_block(
     const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in, int Bn,
-    int N1, int N2, int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2) {
+    int N1, int N2, int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2, int bx,
+    int gx) {
   __shared__ float sw[kLiftMaxG][CM * CIN];
   for (int e = threadIdx.x; e < G * CM * CIN; e += blockDim.x) {
     const int g = e / (CM * CIN), q = e - g * (CM * CIN);
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_wide_kernel(
   __syncthreads();
   const unsigned S = (unsigned)(N1 * N2), HW = (unsigned)(P1 * P2);
   const unsigned total = (unsigned)Bn * S;
-  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+  for (unsigned idx = bx * kBlock + threadIdx.x; idx < total; idx += gx * kBlock) {
     const unsigned n = dS.div(idx), s = idx - n * S;
     const unsigned h = dN2.div(s), w = s - h * (unsigned)N2;
     float acc[CIN];
@@ -211,6 +213,14 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_wide_kernel(
 #pragma unroll
     for (int q = 0; q < CIN / 4; ++q) op[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
   }
+}
+
+template <int CIN, int CM>
+__global__ __launch_bounds__(kBlock) void lift_bwd_in_wide_kernel(
+    const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in, int Bn,
+    int N1, int N2, int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2) {
+  lift_bwd_in_wide_block<CIN, CM>(dx0, w0, d_in, Bn, N1, N2, C, P1, P2, G, wgs, dS, dN2, blockIdx.x,
+                                  gridDim.x);
 }
 
 // Tiled outer-product reductions: partial[block][a*Cb + b] = sum_p A[a][p] B[b][p] and
@@ -355,25 +365,25 @@ __global__ __launch_bounds__(kBlock) void conv_wgrad_kernel(const float* __restr
 // (c16, g4) feeds float4 dx0[c = c16][h][w0 + 4 g4 ..] (A) and in[p][j = 16 jt + c16] at
 // the same four points (B; column Cin is 1.0).  Waves add their blocks in wave order; the
 // partial layout is lift_bwd_w_kernel's: partial[blockIdx.x][g][C Cin + C].
+// (workgroup (bx, grp) of (gx, gy) explicit: lift_bwd_both_kernel hosts it)
 template <int JT>
-__global__ __launch_bounds__(256) void lift_bwd_w_mfma_kernel(const float* __restrict__ dx0,
-                                                              const float* __restrict__ in,
-                                                              float* __restrict__ partial, int Bn,
-                                                              int N1, int N2, int Cin, int C,
-                                                              int P1, int P2) {
+__device__ __forceinline__ void lift_bwd_w_mfma_block(const float* __restrict__ dx0,
+                                                      const float* __restrict__ in,
+                                                      float* __restrict__ partial, int Bn, int N1,
+                                                      int N2, int Cin, int C, int P1, int P2,
+                                                      int bx, int gx, int grp, int gy) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   __shared__ f32x4 sacc[4][JT][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int c16 = lane & 15, g4 = lane >> 4;
-  const int grp = blockIdx.y;
   dx0 += (int64_t)grp * Bn * C * P1 * P2;
   const int cpr = N2 >> 4;                         // 16-point chunks per grid row
   const int64_t nch = (int64_t)Bn * N1 * cpr;
   f32x4 acc[JT];
 #pragma unroll
   for (int t = 0; t < JT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int64_t ch = (int64_t)blockIdx.x * 4 + wave; ch < nch; ch += (int64_t)gridDim.x * 4) {
+  for (int64_t ch = (int64_t)bx * 4 + wave; ch < nch; ch += (int64_t)gx * 4) {
     const int64_t r = ch / cpr;                    // grid row (n, h)
     const int w0 = (int)(ch - r * cpr) * 16 + 4 * g4;
     const int n = (int)(r / N1), h = (int)(r - (r / N1) * N1);
@@ -398,13 +408,41 @@ __global__ __launch_bounds__(256) void lift_bwd_w_mfma_kernel(const float* __res
   __syncthreads();
   // D[c = 4 g4 + r][j = 16 t + c16]
   const int np = C * Cin + C;
-  float* pp = partial + ((int64_t)blockIdx.x * gridDim.y + grp) * np;
-  for (int e = threadIdx.x; e < np; e += blockDim.x) {
+  float* pp = partial + ((int64_t)bx * gy + grp) * np;
+  for (int e = threadIdx.x; e < np; e += 256) {
     const int c = e < C * Cin ? e / Cin : e - C * Cin;
     const int j = e < C * Cin ? e - (e / Cin) * Cin : Cin;
     const int t = j >> 4, ln = 16 * (c >> 2) + (j & 15), rr = c & 3;
     pp[e] = ((sacc[0][t][ln][rr] + sacc[1][t][ln][rr]) + sacc[2][t][ln][rr]) + sacc[3][t][ln][rr];
   }
+}
+
+template <int JT>
+__global__ __launch_bounds__(256) void lift_bwd_w_mfma_kernel(const float* __restrict__ dx0,
+                                                              const float* __restrict__ in,
+                                                              float* __restrict__ partial, int Bn,
+                                                              int N1, int N2, int Cin, int C,
+                                                              int P1, int P2) {
+  lift_bwd_w_mfma_block<JT>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2, blockIdx.x, gridDim.x,
+                            blockIdx.y, gridDim.y);
+}
+
+// The heads' lift backward in one launch: its input gradient (workgroups [0, nbi)) and its
+// weight / bias gradient partials (the rest, nchunk x G) read the same dx0 and are independent;
+// each part keeps the grid of its own launch (bit-identical results).
+template <int JT>
+__global__ __launch_bounds__(256) void lift_bwd_both_kernel(
+    const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in,
+    const float* __restrict__ in, float* __restrict__ partial, int Bn, int N1, int N2, int Cin,
+    int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2, int nbi, int nchunk) {
+  const int b = blockIdx.x;
+  if (b < nbi) {
+    lift_bwd_in_wide_block<12, 16>(dx0, w0, d_in, Bn, N1, N2, C, P1, P2, G, wgs, dS, dN2, b, nbi);
+    return;
+  }
+  const int r = b - nbi;
+  lift_bwd_w_mfma_block<JT>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2, r % nchunk, nchunk,
+                            r / nchunk, G);
 }
 
 template <int ACT>
@@ -421,9 +459,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_kernel(const float* __res
 // slice t / PB); every slice sums its chunks with four independent accumulators in a fixed
 // order, then the slices are added in slice order.  Small parameter counts (the lift's 16,
 // a conv's 20) therefore still use all 1024 threads instead of 16 lanes.
+// (e0, e1): only parameters p in [e0, e1) are stored, at out[p - e0] -- a piece of a reduction
+// whose parameters land in different buffers (blindno_reduce_partials_pieces)
 __device__ __forceinline__ void reduce_partials_block(const float* __restrict__ partial,
                                                       float* __restrict__ out, int nchunk, int np,
-                                                      int PB, int blk, float* red) {
+                                                      int PB, int blk, float* red, int e0 = 0,
+                                                      int e1 = INT32_MAX) {
   const int S = 1024 / PB;
   const int t = threadIdx.x;
   const int pl = t % PB, sl = t / PB;
@@ -441,10 +482,10 @@ __device__ __forceinline__ void reduce_partials_block(const float* __restrict__ 
   }
   red[t] = (a0 + a1) + (a2 + a3);
   __syncthreads();
-  if (sl == 0 && p < np) {
+  if (sl == 0 && p < np && p >= e0 && p < e1) {
     float v = red[pl];
     for (int k = 1; k < S; ++k) v += red[k * PB + pl];
-    out[p] = v;
+    out[p - e0] = v;
   }
 }
 
@@ -458,12 +499,15 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __re
 // Several reductions in one launch (the deferred weight-gradient reductions of one backward
 // pass, blindno.ops.deferred_reductions): segment i owns workgroups [cum[i], cum[i+1]), each
 // reduced exactly as by reduce_partials_kernel, so the results are bit-identical to separate
-// launches.  Segments are passed by value (a graph capture bakes them in).
-constexpr int kRedSegs = 32;
+// launches.  A segment may be a piece of a reduction: its workgroups blk0[i] .. of that
+// reduction's block grid (same PB, so the same summation order), storing only parameters
+// [e0, e1) at out[p - e0] (the gradients written straight into an optimizer's flat buffer).
+// Segments are passed by value (a graph capture bakes them in).
+constexpr int kRedSegs = 48;
 struct ReduceSegs {
   const float* src[kRedSegs];
   float* out[kRedSegs];
-  int nchunk[kRedSegs], np[kRedSegs], pb[kRedSegs];
+  int nchunk[kRedSegs], np[kRedSegs], pb[kRedSegs], blk0[kRedSegs], e0[kRedSegs], e1[kRedSegs];
   int cum[kRedSegs + 1];
   int nseg;
 };
@@ -474,7 +518,7 @@ __global__ __launch_bounds__(1024) void reduce_partials_multi_kernel(ReduceSegs 
   int sg = 0;
   while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;    // uniform scan
   reduce_partials_block(segs.src[sg], segs.out[sg], segs.nchunk[sg], segs.np[sg], segs.pb[sg],
-                        b - segs.cum[sg], red);
+                        segs.blk0[sg] + b - segs.cum[sg], red, segs.e0[sg], segs.e1[sg]);
 }
 
 // ---------------------------------------------------------------- projection MLP
@@ -749,10 +793,9 @@ __global__ __launch_bounds__(kBlock) void mse_kernel(const float* __restrict__ p
 
 // loss = (sum of the nblk partials, fixed order) / n: the scalar of nn.MSELoss's forward in one
 // single-workgroup launch (instead of a torch sum and a torch division)
-__global__ __launch_bounds__(kBlock) void mse_finish_kernel(const float* __restrict__ partial,
-                                                            int nblk, int64_t n,
-                                                            float* __restrict__ loss,
-                                                            float* __restrict__ lsum) {
+__device__ __forceinline__ void mse_finish_block(const float* __restrict__ partial, int nblk,
+                                                 int64_t n, float* __restrict__ loss,
+                                                 float* __restrict__ lsum) {
   __shared__ float red[kBlock];
   float acc = 0.f;
   for (int i = threadIdx.x; i < nblk; i += kBlock) acc += partial[i];
@@ -766,6 +809,51 @@ __global__ __launch_bounds__(kBlock) void mse_finish_kernel(const float* __restr
     const float l = red[0] / (float)n;
     loss[0] = l;
     if (lsum) lsum[0] += l;                      // running loss sum of a training loop
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void mse_finish_kernel(const float* __restrict__ partial,
+                                                            int nblk, int64_t n,
+                                                            float* __restrict__ loss,
+                                                            float* __restrict__ lsum) {
+  mse_finish_block(partial, nblk, n, loss, lsum);
+}
+
+// The forward's partials and the finish in ONE launch: every workgroup stores its partial as
+// mse_kernel does, then counts itself done on a device counter (release fence, atomic add);
+// the workgroup that counts last (acquire fence) sums the partials exactly as
+// mse_finish_kernel, writes the loss and resets the counter for the next launch (graph replays
+// reuse it).  Bit-identical to mse_kernel + mse_finish_kernel.
+__global__ __launch_bounds__(kBlock) void mse_fwd_fused_kernel(const float* __restrict__ p,
+                                                               const float* __restrict__ t,
+                                                               float* __restrict__ partial,
+                                                               int64_t n, float* __restrict__ loss,
+                                                               float* __restrict__ lsum,
+                                                               unsigned* __restrict__ counter) {
+  __shared__ float red[kBlock];
+  __shared__ unsigned last;
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float d = p[i] - t[i];
+    acc = fmaf(d, d, acc);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kBlock / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = red[0];
+    __threadfence();
+    last = atomicAdd(counter, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (last) {
+    __threadfence();
+    mse_finish_block(partial, (int)gridDim.x, n, loss, lsum);
+    if (threadIdx.x == 0) counter[0] = 0u;
   }
 }
 
@@ -875,6 +963,10 @@ BLINDNO_API int blindno_lift_bwd_nchunk(int Bn, int N1, int N2) {
   return nt < 1024 ? nt : 1024;
 }
 
+// the heads' lift input and weight gradients in one launch (0: two launches, for A/B)
+#ifndef LIFT_BWD_BOTH
+#define LIFT_BWD_BOTH 1
+#endif
 BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const float* w0,
                                    float* d_in, float* partial, int nchunk, int G, int64_t wgs,
                                    int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
@@ -882,10 +974,30 @@ BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const floa
   if (G < 1 || Bn % G) return (int)hipErrorInvalidValue;
   const int Bg = Bn / G;
   hipStream_t st = (hipStream_t)stream;
+  const bool wide_in = d_in && Cin == 12 && C <= kLiftMaxC && G <= kLiftMaxG &&
+                       (int64_t)Bn * C * P1 * P2 < INT32_MAX &&
+                       (int64_t)Bg * N1 * N2 * Cin < INT32_MAX && (((uintptr_t)d_in) & 15) == 0;
+  const bool mf = C >= 5 && C <= 16 && Cin + 1 <= 32 && N2 % 16 == 0 && P2 % 4 == 0 &&
+                  (((uintptr_t)dx0) & 15) == 0;
+  if (wide_in && partial && mf && LIFT_BWD_BOTH) {
+    if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)
+      return (int)hipErrorInvalidValue;
+    const int nbi = grid_for((int64_t)Bg * N1 * N2, kBlock, 8192);
+    const int64_t nb = nbi + (int64_t)nchunk * G;
+    const FastDiv dS = FastDiv::make((unsigned)(N1 * N2)), dN2 = FastDiv::make((unsigned)N2);
+    if (Cin + 1 <= 16)
+      lift_bwd_both_kernel<1><<<(unsigned)nb, 256, 0, st>>>(dx0, w0, d_in, in, partial, Bg, N1, N2,
+                                                            Cin, C, P1, P2, G, G > 1 ? wgs : 0, dS,
+                                                            dN2, nbi, nchunk);
+    else
+      lift_bwd_both_kernel<2><<<(unsigned)nb, 256, 0, st>>>(dx0, w0, d_in, in, partial, Bg, N1, N2,
+                                                            Cin, C, P1, P2, G, G > 1 ? wgs : 0, dS,
+                                                            dN2, nbi, nchunk);
+    return (int)hipGetLastError();
+  }
   if (d_in) {
     const int64_t total = (int64_t)Bg * N1 * N2 * Cin;
-    if (Cin == 12 && C <= kLiftMaxC && G <= kLiftMaxG && (int64_t)Bn * C * P1 * P2 < INT32_MAX &&
-        total < INT32_MAX && (((uintptr_t)d_in) & 15) == 0) {
+    if (wide_in) {
       lift_bwd_in_wide_kernel<12, 16><<<grid_for((int64_t)Bg * N1 * N2, kBlock, 8192), kBlock, 0, st>>>(
           dx0, w0, d_in, Bg, N1, N2, C, P1, P2, G, G > 1 ? wgs : 0,
           FastDiv::make((unsigned)(N1 * N2)), FastDiv::make((unsigned)N2));
@@ -897,8 +1009,6 @@ BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const floa
   if (partial) {
     if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)
       return (int)hipErrorInvalidValue;
-    const bool mf = C >= 5 && C <= 16 && Cin + 1 <= 32 && N2 % 16 == 0 && P2 % 4 == 0 &&
-                    (((uintptr_t)dx0) & 15) == 0;
     if (mf) {
       if (Cin + 1 <= 16)
         lift_bwd_w_mfma_kernel<1><<<dim3(nchunk, G), 256, 0, st>>>(dx0, in, partial, Bg, N1, N2,
@@ -969,9 +1079,9 @@ BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nc
   return (int)hipGetLastError();
 }
 
-BLINDNO_API int blindno_reduce_partials_multi(const void* const* partials, void* const* outs,
-                                              const int* nchunks, const int* nps, int nseg,
-                                              void* stream) {
+BLINDNO_API int blindno_reduce_partials_pieces(const void* const* partials, void* const* outs,
+                                               const int* nchunks, const int* nps, const int* e0s,
+                                               const int* e1s, int nseg, void* stream) {
   if (nseg < 0) return (int)hipErrorInvalidValue;
   for (int s0 = 0; s0 < nseg; s0 += kRedSegs) {
     ReduceSegs segs{};
@@ -980,20 +1090,32 @@ BLINDNO_API int blindno_reduce_partials_multi(const void* const* partials, void*
     int blocks = 0;
     for (int i = 0; i < k; ++i) {
       const int nc = nchunks[s0 + i], np = nps[s0 + i];
-      if (nc < 1 || np < 1) return (int)hipErrorInvalidValue;
+      const int e0 = e0s ? e0s[s0 + i] : 0, e1 = e1s ? e1s[s0 + i] : np;
+      if (nc < 1 || np < 1 || e0 < 0 || e1 > np || e0 >= e1) return (int)hipErrorInvalidValue;
       segs.src[i] = (const float*)partials[s0 + i];
       segs.out[i] = (float*)outs[s0 + i];
       segs.nchunk[i] = nc;
       segs.np[i] = np;
-      segs.pb[i] = np < 64 ? np : 64;
+      const int pb = np < 64 ? np : 64;
+      segs.pb[i] = pb;
+      segs.blk0[i] = e0 / pb;
+      segs.e0[i] = e0;
+      segs.e1[i] = e1;
       segs.cum[i] = blocks;
-      blocks += cdiv(np, segs.pb[i]);
+      blocks += cdiv(e1, pb) - e0 / pb;
     }
     segs.cum[k] = blocks;
     if (blocks == 0) continue;
     reduce_partials_multi_kernel<<<blocks, 1024, 0, (hipStream_t)stream>>>(segs);
   }
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_reduce_partials_multi(const void* const* partials, void* const* outs,
+                                              const int* nchunks, const int* nps, int nseg,
+                                              void* stream) {
+  return blindno_reduce_partials_pieces(partials, outs, nchunks, nps, nullptr, nullptr, nseg,
+                                        stream);
 }
 
 BLINDNO_API int blindno_project_fwd_g(const float* z, const float* w1, const float* b1,
@@ -1124,6 +1246,16 @@ BLINDNO_API int blindno_mse_finish_acc(const float* partial, int nblk, int64_t n
                                        float* acc, void* stream) {
   if (nblk < 1 || n < 1) return (int)hipErrorInvalidValue;
   mse_finish_kernel<<<1, kBlock, 0, (hipStream_t)stream>>>(partial, nblk, n, loss, acc);
+  return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_mse_fwd(const float* p, const float* t, float* partial, int64_t n,
+                                int nblk, float* loss, float* acc, unsigned* counter,
+                                void* stream) {
+  if (n < 1 || nblk < 1 || !p || !t || !partial || !loss || !counter)
+    return (int)hipErrorInvalidValue;
+  mse_fwd_fused_kernel<<<nblk, kBlock, 0, (hipStream_t)stream>>>(p, t, partial, n, loss, acc,
+                                                                 counter);
   return (int)hipGetLastError();
 }
 

@@ -920,6 +920,26 @@ __global__ __launch_bounds__(256) void rowdft_wgrad_kernel(const float* __restri
                   (b / mw.gx) % mw.gy, b / (mw.gx * mw.gy), mw.gx, mw.gy, mw.gz);
 }
 
+// Several spectral weight gradients in one launch (the deferred ones of a backward pass,
+// blindno.ops.deferred_reductions: the heads' layers and the encoder's): job q owns workgroups
+// [cum[q], cum[q+1]) with the grid of its own blindno_mix_wgrad_g launch (bit-identical).
+constexpr int kMixJobs = 8;
+struct MixJobs {
+  MixWgradJob j[kMixJobs];
+  int cum[kMixJobs + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(kBlock) void mix_wgrad_multi_kernel(MixJobs jobs) {
+  const int b = blockIdx.x;
+  int q = 0;
+  while (q + 1 < jobs.n && jobs.cum[q + 1] <= b) ++q;             // uniform scan
+  const MixWgradJob& m = jobs.j[q];
+  const int r = b - jobs.cum[q];
+  mix_wgrad_block(m.X, m.Gs, m.out, m.Bn, m.Ci, m.Co, m.K1, m.m2, r % m.gx, (r / m.gx) % m.gy,
+                  r / (m.gx * m.gy), m.gx, m.gy, m.gz);
+}
+
 // ------------------------------------------------------------------------------ 1D mode mix
 // At[n][k][c] (P1 = 1).  Forward: Xs = h_k At (DC halved) ; Z[n][k][o] = c_k/P2 sum_i Xs W.
 // Backward: Xs = c_k/P2 At (= spectrum gradient) ; Z[n][k][i] = h_k sum_o conj(W) Xs.
@@ -1379,6 +1399,43 @@ BLINDNO_API int blindno_rowdft_wgrad_g(const float* dz, const float* src, float*
   e = (int)hipGetLastError();
   if (e || !Xs || mnsplit == 1) return e;
   return blindno_reduce_partials(mpartial, dWt, mnsplit, (int)(2 * total * G), stream);
+}
+
+// jobs q < njobs: X[q], G[q] -> out[q] (dWt when nsplit == 1, else the nsplit x Gw partials,
+// reduced by the caller); shp[7 q ..] = (Bn, Ci, Co, K1, m2, nsplit, Gw)
+BLINDNO_API int blindno_mix_wgrad_multi(const void* const* X, const void* const* G,
+                                        void* const* out, const int* shp, int njobs,
+                                        void* stream) {
+  if (njobs < 0) return (int)hipErrorInvalidValue;
+  for (int q0 = 0; q0 < njobs; q0 += kMixJobs) {
+    MixJobs jobs{};
+    const int k = njobs - q0 < kMixJobs ? njobs - q0 : kMixJobs;
+    jobs.n = k;
+    int64_t blocks = 0;
+    for (int i = 0; i < k; ++i) {
+      const int* sh = shp + 7 * (q0 + i);
+      const int Bn = sh[0], Ci = sh[1], Co = sh[2], K1 = sh[3], m2 = sh[4], ns = sh[5], Gw = sh[6];
+      const int64_t total = (int64_t)m2 * K1 * Ci * Co;
+      if (Bn < 1 || Ci < 1 || Co < 1 || K1 < 1 || m2 < 1 || ns < 1 || Gw < 1 || Bn % Gw ||
+          total >= INT32_MAX / 2 || !X[q0 + i] || !G[q0 + i] || !out[q0 + i])
+        return (int)hipErrorInvalidValue;
+      MixWgradJob& m = jobs.j[i];
+      m.X = (const float2*)X[q0 + i];
+      m.Gs = (const float2*)G[q0 + i];
+      m.out = (float2*)out[q0 + i];
+      m.Bn = Bn; m.Ci = Ci; m.Co = Co; m.K1 = K1; m.m2 = m2;
+      m.gx = (int)cdiv(total, kBlock);
+      m.gy = ns;
+      m.gz = Gw;
+      jobs.cum[i] = (int)blocks;
+      blocks += (int64_t)m.gx * ns * Gw;
+    }
+    if (blocks >= INT32_MAX) return (int)hipErrorInvalidValue;
+    jobs.cum[k] = (int)blocks;
+    if (blocks == 0) continue;
+    mix_wgrad_multi_kernel<<<(unsigned)blocks, kBlock, 0, (hipStream_t)stream>>>(jobs);
+  }
+  return (int)hipGetLastError();
 }
 
 BLINDNO_API int blindno_mix_wgrad_g(const float* X, const float* G, float* dWt, float* partial,
