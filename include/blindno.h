@@ -156,6 +156,13 @@ int blindno_mix_wgrad_part(const float* X, const float* G, float* partial, int n
  * nsplit x Gw partials for the caller to reduce; shp[7 q ..] = (Bn, Ci, Co, K1, m2, nsplit, Gw). */
 int blindno_mix_wgrad_multi(const void* const* X, const void* const* G, void* const* out,
                             const int* shp, int njobs, blindno_stream_t stream);
+/* ... with the unpack folded into the store: for job q with um1[q] > 0 (nsplit 1, K1 = 2 um1,
+ * Gw <= 4), dWt of group g is written straight into the reference layouts (Ci, Co, um1, m2) of
+ * the weights1 / weights2 gradients ud[8 q + 2 g], ud[8 q + 2 g + 1] (blindno_unpack_w2d's
+ * result; out[q] is then not written).  ud / um1 NULL: blindno_mix_wgrad_multi. */
+int blindno_mix_wgrad_multi_u(const void* const* X, const void* const* G, void* const* out,
+                              const int* shp, void* const* ud, const int* um1, int njobs,
+                              blindno_stream_t stream);
 
 /* 1D mode mix (compl_mul1d + DC halving, 1d_FPE/FNOModules.py:43-58).  At (Bn,m,C,1).
  * dir 0 (forward):  Xs = At with X[.,0] *= 0.5 (saved); Z[n][0][k][o] = c_k/P2 sum_i Xs W.
@@ -357,6 +364,14 @@ int blindno_reduce_partials_multi(const void* const* partials, void* const* outs
 int blindno_reduce_partials_pieces(const void* const* partials, void* const* outs,
                                    const int* nchunks, const int* nps, const int* e0s,
                                    const int* e1s, int nseg, blindno_stream_t stream);
+/* ... where a whole segment i with upks[i] = u >= 0 is a packed spectral weight gradient
+ * (m2, 2 m1, Ci, Co) complex stored unpacked into the weights1 / weights2 gradient layouts
+ * ud[2 u], ud[2 u + 1] with ushp[4 u ..] = (Ci, Co, m1, m2) (the unpack folded into the
+ * reduction; at most 8 per launch of 48 segments). */
+int blindno_reduce_partials_pieces_u(const void* const* partials, void* const* outs,
+                                     const int* nchunks, const int* nps, const int* e0s,
+                                     const int* e1s, const int* upks, void* const* ud,
+                                     const int* ushp, int nseg, blindno_stream_t stream);
 
 /* Pack reference-layout 2D weights (Ci,Co,m1,m2,2) x2 into Wt (m2,K1,Ci,Co) complex. */
 int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, int Ci, int Co, int m1,
@@ -535,6 +550,14 @@ int blindno_lift_fwd_g(const float* in, const float* w0, const float* b0, float*
 int blindno_lift_bwd_g(const float* dx0, const float* in, const float* w0, float* d_in,
                        float* partial, int nchunk, int G, int64_t wgs, int Bn, int N1, int N2,
                        int Cin, int C, int P1, int P2, blindno_stream_t stream);
+/* lift_bwd_g with, when Xs != NULL, the spectral weight gradient mix_wgrad_g(Xs, Gs) -> dWt of
+ * the heads' first layer (Ci = Co = C, Bn samples) in the same launch (mnsplit =
+ * blindno_mix_wgrad_nsplit(Bn / G, ...); mpartial as mix_wgrad_g's). */
+int blindno_lift_bwd_mix_g(const float* dx0, const float* in, const float* w0, float* d_in,
+                           float* partial, int nchunk, int G, int64_t wgs, int Bn, int N1, int N2,
+                           int Cin, int C, int P1, int P2, const float* Xs, const float* Gs,
+                           float* dWt, float* mpartial, int mnsplit, int K1, int m2,
+                           blindno_stream_t stream);
 int blindno_project_fwd_g(const float* z, const float* w1, const float* b1, const float* w2,
                           const float* b2, float* out, int G, int64_t wgs, int Bn, int C, int P1,
                           int P2, int Ho, int Wo, int Hd, int Cout, int ostride, int ooff,

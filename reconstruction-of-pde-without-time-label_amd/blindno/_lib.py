@@ -45,6 +45,7 @@ SIGNATURES = {
     "blindno_mix_wgrad": "ppppiiiiiis",
     "blindno_mix_wgrad_part": "pppiiiiiiis",
     "blindno_mix_wgrad_multi": "ppppis",
+    "blindno_mix_wgrad_multi_u": "ppppppis",
     "blindno_mix1d": "ppppiiiiiis",
     "blindno_rowidft_epi": "ppppppiiiiiis",
     "blindno_rowidft_epi_crop": "pppppp" + "iiiiiiii" + "s",
@@ -79,6 +80,7 @@ SIGNATURES = {
     "blindno_mix_wgrad_nsplit": "iiiii",
     "blindno_lift_fwd_g": "ppppiliiiiiiis",
     "blindno_lift_bwd_g": "pppppiiliiiiiiis",
+    "blindno_lift_bwd_mix_g": "pppppiiliiiiiiippppiiis",
     "blindno_project_fwd_g": "ppppppiliiiiiiiiiis",
     "blindno_project_bwd_g": "pppppppiiliiiiiiiiiis",
     "blindno_colpass_g": "pppppppiliiiiiiiis",
@@ -103,6 +105,7 @@ SIGNATURES = {
     "blindno_gather_batch": "ppppipis",
     "blindno_reduce_partials_multi": "ppppis",
     "blindno_reduce_partials_pieces": "ppppppis",
+    "blindno_reduce_partials_pieces_u": "pppppppppis",
     "blindno_unpack_w2d_multi": "ppppis",
     "blindno_pack_w2d_multi": "ppppis",
     "blindno_fp_propagate": "pppiiiiiids",

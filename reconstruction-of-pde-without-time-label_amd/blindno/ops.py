@@ -52,6 +52,9 @@ BAG_DZ_ON_LOAD = os.environ.get("BLINDNO_BAGDZ", "1") != "0"
 # the grouped heads' backward: row DFT + conv gradient + the previous layer's mix gradient in
 # one launch per layer (BLINDNO_HEADBWD_MERGED=0: three launches)
 HEAD_BWD_MERGED = os.environ.get("BLINDNO_HEADBWD_MERGED", "1") != "0"
+# the deferred finalisation stores the spectral weight gradients unpacked from the kernel that
+# finishes them (BLINDNO_UNPACK_FOLD=0: a separate unpack launch)
+UNPACK_FOLD = os.environ.get("BLINDNO_UNPACK_FOLD", "1") != "0"
 
 
 def set_mix_precision(name: str) -> None:
@@ -287,25 +290,76 @@ class _Deferred:
                 done.append(p)
         return done
 
+    def _fold_unpacks(self):
+        """Match each recorded unpack to the kernel that finishes its dWt -- a mix job with no
+        sample split (all its weight groups unpacked) or a whole reduction -- so that kernel
+        stores dWt unpacked (W2dUnpack, csrc/wgrad.h) and the unpack launch goes.  Returns
+        ({mix job: {group: (dw1, dw2)}}, {reduction: (dw1, dw2, (Ci, Co, m1, m2))}, the
+        unpacks left for blindno_unpack_w2d_multi)."""
+        mixu, redu, rest = {}, {}, []
+        taken = {}
+        for u in self.unp:
+            dW, d1, d2, (Ci, Co, m1, m2, P1), _ = u
+            hit = False
+            if UNPACK_FOLD and 2 * m1 < P1:
+                p = dW.data_ptr()
+                for qi, (_, _, out, sh) in enumerate(self.mix):
+                    Bn, ci, co, K1, mm2, ns, Gw = sh
+                    per = mm2 * K1 * ci * co * 2 * 4
+                    off = p - out.data_ptr()
+                    if (ns == 1 and Gw <= 4 and K1 == 2 * m1 and (ci, co, mm2) == (Ci, Co, m2)
+                            and 4 * dW.numel() == per and 0 <= off < per * Gw and off % per == 0):
+                        mixu.setdefault(qi, {})[off // per] = (d1, d2)
+                        taken.setdefault(qi, []).append(u)
+                        hit = True
+                        break
+                if not hit:
+                    for ri, r in enumerate(self.red):
+                        if (r[1].data_ptr() == p and r[3] == dW.numel() and not r[4] and ri not in redu
+                                and r[3] == 4 * Ci * Co * m1 * m2):
+                            redu[ri] = (d1, d2, (Ci, Co, m1, m2))
+                            hit = True
+                            break
+            if not hit:
+                rest.append(u)
+        for qi in list(mixu):
+            if len(mixu[qi]) != self.mix[qi][3][6]:      # every group of the job, or none
+                rest.extend(taken[qi])
+                del mixu[qi]
+        return mixu, redu, rest
+
     def flush(self):
+        mixu, redu, rest = self._fold_unpacks()
         if self.mix:
             n = len(self.mix)
             xs = (ctypes.c_void_p * n)(*[m[0].data_ptr() for m in self.mix])
             gs = (ctypes.c_void_p * n)(*[m[1].data_ptr() for m in self.mix])
             os_ = (ctypes.c_void_p * n)(*[m[2].data_ptr() for m in self.mix])
             shp = (ctypes.c_int * (7 * n))(*[v for m in self.mix for v in m[3]])
-            call("blindno_mix_wgrad_multi", xs, gs, os_, shp, n, stream_ptr())
+            ud = [None] * (8 * n)
+            um1 = [0] * n
+            for qi, groups in mixu.items():
+                for g, (d1, d2) in groups.items():
+                    ud[8 * qi + 2 * g], ud[8 * qi + 2 * g + 1] = d1.data_ptr(), d2.data_ptr()
+                um1[qi] = self.mix[qi][3][3] // 2
+            call("blindno_mix_wgrad_multi_u", xs, gs, os_, shp, (ctypes.c_void_p * (8 * n))(*ud),
+                 (ctypes.c_int * n)(*um1), n, stream_ptr())
         if self.red:
-            segs = []          # (partial, dst address, nchunk, np, e0, e1)
-            for partial, out, nchunk, np_, pieces in self.red:
+            segs = []          # (partial, dst address, nchunk, np, e0, e1, unpack descriptor)
+            descs = []
+            for ri, (partial, out, nchunk, np_, pieces) in enumerate(self.red):
+                if ri in redu:
+                    descs.append(redu[ri])
+                    segs.append((partial, out.data_ptr(), nchunk, np_, 0, np_, len(descs) - 1))
+                    continue
                 pos = 0
                 for e0, e1, dst in sorted(pieces, key=lambda t: t[0]):
                     if e0 > pos:
-                        segs.append((partial, out.data_ptr() + 4 * pos, nchunk, np_, pos, e0))
-                    segs.append((partial, dst.data_ptr(), nchunk, np_, e0, e1))
+                        segs.append((partial, out.data_ptr() + 4 * pos, nchunk, np_, pos, e0, -1))
+                    segs.append((partial, dst.data_ptr(), nchunk, np_, e0, e1, -1))
                     pos = e1
                 if pos < np_:
-                    segs.append((partial, out.data_ptr() + 4 * pos, nchunk, np_, pos, np_))
+                    segs.append((partial, out.data_ptr() + 4 * pos, nchunk, np_, pos, np_, -1))
             n = len(segs)
             srcs = (ctypes.c_void_p * n)(*[t[0].data_ptr() for t in segs])
             outs = (ctypes.c_void_p * n)(*[t[1] for t in segs])
@@ -313,13 +367,18 @@ class _Deferred:
             nps = (ctypes.c_int * n)(*[t[3] for t in segs])
             e0s = (ctypes.c_int * n)(*[t[4] for t in segs])
             e1s = (ctypes.c_int * n)(*[t[5] for t in segs])
-            call("blindno_reduce_partials_pieces", srcs, outs, ncs, nps, e0s, e1s, n, stream_ptr())
-        if self.unp:
-            n = len(self.unp)
-            srcs = (ctypes.c_void_p * n)(*[u[0].data_ptr() for u in self.unp])
-            d1 = (ctypes.c_void_p * n)(*[u[1].data_ptr() for u in self.unp])
-            d2 = (ctypes.c_void_p * n)(*[u[2].data_ptr() for u in self.unp])
-            shp = (ctypes.c_int * (5 * n))(*[v for u in self.unp for v in u[3]])
+            upks = (ctypes.c_int * n)(*[t[6] for t in segs])
+            nd = max(1, len(descs))
+            ud = (ctypes.c_void_p * (2 * nd))(*[v for d in descs for v in (d[0].data_ptr(), d[1].data_ptr())])
+            ushp = (ctypes.c_int * (4 * nd))(*[v for d in descs for v in d[2]])
+            call("blindno_reduce_partials_pieces_u", srcs, outs, ncs, nps, e0s, e1s, upks, ud, ushp, n,
+                 stream_ptr())
+        if rest:
+            n = len(rest)
+            srcs = (ctypes.c_void_p * n)(*[u[0].data_ptr() for u in rest])
+            d1 = (ctypes.c_void_p * n)(*[u[1].data_ptr() for u in rest])
+            d2 = (ctypes.c_void_p * n)(*[u[2].data_ptr() for u in rest])
+            shp = (ctypes.c_int * (5 * n))(*[v for u in rest for v in u[3]])
             call("blindno_unpack_w2d_multi", srcs, d1, d2, shp, n, stream_ptr())
         self.mix, self.red, self.unp = [], [], []
 
@@ -976,8 +1035,9 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         for g in range(G):
             grads[g][o], grads[g][o + 1] = dws[2 * g], dws[2 * g + 1]
 
-    # under deferred_reductions() the mix gradients join the batched finalisation instead
-    defer_mix = _DEFER is not None
+    # hosted in the merged launches (the next layer's row DFT, the lift backward for the last);
+    # otherwise, under deferred_reductions(), the mix gradients join the batched finalisation
+    defer_mix = _DEFER is not None and not merged
 
     def mix_launch(kk, Xk, Gk):
         dWt, part = mix_buffers()
@@ -1028,14 +1088,19 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
         call("blindno_rowidft_bwd_g", ptr(GZ), ptr(dz), small.p(2 + 2 * k), ptr(src),
              ptr(dz_new), ptr(tb), G, S, Bn, C, P1, P2, meta.m2, act, stream_ptr())
         dz = dz_new
-    if pending is not None:
-        mix_launch(*pending)
     np_l = C * Cin + C
     nchunk = query("blindno_lift_bwd_nchunk", Bg, N1, N2)
     partial = _empty(nchunk, G, np_l, like=inp)
     d_inp = torch.empty_like(inp) if need_inp_grad else None
-    call("blindno_lift_bwd_g", ptr(dz), ptr(inp), small.p(0), ptr(d_inp), ptr(partial), nchunk, G, S,
-         Bn, N1, N2, Cin, C, P1, P2, stream_ptr())
+    mx = (None, None, None, None)
+    if pending is not None:            # the first layer's mix gradient in the lift's launch
+        dWt, part = mix_buffers()
+        mx = (pending[1], pending[2], dWt, part)
+    call("blindno_lift_bwd_mix_g", ptr(dz), ptr(inp), small.p(0), ptr(d_inp), ptr(partial), nchunk, G,
+         S, Bn, N1, N2, Cin, C, P1, P2, *[ptr(t) if t is not None else None for t in mx], ns, K1,
+         meta.m2, stream_ptr())
+    if pending is not None:
+        mix_grads(pending[0], dWt)
     gl = reduce_partials(partial, nchunk, G * np_l).view(G, np_l)
     for g in range(G):
         grads[g][0] = gl[g, :C * Cin].view(C, Cin)

@@ -428,21 +428,29 @@ __global__ __launch_bounds__(256) void lift_bwd_w_mfma_kernel(const float* __res
 }
 
 // The heads' lift backward in one launch: its input gradient (workgroups [0, nbi)) and its
-// weight / bias gradient partials (the rest, nchunk x G) read the same dx0 and are independent;
-// each part keeps the grid of its own launch (bit-identical results).
+// weight / bias gradient partials (the next nchunk x G) read the same dx0 and are independent;
+// the rest (nbm) runs the spectral weight gradient of the heads' first layer, whose column pass
+// has just run (wgrad.h).  Each part keeps the grid of its own launch (bit-identical results).
 template <int JT>
 __global__ __launch_bounds__(256) void lift_bwd_both_kernel(
     const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in,
     const float* __restrict__ in, float* __restrict__ partial, int Bn, int N1, int N2, int Cin,
-    int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2, int nbi, int nchunk) {
+    int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2, int nbi, int nchunk,
+    MixWgradJob mw) {
   const int b = blockIdx.x;
   if (b < nbi) {
     lift_bwd_in_wide_block<12, 16>(dx0, w0, d_in, Bn, N1, N2, C, P1, P2, G, wgs, dS, dN2, b, nbi);
     return;
   }
-  const int r = b - nbi;
-  lift_bwd_w_mfma_block<JT>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2, r % nchunk, nchunk,
-                            r / nchunk, G);
+  int r = b - nbi;
+  if (r < nchunk * G) {
+    lift_bwd_w_mfma_block<JT>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2, r % nchunk, nchunk,
+                              r / nchunk, G);
+    return;
+  }
+  r -= nchunk * G;
+  mix_wgrad_block(mw.X, mw.Gs, mw.out, mw.Bn, mw.Ci, mw.Co, mw.K1, mw.m2, r % mw.gx,
+                  (r / mw.gx) % mw.gy, r / (mw.gx * mw.gy), mw.gx, mw.gy, mw.gz);
 }
 
 template <int ACT>
@@ -461,10 +469,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_kernel(const float* __res
 // a conv's 20) therefore still use all 1024 threads instead of 16 lanes.
 // (e0, e1): only parameters p in [e0, e1) are stored, at out[p - e0] -- a piece of a reduction
 // whose parameters land in different buffers (blindno_reduce_partials_pieces)
+// upk: out is a packed spectral weight gradient, stored unpacked (wgrad.h, W2dUnpack)
 __device__ __forceinline__ void reduce_partials_block(const float* __restrict__ partial,
                                                       float* __restrict__ out, int nchunk, int np,
                                                       int PB, int blk, float* red, int e0 = 0,
-                                                      int e1 = INT32_MAX) {
+                                                      int e1 = INT32_MAX, bool upk = false,
+                                                      W2dUnpack uw = W2dUnpack{}) {
   const int S = 1024 / PB;
   const int t = threadIdx.x;
   const int pl = t % PB, sl = t / PB;
@@ -485,7 +495,10 @@ __device__ __forceinline__ void reduce_partials_block(const float* __restrict__ 
   if (sl == 0 && p < np && p >= e0 && p < e1) {
     float v = red[pl];
     for (int k = 1; k < S; ++k) v += red[k * PB + pl];
-    out[p - e0] = v;
+    if (upk)
+      w2d_unpacked(uw, p >> 1)[p & 1] = v;
+    else
+      out[p - e0] = v;
   }
 }
 
@@ -503,11 +516,15 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const float* __re
 // reduction's block grid (same PB, so the same summation order), storing only parameters
 // [e0, e1) at out[p - e0] (the gradients written straight into an optimizer's flat buffer).
 // Segments are passed by value (a graph capture bakes them in).
-constexpr int kRedSegs = 48;
+// A segment with upk[i] >= 0 is a packed spectral weight gradient stored unpacked through
+// ut[upk[i]] (whole reductions only).
+constexpr int kRedSegs = 48, kRedUnpack = 8;
 struct ReduceSegs {
   const float* src[kRedSegs];
   float* out[kRedSegs];
   int nchunk[kRedSegs], np[kRedSegs], pb[kRedSegs], blk0[kRedSegs], e0[kRedSegs], e1[kRedSegs];
+  int upk[kRedSegs];
+  W2dUnpack ut[kRedUnpack];
   int cum[kRedSegs + 1];
   int nseg;
 };
@@ -517,8 +534,10 @@ __global__ __launch_bounds__(1024) void reduce_partials_multi_kernel(ReduceSegs 
   const int b = blockIdx.x;
   int sg = 0;
   while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;    // uniform scan
+  const int u = segs.upk[sg];
   reduce_partials_block(segs.src[sg], segs.out[sg], segs.nchunk[sg], segs.np[sg], segs.pb[sg],
-                        segs.blk0[sg] + b - segs.cum[sg], red, segs.e0[sg], segs.e1[sg]);
+                        segs.blk0[sg] + b - segs.cum[sg], red, segs.e0[sg], segs.e1[sg], u >= 0,
+                        segs.ut[u >= 0 ? u : 0]);
 }
 
 // ---------------------------------------------------------------- projection MLP
@@ -967,10 +986,12 @@ BLINDNO_API int blindno_lift_bwd_nchunk(int Bn, int N1, int N2) {
 #ifndef LIFT_BWD_BOTH
 #define LIFT_BWD_BOTH 1
 #endif
-BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const float* w0,
-                                   float* d_in, float* partial, int nchunk, int G, int64_t wgs,
-                                   int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
-                                   void* stream) {
+BLINDNO_API int blindno_lift_bwd_mix_g(const float* dx0, const float* in, const float* w0,
+                                       float* d_in, float* partial, int nchunk, int G,
+                                       int64_t wgs, int Bn, int N1, int N2, int Cin, int C, int P1,
+                                       int P2, const float* Xs, const float* Gs, float* dWt,
+                                       float* mpartial, int mnsplit, int K1, int m2,
+                                       void* stream) {
   if (G < 1 || Bn % G) return (int)hipErrorInvalidValue;
   const int Bg = Bn / G;
   hipStream_t st = (hipStream_t)stream;
@@ -979,21 +1000,45 @@ BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const floa
                        (int64_t)Bg * N1 * N2 * Cin < INT32_MAX && (((uintptr_t)d_in) & 15) == 0;
   const bool mf = C >= 5 && C <= 16 && Cin + 1 <= 32 && N2 % 16 == 0 && P2 % 4 == 0 &&
                   (((uintptr_t)dx0) & 15) == 0;
+  // the spectral weight gradient hosted in the same launch (Xs != NULL; Ci = Co = C)
+  MixWgradJob mw{};
+  int64_t nbm = 0;
+  const int64_t mtotal = (int64_t)m2 * K1 * C * C;
+  if (Xs) {
+    if (!Gs || !dWt || K1 < 1 || m2 < 1 || mtotal >= INT32_MAX / 2 || mnsplit < 1 ||
+        (mnsplit > 1 && !mpartial))
+      return (int)hipErrorInvalidValue;
+    mw.X = (const float2*)Xs;
+    mw.Gs = (const float2*)Gs;
+    mw.out = (float2*)(mnsplit > 1 ? mpartial : dWt);
+    mw.Bn = Bn; mw.Ci = C; mw.Co = C; mw.K1 = K1; mw.m2 = m2;
+    mw.gx = (int)cdiv(mtotal, kBlock);
+    mw.gy = mnsplit;
+    mw.gz = G;
+    nbm = (int64_t)mw.gx * mnsplit * G;
+  }
   if (wide_in && partial && mf && LIFT_BWD_BOTH) {
     if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)
       return (int)hipErrorInvalidValue;
     const int nbi = grid_for((int64_t)Bg * N1 * N2, kBlock, 8192);
-    const int64_t nb = nbi + (int64_t)nchunk * G;
+    const int64_t nb = nbi + (int64_t)nchunk * G + nbm;
+    if (nb >= INT32_MAX) return (int)hipErrorInvalidValue;
     const FastDiv dS = FastDiv::make((unsigned)(N1 * N2)), dN2 = FastDiv::make((unsigned)N2);
     if (Cin + 1 <= 16)
       lift_bwd_both_kernel<1><<<(unsigned)nb, 256, 0, st>>>(dx0, w0, d_in, in, partial, Bg, N1, N2,
                                                             Cin, C, P1, P2, G, G > 1 ? wgs : 0, dS,
-                                                            dN2, nbi, nchunk);
+                                                            dN2, nbi, nchunk, mw);
     else
       lift_bwd_both_kernel<2><<<(unsigned)nb, 256, 0, st>>>(dx0, w0, d_in, in, partial, Bg, N1, N2,
                                                             Cin, C, P1, P2, G, G > 1 ? wgs : 0, dS,
-                                                            dN2, nbi, nchunk);
-    return (int)hipGetLastError();
+                                                            dN2, nbi, nchunk, mw);
+    const int e = (int)hipGetLastError();
+    if (e || !Xs || mnsplit == 1) return e;
+    return blindno_reduce_partials(mpartial, dWt, mnsplit, (int)(2 * mtotal * G), stream);
+  }
+  if (Xs) {
+    const int e = blindno_mix_wgrad_g(Xs, Gs, dWt, mpartial, mnsplit, G, Bn, C, C, K1, m2, stream);
+    if (e) return e;
   }
   if (d_in) {
     const int64_t total = (int64_t)Bg * N1 * N2 * Cin;
@@ -1023,6 +1068,14 @@ BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const floa
                                                           P1, P2);
   }
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_lift_bwd_g(const float* dx0, const float* in, const float* w0,
+                                   float* d_in, float* partial, int nchunk, int G, int64_t wgs,
+                                   int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
+                                   void* stream) {
+  return blindno_lift_bwd_mix_g(dx0, in, w0, d_in, partial, nchunk, G, wgs, Bn, N1, N2, Cin, C,
+                                P1, P2, nullptr, nullptr, nullptr, nullptr, 1, 0, 0, stream);
 }
 
 BLINDNO_API int blindno_lift_bwd(const float* dx0, const float* in, const float* w0,
@@ -1079,19 +1132,32 @@ BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nc
   return (int)hipGetLastError();
 }
 
-BLINDNO_API int blindno_reduce_partials_pieces(const void* const* partials, void* const* outs,
-                                               const int* nchunks, const int* nps, const int* e0s,
-                                               const int* e1s, int nseg, void* stream) {
+BLINDNO_API int blindno_reduce_partials_pieces_u(const void* const* partials, void* const* outs,
+                                                 const int* nchunks, const int* nps,
+                                                 const int* e0s, const int* e1s, const int* upks,
+                                                 void* const* ud, const int* ushp, int nseg,
+                                                 void* stream) {
   if (nseg < 0) return (int)hipErrorInvalidValue;
   for (int s0 = 0; s0 < nseg; s0 += kRedSegs) {
     ReduceSegs segs{};
     const int k = nseg - s0 < kRedSegs ? nseg - s0 : kRedSegs;
     segs.nseg = k;
-    int blocks = 0;
+    int blocks = 0, nu = 0;
     for (int i = 0; i < k; ++i) {
       const int nc = nchunks[s0 + i], np = nps[s0 + i];
       const int e0 = e0s ? e0s[s0 + i] : 0, e1 = e1s ? e1s[s0 + i] : np;
       if (nc < 1 || np < 1 || e0 < 0 || e1 > np || e0 >= e1) return (int)hipErrorInvalidValue;
+      segs.upk[i] = -1;
+      const int uq = upks ? upks[s0 + i] : -1;
+      if (uq >= 0) {
+        const int* sh = ushp + 4 * uq;      // (Ci, Co, m1, m2) of descriptor uq
+        if (nu == kRedUnpack || e0 != 0 || e1 != np || !ud[2 * uq] || !ud[2 * uq + 1] ||
+            sh[0] < 1 || sh[1] < 1 || sh[2] < 1 || sh[3] < 1 ||
+            (int64_t)4 * sh[0] * sh[1] * sh[2] * sh[3] != np)
+          return (int)hipErrorInvalidValue;
+        segs.ut[nu] = W2dUnpack{(float*)ud[2 * uq], (float*)ud[2 * uq + 1], sh[0], sh[1], sh[2], sh[3]};
+        segs.upk[i] = nu++;
+      }
       segs.src[i] = (const float*)partials[s0 + i];
       segs.out[i] = (float*)outs[s0 + i];
       segs.nchunk[i] = nc;
@@ -1109,6 +1175,13 @@ BLINDNO_API int blindno_reduce_partials_pieces(const void* const* partials, void
     reduce_partials_multi_kernel<<<blocks, 1024, 0, (hipStream_t)stream>>>(segs);
   }
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_reduce_partials_pieces(const void* const* partials, void* const* outs,
+                                               const int* nchunks, const int* nps, const int* e0s,
+                                               const int* e1s, int nseg, void* stream) {
+  return blindno_reduce_partials_pieces_u(partials, outs, nchunks, nps, e0s, e1s, nullptr,
+                                          nullptr, nullptr, nseg, stream);
 }
 
 BLINDNO_API int blindno_reduce_partials_multi(const void* const* partials, void* const* outs,

@@ -825,47 +825,6 @@ __global__ __launch_bounds__(256) void colidft_kernel(const float2* __restrict__
   }
 }
 
-// dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]
-// workgroup (bx, by, bz) of (gx, gy, gz), kBlock threads:
-//   by = sample slice: out[y][idx] = sum over this slice's samples (partials when gy > 1,
-//   reduced in fixed order afterwards)
-//   bz = weight group: its Bn / gz samples only; out[(y G + g)][idx]
-__device__ __forceinline__ void mix_wgrad_block(const float2* __restrict__ X,
-                                                const float2* __restrict__ G,
-                                                float2* __restrict__ out, int Bn, int Ci, int Co,
-                                                int K1, int m2, int bx, int by, int bz, int gx,
-                                                int gy, int gz) {
-  const int total = m2 * K1 * Ci * Co;
-  const int Bg = Bn / gz, grp = bz;
-  const int ns = (Bg + gy - 1) / gy;
-  const int n0 = grp * Bg + by * ns, n1 = min(grp * Bg + Bg, n0 + ns);
-  const int sX = m2 * Ci * K1, sG = m2 * Co * K1;
-  for (int idx = bx * kBlock + threadIdx.x; idx < total; idx += gx * kBlock) {
-    const int o = idx % Co;
-    int t = idx / Co;
-    const int i = t % Ci;
-    t /= Ci;
-    const int j = t % K1;
-    const int k = t / K1;
-    const float2* xp = X + ((int64_t)n0 * m2 + k) * Ci * K1 + i * K1 + j;
-    const float2* gp = G + ((int64_t)n0 * m2 + k) * Co * K1 + o * K1 + j;
-    // fp64 accumulation: the sum over hundreds of snapshots cancels heavily once the weights
-    // are trained (terms ~1e3 x the result for the encoder's first layer), and an fp32 running
-    // sum then loses ~n eps of the terms' scale -- measured 4e-3 rel-L2 on
-    // FNO_input.spectral_list.0.weights2 vs fp64 at config C, against 6e-5 for the reference's
-    // blocked fp32 GEMM.  The kernel is memory-bound; the fp64 FMAs are free.
-    double re = 0.0, im = 0.0;
-#pragma unroll 4
-    for (int n = n0; n < n1; ++n, xp += sX, gp += sG) {
-      const float2 a = *xp;
-      const float2 g = *gp;
-      re = fma((double)a.x, (double)g.x, fma((double)a.y, (double)g.y, re));
-      im = fma((double)a.x, (double)g.y, fma(-(double)a.y, (double)g.x, im));
-    }
-    out[((int64_t)by * gz + grp) * total + idx] = make_float2((float)re, (float)im);
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void mix_wgrad_kernel(const float2* __restrict__ X,
                                                            const float2* __restrict__ G,
                                                            float2* __restrict__ out, int Bn,
@@ -886,12 +845,6 @@ struct ConvWgradJob {
   const float* x;
   float* partial;
   int C, HW, Bg, nchunk, G;
-};
-struct MixWgradJob {
-  const float2* X;
-  const float2* Gs;
-  float2* out;
-  int Bn, Ci, Co, K1, m2, gx, gy, gz;
 };
 
 template <int NT, int ALIGNED, int ACT>
@@ -936,8 +889,12 @@ __global__ __launch_bounds__(kBlock) void mix_wgrad_multi_kernel(MixJobs jobs) {
   while (q + 1 < jobs.n && jobs.cum[q + 1] <= b) ++q;             // uniform scan
   const MixWgradJob& m = jobs.j[q];
   const int r = b - jobs.cum[q];
+  const int grp = r / (m.gx * m.gy);
+  const bool upk = m.um1 > 0;
+  W2dUnpack uw{};
+  if (upk) uw = W2dUnpack{m.u1[grp], m.u2[grp], m.Ci, m.Co, m.um1, m.m2};
   mix_wgrad_block(m.X, m.Gs, m.out, m.Bn, m.Ci, m.Co, m.K1, m.m2, r % m.gx, (r / m.gx) % m.gy,
-                  r / (m.gx * m.gy), m.gx, m.gy, m.gz);
+                  grp, m.gx, m.gy, m.gz, upk, uw);
 }
 
 // ------------------------------------------------------------------------------ 1D mode mix
@@ -1403,9 +1360,9 @@ BLINDNO_API int blindno_rowdft_wgrad_g(const float* dz, const float* src, float*
 
 // jobs q < njobs: X[q], G[q] -> out[q] (dWt when nsplit == 1, else the nsplit x Gw partials,
 // reduced by the caller); shp[7 q ..] = (Bn, Ci, Co, K1, m2, nsplit, Gw)
-BLINDNO_API int blindno_mix_wgrad_multi(const void* const* X, const void* const* G,
-                                        void* const* out, const int* shp, int njobs,
-                                        void* stream) {
+BLINDNO_API int blindno_mix_wgrad_multi_u(const void* const* X, const void* const* G,
+                                          void* const* out, const int* shp, void* const* ud,
+                                          const int* um1, int njobs, void* stream) {
   if (njobs < 0) return (int)hipErrorInvalidValue;
   for (int q0 = 0; q0 < njobs; q0 += kMixJobs) {
     MixJobs jobs{};
@@ -1427,6 +1384,15 @@ BLINDNO_API int blindno_mix_wgrad_multi(const void* const* X, const void* const*
       m.gx = (int)cdiv(total, kBlock);
       m.gy = ns;
       m.gz = Gw;
+      m.um1 = um1 ? um1[q0 + i] : 0;
+      if (m.um1 > 0) {
+        if (ns != 1 || Gw > kMixMaxGw || K1 != 2 * m.um1) return (int)hipErrorInvalidValue;
+        for (int g = 0; g < Gw; ++g) {
+          m.u1[g] = (float*)ud[(q0 + i) * 2 * kMixMaxGw + 2 * g];
+          m.u2[g] = (float*)ud[(q0 + i) * 2 * kMixMaxGw + 2 * g + 1];
+          if (!m.u1[g] || !m.u2[g]) return (int)hipErrorInvalidValue;
+        }
+      }
       jobs.cum[i] = (int)blocks;
       blocks += (int64_t)m.gx * ns * Gw;
     }
@@ -1436,6 +1402,12 @@ BLINDNO_API int blindno_mix_wgrad_multi(const void* const* X, const void* const*
     mix_wgrad_multi_kernel<<<(unsigned)blocks, kBlock, 0, (hipStream_t)stream>>>(jobs);
   }
   return (int)hipGetLastError();
+}
+
+BLINDNO_API int blindno_mix_wgrad_multi(const void* const* X, const void* const* G,
+                                        void* const* out, const int* shp, int njobs,
+                                        void* stream) {
+  return blindno_mix_wgrad_multi_u(X, G, out, shp, nullptr, nullptr, njobs, stream);
 }
 
 BLINDNO_API int blindno_mix_wgrad_g(const float* X, const float* G, float* dWt, float* partial,

@@ -75,6 +75,89 @@ __device__ __forceinline__ void conv_wgrad_mfma_block(const float* __restrict__ 
   }
 }
 
+// The spectral weight gradient's packed layout dWt (m2, K1 = 2 m1, Ci, Co) complex (the mix
+// GEMM's) -> the reference layout (Ci, Co, m1, m2) of weights1 (kept rows j < m1) and weights2
+// (rows m1 .. 2 m1 - 1): what blindno_unpack_w2d does as its own launch, folded into the store
+// of the kernel that finishes dWt (the deferred finalisation's mix or reduction).  Only for
+// non-overlapping kept rows (2 m1 < P1, K1 = 2 m1).
+struct W2dUnpack {
+  float* d1;
+  float* d2;
+  int Ci, Co, m1, m2;
+};
+__device__ __forceinline__ float* w2d_unpacked(const W2dUnpack& u, int e) {
+  const int o = e % u.Co;
+  int t = e / u.Co;
+  const int i = t % u.Ci;
+  t /= u.Ci;
+  const int j = t % (2 * u.m1), k = t / (2 * u.m1);
+  const bool second = j >= u.m1;
+  return (second ? u.d2 : u.d1) +
+         ((((int64_t)i * u.Co + o) * u.m1 + (second ? j - u.m1 : j)) * u.m2 + k) * 2;
+}
+
+// Spectral weight gradient (the mix GEMM over the samples, spectral.hip / fields.hip hosts):
+// dWt[k,j,i,o] = sum_n conj(X[n,k,i,j]) G[n,k,o,j]
+// workgroup (bx, by, bz) of (gx, gy, gz), kBlock threads:
+//   by = sample slice: out[y][idx] = sum over this slice's samples (partials when gy > 1,
+//   reduced in fixed order afterwards)
+//   bz = weight group: its Bn / gz samples only; out[(y G + g)][idx]
+// upk (gy == 1 only): dWt of weight group bz stored unpacked through uw (wgrad.h)
+__device__ __forceinline__ void mix_wgrad_block(const float2* __restrict__ X,
+                                                const float2* __restrict__ G,
+                                                float2* __restrict__ out, int Bn, int Ci, int Co,
+                                                int K1, int m2, int bx, int by, int bz, int gx,
+                                                int gy, int gz, bool upk = false,
+                                                W2dUnpack uw = W2dUnpack{}) {
+  const int total = m2 * K1 * Ci * Co;
+  const int Bg = Bn / gz, grp = bz;
+  const int ns = (Bg + gy - 1) / gy;
+  const int n0 = grp * Bg + by * ns, n1 = min(grp * Bg + Bg, n0 + ns);
+  const int sX = m2 * Ci * K1, sG = m2 * Co * K1;
+  for (int idx = bx * kBlock + threadIdx.x; idx < total; idx += gx * kBlock) {
+    const int o = idx % Co;
+    int t = idx / Co;
+    const int i = t % Ci;
+    t /= Ci;
+    const int j = t % K1;
+    const int k = t / K1;
+    const float2* xp = X + ((int64_t)n0 * m2 + k) * Ci * K1 + i * K1 + j;
+    const float2* gp = G + ((int64_t)n0 * m2 + k) * Co * K1 + o * K1 + j;
+    // fp64 accumulation: the sum over hundreds of snapshots cancels heavily once the weights
+    // are trained (terms ~1e3 x the result for the encoder's first layer), and an fp32 running
+    // sum then loses ~n eps of the terms' scale -- measured 4e-3 rel-L2 on
+    // FNO_input.spectral_list.0.weights2 vs fp64 at config C, against 6e-5 for the reference's
+    // blocked fp32 GEMM.  The kernel is memory-bound; the fp64 FMAs are free.
+    double re = 0.0, im = 0.0;
+#pragma unroll 4
+    for (int n = n0; n < n1; ++n, xp += sX, gp += sG) {
+      const float2 a = *xp;
+      const float2 g = *gp;
+      re = fma((double)a.x, (double)g.x, fma((double)a.y, (double)g.y, re));
+      im = fma((double)a.x, (double)g.y, fma(-(double)a.y, (double)g.x, im));
+    }
+    if (upk) {
+      float* d = w2d_unpacked(uw, idx);
+      d[0] = (float)re;
+      d[1] = (float)im;
+    } else {
+      out[((int64_t)by * gz + grp) * total + idx] = make_float2((float)re, (float)im);
+    }
+  }
+}
+
+
+constexpr int kMixMaxGw = 4;
+struct MixWgradJob {
+  const float2* X;
+  const float2* Gs;
+  float2* out;
+  int Bn, Ci, Co, K1, m2, gx, gy, gz;
+  int um1;                          // > 0: dWt stored unpacked (K1 = 2 um1, gy = 1) at
+  float* u1[kMixMaxGw];             // weights1 / weights2 gradients of group g
+  float* u2[kMixMaxGw];
+};
+
 // the conv_wgrad_mfma_block shapes (fields.hip's launcher and the hosted form)
 __host__ __forceinline__ bool conv_wgrad_mfma_ok(int C, int64_t HW) {
   return C >= 5 && C <= 15 && HW < INT32_MAX / 16;
