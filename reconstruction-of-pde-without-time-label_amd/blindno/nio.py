@@ -11,6 +11,7 @@ seeded run sees the same bags.  ``bag_idx=`` overrides the draw (parity harness)
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -58,6 +59,9 @@ _SIDE = {}
 
 
 HEAD_STREAMS = True     # fork the two heads over two streams (ops.HeadPairFn)
+# the grouped heads' spectral weights packed by the encoder's pack launch (BLINDNO_PACK_AHEAD=0:
+# their own launch)
+PACK_HEADS_AHEAD = os.environ.get("BLINDNO_PACK_AHEAD", "1") != "0"
 DEDUP_BAGS = True       # run the snapshot encoder once per distinct snapshot of a bag
 
 
@@ -138,7 +142,17 @@ class NIOFP2D_FNO(nn.Module):
         Without input gradients the snapshot encoder + bag mean run as the fused HIP path
         (ops.BagEncoderFn: snapshots read from x through the bag's indices); otherwise as the
         generic composition below (same numerics, gradients for x and grid)."""
-        return self.forward_heads(self.forward_encoder(x, grid, bag_idx))
+        # the grouped heads' spectral weights are packed by the encoder's pack launch
+        if PACK_HEADS_AHEAD and x.is_cuda and HEAD_STREAMS and len(self._heads) == 2 and x.dim() == 4:
+            hs = [getattr(self, nm) for nm in self._heads]
+            w = self.fc0.out_features
+            if all(isinstance(hd, FNO2d) for hd in hs) and hs[0].meta(w).__dict__ == hs[1].meta(w).__dict__:
+                ops.pack_heads_ahead(hs[0].meta(w), (x.shape[0], x.shape[2], x.shape[3], w),
+                                     [fno_params(hd, 2) for hd in hs], x.device)
+        try:
+            return self.forward_heads(self.forward_encoder(x, grid, bag_idx))
+        finally:
+            ops.drop_pack_ahead()
 
     def forward_heads(self, h):
         """The two FNO heads on the bag-mean field h (B, Nx, Ny, width) (:577-581)."""

@@ -492,18 +492,63 @@ def k_pack_w2d(w1, w2, P1):
     return Wt
 
 
+# Packs requested ahead of their consumer (pack_ahead): they ride along the next _pack_into
+# launch -- the grouped heads' spectral weights are packed by the snapshot encoder's pack
+# launch at the start of the forward instead of by a launch of their own between the encoder
+# and the heads.  The consumer collects its buffers with take_packed.
+_PACK_AHEAD = []       # [(pairs, Wts, P1, handle)] not yet launched
+_PACKED = {}           # key -> (handle, request)
+
+
+def _pack_key(pairs, P1):
+    return tuple((w1.data_ptr(), w2.data_ptr()) for w1, w2 in pairs), int(P1)
+
+
+def pack_ahead(pairs, Wts, P1, handle):
+    """Register a pack of ``pairs`` into ``Wts`` (row count P1) for the next pack launch;
+    ``handle`` (e.g. the tensor the Wts are views of) is what take_packed returns."""
+    req = (list(pairs), list(Wts), int(P1), handle)
+    _PACK_AHEAD.append(req)
+    _PACKED[_pack_key(pairs, P1)] = (handle, req)
+
+
+def take_packed(pairs, P1):
+    """The handle of an earlier pack_ahead of exactly these pairs (launched now if no pack
+    launch has taken it along yet), or None."""
+    hit = _PACKED.pop(_pack_key(pairs, P1), None)
+    if hit is None:
+        return None
+    handle, req = hit
+    if any(r is req for r in _PACK_AHEAD):
+        _PACK_AHEAD[:] = [r for r in _PACK_AHEAD if r is not req]
+        _pack_into(req[0], req[1], req[2])
+    return handle
+
+
+def drop_pack_ahead():
+    """Forget every request (end of a forward): nothing stale survives into the next one."""
+    _PACK_AHEAD.clear()
+    _PACKED.clear()
+
+
 def _pack_into(pairs, Wts, P1):
     """Pack the spectral weights (w1, w2) of several 2D layers into the contiguous Wts[i]
-    (m2, K1, Ci, Co, 2) with ONE launch (blindno_pack_w2d_multi)."""
+    (m2, K1, Ci, Co, 2) with ONE launch (blindno_pack_w2d_multi), together with every pending
+    pack_ahead request."""
+    jobs = [(pr, W, P1) for pr, W in zip(pairs, Wts)]
+    for r in _PACK_AHEAD:
+        jobs += [(pr, W, r[2]) for pr, W in zip(r[0], r[1])]
+    _PACK_AHEAD.clear()
     w1s, w2s, shp = [], [], []
-    for (w1, w2), W in zip(pairs, Wts):
+    for (w1, w2), W, P1j in jobs:
         w1, w2 = _c(w1), _c(w2)
         Ci, Co, m1, m2 = w1.shape[:4]
-        if W.shape != (m2, kept_rows_count(m1, P1), Ci, Co, 2) or not W.is_contiguous():
+        if W.shape != (m2, kept_rows_count(m1, P1j), Ci, Co, 2) or not W.is_contiguous():
             raise BlindnoError("pack: bad Wt buffer")
         w1s.append(w1.data_ptr())
         w2s.append(w2.data_ptr())
-        shp += [Ci, Co, m1, m2, P1]
+        shp += [Ci, Co, m1, m2, P1j]
+    Wts = [j[1] for j in jobs]
     n = len(Wts)
     call("blindno_pack_w2d_multi", (ctypes.c_void_p * n)(*w1s), (ctypes.c_void_p * n)(*w2s),
          (ctypes.c_void_p * n)(*[W.data_ptr() for W in Wts]), (ctypes.c_int * (5 * n))(*shp), n,
@@ -704,13 +749,15 @@ class FNOMeta:
 
 
 def _fno_geometry(inp, meta: FNOMeta):
+    """(Bn, N1, N2, Cin, P1, P2, Ho, Wo) of an FNO input (a tensor or its shape)."""
+    shape = inp.shape if hasattr(inp, "shape") else tuple(inp)
     if meta.dim == 2:
-        Bn, N1, N2, Cin = inp.shape
+        Bn, N1, N2, Cin = shape
         pH, pW = pad_amount(N1), pad_amount(N2)   # x2_padding (H), x1_padding (W)
         P1, P2 = N1 + pH, N2 + pW
         Ho, Wo = P1 - pW, P2 - pH                 # x[..., :-x1_padding, :-x2_padding]
     else:
-        Bn, N2, Cin = inp.shape
+        Bn, N2, Cin = shape
         N1 = 1
         pW = pad_amount(N2)
         P1, P2 = 1, N2 + pW
@@ -866,6 +913,20 @@ def _offsets(tensors):
     return offs, o
 
 
+def pack_heads_ahead(meta: FNOMeta, shape, prms, device):
+    """Request the grouped heads' spectral weight pack (fno_forward_grouped's) ahead of the
+    forward that reaches them, for input ``shape`` (Bg, N1, N2, width)."""
+    if not (GROUPED_HEADS and grouped_ok(meta, shape, prms)):
+        return
+    G, n = len(prms), meta.n_layers
+    P1 = _fno_geometry(shape, meta)[4]
+    K1 = kept_rows_count(meta.m1, P1)
+    C = meta.width
+    Wt_all = torch.empty(n, G, meta.m2, K1, C, C, 2, dtype=F32, device=device)
+    segs = [(prms[g][2 + 4 * k], prms[g][3 + 4 * k]) for k in range(n) for g in range(G)]
+    pack_ahead(segs, [Wt_all[k, g] for k in range(n) for g in range(G)], P1, Wt_all)
+
+
 def grouped_ok(meta: FNOMeta, inp, prms) -> bool:
     if meta.dim != 2 or len(prms) != 2:
         return False
@@ -931,9 +992,11 @@ def fno_forward_grouped(meta: FNOMeta, inp, prms):
     src, act = x0, 0
     Xs, Wts, zs = [], [], []
     # every layer's spectral weights of both heads in one launch: Wt_all[k] = (G, m2, K1, C, C, 2)
-    Wt_all = _empty(n, G, meta.m2, K1, C, C, 2, like=inp)
     segs = [(prms[g][2 + 4 * k], prms[g][3 + 4 * k]) for k in range(n) for g in range(G)]
-    _pack_into(segs, [Wt_all[k, g] for k in range(n) for g in range(G)], P1)
+    Wt_all = take_packed(segs, P1)                 # packed ahead (pack_heads_ahead)?
+    if Wt_all is None:
+        Wt_all = _empty(n, G, meta.m2, K1, C, C, 2, like=inp)
+        _pack_into(segs, [Wt_all[k, g] for k in range(n) for g in range(G)], P1)
     for k in range(n):
         Wt = Wt_all[k]
         At = k_rowdft(src, Bn, C, P1, P2, meta.m2, act)
