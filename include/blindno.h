@@ -372,6 +372,14 @@ int blindno_reduce_partials_pieces_u(const void* const* partials, void* const* o
                                      const int* nchunks, const int* nps, const int* e0s,
                                      const int* e1s, const int* upks, void* const* ud,
                                      const int* ushp, int nseg, blindno_stream_t stream);
+/* The deferred finalisation in one launch: blindno_reduce_partials_pieces_u(...) and
+ * blindno_unpack_w2d_multi(dWts, dw1s, dw2s, shapes, nunp) together (independent work;
+ * bit-identical results); two launches when the segments do not fit one table. */
+int blindno_finish_multi(const void* const* partials, void* const* outs, const int* nchunks,
+                         const int* nps, const int* e0s, const int* e1s, const int* upks,
+                         void* const* ud, const int* ushp, int nseg, const void* const* dWts,
+                         void* const* dw1s, void* const* dw2s, const int* shapes, int nunp,
+                         blindno_stream_t stream);
 
 /* Pack reference-layout 2D weights (Ci,Co,m1,m2,2) x2 into Wt (m2,K1,Ci,Co) complex. */
 int blindno_pack_w2d(const float* w1, const float* w2, float* Wt, int Ci, int Co, int m1,

@@ -106,6 +106,7 @@ SIGNATURES = {
     "blindno_reduce_partials_multi": "ppppis",
     "blindno_reduce_partials_pieces": "ppppppis",
     "blindno_reduce_partials_pieces_u": "pppppppppis",
+    "blindno_finish_multi": "pppppppppippppis",
     "blindno_unpack_w2d_multi": "ppppis",
     "blindno_pack_w2d_multi": "ppppis",
     "blindno_fp_propagate": "pppiiiiiids",

@@ -371,15 +371,19 @@ class _Deferred:
             nd = max(1, len(descs))
             ud = (ctypes.c_void_p * (2 * nd))(*[v for d in descs for v in (d[0].data_ptr(), d[1].data_ptr())])
             ushp = (ctypes.c_int * (4 * nd))(*[v for d in descs for v in d[2]])
-            call("blindno_reduce_partials_pieces_u", srcs, outs, ncs, nps, e0s, e1s, upks, ud, ushp, n,
-                 stream_ptr())
+            red_args = (srcs, outs, ncs, nps, e0s, e1s, upks, ud, ushp, n)
+            if not rest:
+                call("blindno_reduce_partials_pieces_u", *red_args, stream_ptr())
         if rest:
             n = len(rest)
             srcs = (ctypes.c_void_p * n)(*[u[0].data_ptr() for u in rest])
             d1 = (ctypes.c_void_p * n)(*[u[1].data_ptr() for u in rest])
             d2 = (ctypes.c_void_p * n)(*[u[2].data_ptr() for u in rest])
             shp = (ctypes.c_int * (5 * n))(*[v for u in rest for v in u[3]])
-            call("blindno_unpack_w2d_multi", srcs, d1, d2, shp, n, stream_ptr())
+            if self.red:        # the reductions and the unpacks in one launch
+                call("blindno_finish_multi", *red_args, srcs, d1, d2, shp, n, stream_ptr())
+            else:
+                call("blindno_unpack_w2d_multi", srcs, d1, d2, shp, n, stream_ptr())
         self.mix, self.red, self.unp = [], [], []
 
 

@@ -15,6 +15,7 @@
 #include "blindno.h"
 #include "kernels.h"
 #include "wgrad.h"
+#include "packw.h"
 
 using namespace blindno;
 
@@ -1132,6 +1133,50 @@ BLINDNO_API int blindno_reduce_partials(const float* partial, float* out, int nc
   return (int)hipGetLastError();
 }
 
+// the deferred finalisation's reductions and unpacks in one launch (0: two launches, for A/B)
+#ifndef FINISH_ONE_LAUNCH
+#define FINISH_ONE_LAUNCH 1
+#endif
+// segments s0 .. s0 + k - 1 of a blindno_reduce_partials_pieces_u call -> ReduceSegs
+static int reduce_segs_build(const void* const* partials, void* const* outs, const int* nchunks,
+                             const int* nps, const int* e0s, const int* e1s, const int* upks,
+                             void* const* ud, const int* ushp, int s0, int k, ReduceSegs& segs,
+                             int& blocks) {
+  segs = ReduceSegs{};
+  segs.nseg = k;
+  blocks = 0;
+  int nu = 0;
+  for (int i = 0; i < k; ++i) {
+    const int nc = nchunks[s0 + i], np = nps[s0 + i];
+    const int e0 = e0s ? e0s[s0 + i] : 0, e1 = e1s ? e1s[s0 + i] : np;
+    if (nc < 1 || np < 1 || e0 < 0 || e1 > np || e0 >= e1) return (int)hipErrorInvalidValue;
+    segs.upk[i] = -1;
+    const int uq = upks ? upks[s0 + i] : -1;
+    if (uq >= 0) {
+      const int* sh = ushp + 4 * uq;      // (Ci, Co, m1, m2) of descriptor uq
+      if (nu == kRedUnpack || e0 != 0 || e1 != np || !ud[2 * uq] || !ud[2 * uq + 1] ||
+          sh[0] < 1 || sh[1] < 1 || sh[2] < 1 || sh[3] < 1 ||
+          (int64_t)4 * sh[0] * sh[1] * sh[2] * sh[3] != np)
+        return (int)hipErrorInvalidValue;
+      segs.ut[nu] = W2dUnpack{(float*)ud[2 * uq], (float*)ud[2 * uq + 1], sh[0], sh[1], sh[2], sh[3]};
+      segs.upk[i] = nu++;
+    }
+    segs.src[i] = (const float*)partials[s0 + i];
+    segs.out[i] = (float*)outs[s0 + i];
+    segs.nchunk[i] = nc;
+    segs.np[i] = np;
+    const int pb = np < 64 ? np : 64;
+    segs.pb[i] = pb;
+    segs.blk0[i] = e0 / pb;
+    segs.e0[i] = e0;
+    segs.e1[i] = e1;
+    segs.cum[i] = blocks;
+    blocks += cdiv(e1, pb) - e0 / pb;
+  }
+  segs.cum[k] = blocks;
+  return 0;
+}
+
 BLINDNO_API int blindno_reduce_partials_pieces_u(const void* const* partials, void* const* outs,
                                                  const int* nchunks, const int* nps,
                                                  const int* e0s, const int* e1s, const int* upks,
@@ -1139,41 +1184,80 @@ BLINDNO_API int blindno_reduce_partials_pieces_u(const void* const* partials, vo
                                                  void* stream) {
   if (nseg < 0) return (int)hipErrorInvalidValue;
   for (int s0 = 0; s0 < nseg; s0 += kRedSegs) {
-    ReduceSegs segs{};
+    ReduceSegs segs;
+    int blocks;
     const int k = nseg - s0 < kRedSegs ? nseg - s0 : kRedSegs;
-    segs.nseg = k;
-    int blocks = 0, nu = 0;
-    for (int i = 0; i < k; ++i) {
-      const int nc = nchunks[s0 + i], np = nps[s0 + i];
-      const int e0 = e0s ? e0s[s0 + i] : 0, e1 = e1s ? e1s[s0 + i] : np;
-      if (nc < 1 || np < 1 || e0 < 0 || e1 > np || e0 >= e1) return (int)hipErrorInvalidValue;
-      segs.upk[i] = -1;
-      const int uq = upks ? upks[s0 + i] : -1;
-      if (uq >= 0) {
-        const int* sh = ushp + 4 * uq;      // (Ci, Co, m1, m2) of descriptor uq
-        if (nu == kRedUnpack || e0 != 0 || e1 != np || !ud[2 * uq] || !ud[2 * uq + 1] ||
-            sh[0] < 1 || sh[1] < 1 || sh[2] < 1 || sh[3] < 1 ||
-            (int64_t)4 * sh[0] * sh[1] * sh[2] * sh[3] != np)
-          return (int)hipErrorInvalidValue;
-        segs.ut[nu] = W2dUnpack{(float*)ud[2 * uq], (float*)ud[2 * uq + 1], sh[0], sh[1], sh[2], sh[3]};
-        segs.upk[i] = nu++;
-      }
-      segs.src[i] = (const float*)partials[s0 + i];
-      segs.out[i] = (float*)outs[s0 + i];
-      segs.nchunk[i] = nc;
-      segs.np[i] = np;
-      const int pb = np < 64 ? np : 64;
-      segs.pb[i] = pb;
-      segs.blk0[i] = e0 / pb;
-      segs.e0[i] = e0;
-      segs.e1[i] = e1;
-      segs.cum[i] = blocks;
-      blocks += cdiv(e1, pb) - e0 / pb;
-    }
-    segs.cum[k] = blocks;
+    const int e = reduce_segs_build(partials, outs, nchunks, nps, e0s, e1s, upks, ud, ushp, s0, k,
+                                    segs, blocks);
+    if (e) return e;
     if (blocks == 0) continue;
     reduce_partials_multi_kernel<<<blocks, 1024, 0, (hipStream_t)stream>>>(segs);
   }
+  return (int)hipGetLastError();
+}
+
+// The deferred finalisation's reductions and its spectral-weight unpacks (independent of each
+// other) in ONE launch of 1024-thread workgroups: [0, nred) reduce exactly as
+// reduce_partials_multi_kernel, the rest run four 256-thread unpack tile teams each
+// (w2d_transpose_tile, as w2d_transpose_kernel<1>).  Bit-identical to the two launches.
+__global__ __launch_bounds__(1024) void finish_multi_kernel(ReduceSegs segs, PackSegs ps, int nred,
+                                                           int ntr) {
+  __shared__ float red[1024];
+  __shared__ float2 tile[4][32][33];
+  const int b = blockIdx.x;
+  if (b < nred) {
+    int sg = 0;
+    while (sg + 1 < segs.nseg && segs.cum[sg + 1] <= b) ++sg;  // uniform scan
+    const int u = segs.upk[sg];
+    reduce_partials_block(segs.src[sg], segs.out[sg], segs.nchunk[sg], segs.np[sg], segs.pb[sg],
+                          segs.blk0[sg] + b - segs.cum[sg], red, segs.e0[sg], segs.e1[sg], u >= 0,
+                          segs.ut[u >= 0 ? u : 0]);
+    return;
+  }
+  const int team = threadIdx.x >> 8;
+  const int tb = 4 * (b - nred) + team;
+  w2d_transpose_tile<1>(ps, tb < ntr ? tb : 0, threadIdx.x & 255, tile[team], tb < ntr);
+}
+
+BLINDNO_API int blindno_finish_multi(const void* const* partials, void* const* outs,
+                                     const int* nchunks, const int* nps, const int* e0s,
+                                     const int* e1s, const int* upks, void* const* ud,
+                                     const int* ushp, int nseg, const void* const* dWts,
+                                     void* const* dw1s, void* const* dw2s, const int* shapes,
+                                     int nunp, void* stream) {
+  if (nseg < 0 || nunp < 0) return (int)hipErrorInvalidValue;
+  // one launch when everything fits one segment table and every unpack takes the tiled path
+  bool one = nseg <= kRedSegs && nunp <= kPackSegs && nseg > 0 && nunp > 0 && FINISH_ONE_LAUNCH;
+  PackSegs ps{};
+  int64_t ntr = 0;
+  if (one) {
+    ps.nseg = nunp;
+    for (int i = 0; i < nunp; ++i) {
+      const int* sh = shapes + 5 * i;
+      if (sh[2] > sh[4] || sh[0] < 1 || sh[1] < 1 || sh[2] < 1 || sh[3] < 1 || !dWts[i] ||
+          !dw1s[i] || !dw2s[i])
+        return (int)hipErrorInvalidValue;
+      ps.w1[i] = (const float*)dw1s[i];
+      ps.w2[i] = (const float*)dw2s[i];
+      ps.Wt[i] = (float2*)const_cast<void*>(dWts[i]);
+      ps.Ci[i] = sh[0]; ps.Co[i] = sh[1]; ps.m1[i] = sh[2]; ps.m2[i] = sh[3]; ps.P1[i] = sh[4];
+    }
+    one = w2d_tiled_segs(ps, ntr);
+  }
+  if (!one) {
+    const int e = blindno_reduce_partials_pieces_u(partials, outs, nchunks, nps, e0s, e1s, upks, ud,
+                                                   ushp, nseg, stream);
+    if (e || nunp == 0) return e;
+    return blindno_unpack_w2d_multi(dWts, dw1s, dw2s, shapes, nunp, stream);
+  }
+  ReduceSegs segs;
+  int nred;
+  const int e = reduce_segs_build(partials, outs, nchunks, nps, e0s, e1s, upks, ud, ushp, 0, nseg,
+                                  segs, nred);
+  if (e) return e;
+  const int64_t nb = nred + (ntr + 3) / 4;
+  if (nb >= INT32_MAX) return (int)hipErrorInvalidValue;
+  finish_multi_kernel<<<(unsigned)nb, 1024, 0, (hipStream_t)stream>>>(segs, ps, nred, (int)ntr);
   return (int)hipGetLastError();
 }
 
