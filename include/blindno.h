@@ -472,11 +472,13 @@ int blindno_mse_finish(const float* partial, int nblk, int64_t n, float* loss,
  * launch instead of a separate add); acc may be NULL. */
 int blindno_mse_finish_acc(const float* partial, int nblk, int64_t n, float* loss, float* acc,
                            blindno_stream_t stream);
-/* blindno_mse (no gradient) + blindno_mse_finish_acc in ONE launch (bit-identical): the
- * workgroup that finishes last sums the partials.  counter: one unsigned in device memory,
- * zero before the first call; every call leaves it zero again. */
+/* blindno_mse + blindno_mse_finish_acc in ONE launch (bit-identical): the workgroup that
+ * finishes last sums the partials.  counter: one unsigned in device memory, zero before the
+ * first call; every call leaves it zero again.  grad (may be NULL): blindno_mse's gradient for
+ * gscale = 1 (a backward seeded with exactly 1 then needs no launch of its own). */
 int blindno_mse_fwd(const float* p, const float* t, float* partial, int64_t n, int nblk,
-                    float* loss, float* acc, unsigned* counter, blindno_stream_t stream);
+                    float* loss, float* acc, unsigned* counter, float* grad,
+                    blindno_stream_t stream);
 
 /* Per-row sums of squares in fp64 for relative-L2 metrics (2d_FPE/train_fno.py:160-163,
  * eval_fno.py:124-128, 2d_Non_conservative_FPE/compute_time_error.py:321-333).

@@ -65,7 +65,7 @@ SIGNATURES = {
     "blindno_mse": "pppplips",
     "blindno_mse_finish": "pilps",
     "blindno_mse_finish_acc": "pilpps",
-    "blindno_mse_fwd": "ppplippps",
+    "blindno_mse_fwd": "ppplipppps",
     "blindno_rowsq": "pppiiiiiis",
     "blindno_adam": "pppplffffffs",
     "blindno_gpe_solve": "ppppddiiipppiiis",

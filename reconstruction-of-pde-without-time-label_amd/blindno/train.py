@@ -14,6 +14,7 @@ gradients give Adam updates of exactly zero.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 import os
@@ -31,6 +32,9 @@ from ._lib import call, ptr, stream_ptr
 # the graphed step's deferred finalisation writes the gradients straight into the flat buffer
 # (BLINDNO_REDIRECT=0: into their own tensors, then one gather copy)
 REDIRECT_GRADS = os.environ.get("BLINDNO_REDIRECT", "1") != "0"
+# the loss's gradient for the step's unit seed formed in the loss's forward pass
+# (BLINDNO_UNIT_SEED=0: its own launch in backward)
+UNIT_SEED_LOSS = os.environ.get("BLINDNO_UNIT_SEED", "1") != "0"
 
 
 def _real(t: torch.Tensor) -> torch.Tensor:
@@ -256,6 +260,10 @@ class GraphedBagStep:
         self._ev = [None] * len(self._ring)
         self._k = 0
 
+    def _seeded(self):
+        """The loss's gradient for the unit seed formed in its forward pass (ops.unit_seed)."""
+        return ops.unit_seed(self._one) if UNIT_SEED_LOSS else contextlib.nullcontext()
+
     def _loss(self, out, accumulate):
         """The step's loss; with the fused MSE the running loss sum is accumulated by the loss
         kernel itself (no separate add launch)."""
@@ -268,7 +276,8 @@ class GraphedBagStep:
     def _body(self, L, accumulate=True):
         bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
         out = self.model(self.x, self.grid, bag_idx=bag)
-        loss, add = self._loss(out, accumulate)
+        with self._seeded():                          # backward is seeded with self._one
+            loss, add = self._loss(out, accumulate)
         with ops.deferred_reductions() as fin:        # one batched gradient finalisation,
             loss.backward(self._one)
             if REDIRECT_GRADS:                        # storing into the flat buffer
@@ -285,7 +294,8 @@ class GraphedBagStep:
         h = self.model.forward_encoder(self.x, self.grid, bag_idx=bag)
         hd = h.detach().requires_grad_(True)
         out = self.model.forward_heads(hd)
-        loss, add = self._loss(out, accumulate)
+        with self._seeded():
+            loss, add = self._loss(out, accumulate)
         with ops.deferred_reductions() as fin:
             loss.backward(self._one)
             if REDIRECT_GRADS:

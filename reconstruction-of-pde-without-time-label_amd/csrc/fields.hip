@@ -844,19 +844,24 @@ __global__ __launch_bounds__(kBlock) void mse_finish_kernel(const float* __restr
 // the workgroup that counts last (acquire fence) sums the partials exactly as
 // mse_finish_kernel, writes the loss and resets the counter for the next launch (graph replays
 // reuse it).  Bit-identical to mse_kernel + mse_finish_kernel.
+// grad != NULL: also the gradient for a unit upstream gradient, 2 (p - t) / n (as mse_kernel
+// with gscale 1), for a backward seeded with exactly 1 (blindno.ops.MSEFn).
 __global__ __launch_bounds__(kBlock) void mse_fwd_fused_kernel(const float* __restrict__ p,
                                                                const float* __restrict__ t,
                                                                float* __restrict__ partial,
                                                                int64_t n, float* __restrict__ loss,
                                                                float* __restrict__ lsum,
-                                                               unsigned* __restrict__ counter) {
+                                                               unsigned* __restrict__ counter,
+                                                               float* __restrict__ grad) {
   __shared__ float red[kBlock];
   __shared__ unsigned last;
   float acc = 0.f;
+  const float gs = 1.0f * 2.0f / (float)n;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float d = p[i] - t[i];
     acc = fmaf(d, d, acc);
+    if (grad) grad[i] = gs * d;
   }
   red[threadIdx.x] = acc;
   __syncthreads();
@@ -1407,12 +1412,12 @@ BLINDNO_API int blindno_mse_finish_acc(const float* partial, int nblk, int64_t n
 }
 
 BLINDNO_API int blindno_mse_fwd(const float* p, const float* t, float* partial, int64_t n,
-                                int nblk, float* loss, float* acc, unsigned* counter,
+                                int nblk, float* loss, float* acc, unsigned* counter, float* grad,
                                 void* stream) {
   if (n < 1 || nblk < 1 || !p || !t || !partial || !loss || !counter)
     return (int)hipErrorInvalidValue;
   mse_fwd_fused_kernel<<<nblk, kBlock, 0, (hipStream_t)stream>>>(p, t, partial, n, loss, acc,
-                                                                 counter);
+                                                                 counter, grad);
   return (int)hipGetLastError();
 }
 
