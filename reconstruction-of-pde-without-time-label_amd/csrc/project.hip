@@ -40,8 +40,10 @@ constexpr int kFwdNP4 = PROJ_FWD_NP4;
 #ifndef PF_TPW
 #define PF_TPW 2
 #endif
+// point tiles per wave of the backward: 4 halves the workgroup partials of 2 (config C heads:
+// 3417 -> 3430 bags/s; 8: 3383, 1: 3405; profiles/r05/r05u_ab_project_bwd_tpw.txt)
 #ifndef PB_TPW
-#define PB_TPW 2
+#define PB_TPW 4
 #endif
 constexpr int kBwdNP4 = PROJ_BWD_NP4;
 // hidden-tile loop unroll of the backward (1: rolled)
