@@ -563,6 +563,24 @@ int blindno_lift_bwd_g(const float* dx0, const float* in, const float* w0, float
 /* lift_bwd_g with, when Xs != NULL, the spectral weight gradient mix_wgrad_g(Xs, Gs) -> dWt of
  * the heads' first layer (Ci = Co = C, Bn samples) in the same launch (mnsplit =
  * blindno_mix_wgrad_nsplit(Bn / G, ...); mpartial as mix_wgrad_g's). */
+/* The heads' lift on the bag mean's input formed on the fly (NIOFP2D_FNO: h = fc0([grid,
+ * ubar]) with fc0 = (bw (width, 3): gx, gy, u columns; bb), 2d_FPE/NIOModules.py:569-575):
+ * with ubar != NULL the lift reads ubar (B, N1 N2) and grid (N1 N2, 2) instead of in (Cin =
+ * width = 12), forming h exactly as blindno_bagmean_fwd_w with L = 1 and u scale invL; the
+ * adjoint writes d ubar (B, N1 N2) = blindno_bagmean_bwd's reduction (its 1 / L = invLb) into
+ * d_in instead of d h, and reduces fc0-of-the-heads' gradient against the same on-the-fly h.
+ * The bag-mean launches and the h field go.  ubar NULL: lift_fwd_g / lift_bwd_mix_g. */
+int blindno_lift_bag_ok(int G, int Bn, int N1, int N2, int Cin, int C, int P1, int P2);
+int blindno_lift_fwd_bag_g(const float* in, const float* w0, const float* b0, float* x0, int G,
+                           int64_t wgs, int Bn, int N1, int N2, int Cin, int C, int P1, int P2,
+                           const float* ubar, const float* grid, const float* bw, const float* bb,
+                           float invL, blindno_stream_t stream);
+int blindno_lift_bwd_bag_mix_g(const float* dx0, const float* in, const float* w0, float* d_in,
+                               float* partial, int nchunk, int G, int64_t wgs, int Bn, int N1,
+                               int N2, int Cin, int C, int P1, int P2, const float* Xs,
+                               const float* Gs, float* dWt, float* mpartial, int mnsplit, int K1,
+                               int m2, const float* ubar, const float* grid, const float* bw,
+                               const float* bb, float invL, float invLb, blindno_stream_t stream);
 int blindno_lift_bwd_mix_g(const float* dx0, const float* in, const float* w0, float* d_in,
                            float* partial, int nchunk, int G, int64_t wgs, int Bn, int N1, int N2,
                            int Cin, int C, int P1, int P2, const float* Xs, const float* Gs,

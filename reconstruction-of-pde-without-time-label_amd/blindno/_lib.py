@@ -79,8 +79,11 @@ SIGNATURES = {
     "blindno_project_bwd_nchunk": "iii",
     "blindno_mix_wgrad_nsplit": "iiiii",
     "blindno_lift_fwd_g": "ppppiliiiiiiis",
+    "blindno_lift_fwd_bag_g": "ppppiliiiiiiippppfs",
+    "blindno_lift_bag_ok": "iiiiiiii",
     "blindno_lift_bwd_g": "pppppiiliiiiiiis",
     "blindno_lift_bwd_mix_g": "pppppiiliiiiiiippppiiis",
+    "blindno_lift_bwd_bag_mix_g": "pppppiiliiiiiiippppiiippppffs",
     "blindno_project_fwd_g": "ppppppiliiiiiiiiiis",
     "blindno_project_bwd_g": "pppppppiiliiiiiiiiiis",
     "blindno_colpass_g": "pppppppiliiiiiiiis",

@@ -62,6 +62,9 @@ HEAD_STREAMS = True     # fork the two heads over two streams (ops.HeadPairFn)
 # the grouped heads' spectral weights packed by the encoder's pack launch (BLINDNO_PACK_AHEAD=0:
 # their own launch)
 PACK_HEADS_AHEAD = os.environ.get("BLINDNO_PACK_AHEAD", "1") != "0"
+# the encoder hands the grouped heads the bag mean ubar, the heads' lift forms their input
+# (BLINDNO_BAG_HEADS=0: the (B, N, N, width) field between them and two bag-mean launches)
+BAG_INPUT_HEADS = os.environ.get("BLINDNO_BAG_HEADS", "1") != "0"
 DEDUP_BAGS = True       # run the snapshot encoder once per distinct snapshot of a bag
 
 
@@ -150,9 +153,65 @@ class NIOFP2D_FNO(nn.Module):
                 ops.pack_heads_ahead(hs[0].meta(w), (x.shape[0], x.shape[2], x.shape[3], w),
                                      [fno_params(hd, 2) for hd in hs], x.device)
         try:
+            out = self._encoder_heads_fused(x, grid, bag_idx)
+            if out is not None:
+                return out
             return self.forward_heads(self.forward_encoder(x, grid, bag_idx))
         finally:
             ops.drop_pack_ahead()
+
+    def _encoder_heads_fused(self, x, grid, bag_idx):
+        """Encoder -> grouped heads with the bag mean handed over as ubar (B, Nx, Ny): the heads'
+        lift forms fc0([grid, ubar]) itself and its adjoint returns d ubar (ops.BagHeadsIn), so
+        the (B, Nx, Ny, width) field and the two bag-mean launches do not exist.  None where it
+        does not apply (the composition forward_heads(forward_encoder(...)) then runs)."""
+        if not (BAG_INPUT_HEADS and HEAD_STREAMS and len(self._heads) == 2 and self._fused_ok(x, grid)):
+            return None
+        hs = [getattr(self, nm) for nm in self._heads]
+        if not all(isinstance(hd, FNO2d) for hd in hs):
+            return None
+        w = self.fc0.out_features
+        m0, m1 = hs[0].meta(w), hs[1].meta(w)
+        p0, p1 = fno_params(hs[0], 2), fno_params(hs[1], 2)
+        if m0.__dict__ != m1.__dict__ or not ops.GROUPED_HEADS or \
+                not ops.grouped_ok(m0, (x.shape[0], x.shape[2], x.shape[3], w), [p0, p1]):
+            return None
+        fno = self.FNO_input
+        fp = fno_params(fno, 2)
+        n = len(fno.spectral_list)
+        idx_t, lw = self._encoder_bag(x, bag_idx)
+        if not ops.bag_ubar_ok(fno.meta(3), x.shape[0], idx_t.numel(), x.shape[2], x.shape[3],
+                               fp[2 + 4 * n], fp[4 + 4 * n], m0, 2, w):
+            return None
+        ubar = ops.BagEncoderFn.apply(fno.meta(3), True, x, idx_t, lw, grid, self.fc0.weight.data,
+                                      self.fc0.bias.data, *fp)
+        side = _SIDE.get(x.device)
+        if side is None:
+            side = _SIDE[x.device] = torch.cuda.Stream(x.device)
+        bag = ops.BagHeadsIn(grid, self.fc0.weight.data, self.fc0.bias.data)
+        return ops.HeadPairFn.apply((m0, bag), m1, len(p0), side, ubar, *p0, *p1)
+
+    def _encoder_bag(self, x, bag_idx):
+        """(device bag indices, multiplicity weights or None) of the fused encoder."""
+        lw = None
+        if isinstance(bag_idx, tuple):
+            # device-resident deduplicated bag (train.GraphedBagStep): unique indices and
+            # multiplicity weights
+            idx_t, lw = bag_idx
+        elif torch.is_tensor(bag_idx) and bag_idx.is_cuda and bag_idx.dtype == torch.int32:
+            idx_t = bag_idx                  # device-resident bag indices
+        else:
+            if bag_idx is not None:
+                idx = np.asarray(bag_idx)
+            elif self.training:
+                _, idx = draw_bag(x.shape[1])
+            else:
+                idx = np.arange(x.shape[1])
+            idx, w = dedup_bag(idx)
+            idx_t = torch.as_tensor(idx, device=x.device)
+            if w is not None:
+                lw = torch.as_tensor(w, device=x.device)
+        return idx_t, lw
 
     def forward_heads(self, h):
         """The two FNO heads on the bag-mean field h (B, Nx, Ny, width) (:577-581)."""
@@ -164,25 +223,8 @@ class NIOFP2D_FNO(nn.Module):
         gradient all-reduce overlap the encoder's backward (train.GraphedBagStep, overlap)."""
         if self._fused_ok(x, grid):
             fno = self.FNO_input
-            lw = None
-            if isinstance(bag_idx, tuple):
-                # device-resident deduplicated bag (train.GraphedBagStep): unique indices and
-                # multiplicity weights
-                idx_t, lw = bag_idx
-            elif torch.is_tensor(bag_idx) and bag_idx.is_cuda and bag_idx.dtype == torch.int32:
-                idx_t = bag_idx                  # device-resident bag indices
-            else:
-                if bag_idx is not None:
-                    idx = np.asarray(bag_idx)
-                elif self.training:
-                    _, idx = draw_bag(x.shape[1])
-                else:
-                    idx = np.arange(x.shape[1])
-                idx, w = dedup_bag(idx)
-                idx_t = torch.as_tensor(idx, device=x.device)
-                if w is not None:
-                    lw = torch.as_tensor(w, device=x.device)
-            return ops.BagEncoderFn.apply(fno.meta(3), x, idx_t, lw, grid, self.fc0.weight.data,
+            idx_t, lw = self._encoder_bag(x, bag_idx)
+            return ops.BagEncoderFn.apply(fno.meta(3), False, x, idx_t, lw, grid, self.fc0.weight.data,
                                           self.fc0.bias.data, *fno_params(fno, 2))
         x, L, lw = _select(self, x, bag_idx, dedup=True)
         B, _, nx, ny = x.shape

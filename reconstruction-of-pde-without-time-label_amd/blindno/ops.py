@@ -978,18 +978,23 @@ class _GroupWeights:
         return ptr(self.base[i]) if self.base is not None else ptr(_sub(self.buf, self.offs[i]))
 
 
-def fno_forward_grouped(meta: FNOMeta, inp, prms):
-    """Both heads' FNO2d forward in one chain; returns (out (Bg, Ho, Wo, G*Cout), saved)."""
+def fno_forward_grouped(meta: FNOMeta, inp, prms, bag=None):
+    """Both heads' FNO2d forward in one chain; returns (out (Bg, Ho, Wo, G*Cout), saved).
+    ``bag`` (BagHeadsIn): inp is the bag mean ubar, the lift forms the heads' input."""
     G = len(prms)
-    Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
+    Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp if bag is None else bag.shape(inp), meta)
     Bn = G * Bg
     C, n = meta.width, meta.n_layers
     smalls = [_small_params(p, n, 2) for p in prms]
     small = _GroupWeights(smalls)
     S = small.S
     x0 = _empty(Bn, C, P1, P2, like=inp)
-    call("blindno_lift_fwd_g", ptr(inp), small.p(0), small.p(1), ptr(x0),
-         G, S, Bn, N1, N2, Cin, C, P1, P2, stream_ptr())
+    if bag is None:
+        call("blindno_lift_fwd_g", ptr(inp), small.p(0), small.p(1), ptr(x0),
+             G, S, Bn, N1, N2, Cin, C, P1, P2, stream_ptr())
+    else:
+        call("blindno_lift_fwd_bag_g", None, small.p(0), small.p(1), ptr(x0), G, S, Bn, N1, N2, Cin, C,
+             P1, P2, ptr(inp), ptr(bag.grid), ptr(bag.w), ptr(bag.b), 1.0, stream_ptr())
     K1 = kept_rows_count(meta.m1, P1)
     K1p = 16 * ((K1 + 15) // 16)
     FB, GB = twiddle_cols(P1, meta.m1, inp.device)
@@ -1044,10 +1049,11 @@ def _padded_grad_buffer(shape, device):
     return t
 
 
-def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
-    """Adjoint of fno_forward_grouped: (d_inp summed over the heads, [grads of head g])."""
+def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad, bag=None):
+    """Adjoint of fno_forward_grouped: (d_inp summed over the heads, [grads of head g]); with
+    ``bag`` d_inp is d ubar."""
     G = len(prms)
-    Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp, meta)
+    Bg, N1, N2, Cin, P1, P2, Ho, Wo = _fno_geometry(inp if bag is None else bag.shape(inp), meta)
     Bn = G * Bg
     C, n = meta.width, meta.n_layers
     small, x0, Xs, Wts, zs = saved
@@ -1163,9 +1169,16 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad):
     if pending is not None:            # the first layer's mix gradient in the lift's launch
         dWt, part = mix_buffers()
         mx = (pending[1], pending[2], dWt, part)
-    call("blindno_lift_bwd_mix_g", ptr(dz), ptr(inp), small.p(0), ptr(d_inp), ptr(partial), nchunk, G,
-         S, Bn, N1, N2, Cin, C, P1, P2, *[ptr(t) if t is not None else None for t in mx], ns, K1,
-         meta.m2, stream_ptr())
+    if bag is None:
+        call("blindno_lift_bwd_mix_g", ptr(dz), ptr(inp), small.p(0), ptr(d_inp), ptr(partial), nchunk, G,
+             S, Bn, N1, N2, Cin, C, P1, P2, *[ptr(t) if t is not None else None for t in mx], ns, K1,
+             meta.m2, stream_ptr())
+    else:
+        if d_inp is None:
+            d_inp = torch.empty_like(inp)       # the merged kernel always forms d ubar
+        call("blindno_lift_bwd_bag_mix_g", ptr(dz), None, small.p(0), ptr(d_inp), ptr(partial), nchunk,
+             G, S, Bn, N1, N2, Cin, C, P1, P2, *[ptr(t) if t is not None else None for t in mx], ns,
+             K1, meta.m2, ptr(inp), ptr(bag.grid), ptr(bag.w), ptr(bag.b), 1.0, 1.0, stream_ptr())
     if pending is not None:
         mix_grads(pending[0], dWt)
     gl = reduce_partials(partial, nchunk, G * np_l).view(G, np_l)
@@ -1188,13 +1201,21 @@ class HeadPairFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, meta0, meta1, n0, side, h, *prm):
+        """``meta0`` may be (meta0, BagHeadsIn): h is then the bag mean ubar (grouped path)."""
+        bag = None
+        if isinstance(meta0, tuple):
+            meta0, bag = meta0
         require_device(h, *prm)
         h = _c(h)
         prm = [_c(p) for p in prm]
         p0, p1 = prm[:n0], prm[n0:]
-        ctx.grouped = GROUPED_HEADS and meta0.__dict__ == meta1.__dict__ and grouped_ok(meta0, h, [p0, p1])
+        hin = h if bag is None else bag.shape(h)
+        ctx.grouped = GROUPED_HEADS and meta0.__dict__ == meta1.__dict__ and grouped_ok(meta0, hin, [p0, p1])
+        ctx.bag = bag
+        if bag is not None and not ctx.grouped:
+            raise BlindnoError("HeadPairFn: a bag-mean input needs the grouped heads")
         if ctx.grouped:
-            out, saved = fno_forward_grouped(meta0, h, [p0, p1])
+            out, saved = fno_forward_grouped(meta0, h, [p0, p1], bag=bag)
             ctx.save_for_backward(h, *prm)
             ctx.meta = (meta0, meta1, n0, side, None)
             ctx.s0, ctx.s1 = saved, None
@@ -1222,8 +1243,8 @@ class HeadPairFn(torch.autograd.Function):
         need = ctx.needs_input_grad[4]
         gout = _c(gout)
         if ctx.grouped:
-            dh, gr = fno_backward_grouped(meta0, h, [p0, p1], ctx.s0, gout, need)
-            ctx.s0 = None
+            dh, gr = fno_backward_grouped(meta0, h, [p0, p1], ctx.s0, gout, need, bag=ctx.bag)
+            ctx.s0 = ctx.bag = None
             grads = [g if ctx.needs_input_grad[5 + i] else None for i, g in enumerate(gr[0] + gr[1])]
             return (None, None, None, None, dh, *grads)
         g0 = gout[..., :c0].contiguous()
@@ -1344,6 +1365,41 @@ class _ColSpec:
         return Xs, Y
 
 
+def _bag_stats_ok(B, L, C, P1, P2, Ho, Wo, Hd, Cout):
+    """The bag-level projection (csrc/bagproj.hip) applies: fc1 of 128, one output channel."""
+    if not (BAG_STATS and Hd == 128 and Cout == 1 and L <= 1024):
+        return False
+    nstats = query("blindno_project_bag_stats_floats", B, Ho, Wo)
+    return 4 * (nstats + B * L * C * P1 * P2) <= BAG_STATS_MAX_BYTES
+
+
+def bag_ubar_ok(meta, B, L, N1, N2, fc1w, fc2w, head_meta, G, width):
+    """BagEncoderFn can hand its heads the bag mean ubar itself (emit_ubar), and the G grouped
+    heads' lift kernels take it (blindno_lift_bag_ok: the 12-channel wide lift forms)."""
+    fake = (B * L, N1, N2, 3)
+    _, _, _, _, P1, P2, Ho, Wo = _fno_geometry(fake, meta)
+    if not _bag_stats_ok(B, L, meta.width, P1, P2, Ho, Wo, fc1w.shape[0], fc2w.shape[0]):
+        return False
+    hP1, hP2 = _fno_geometry((B, N1, N2, width), head_meta)[4:6]
+    return query("blindno_lift_bag_ok", G, G * B, N1, N2, width, head_meta.width, hP1, hP2) == 1
+
+
+class BagHeadsIn:
+    """The grouped heads' input given as the bag mean of the snapshot projections ubar (B, N1,
+    N2) plus the fixed fc0 (bw (width, 3), bb) that maps [gx, gy, ubar] to the heads' width
+    (NIOFP2D_FNO, 2d_FPE/NIOModules.py:569-575): the heads' lift forms that field on the fly
+    and its adjoint returns d ubar (blindno_lift_fwd_bag_g / blindno_lift_bwd_bag_mix_g), so
+    neither the (B, N1, N2, width) field nor the bag-mean launches exist.  Passed to
+    HeadPairFn as (meta0, BagHeadsIn)."""
+
+    def __init__(self, grid, bw, bb):
+        self.grid, self.w, self.b = _c(grid), _c(bw.detach()), _c(bb.detach())
+        self.width = bw.shape[0]
+
+    def shape(self, ubar):
+        return (ubar.shape[0], ubar.shape[1], ubar.shape[2], self.width)
+
+
 class BagEncoderFn(torch.autograd.Function):
     """The snapshot-bag encoder of NIOFP2D_FNO as ONE autograd node (2d_FPE/NIOModules.py:
     548-575): FNO_input (an FNO2d of input [u, gx, gy]) on every snapshot of the bag, then the
@@ -1362,7 +1418,10 @@ class BagEncoderFn(torch.autograd.Function):
     per-bag gradient by lw (exact up to fp32 summation order)."""
 
     @staticmethod
-    def forward(ctx, meta, X, idx_t, lw, grid, bw, bb, *prm):
+    def forward(ctx, meta, emit_ubar, X, idx_t, lw, grid, bw, bb, *prm):
+        """``emit_ubar``: return the bag mean of the projections ubar (B, N1, N2) instead of the
+        fc0 (bw, bb) of [grid, ubar] -- the grouped heads form that field themselves
+        (BagHeadsIn); only where bag_ubar_ok holds."""
         require_device(X, grid, *prm)
         X, grid = _c(X), _c(grid)
         prm = [_c(p) for p in prm]
@@ -1457,21 +1516,22 @@ class BagEncoderFn(torch.autograd.Function):
         width = bw.shape[0]
         h = _empty(B, S, width, like=X)
         ctx.bag = None
-        nstats = query("blindno_project_bag_stats_floats", B, Ho, Wo) if Hd == 128 else 0
-        if (BAG_STATS and Hd == 128 and Cout == 1 and L <= 1024
-                and 4 * (nstats + Bn * C * P1 * P2) <= BAG_STATS_MAX_BYTES):
+        if _bag_stats_ok(B, L, C, P1, P2, Ho, Wo, Hd, Cout):
             # projection + bag mean at bag level: the backward becomes a reduction of the
             # statistics the forward leaves (csrc/bagproj.hip).  stats and v are fresh buffers
             # only this forward writes and only this backward reads (never handed to the caller),
             # so they ride on ctx without save_for_backward's version check
             ubar = _empty(B, S, like=X)
-            stats = _empty(nstats, like=X)
+            stats = _empty(query("blindno_project_bag_stats_floats", B, Ho, Wo), like=X)
             v = _empty(Bn, C, P1, P2, like=X)
             call("blindno_project_bag_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b),
                  ptr(lw), ptr(ubar), ptr(stats), ptr(v), B, L, C, P1, P2, Ho, Wo, Hd, stream_ptr())
-            call("blindno_bagmean_fwd_w", ptr(ubar), ptr(grid), ptr(bw), ptr(bb), None, ptr(h), B, 1, S,
-                 2, width, stream_ptr())
+            if not emit_ubar:
+                call("blindno_bagmean_fwd_w", ptr(ubar), ptr(grid), ptr(bw), ptr(bb), None, ptr(h), B, 1,
+                     S, 2, width, stream_ptr())
             ctx.bag = (stats, v)
+        elif emit_ubar:
+            raise BlindnoError("BagEncoderFn: emit_ubar needs the bag-level projection (bag_ubar_ok)")
         else:
             u = _empty(Bn, Ho, Wo, Cout, like=X)
             call("blindno_project_fwd", ptr(zs[-1]), ptr(fc1w), ptr(fc1b), ptr(fc2w), ptr(fc2b), ptr(u),
@@ -1480,7 +1540,10 @@ class BagEncoderFn(torch.autograd.Function):
                  2, width, stream_ptr())
         ctx.meta, ctx.n, ctx.dims = meta, n, (B, T, L, N1, N2, C, P1, P2, Ho, Wo, Hd, Cout, width)
         ctx.lw = lw
+        ctx.emit_ubar = bool(emit_ubar)
         ctx.save_for_backward(X, idx_t, grid, bw, *Xs, *Wts, *zs, *prm)
+        if emit_ubar:
+            return ubar.view(B, N1, N2)
         return h.view(B, N1, N2, width)
 
     @staticmethod
@@ -1494,13 +1557,17 @@ class BagEncoderFn(torch.autograd.Function):
         Bn, S = B * L, Ho * Wo
         gh = _c(gh)
         grads = [None] * len(prm)
-        # bag mean: every snapshot of bag b receives the same gradient s[b]
-        sgr = _empty(B, S, like=gh)
+        # bag mean: every snapshot of bag b receives the same gradient s[b] (emit_ubar: the
+        # heads' lift adjoint handed back d ubar = s itself)
         lw = ctx.lw
         bag = ctx.bag
         ctx.bag = None
-        call("blindno_bagmean_bwd", ptr(gh), ptr(bw), ptr(sgr), B, S, 2, width,
-             1 if (lw is not None or bag is not None) else L, stream_ptr())
+        if ctx.emit_ubar:
+            sgr = gh.view(B, S)
+        else:
+            sgr = _empty(B, S, like=gh)
+            call("blindno_bagmean_bwd", ptr(gh), ptr(bw), ptr(sgr), B, S, 2, width,
+                 1 if (lw is not None or bag is not None) else L, stream_ptr())
         # projection (dout read per bag: dout_div = L)
         off_fc1 = 2 + 4 * n
         fc1w, fc1b, fc2w = prm[off_fc1:off_fc1 + 3]
@@ -1611,8 +1678,8 @@ class BagEncoderFn(torch.autograd.Function):
                 grads[0] = g[C * C + C:C * C + 4 * C].view(C, 3)
                 grads[1] = g[C * C + 4 * C:]
         ctx.lw = None
-        grads = [gr if ctx.needs_input_grad[7 + i] else None for i, gr in enumerate(grads)]
-        return (None, None, None, None, None, None, None, *grads)
+        grads = [gr if ctx.needs_input_grad[8 + i] else None for i, gr in enumerate(grads)]
+        return (None, None, None, None, None, None, None, None, *grads)
 
 
 # ---------------------------------------------------------------------------- bag mean

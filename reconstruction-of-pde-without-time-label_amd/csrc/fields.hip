@@ -19,6 +19,11 @@
 
 using namespace blindno;
 
+// the heads' lift input and weight gradients in one launch (0: two launches, for A/B)
+#ifndef LIFT_BWD_BOTH
+#define LIFT_BWD_BOTH 1
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------- lift
@@ -127,11 +132,40 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_kernel(const float* __rest
 // invariant divisors.  Forward writes all C channels of x0 (zero on the padding); the input
 // gradient sums the groups' fields: d_in[n'][h][w][j] = sum_g sum_c W_g[c][j] dx0[g Bg + n'][c].
 constexpr int kLiftMaxG = 4, kLiftMaxC = 16;
+
+// The heads' input h formed on the fly from the bag mean instead of read from a materialised
+// (B, N1, N2, width) field (NIOFP2D_FNO: h = fc0([grid, ubar]), 2d_FPE/NIOModules.py:569-575;
+// bagmean_fwd_kernel below): the heads' lift reads ubar (1 value per point) and the grid, and
+// its adjoint hands back d ubar (bagmean_bwd_kernel's reduction) -- no h written or read, two
+// launches less.  Every value is formed with bagmean_fwd / _bwd's own fma order
+// (bit-identical).
+struct BagIn {
+  const float* u;      // ubar (B, N1 N2); nullptr: the input is a materialised field
+  const float* grid;   // (N1 N2, 2)
+  const float* w;      // fc0 weight (width, 3): gx, gy, u
+  const float* bias;   // (width)
+  float invL;          // the u scale of bagmean_fwd (1 for a bag-level ubar)
+  float invLb;         // the 1 / L of bagmean_bwd
+};
+// h[p][j], j < CIN, at point p (flattened over (B, N1 N2)) with grid point s
+template <int CIN>
+__device__ __forceinline__ void bag_point(const BagIn& bi, unsigned p, unsigned s, float (&v)[CIN]) {
+  const float uu = bi.u[p];
+  const float g0 = bi.grid[2 * s], g1 = bi.grid[2 * s + 1];
+#pragma unroll
+  for (int j = 0; j < CIN; ++j) {
+    float a = bi.bias[j];
+    a = fmaf(bi.w[j * 3], g0, a);
+    a = fmaf(bi.w[j * 3 + 1], g1, a);
+    v[j] = fmaf(bi.w[j * 3 + 2] * bi.invL, uu, a);
+  }
+}
+
 template <int CIN, int CM>
 __global__ __launch_bounds__(kBlock) void lift_fwd_wide_kernel(
     const float* __restrict__ in, const float* __restrict__ w0, const float* __restrict__ b0,
     float* __restrict__ x0, int Bn, int N1, int N2, int C, int P1, int P2, int Bg, int G,
-    int64_t wgs, FastDiv dHW, FastDiv dP2) {
+    int64_t wgs, FastDiv dHW, FastDiv dP2, BagIn bi) {
   __shared__ float sw[kLiftMaxG][CM * CIN + CM];
   for (int e = threadIdx.x; e < G * (CM * CIN + CM); e += blockDim.x) {
     const int g = e / (CM * CIN + CM), q = e - g * (CM * CIN + CM);
@@ -159,12 +193,16 @@ __global__ __launch_bounds__(kBlock) void lift_fwd_wide_kernel(
     }
     const int g = G > 1 ? (int)(n / (unsigned)Bg) : 0;
     const unsigned ni = n - (unsigned)g * (unsigned)Bg;
-    const float4* ip = reinterpret_cast<const float4*>(in + ((size_t)(ni * N1 + h) * N2 + w) * CIN);
     float v[CIN];
+    if (bi.u) {
+      bag_point<CIN>(bi, (ni * N1 + h) * N2 + w, h * N2 + w, v);
+    } else {
+      const float4* ip = reinterpret_cast<const float4*>(in + ((size_t)(ni * N1 + h) * N2 + w) * CIN);
 #pragma unroll
-    for (int q = 0; q < CIN / 4; ++q) {
-      const float4 t = ip[q];
-      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      for (int q = 0; q < CIN / 4; ++q) {
+        const float4 t = ip[q];
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      }
     }
     const float* wg = sw[g];
 #pragma unroll
@@ -183,7 +221,7 @@ template <int CIN, int CM>
 __device__ __forceinline__ void lift_bwd_in_wide_block(
     const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in, int Bn,
     int N1, int N2, int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2, int bx,
-    int gx) {
+    int gx, BagIn bi) {
   __shared__ float sw[kLiftMaxG][CM * CIN];
   for (int e = threadIdx.x; e < G * CM * CIN; e += blockDim.x) {
     const int g = e / (CM * CIN), q = e - g * (CM * CIN);
@@ -210,6 +248,14 @@ __device__ __forceinline__ void lift_bwd_in_wide_block(
         for (int j = 0; j < CIN; ++j) acc[j] = fmaf(wg[c * CIN + j], d, acc[j]);
       }
     }
+    if (bi.u) {
+      // d ubar: bagmean_bwd_kernel's reduction of d h over the channels
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < CIN; ++j) v = fmaf(bi.w[j * 3 + 2] * bi.invLb, acc[j], v);
+      d_in[idx] = v;
+      continue;
+    }
     float4* op = reinterpret_cast<float4*>(d_in + (size_t)idx * CIN);
 #pragma unroll
     for (int q = 0; q < CIN / 4; ++q) op[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
@@ -221,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void lift_bwd_in_wide_kernel(
     const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in, int Bn,
     int N1, int N2, int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2) {
   lift_bwd_in_wide_block<CIN, CM>(dx0, w0, d_in, Bn, N1, N2, C, P1, P2, G, wgs, dS, dN2, blockIdx.x,
-                                  gridDim.x);
+                                  gridDim.x, BagIn{});
 }
 
 // Tiled outer-product reductions: partial[block][a*Cb + b] = sum_p A[a][p] B[b][p] and
@@ -372,7 +418,8 @@ __device__ __forceinline__ void lift_bwd_w_mfma_block(const float* __restrict__ 
                                                       const float* __restrict__ in,
                                                       float* __restrict__ partial, int Bn, int N1,
                                                       int N2, int Cin, int C, int P1, int P2,
-                                                      int bx, int gx, int grp, int gy) {
+                                                      int bx, int gx, int grp, int gy,
+                                                      BagIn bi) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   __shared__ f32x4 sacc[4][JT][64];
   const int lane = threadIdx.x & 63;
@@ -394,12 +441,37 @@ __device__ __forceinline__ void lift_bwd_w_mfma_block(const float* __restrict__ 
       a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
     }
     const float* ip = in + (r * N2 + w0) * Cin;    // point (n, h, w0), channels-last
+    float bu[4], bg0[4], bg1[4];                   // bag input: ubar and the grid at the 4 points
+    if (bi.u) {
+      const int64_t pp = r * N2 + w0;
+      const int sp = h * N2 + w0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bu[s] = bi.u[pp + s];
+        bg0[s] = bi.grid[2 * (sp + s)];
+        bg1[s] = bi.grid[2 * (sp + s) + 1];
+      }
+    }
 #pragma unroll
     for (int t = 0; t < JT; ++t) {
       const int j = 16 * t + c16;
       float b[4];
+      if (bi.u) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) b[s] = j < Cin ? ip[s * Cin + j] : (j == Cin ? 1.0f : 0.f);
+        for (int s = 0; s < 4; ++s) {
+          if (j < Cin) {
+            float a = bi.bias[j];
+            a = fmaf(bi.w[j * 3], bg0[s], a);
+            a = fmaf(bi.w[j * 3 + 1], bg1[s], a);
+            b[s] = fmaf(bi.w[j * 3 + 2] * bi.invL, bu[s], a);
+          } else {
+            b[s] = j == Cin ? 1.0f : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[s] = j < Cin ? ip[s * Cin + j] : (j == Cin ? 1.0f : 0.f);
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc[t], 0, 0, 0);
     }
@@ -425,7 +497,7 @@ __global__ __launch_bounds__(256) void lift_bwd_w_mfma_kernel(const float* __res
                                                               int N1, int N2, int Cin, int C,
                                                               int P1, int P2) {
   lift_bwd_w_mfma_block<JT>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2, blockIdx.x, gridDim.x,
-                            blockIdx.y, gridDim.y);
+                            blockIdx.y, gridDim.y, BagIn{});
 }
 
 // The heads' lift backward in one launch: its input gradient (workgroups [0, nbi)) and its
@@ -437,16 +509,17 @@ __global__ __launch_bounds__(256) void lift_bwd_both_kernel(
     const float* __restrict__ dx0, const float* __restrict__ w0, float* __restrict__ d_in,
     const float* __restrict__ in, float* __restrict__ partial, int Bn, int N1, int N2, int Cin,
     int C, int P1, int P2, int G, int64_t wgs, FastDiv dS, FastDiv dN2, int nbi, int nchunk,
-    MixWgradJob mw) {
+    MixWgradJob mw, BagIn bi) {
   const int b = blockIdx.x;
   if (b < nbi) {
-    lift_bwd_in_wide_block<12, 16>(dx0, w0, d_in, Bn, N1, N2, C, P1, P2, G, wgs, dS, dN2, b, nbi);
+    lift_bwd_in_wide_block<12, 16>(dx0, w0, d_in, Bn, N1, N2, C, P1, P2, G, wgs, dS, dN2, b, nbi,
+                                   bi);
     return;
   }
   int r = b - nbi;
   if (r < nchunk * G) {
     lift_bwd_w_mfma_block<JT>(dx0, in, partial, Bn, N1, N2, Cin, C, P1, P2, r % nchunk, nchunk,
-                              r / nchunk, G);
+                              r / nchunk, G, bi);
     return;
   }
   r -= nchunk * G;
@@ -949,22 +1022,58 @@ BLINDNO_API const char* blindno_error_string(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
+BLINDNO_API int blindno_lift_fwd_bag_g(const float* in, const float* w0, const float* b0,
+                                       float* x0, int G, int64_t wgs, int Bn, int N1, int N2,
+                                       int Cin, int C, int P1, int P2, const float* ubar,
+                                       const float* grid, const float* bw, const float* bb,
+                                       float invL, void* stream);
+
+// the shapes for which lift_fwd_bag_g and lift_bwd_bag_mix_g take a bag-mean input (the wide
+// 12-channel lift forms, the merged adjoint with its matrix-core weight gradient)
+BLINDNO_API int blindno_lift_bag_ok(int G, int Bn, int N1, int N2, int Cin, int C, int P1,
+                                    int P2) {
+  if (G < 1 || Bn % G || N1 > P1 || N2 > P2) return 0;
+  const int Bg = Bn / G;
+  const int64_t npts = (int64_t)Bn * P1 * P2;
+  const bool fwd = Cin == 12 && C > 4 && C <= kLiftMaxC && G <= kLiftMaxG &&
+                   npts * (C > Cin ? C : Cin) < INT32_MAX;
+  const bool bwd = Cin == 12 && C <= kLiftMaxC && G <= kLiftMaxG &&
+                   (int64_t)Bn * C * P1 * P2 < INT32_MAX && (int64_t)Bg * N1 * N2 * Cin < INT32_MAX &&
+                   C >= 5 && C <= 16 && N2 % 16 == 0 && P2 % 4 == 0 && LIFT_BWD_BOTH;
+  return fwd && bwd ? 1 : 0;
+}
+
+
+
 BLINDNO_API int blindno_lift_fwd_g(const float* in, const float* w0, const float* b0, float* x0,
                                    int G, int64_t wgs, int Bn, int N1, int N2, int Cin, int C,
                                    int P1, int P2, void* stream) {
+  return blindno_lift_fwd_bag_g(in, w0, b0, x0, G, wgs, Bn, N1, N2, Cin, C, P1, P2, nullptr,
+                                nullptr, nullptr, nullptr, 1.0f, stream);
+}
+
+BLINDNO_API int blindno_lift_fwd_bag_g(const float* in, const float* w0, const float* b0,
+                                       float* x0, int G, int64_t wgs, int Bn, int N1, int N2,
+                                       int Cin, int C, int P1, int P2, const float* ubar,
+                                       const float* grid, const float* bw, const float* bb,
+                                       float invL, void* stream) {
   if (N1 > P1 || N2 > P2 || G < 1 || Bn % G) return (int)hipErrorInvalidValue;
+  const BagIn bi{ubar, grid, bw, bb, invL, 1.0f};
+  if (ubar && (!grid || !bw || !bb || Cin != 12 || C <= 4 || C > kLiftMaxC || G > kLiftMaxG))
+    return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const int Bg = G > 1 ? Bn / G : Bn;
   if (G == 1) wgs = 0;
   const int64_t npts = (int64_t)Bn * P1 * P2;
   if (Cin == 12 && C > 4 && C <= kLiftMaxC && G <= kLiftMaxG && npts * (C > Cin ? C : Cin) < INT32_MAX &&
-      (((uintptr_t)in) & 15) == 0) {
+      (ubar || (((uintptr_t)in) & 15) == 0)) {
     // the heads (width 12): thread per point, weights in LDS (lift_fwd_wide_kernel)
     lift_fwd_wide_kernel<12, 16><<<grid_for(npts, kBlock, 8192), kBlock, 0, st>>>(
         in, w0, b0, x0, Bn, N1, N2, C, P1, P2, Bg, G, wgs, FastDiv::make((unsigned)(P1 * P2)),
-        FastDiv::make((unsigned)P2));
+        FastDiv::make((unsigned)P2), bi);
     return (int)hipGetLastError();
   }
+  if (ubar) return (int)hipErrorInvalidValue;
   if (C > 4 && C <= 16) {         // wide lifts (the heads): one thread per point, all channels
     const int64_t pts = (int64_t)Bn * P1 * P2;
     lift_fwd_pt_kernel<16><<<grid_for(4 * pts, kBlock, 65536), kBlock, 0, st>>>(
@@ -988,22 +1097,43 @@ BLINDNO_API int blindno_lift_bwd_nchunk(int Bn, int N1, int N2) {
   return nt < 1024 ? nt : 1024;
 }
 
-// the heads' lift input and weight gradients in one launch (0: two launches, for A/B)
-#ifndef LIFT_BWD_BOTH
-#define LIFT_BWD_BOTH 1
-#endif
+BLINDNO_API int blindno_lift_bwd_bag_mix_g(const float* dx0, const float* in, const float* w0,
+                                           float* d_in, float* partial, int nchunk, int G,
+                                           int64_t wgs, int Bn, int N1, int N2, int Cin, int C,
+                                           int P1, int P2, const float* Xs, const float* Gs,
+                                           float* dWt, float* mpartial, int mnsplit, int K1,
+                                           int m2, const float* ubar, const float* grid,
+                                           const float* bw, const float* bb, float invL,
+                                           float invLb, void* stream);
+
 BLINDNO_API int blindno_lift_bwd_mix_g(const float* dx0, const float* in, const float* w0,
                                        float* d_in, float* partial, int nchunk, int G,
                                        int64_t wgs, int Bn, int N1, int N2, int Cin, int C, int P1,
                                        int P2, const float* Xs, const float* Gs, float* dWt,
                                        float* mpartial, int mnsplit, int K1, int m2,
                                        void* stream) {
+  return blindno_lift_bwd_bag_mix_g(dx0, in, w0, d_in, partial, nchunk, G, wgs, Bn, N1, N2, Cin,
+                                    C, P1, P2, Xs, Gs, dWt, mpartial, mnsplit, K1, m2, nullptr,
+                                    nullptr, nullptr, nullptr, 1.0f, 1.0f, stream);
+}
+
+BLINDNO_API int blindno_lift_bwd_bag_mix_g(const float* dx0, const float* in, const float* w0,
+                                           float* d_in, float* partial, int nchunk, int G,
+                                           int64_t wgs, int Bn, int N1, int N2, int Cin, int C,
+                                           int P1, int P2, const float* Xs, const float* Gs,
+                                           float* dWt, float* mpartial, int mnsplit, int K1,
+                                           int m2, const float* ubar, const float* grid,
+                                           const float* bw, const float* bb, float invL,
+                                           float invLb, void* stream) {
   if (G < 1 || Bn % G) return (int)hipErrorInvalidValue;
+  const BagIn bi{ubar, grid, bw, bb, invL, invLb};
+  if (ubar && (!grid || !bw || !bb)) return (int)hipErrorInvalidValue;
   const int Bg = Bn / G;
   hipStream_t st = (hipStream_t)stream;
   const bool wide_in = d_in && Cin == 12 && C <= kLiftMaxC && G <= kLiftMaxG &&
                        (int64_t)Bn * C * P1 * P2 < INT32_MAX &&
-                       (int64_t)Bg * N1 * N2 * Cin < INT32_MAX && (((uintptr_t)d_in) & 15) == 0;
+                       (int64_t)Bg * N1 * N2 * Cin < INT32_MAX &&
+                       (ubar || (((uintptr_t)d_in) & 15) == 0);
   const bool mf = C >= 5 && C <= 16 && Cin + 1 <= 32 && N2 % 16 == 0 && P2 % 4 == 0 &&
                   (((uintptr_t)dx0) & 15) == 0;
   // the spectral weight gradient hosted in the same launch (Xs != NULL; Ci = Co = C)
@@ -1023,6 +1153,8 @@ BLINDNO_API int blindno_lift_bwd_mix_g(const float* dx0, const float* in, const 
     mw.gz = G;
     nbm = (int64_t)mw.gx * mnsplit * G;
   }
+  // the bag input only on the merged wide path (the generic kernels read a materialised field)
+  if (ubar && !(wide_in && partial && mf && LIFT_BWD_BOTH)) return (int)hipErrorInvalidValue;
   if (wide_in && partial && mf && LIFT_BWD_BOTH) {
     if (nchunk != blindno_lift_bwd_nchunk(Bg, N1, N2) || C * Cin + C > PPT * kBlock)
       return (int)hipErrorInvalidValue;
@@ -1033,11 +1165,11 @@ BLINDNO_API int blindno_lift_bwd_mix_g(const float* dx0, const float* in, const 
     if (Cin + 1 <= 16)
       lift_bwd_both_kernel<1><<<(unsigned)nb, 256, 0, st>>>(dx0, w0, d_in, in, partial, Bg, N1, N2,
                                                             Cin, C, P1, P2, G, G > 1 ? wgs : 0, dS,
-                                                            dN2, nbi, nchunk, mw);
+                                                            dN2, nbi, nchunk, mw, bi);
     else
       lift_bwd_both_kernel<2><<<(unsigned)nb, 256, 0, st>>>(dx0, w0, d_in, in, partial, Bg, N1, N2,
                                                             Cin, C, P1, P2, G, G > 1 ? wgs : 0, dS,
-                                                            dN2, nbi, nchunk, mw);
+                                                            dN2, nbi, nchunk, mw, bi);
     const int e = (int)hipGetLastError();
     if (e || !Xs || mnsplit == 1) return e;
     return blindno_reduce_partials(mpartial, dWt, mnsplit, (int)(2 * mtotal * G), stream);

@@ -621,3 +621,36 @@ def test_fused_column_pass_fp16_mix(Bn, C, m, P, Gw):
         assert torch.isfinite(res[(1, d, 2)]).all()
         assert e_f <= 2e-3 and e_s <= 2e-3, (d, e_f, e_s)
         assert e_f <= 1.5 * e_s + 1e-4, (d, e_f, e_s)
+
+
+def test_bag_mean_handed_to_heads_bit_identical():
+    """NIOFP2D_FNO with the bag mean handed to the grouped heads as ubar (the heads' lift forms
+    fc0([grid, ubar]) and returns d ubar: ops.BagHeadsIn) against the materialised
+    (B, N, N, width) field with the two bag-mean launches: output and every gradient
+    bit-identical (the same fma order in both forms)."""
+    from blindno import NIOFP2D_FNO, nio
+    torch.manual_seed(31)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 16, 2).cuda().train()
+    B, T, N = 2, 40, 64
+    x = torch.randn(B, T, N, N, device="cuda")
+    gx, gy = np.meshgrid(np.linspace(-1, 1, N, dtype=np.float32), np.linspace(-1, 1, N, dtype=np.float32),
+                         indexing="ij")
+    grid = torch.tensor(np.stack([gx, gy], 2)).cuda()
+    idx = np.random.RandomState(6).choice(T, 33)
+    cot = torch.randn(B, N, N, 2, generator=torch.Generator().manual_seed(2)).cuda()
+    res = {}
+    prev = nio.BAG_INPUT_HEADS
+    try:
+        for on in (False, True):
+            nio.BAG_INPUT_HEADS = on
+            m.zero_grad(set_to_none=True)
+            out = m(x, grid, bag_idx=idx)
+            (out * cot).sum().backward()
+            torch.cuda.synchronize()
+            res[on] = [out.detach().clone()] + [p.grad.clone() for _, p in m.named_parameters()
+                                                if p.grad is not None]
+    finally:
+        nio.BAG_INPUT_HEADS = prev
+    assert len(res[True]) == len(res[False]) > 20
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
