@@ -76,6 +76,9 @@ int blindno_project_bwd(const float* z, const float* w1, const float* b1, const 
                         int Bn, int C, int P1, int P2, int Ho, int Wo, int Hd, int Cout,
                         int ostride, int ooff, int dout_div, blindno_stream_t stream);
 int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo);
+/* the partial count for the grouped 2D heads' blindno_project_bwd_g (a coarser grid that suits
+ * them; any nchunk >= 1 is valid) */
+int blindno_project_bwd_nchunk_heads(int Bg, int Ho, int Wo);
 /* blindno_project_bwd (matrix-core path) with dout of sample n scaled by lscale[n % dout_div]
  * (the multiplicity weights of a deduplicated bag). */
 int blindno_project_bwd_w(const float* z, const float* w1, const float* b1, const float* w2,

@@ -77,6 +77,7 @@ SIGNATURES = {
     "blindno_set_rowfuse": "i",
     "blindno_set_colfuse": "i",
     "blindno_project_bwd_nchunk": "iii",
+    "blindno_project_bwd_nchunk_heads": "iii",
     "blindno_mix_wgrad_nsplit": "iiiii",
     "blindno_lift_fwd_g": "ppppiliiiiiiis",
     "blindno_lift_fwd_bag_g": "ppppiliiiiiiippppfs",

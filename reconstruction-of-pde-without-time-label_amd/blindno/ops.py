@@ -1067,7 +1067,7 @@ def fno_backward_grouped(meta: FNOMeta, inp, prms, saved, gout, need_inp_grad, b
     # projection
     dz = _padded_grad_buffer((Bn, C, P1, P2), inp.device)
     np_p = Hd * C + Hd + Cout * Hd + Cout
-    nchunk = query("blindno_project_bwd_nchunk", Bg, Ho, Wo)
+    nchunk = query("blindno_project_bwd_nchunk_heads", Bg, Ho, Wo)
     partial = _empty(nchunk, G, np_p, like=inp)
     call("blindno_project_bwd_g", ptr(zs[-1]), small.p(o1), small.p(o1 + 1),
          small.p(o1 + 2), ptr(gout), ptr(dz), ptr(partial), nchunk, G, S, Bn, C, P1, P2,

@@ -1379,6 +1379,12 @@ BLINDNO_API int blindno_project_bwd_nchunk(int Bn, int Ho, int Wo) {
   return project_bwd_mfma_nchunk((int64_t)Bn * Ho * Wo);
 }
 
+// the partial count the grouped heads' projection backward takes (a grid of 4 point tiles per
+// wave there; any count >= 1 is valid for the kernel, which strides over its tiles)
+BLINDNO_API int blindno_project_bwd_nchunk_heads(int Bg, int Ho, int Wo) {
+  return project_bwd_mfma_nchunk_wide((int64_t)Bg * Ho * Wo);
+}
+
 BLINDNO_API int blindno_project_bwd_g(const float* z, const float* w1, const float* b1,
                                       const float* w2, const float* dout, float* dz,
                                       float* partial, int nchunk, int G, int64_t wgs, int Bn,

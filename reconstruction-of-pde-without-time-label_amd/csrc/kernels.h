@@ -13,6 +13,7 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
                      const float* b2, float* out, int Bn, int C, int P1, int P2, int Ho, int Wo,
                      int Cout, int ostride, int ooff, int G, int64_t wgs, hipStream_t st);
 int project_bwd_mfma_nchunk(int64_t npts);
+int project_bwd_mfma_nchunk_wide(int64_t npts);   // the grouped 2D heads' grid
 int project_bwd_mfma(const float* z, const float* w1, const float* b1, const float* w2,
                      const float* dout, float* dz, float* partial, int nchunk, int Bn, int C,
                      int P1, int P2, int Ho, int Wo, int Cout, int ostride, int ooff,

@@ -40,10 +40,15 @@ constexpr int kFwdNP4 = PROJ_FWD_NP4;
 #ifndef PF_TPW
 #define PF_TPW 2
 #endif
-// point tiles per wave of the backward: 4 halves the workgroup partials of 2 (config C heads:
-// 3417 -> 3430 bags/s; 8: 3383, 1: 3405; profiles/r05/r05u_ab_project_bwd_tpw.txt)
+// point tiles per wave of the backward (the grid size: the kernel strides over its tiles);
+// the grouped 2D heads take PB_TPW_WIDE (project_bwd_mfma_nchunk_tpw): 4 halves their workgroup
+// partials (config C 3417 -> 3430 bags/s; 8: 3383, 1: 3405), while the 1D configs lose
+// 12-18 % with 4 (profiles/r05/r05u_ab_project_bwd_tpw.txt)
 #ifndef PB_TPW
-#define PB_TPW 4
+#define PB_TPW 2
+#endif
+#ifndef PB_TPW_WIDE
+#define PB_TPW_WIDE 4
 #endif
 constexpr int kBwdNP4 = PROJ_BWD_NP4;
 // hidden-tile loop unroll of the backward (1: rolled)
@@ -583,10 +588,16 @@ int project_fwd_mfma(const float* z, const float* w1, const float* b1, const flo
   return (int)hipGetLastError();
 }
 
-int project_bwd_mfma_nchunk(int64_t npts) {
+int project_bwd_mfma_nchunk_tpw(int64_t npts, int tpw) {
   const int64_t tiles = (npts + 15) / 16;
-  int64_t b = (tiles + kWaves * PB_TPW - 1) / (kWaves * PB_TPW);
+  int64_t b = (tiles + kWaves * tpw - 1) / (kWaves * tpw);
   return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
+int project_bwd_mfma_nchunk(int64_t npts) { return project_bwd_mfma_nchunk_tpw(npts, PB_TPW); }
+
+int project_bwd_mfma_nchunk_wide(int64_t npts) {
+  return project_bwd_mfma_nchunk_tpw(npts, PB_TPW_WIDE);
 }
 
 int project_bwd_mfma(const float* z, const float* w1, const float* b1, const float* w2,

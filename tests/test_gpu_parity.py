@@ -268,8 +268,11 @@ def test_head_pair_grouped_matches_separate_heads(width, modes, N, B):
     assert rel_l2(out.detach().cpu().numpy(), ref.detach().cpu().numpy()) <= 1e-6
     (ref * cot).sum().backward()
     want = [p.grad for hd in heads for p in hd.parameters()]
+    # the grouped projection backward runs a coarser partial grid than the single head's
+    # (blindno_project_bwd_nchunk_heads): fp32 sums over N^2 B points in another order,
+    # ~sqrt(N^2 B) eps = 1.5e-5 apart at N = 64, B = 3
     for a, b in zip(got, want):
-        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-5
+        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 5e-5
     assert rel_l2(gh.cpu().numpy(), h.grad.cpu().numpy()) <= 1e-6
 
 
