@@ -67,6 +67,11 @@ struct BagGeom {
 //     multiply), zbar summed by the staging threads, w2 re-read at the statistics write:
 //     no per-snapshot register moves and 20 fewer live VGPRs;
 //   * double-buffered 8-snapshot chunks: one barrier per chunk instead of three per 16.
+// statistics tiles of a backward step whose loads the compiler may overlap (1: one tile's 12
+// float4 at a time)
+#ifndef BAGPROJ_BWD_UNROLL
+#define BAGPROJ_BWD_UNROLL 1
+#endif
 #ifndef BAGPROJ_SC
 #define BAGPROJ_SC 8
 #endif
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(256) void bagproj_bwd_kernel(
         for (; l < U; ++l) dz[bo + (unsigned)l * ls] = slw[l] * gh * v[bo + (unsigned)l * ls];
       }
     }
-#pragma unroll 1
+#pragma unroll BAGPROJ_BWD_UNROLL
     for (int t4 = 0; t4 < 4; ++t4) {
       const unsigned tile = tg * 4 + (unsigned)t4;
       if (tile >= ntiles) break;
@@ -439,9 +444,12 @@ BLINDNO_API int64_t blindno_project_bag_stats_floats(int B, int Ho, int Wo) {
   return ((int64_t)B * Ho * Wo + 15) / 16 * (int64_t)kTileF4 * 4;
 }
 
+#ifndef BAGPROJ_BWD_BLOCKS
+#define BAGPROJ_BWD_BLOCKS 1024
+#endif
 BLINDNO_API int blindno_project_bag_bwd_nchunk(int B, int Ho, int Wo) {
   const int64_t tiles = ((int64_t)B * Ho * Wo + 15) / 16;
-  return (int)(tiles < 1 ? 1 : (tiles > 1024 ? 1024 : tiles));
+  return (int)(tiles < 1 ? 1 : (tiles > BAGPROJ_BWD_BLOCKS ? BAGPROJ_BWD_BLOCKS : tiles));
 }
 
 BLINDNO_API int blindno_project_bag_fwd(const float* z, const float* w1, const float* b1,
