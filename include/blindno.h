@@ -337,6 +337,17 @@ int blindno_rowidft_bwd_zc_bag(const float* Y, const float* v, const float* ghat
                                const float* tab, float* part, const float* Tp, float* partial,
                                int Bn, int C, int P1, int P2, int m1, int m2, int act, int Ho, int Wo,
                                blindno_stream_t stream);
+/* blindno_rowidft_bwd_lift_zc hosting up to two spectral weight gradients in the same launch
+ * (the encoder's: both layers' Gs exist once this adjoint starts): job q as
+ * blindno_mix_wgrad_multi's (mX, mG, mOut, mshp[7 q ..] = Bn, Ci, Co, K1, m2, nsplit, Gw),
+ * with the grid of its own launch (bit-identical); nmj = 0: blindno_rowidft_bwd_lift_zc. */
+int blindno_rowidft_bwd_lift_zc_mix(const float* Y, const float* dz, const float* X, const int* idx,
+                                    const float* grid, const float* w0, const float* b0,
+                                    const float* wc, const float* tb, const float* tab,
+                                    float* partial, int B, int T, int L, int N1, int N2, int C,
+                                    int P1, int P2, int m1, int m2, const void* const* mX,
+                                    const void* const* mG, void* const* mOut, const int* mshp,
+                                    int nmj, blindno_stream_t stream);
 int blindno_rowidft_bwd_lift_zc(const float* Y, const float* dz, const float* X, const int* idx,
                                 const float* grid, const float* w0, const float* b0,
                                 const float* wc, const float* tb, const float* tab, float* partial,

@@ -40,6 +40,7 @@ SIGNATURES = {
     "blindno_rowidft_epi_lift_zc": "ppppppppppppp" + "iiiiiiiiiii" + "s",
     "blindno_rowidft_bwd_zc": "pppppppppp" + "iiiiiiiii" + "s",
     "blindno_rowidft_bwd_lift_zc": "ppppppppppp" + "iiiiiiiiii" + "s",
+    "blindno_rowidft_bwd_lift_zc_mix": "ppppppppppp" + "iiiiiiiiii" + "ppppi" + "s",
     "blindno_rowdft_cd_bag": "pppi" + "ppp" + "iiiiiii" + "s",
     "blindno_rowidft_bwd_zc_bag": "pppp" + "i" + "pppppppp" + "iiiiiiiii" + "s",
     "blindno_mix_wgrad": "ppppiiiiiis",

@@ -55,6 +55,9 @@ HEAD_BWD_MERGED = os.environ.get("BLINDNO_HEADBWD_MERGED", "1") != "0"
 # the deferred finalisation stores the spectral weight gradients unpacked from the kernel that
 # finishes them (BLINDNO_UNPACK_FOLD=0: a separate unpack launch)
 UNPACK_FOLD = os.environ.get("BLINDNO_UNPACK_FOLD", "1") != "0"
+# the encoder's spectral weight gradients hosted by its first layer's adjoint launch
+# (BLINDNO_HOST_ENC_MIX=0: the deferred finalisation's mix launch)
+HOST_ENC_MIX = os.environ.get("BLINDNO_HOST_ENC_MIX", "1") != "0"
 
 
 def set_mix_precision(name: str) -> None:
@@ -466,20 +469,22 @@ def k_colpass(At, Wt, Bn, Ci, Co, P1, m1, m2, P2, direction):
     return Xs, Z
 
 
-def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2, deferrable=False):
+def k_mix_wgrad(X, G, Bn, Ci, Co, K1, m2, deferrable=False, jobs=None):
     """Spectral weight gradient dWt (m2, K1, Ci, Co, 2).  ``deferrable``: the caller's only
     reader of dWt is itself deferred (the 2D unpack), so under deferred_reductions() the
     sample-split reduction may join the batched finalisation."""
     ns = query("blindno_mix_wgrad_nsplit", Bn, Ci, Co, K1, m2)
     if _DEFER is not None and deferrable:
         # the mix gradient itself joins the batched finalisation (one launch for every layer's,
-        # before the reductions and the unpack)
+        # before the reductions and the unpack) -- or, with ``jobs``, a later launch of the
+        # caller's that hosts it (the caller launches it before the finalisation)
+        q = _DEFER.mix if jobs is None else jobs
         if ns > 1:
             part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X)
-            _DEFER.mix.append((X, G, part, (Bn, Ci, Co, K1, m2, ns, 1)))
+            q.append((X, G, part, (Bn, Ci, Co, K1, m2, ns, 1)))
             return reduce_partials(part, ns, m2 * K1 * Ci * Co * 2).view(m2, K1, Ci, Co, 2)
         dWt = _empty(m2, K1, Ci, Co, 2, like=X)
-        _DEFER.mix.append((X, G, dWt, (Bn, Ci, Co, K1, m2, 1, 1)))
+        q.append((X, G, dWt, (Bn, Ci, Co, K1, m2, 1, 1)))
         return dWt
     dWt = _empty(m2, K1, Ci, Co, 2, like=X)
     part = _empty(ns, m2 * K1 * Ci * Co * 2, like=X) if ns > 1 else None
@@ -1618,11 +1623,14 @@ class BagEncoderFn(torch.autograd.Function):
                 call("blindno_rowdft_cd", ptr(dz), ptr(part), ptr(cs.Tp), ptr(cs.tab), Bn, C, P1, P2, meta.m2,
                      0, valid[0], valid[1], stream_ptr())
             nbv = (valid[0] + 15) // 16
+            # the spectral weight gradients of both layers ride along the first layer's adjoint
+            # launch (blindno_rowidft_bwd_lift_zc_mix) under deferred_reductions()
+            hosted = [] if (_DEFER is not None and HOST_ENC_MIX and n <= 2) else None
             for k in reversed(range(n)):
                 off = 2 + 4 * k
                 w1, w2, cw, cb = prm[off:off + 4]
                 G, Yb = cs.mix(part, nbv, Wts[k], 1)
-                dWt = k_mix_wgrad(Xs[k], G, Bn, C, C, sh.K1, meta.m2, deferrable=True)
+                dWt = k_mix_wgrad(Xs[k], G, Bn, C, C, sh.K1, meta.m2, deferrable=True, jobs=hosted)
                 grads[off], grads[off + 1] = unpack_weights(dWt, (w1, w2), P1, 2)
                 dv = crop if (k == n - 1 and crop) else (P1, P2)
                 if k > 0:
@@ -1646,9 +1654,16 @@ class BagEncoderFn(torch.autograd.Function):
                     nchunk = query("blindno_colspec_bwd_nchunk", Bn, P1)
                     npl = C * C + C + 4 * C
                     pl = _empty(nchunk, npl, like=gh)
-                    call("blindno_rowidft_bwd_lift_zc", ptr(Yb), ptr(dz), ptr(X), ptr(idx_t), ptr(grid), ptr(fc0w),
-                         ptr(fc0b), ptr(cw), ptr(cs.tb), ptr(cs.tab), ptr(pl), B, T, L, N1, N2, C, P1, P2,
-                         meta.m1, meta.m2, stream_ptr())
+                    jobs = hosted or []
+                    nj = len(jobs)
+                    call("blindno_rowidft_bwd_lift_zc_mix", ptr(Yb), ptr(dz), ptr(X), ptr(idx_t), ptr(grid),
+                         ptr(fc0w), ptr(fc0b), ptr(cw), ptr(cs.tb), ptr(cs.tab), ptr(pl), B, T, L, N1, N2, C,
+                         P1, P2, meta.m1, meta.m2,
+                         (ctypes.c_void_p * max(1, nj))(*[j[0].data_ptr() for j in jobs]),
+                         (ctypes.c_void_p * max(1, nj))(*[j[1].data_ptr() for j in jobs]),
+                         (ctypes.c_void_p * max(1, nj))(*[j[2].data_ptr() for j in jobs]),
+                         (ctypes.c_int * max(7, 7 * nj))(*[v for j in jobs for v in j[3]]), nj,
+                         stream_ptr())
                     g = reduce_partials(pl, nchunk, npl)
                     grads[off + 2] = g[:C * C].view_as(cw)
                     grads[off + 3] = g[C * C:C * C + C]

@@ -22,6 +22,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "wgrad.h"
 
 namespace blindno {
 
@@ -43,6 +44,11 @@ struct SpecCol {
   const float* dzg;   // ghat (B, S): the bag-level upstream gradient, S = Ho Wo
   const float* dzl;   // lw (U) multiplicity weights, NULL: 1 / U
   int dzU, dzWo, dzS;
+  // spectral weight gradients hosted by the launch (nmixb > 0): workgroups nmain .. run the
+  // nmj jobs mj (job q owns mcum[q] .. mcum[q + 1] - 1 of them), independent of the row kernel
+  int nmain, nmixb, nmj;
+  int mcum[3];
+  MixWgradJob mj[2];
 };
 
 // dz of the encoder's last layer (csrc/bagproj.hip): dz[b U + l][c][h][w] = lw_l ghat[b][h Wo + w]

@@ -578,6 +578,21 @@ void rowfuse_kernel(
   constexpr int NNT = (4 * S + 15) / 16;          // 16-column tiles of the next row DFT
   constexpr int Npad = 16 * NNT;
   static_assert(!CD || RD, "CD takes the column DFT of the next row DFT");
+  // hosted spectral weight gradients (SpecCol.mj): only the encoder's first-layer adjoint
+  // (MODE 1, LIFT) takes them -- the branch costs the other forms registers
+  constexpr bool kHost = MODE == 1 && LIFT;
+  if constexpr (kHost) {
+    if (sc.nmixb > 0 && (int)blockIdx.x >= sc.nmain) {
+      int r = (int)blockIdx.x - sc.nmain;
+      const int q = (sc.nmj > 1 && r >= sc.mcum[1]) ? 1 : 0;
+      r -= sc.mcum[q];
+      const MixWgradJob& mj = sc.mj[q];
+      mix_wgrad_block(mj.X, mj.Gs, mj.out, mj.Bn, mj.Ci, mj.Co, mj.K1, mj.m2, r % mj.gx,
+                      (r / mj.gx) % mj.gy, r / (mj.gx * mj.gy), mj.gx, mj.gy, mj.gz);
+      return;
+    }
+  }
+  const int gxm = (kHost && sc.nmixb > 0) ? sc.nmain : (int)gridDim.x;   // the row kernel's grid
   const int NT = P2 >> 4;                           // MFMA column tiles (NT % NH == 0)
   extern __shared__ float lds[];
   float* sA = lds;                                  // [NT][64 lanes][S]
@@ -634,7 +649,7 @@ void rowfuse_kernel(
   f32x4 znext[S];
   const int item0 = blockIdx.x * kW + wave;
   if (ROWFUSE_ZPRE && !ZY) load_z(item0, znext);
-  for (int item = item0; item < nitems; item += gridDim.x * kW) {
+  for (int item = item0; item < nitems; item += gxm * kW) {
     const int n = item / HB;
     const int h0 = (item - n * HB) << 4;
     const int h = h0 + c16;
@@ -861,7 +876,7 @@ void rowfuse_kernel(
     Ops buf[2];
     load(0, buf[0]);
     if constexpr (ZY) zy_mfma<S, C>(zop, zb);
-    if (ROWFUSE_ZPRE && !ZY) load_z(item + gridDim.x * kW, znext);   // after this item's first loads
+    if (ROWFUSE_ZPRE && !ZY) load_z(item + gxm * kW, znext);   // after this item's first loads
     if constexpr (NSC > 0) {
       // the step count is a compile-time constant: straight-line steps, the waits counted exactly
 #pragma unroll
@@ -1032,6 +1047,7 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
                   int G = 1, int64_t wgs = 0, int dN1 = 0, int dN2 = 0,
                   RowDftNext rd = RowDftNext{nullptr, nullptr, 0, 0},
                   SpecCol sc = SpecCol{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, 0, 0, 0}) {
+  sc.nmain = nblocks;                              // the row kernel's grid (hosted jobs after it)
   if (dN1 <= 0) dN1 = P1;
   if (dN2 <= 0) dN2 = P2;
   if (dN1 > P1 || dN2 > P2) return (int)hipErrorInvalidValue;
@@ -1075,20 +1091,20 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
     if (wc && p160 && crop128 && RD_ == 0)                                                     \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, true, MODE == 0 ? 128 / (16 * NH_) : 0, \
                      ZY_, CD_, ZW_>                                                            \
-          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+          <<<nblocks + sc.nmixb, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
     else if (wc && p160 && (dN2 == P2 || RD_ != 0))                                            \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, true, MODE == 0 ? 160 / (16 * NH_) : 0, \
                      ZY_, CD_, ZW_>                                                            \
-          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+          <<<nblocks + sc.nmixb, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
     else if (wc)                                                                               \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, true, 0, ZY_, CD_, ZW_>                \
-          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+          <<<nblocks + sc.nmixb, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
     else if (!ZY_)                                                                             \
       rowfuse_kernel<MODE, ACT, WG, LIFT, RD_, S_, NH_, false>                                 \
-          <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
+          <<<nblocks + sc.nmixb, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1, \
                                       dN2, rd, sc);                                            \
   } while (0)
 #define RFX(RD_, S_, ZY_, CD_) RFG(RD_, S_, ZY_, CD_, NHX(RD_), 0)
@@ -1108,7 +1124,7 @@ int rowinv_launch(const float* Z, const float* xs, const float* dz, const float*
           if constexpr (MODE == 1 && WG == 1 && LIFT == 0) {
             if (!sc.part || rd.act || !wc) return (int)hipErrorInvalidValue;
             rowfuse_kernel<MODE, ACT, WG, LIFT, 1, 6, ROWFUSE_NH1, true, 0, true, true, 0, true>
-                <<<nblocks, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1,
+                <<<nblocks + sc.nmixb, 256, shf, st>>>(Z, xs, dz, wc, bc, out, TB, partial, Bn, P1, P2, bl, dN1,
                                             dN2, rd, sc);
           } else {
             return (int)hipErrorInvalidValue;
@@ -1539,20 +1555,57 @@ BLINDNO_API int blindno_rowidft_bwd_zc_bag(const float* Y, const float* v, const
 }
 
 // blindno_rowidft_bwd_lift with Z built from Y
+BLINDNO_API int blindno_rowidft_bwd_lift_zc_mix(const float* Y, const float* dz, const float* X,
+                                                const int* idx, const float* grid, const float* w0,
+                                                const float* b0, const float* wc, const float* tb,
+                                                const float* tab, float* partial, int B, int T,
+                                                int L, int N1, int N2, int C, int P1, int P2,
+                                                int m1, int m2, const void* const* mX,
+                                                const void* const* mG, void* const* mOut,
+                                                const int* mshp, int nmj, void* stream) {
+  const int Bn = B * L;
+  if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !tab || !wc || !partial || N1 > P1 ||
+      N2 > P2 || nmj < 0 || nmj > 2)
+    return (int)hipErrorInvalidValue;
+  const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
+  const int nb = zc_blocks1(Bn * (P1 / 16));
+  SpecCol sc = spec_col(Y, nullptr, tab, P1);
+  int64_t blocks = 0;
+  for (int q = 0; q < nmj; ++q) {
+    const int* sh = mshp + 7 * q;
+    const int mBn = sh[0], Ci = sh[1], Co = sh[2], K1 = sh[3], mm2 = sh[4], ns = sh[5], Gw = sh[6];
+    const int64_t total = (int64_t)mm2 * K1 * Ci * Co;
+    if (mBn < 1 || Ci < 1 || Co < 1 || K1 < 1 || mm2 < 1 || ns < 1 || Gw < 1 || mBn % Gw ||
+        total >= INT32_MAX / 2 || !mX[q] || !mG[q] || !mOut[q])
+      return (int)hipErrorInvalidValue;
+    MixWgradJob& m = sc.mj[q];
+    m = MixWgradJob{};
+    m.X = (const float2*)mX[q];
+    m.Gs = (const float2*)mG[q];
+    m.out = (float2*)mOut[q];
+    m.Bn = mBn; m.Ci = Ci; m.Co = Co; m.K1 = K1; m.m2 = mm2;
+    m.gx = (int)cdiv(total, kBlock);
+    m.gy = ns;
+    m.gz = Gw;
+    sc.mcum[q] = (int)blocks;
+    blocks += (int64_t)m.gx * ns * Gw;
+  }
+  if (blocks + nb >= INT32_MAX) return (int)hipErrorInvalidValue;
+  sc.mcum[nmj] = (int)blocks;
+  sc.nmj = nmj;
+  sc.nmixb = (int)blocks;
+  return rowinv_launch<1, 0, 1, 1, true>(nullptr, nullptr, dz, wc, nullptr, nullptr, tb, partial, nb, Bn,
+                                         C, P1, P2, m2, (hipStream_t)stream, bl, 1, 0, 0, 0,
+                                         RowDftNext{nullptr, nullptr, 0, 0}, sc);
+}
+
 BLINDNO_API int blindno_rowidft_bwd_lift_zc(const float* Y, const float* dz, const float* X,
                                             const int* idx, const float* grid, const float* w0,
                                             const float* b0, const float* wc, const float* tb,
                                             const float* tab, float* partial, int B, int T, int L,
                                             int N1, int N2, int C, int P1, int P2, int m1, int m2,
                                             void* stream) {
-  const int Bn = B * L;
-  if (!blindno_colspec_ok(Bn, C, P1, P2, m1, m2) || !Y || !tab || !wc || !partial || N1 > P1 ||
-      N2 > P2)
-    return (int)hipErrorInvalidValue;
-  const BagLift bl{X, idx, grid, w0, b0, T, L, N1, N2};
-  const int nb = zc_blocks1(Bn * (P1 / 16));
-  return rowinv_launch<1, 0, 1, 1, true>(nullptr, nullptr, dz, wc, nullptr, nullptr, tb, partial, nb, Bn,
-                                         C, P1, P2, m2, (hipStream_t)stream, bl, 1, 0, 0, 0,
-                                         RowDftNext{nullptr, nullptr, 0, 0},
-                                         spec_col(Y, nullptr, tab, P1));
+  return blindno_rowidft_bwd_lift_zc_mix(Y, dz, X, idx, grid, w0, b0, wc, tb, tab, partial, B, T, L,
+                                         N1, N2, C, P1, P2, m1, m2, nullptr, nullptr, nullptr,
+                                         nullptr, 0, stream);
 }
