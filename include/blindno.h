@@ -302,6 +302,13 @@ int blindno_rowdft_cd(const float* x, float* part, const float* Tp, const float*
 int blindno_rowdft_bag_lift_cd(const float* X, const int* idx, float* part, const float* Tp,
                                const float* tab, int B, int T, int L, int N1, int N2, int P1,
                                int P2, int m2, blindno_stream_t stream);
+/* blindno_rowdft_bag_lift_cd and blindno_pack_w2d_multi(w1s, w2s, Wts, shapes, npk) -- the
+ * forward's spectral-weight pack, independent of it -- in one launch (bit-identical) */
+int blindno_rowdft_bag_lift_cd_pack(const float* X, const int* idx, float* part, const float* Tp,
+                                    const float* tab, int B, int T, int L, int N1, int N2, int P1,
+                                    int P2, int m2, const void* const* w1s, const void* const* w2s,
+                                    void* const* Wts, const int* shapes, int npk,
+                                    blindno_stream_t stream);
 /* partials of nbv blocks summed in block order -> Xsave (dir 0: X; dir 1: G = c_k/(P1 P2) X) and
  * Y (dir 0: c_k/(P1 P2) sum_c X W; dir 1: sum_o conj(W) G), as blindno_colpass forms them.
  * Lift (w0 != NULL, dir 0, Cp = 1): X[c] = w0[c,0] U + w0[c,1] Dg2[0] + w0[c,2] Dg2[1] +

@@ -35,6 +35,7 @@ SIGNATURES = {
     "blindno_colspec_bwd_nchunk": "ii",
     "blindno_rowdft_cd": "ppppiiiiiiiis",
     "blindno_rowdft_bag_lift_cd": "pppppiiiiiiiis",
+    "blindno_rowdft_bag_lift_cd_pack": "pppppiiiiiiiippppis",
     "blindno_colmix": "pipppiiiiiiiippps",
     "blindno_rowidft_epi_zc": "ppppppppp" + "iiiiiiiiii" + "s",
     "blindno_rowidft_epi_lift_zc": "ppppppppppppp" + "iiiiiiiiiii" + "s",

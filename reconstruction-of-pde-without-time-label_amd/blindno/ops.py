@@ -58,6 +58,9 @@ UNPACK_FOLD = os.environ.get("BLINDNO_UNPACK_FOLD", "1") != "0"
 # the encoder's spectral weight gradients hosted by its first layer's adjoint launch
 # (BLINDNO_HOST_ENC_MIX=0: the deferred finalisation's mix launch)
 HOST_ENC_MIX = os.environ.get("BLINDNO_HOST_ENC_MIX", "1") != "0"
+# the bag encoder's spectral-weight pack (with the heads' pack_ahead requests) hosted by its
+# first row-DFT launch (BLINDNO_HOST_PACK=0: a pack launch of its own)
+HOST_PACK = os.environ.get("BLINDNO_HOST_PACK", "1") != "0"
 
 
 def set_mix_precision(name: str) -> None:
@@ -540,10 +543,28 @@ def drop_pack_ahead():
     _PACKED.clear()
 
 
-def _pack_into(pairs, Wts, P1):
+_PACK_DEFERRED = []     # at most one pack launch's arguments, held for take_deferred_pack
+
+
+def take_deferred_pack():
+    """The arguments (w1s, w2s, Wts, shapes, n) of the pack _pack_into(defer=True) held back, for
+    a launch that hosts it (blindno_rowdft_bag_lift_cd_pack), or None."""
+    return _PACK_DEFERRED.pop() if _PACK_DEFERRED else None
+
+
+def flush_deferred_pack():
+    """Launch a held-back pack now (nothing took it along)."""
+    pk = take_deferred_pack()
+    if pk is not None:
+        call("blindno_pack_w2d_multi", *pk, stream_ptr())
+
+
+def _pack_into(pairs, Wts, P1, defer=False):
     """Pack the spectral weights (w1, w2) of several 2D layers into the contiguous Wts[i]
     (m2, K1, Ci, Co, 2) with ONE launch (blindno_pack_w2d_multi), together with every pending
-    pack_ahead request."""
+    pack_ahead request.  ``defer``: hold the launch's arguments for take_deferred_pack -- the
+    caller's next launch hosts the pack, and nothing may read the Wts before it."""
+    flush_deferred_pack()
     jobs = [(pr, W, P1) for pr, W in zip(pairs, Wts)]
     for r in _PACK_AHEAD:
         jobs += [(pr, W, r[2]) for pr, W in zip(r[0], r[1])]
@@ -559,16 +580,20 @@ def _pack_into(pairs, Wts, P1):
         shp += [Ci, Co, m1, m2, P1j]
     Wts = [j[1] for j in jobs]
     n = len(Wts)
-    call("blindno_pack_w2d_multi", (ctypes.c_void_p * n)(*w1s), (ctypes.c_void_p * n)(*w2s),
-         (ctypes.c_void_p * n)(*[W.data_ptr() for W in Wts]), (ctypes.c_int * (5 * n))(*shp), n,
-         stream_ptr())
+    args = ((ctypes.c_void_p * n)(*w1s), (ctypes.c_void_p * n)(*w2s),
+            (ctypes.c_void_p * n)(*[W.data_ptr() for W in Wts]), (ctypes.c_int * (5 * n))(*shp), n)
+    if defer:
+        _PACK_DEFERRED.append(args)
+    else:
+        call("blindno_pack_w2d_multi", *args, stream_ptr())
 
 
-def pack_w2d_many(pairs, P1):
-    """One packed Wt (m2, K1, Ci, Co, 2) per (w1, w2) pair, all in one launch."""
+def pack_w2d_many(pairs, P1, defer=False):
+    """One packed Wt (m2, K1, Ci, Co, 2) per (w1, w2) pair, all in one launch (``defer``: see
+    _pack_into)."""
     Wts = [_empty(w1.shape[3], kept_rows_count(w1.shape[2], P1), w1.shape[0], w1.shape[1], 2, like=w1)
            for w1, _ in pairs]
-    _pack_into(pairs, Wts, P1)
+    _pack_into(pairs, Wts, P1, defer=defer)
     return Wts
 
 
@@ -1442,18 +1467,24 @@ class BagEncoderFn(torch.autograd.Function):
         fc0w, fc0b = prm[0], prm[1]
         sh = SpecShape(Bn, C, C, P1, P2, meta.m1, meta.m2, 2)
         Xs, Wts, zs = [], [], []
-        Wts_all = pack_w2d_many([(prm[2 + 4 * k], prm[3 + 4 * k]) for k in range(n)], P1)
         cs = _ColSpec(Bn, C, P1, P2, meta.m1, meta.m2, X.device) \
             if colspec_ok(Bn, C, P1, P2, meta.m1, meta.m2) else None
         ctx.cs = cs
+        Wts_all = pack_w2d_many([(prm[2 + 4 * k], prm[3 + 4 * k]) for k in range(n)], P1,
+                                defer=HOST_PACK and cs is not None)
         if cs is not None:
             # the column pass folded into the row kernels: per layer, the kernel that forms the
             # row spectrum leaves its column-DFT partials, blindno_colmix forms Xs and the mixed Y,
             # and the row inverse rebuilds its row coefficients from Y
             Dg2 = _grid_spec2(grid, N1, N2, P1, P2, meta.m1, meta.m2)
             part = cs.part(1, X)
-            call("blindno_rowdft_bag_lift_cd", ptr(X), ptr(idx_t), ptr(part), ptr(cs.Tp), ptr(cs.tab), B, T,
-                 L, N1, N2, P1, P2, meta.m2, stream_ptr())
+            pk = take_deferred_pack()
+            if pk is not None:      # the pack rides along the first row DFT (colmix reads it)
+                call("blindno_rowdft_bag_lift_cd_pack", ptr(X), ptr(idx_t), ptr(part), ptr(cs.Tp),
+                     ptr(cs.tab), B, T, L, N1, N2, P1, P2, meta.m2, *pk, stream_ptr())
+            else:
+                call("blindno_rowdft_bag_lift_cd", ptr(X), ptr(idx_t), ptr(part), ptr(cs.Tp), ptr(cs.tab),
+                     B, T, L, N1, N2, P1, P2, meta.m2, stream_ptr())
             nbv = (N1 + 15) // 16
             for k in range(n):
                 off = 2 + k * 4

@@ -12,6 +12,7 @@
 #include "common.h"
 #include "blindno.h"
 #include "colspec.h"
+#include "packw.h"
 
 using namespace blindno;
 
@@ -32,14 +33,14 @@ constexpr int kCdWaves = 4;
 // x[n][c][h][w], read on the valid region N1v x N2v (zero elsewhere), GELU'd first when act.
 // BDZ: x is the bag projection's v and the rows are dz = lw_l ghat v (the encoder's last-layer
 // gradient formed on load, colspec.h BagDz): ghat (B, N1v N2v), lw (L = U snapshots per bag)
-template <int NNT, bool ALIGNED, bool LIFT, bool BDZ = false>
-__global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
+// Body of one workgroup bx of a gx-workgroup grid (rowdft_cd_kernel, rowdft_cd_pack_kernel).
+template <int NNT, bool ALIGNED, bool LIFT, bool BDZ>
+__device__ __forceinline__ void rowdft_cd_block(
     const float* __restrict__ x, const int* __restrict__ idx, float* __restrict__ part,
     const float* __restrict__ Tp, const float* __restrict__ tab, int Bn, int C, int P1, int P2,
     int m2, int KB, int nbv, int N1v, int N2v, int act, int T, int L,
-    const float* __restrict__ ghat = nullptr, const float* __restrict__ lw = nullptr) {
+    const float* __restrict__ ghat, const float* __restrict__ lw, float* lds, int bx, int gx) {
   constexpr int Npad = 16 * NNT;
-  extern __shared__ float lds[];
   float* sT = lds;                                 // [KB][4][Npad][4]
   stage_to_lds(sT, Tp, KB * 16 * Npad);
   __syncthreads();
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
   const int nb = P1 >> 4;
   const int nch = colspec_nchunk(C, m2);
   const int64_t nitems = (int64_t)Bn * C * nbv;
-  for (int64_t it = (int64_t)blockIdx.x * kCdWaves + wave; it < nitems; it += (int64_t)gridDim.x * kCdWaves) {
+  for (int64_t it = (int64_t)bx * kCdWaves + wave; it < nitems; it += (int64_t)gx * kCdWaves) {
     const int b = (int)(it % nbv);
     const int nc = (int)(it / nbv);
     const int c = nc % C, n = nc / C;
@@ -114,6 +115,35 @@ __global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
     float* blk = part + ((int64_t)n * nb + b) * nch * 128;
     cd_store<NNT>(acc, tabT, h0, lane, blk, c, C, m2);
   }
+}
+
+template <int NNT, bool ALIGNED, bool LIFT, bool BDZ = false>
+__global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_kernel(
+    const float* __restrict__ x, const int* __restrict__ idx, float* __restrict__ part,
+    const float* __restrict__ Tp, const float* __restrict__ tab, int Bn, int C, int P1, int P2,
+    int m2, int KB, int nbv, int N1v, int N2v, int act, int T, int L,
+    const float* __restrict__ ghat = nullptr, const float* __restrict__ lw = nullptr) {
+  extern __shared__ float lds[];
+  rowdft_cd_block<NNT, ALIGNED, LIFT, BDZ>(x, idx, part, Tp, tab, Bn, C, P1, P2, m2, KB, nbv, N1v,
+                                           N2v, act, T, L, ghat, lw, lds, blockIdx.x, gridDim.x);
+}
+
+// The bag lift's rowdft_cd (workgroups [0, nmain)) with the forward's spectral-weight pack
+// (blindno_pack_w2d_multi's tiled transpose, one 256-thread tile team per workgroup past nmain)
+// in one launch: independent work, bit-identical to the two launches.
+template <int NNT, bool ALIGNED>
+__global__ __launch_bounds__(64 * kCdWaves) void rowdft_cd_pack_kernel(
+    const float* __restrict__ x, const int* __restrict__ idx, float* __restrict__ part,
+    const float* __restrict__ Tp, const float* __restrict__ tab, int Bn, int P1, int P2, int m2,
+    int KB, int nbv, int N1v, int N2v, int T, int L, int nmain, PackSegs ps) {
+  extern __shared__ float lds[];
+  const int bx = blockIdx.x;
+  if (bx >= nmain) {
+    w2d_transpose_tile<0>(ps, bx - nmain, threadIdx.x, reinterpret_cast<float2 (*)[33]>(lds), true);
+    return;
+  }
+  rowdft_cd_block<NNT, ALIGNED, true, false>(x, idx, part, Tp, tab, Bn, 1, P1, P2, m2, KB, nbv,
+                                             N1v, N2v, 0, T, L, nullptr, nullptr, lds, bx, nmain);
 }
 
 // One workgroup per (sample n, 8 kept rows j of tile mt2): Xs[k][c][j] = the sum of the nbv
@@ -246,16 +276,33 @@ template <bool LIFT, bool BDZ = false>
 int rowdft_cd_launch(const float* x, const int* idx, float* part, const float* Tp,
                      const float* tab, int Bn, int C, int P1, int P2, int m2, int act, int N1v,
                      int N2v, int T, int L, hipStream_t st, const float* ghat = nullptr,
-                     const float* lw = nullptr) {
+                     const float* lw = nullptr, const PackSegs* ps = nullptr, int ntr = 0) {
   const int KB = (P2 + 15) / 16, NNT = (2 * m2 + 15) / 16, Npad = 16 * NNT;
   const int nbv = (N1v + 15) / 16;
-  const size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
+  size_t sh = sizeof(float) * (size_t)KB * 16 * Npad;
   if (sh > 160 * 1024 || NNT > 2) return (int)hipErrorInvalidValue;
   const int64_t items = (int64_t)Bn * C * nbv;
   const int64_t b = (items + kCdWaves - 1) / kCdWaves;
   const int blocks = (int)(b < COLSPEC_RD_BLOCKS ? b : COLSPEC_RD_BLOCKS);
   const bool aligned = N2v % 4 == 0 && (LIFT || P2 % 4 == 0) && (((uintptr_t)x) & 15) == 0 &&
                        (((uintptr_t)ghat) & 15) == 0;
+  if constexpr (LIFT && !BDZ) {
+    if (ps && ntr > 0) {           // hosted pack: one transpose tile per extra workgroup
+      if ((int64_t)blocks + ntr >= INT32_MAX) return (int)hipErrorInvalidValue;
+      const size_t tsh = sizeof(float2) * 32 * 33;
+      if (sh < tsh) sh = tsh;
+#define CDP(NNT_, AL_)                                                                         \
+  rowdft_cd_pack_kernel<NNT_, AL_><<<blocks + ntr, 64 * kCdWaves, sh, st>>>(                   \
+      x, idx, part, Tp, tab, Bn, P1, P2, m2, KB, nbv, N1v, N2v, T, L, blocks, *ps)
+      if (NNT == 1) {
+        if (aligned) CDP(1, true); else CDP(1, false);
+      } else {
+        if (aligned) CDP(2, true); else CDP(2, false);
+      }
+#undef CDP
+      return (int)hipGetLastError();
+    }
+  }
 #define CDK(NNT_, AL_)                                                                         \
   rowdft_cd_kernel<NNT_, AL_, LIFT, BDZ><<<blocks, 64 * kCdWaves, sh, st>>>(                   \
       x, idx, part, Tp, tab, Bn, C, P1, P2, m2, KB, nbv, N1v, N2v, act, T, L, ghat, lw)
@@ -307,6 +354,46 @@ BLINDNO_API int blindno_rowdft_bag_lift_cd(const float* X, const int* idx, float
     return (int)hipErrorInvalidValue;
   return rowdft_cd_launch<true>(X, idx, part, Tp, tab, B * L, 1, P1, P2, m2, 0, N1, N2, T, L,
                                 (hipStream_t)stream);
+}
+
+// blindno_rowdft_bag_lift_cd with blindno_pack_w2d_multi(w1s, w2s, Wts, shapes, npk) (the
+// forward's spectral-weight pack; independent of it) hosted in the same launch; two launches
+// when the pack does not take the tiled path or does not fit one segment table.
+BLINDNO_API int blindno_rowdft_bag_lift_cd_pack(const float* X, const int* idx, float* part,
+                                                const float* Tp, const float* tab, int B, int T,
+                                                int L, int N1, int N2, int P1, int P2, int m2,
+                                                const void* const* w1s, const void* const* w2s,
+                                                void* const* Wts, const int* shapes, int npk,
+                                                void* stream) {
+  if (!X || !idx || !part || !Tp || !tab || B <= 0 || L <= 0 || T <= 0 || N1 < 1 || N1 > P1 ||
+      N2 < 1 || N2 > P2 || !cd_geom_ok(B * L, 1, P1, P2, m2) ||
+      (int64_t)B * T * N1 * N2 >= ((int64_t)1 << 40) || npk < 0)
+    return (int)hipErrorInvalidValue;
+  PackSegs ps{};
+  int64_t ntr = 0;
+  bool host = npk > 0 && npk <= kPackSegs;
+  if (host) {
+    ps.nseg = npk;
+    for (int i = 0; i < npk; ++i) {
+      const int* sh = shapes + 5 * i;
+      if (sh[2] > sh[4] || sh[0] < 1 || sh[1] < 1 || sh[2] < 1 || sh[3] < 1 || !w1s[i] ||
+          !w2s[i] || !Wts[i] ||
+          (int64_t)sh[3] * 2 * sh[2] * sh[0] * sh[1] >= INT32_MAX)
+        return (int)hipErrorInvalidValue;
+      ps.w1[i] = (const float*)w1s[i];
+      ps.w2[i] = (const float*)w2s[i];
+      ps.Wt[i] = (float2*)Wts[i];
+      ps.Ci[i] = sh[0]; ps.Co[i] = sh[1]; ps.m1[i] = sh[2]; ps.m2[i] = sh[3]; ps.P1[i] = sh[4];
+    }
+    host = w2d_tiled_segs(ps, ntr) && ntr > 0;
+  }
+  if (!host && npk > 0) {
+    const int e = blindno_pack_w2d_multi(w1s, w2s, Wts, shapes, npk, stream);
+    if (e) return e;
+  }
+  return rowdft_cd_launch<true>(X, idx, part, Tp, tab, B * L, 1, P1, P2, m2, 0, N1, N2, T, L,
+                                (hipStream_t)stream, nullptr, nullptr, host ? &ps : nullptr,
+                                host ? (int)ntr : 0);
 }
 
 // The column pass's mix stage on the block partials (see colmix_kernel): part holds Cp-channel

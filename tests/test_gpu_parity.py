@@ -657,3 +657,36 @@ def test_bag_mean_handed_to_heads_bit_identical():
     assert len(res[True]) == len(res[False]) > 20
     for a, b in zip(res[False], res[True]):
         assert torch.equal(a, b)
+
+
+def test_pack_hosted_by_bag_rowdft_bit_identical():
+    """The encoder's (and the heads' pack_ahead) spectral-weight pack hosted by the bag's first
+    row-DFT launch (blindno_rowdft_bag_lift_cd_pack) against its own pack launch: output and
+    every gradient bit-identical, and nothing left held back."""
+    from blindno import NIOFP2D_FNO, ops
+    torch.manual_seed(33)
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 16, 2).cuda().train()
+    B, T, N = 2, 40, 64
+    x = torch.randn(B, T, N, N, device="cuda")
+    gx, gy = np.meshgrid(np.linspace(-1, 1, N, dtype=np.float32), np.linspace(-1, 1, N, dtype=np.float32),
+                         indexing="ij")
+    grid = torch.tensor(np.stack([gx, gy], 2)).cuda()
+    idx = np.random.RandomState(7).choice(T, 33)
+    cot = torch.randn(B, N, N, 2, generator=torch.Generator().manual_seed(3)).cuda()
+    res = {}
+    prev = ops.HOST_PACK
+    try:
+        for on in (False, True):
+            ops.HOST_PACK = on
+            m.zero_grad(set_to_none=True)
+            out = m(x, grid, bag_idx=idx)
+            (out * cot).sum().backward()
+            torch.cuda.synchronize()
+            assert ops.take_deferred_pack() is None
+            res[on] = [out.detach().clone()] + [p.grad.clone() for _, p in m.named_parameters()
+                                                if p.grad is not None]
+    finally:
+        ops.HOST_PACK = prev
+    assert len(res[True]) == len(res[False]) > 20
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
