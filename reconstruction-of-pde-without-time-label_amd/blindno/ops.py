@@ -334,6 +334,22 @@ class _Deferred:
                 del mixu[qi]
         return mixu, redu, rest
 
+    def _unpacks_read_reductions(self, rest):
+        """True when the dWt an unpack of ``rest`` reads overlaps memory a recorded reduction
+        writes (its output buffer or a redirected piece) -- e.g. the grouped heads' (G, ...)
+        reduction whose slice dWt[g] an unpack reads.  Such unpacks must run after the
+        reductions, not beside them."""
+        spans = []
+        for _, out, _, _, pieces in self.red:
+            spans.append((out.data_ptr(), out.data_ptr() + 4 * out.numel()))
+            spans += [(d.data_ptr(), d.data_ptr() + 4 * d.numel()) for _, _, d in pieces]
+        for u in rest:
+            a = u[0].data_ptr()
+            b = a + u[0].element_size() * u[0].numel()
+            if any(a < e and s < b for s, e in spans):
+                return True
+        return False
+
     def flush(self):
         mixu, redu, rest = self._fold_unpacks()
         if self.mix:
@@ -386,9 +402,14 @@ class _Deferred:
             d1 = (ctypes.c_void_p * n)(*[u[1].data_ptr() for u in rest])
             d2 = (ctypes.c_void_p * n)(*[u[2].data_ptr() for u in rest])
             shp = (ctypes.c_int * (5 * n))(*[v for u in rest for v in u[3]])
-            if self.red:        # the reductions and the unpacks in one launch
+            if self.red and not self._unpacks_read_reductions(rest):
+                # the reductions and the unpacks in one launch: no unpack reads what a
+                # reduction of the same launch writes (blindno_finish_multi runs both
+                # job lists concurrently)
                 call("blindno_finish_multi", *red_args, srcs, d1, d2, shp, n, stream_ptr())
             else:
+                if self.red:    # ordered: an unpack reads a reduction's output
+                    call("blindno_reduce_partials_pieces_u", *red_args, stream_ptr())
                 call("blindno_unpack_w2d_multi", srcs, d1, d2, shp, n, stream_ptr())
         self.mix, self.red, self.unp = [], [], []
 
@@ -538,9 +559,11 @@ def take_packed(pairs, P1):
 
 
 def drop_pack_ahead():
-    """Forget every request (end of a forward): nothing stale survives into the next one."""
+    """Forget every request (end of a forward): nothing stale survives into the next one --
+    including a held-back pack whose Wts a failed forward may already have freed."""
     _PACK_AHEAD.clear()
     _PACKED.clear()
+    _PACK_DEFERRED.clear()
 
 
 _PACK_DEFERRED = []     # at most one pack launch's arguments, held for take_deferred_pack
@@ -1476,9 +1499,11 @@ class BagEncoderFn(torch.autograd.Function):
             # the column pass folded into the row kernels: per layer, the kernel that forms the
             # row spectrum leaves its column-DFT partials, blindno_colmix forms Xs and the mixed Y,
             # and the row inverse rebuilds its row coefficients from Y
-            Dg2 = _grid_spec2(grid, N1, N2, P1, P2, meta.m1, meta.m2)
-            part = cs.part(1, X)
-            pk = take_deferred_pack()
+            try:
+                Dg2 = _grid_spec2(grid, N1, N2, P1, P2, meta.m1, meta.m2)
+                part = cs.part(1, X)
+            finally:            # never leave the held-back pack behind (its Wts die with us)
+                pk = take_deferred_pack()
             if pk is not None:      # the pack rides along the first row DFT (colmix reads it)
                 call("blindno_rowdft_bag_lift_cd_pack", ptr(X), ptr(idx_t), ptr(part), ptr(cs.Tp),
                      ptr(cs.tab), B, T, L, N1, N2, P1, P2, meta.m2, *pk, stream_ptr())
@@ -1871,7 +1896,7 @@ def _mse_blocks(n):
     return max(1, min(1024, (n + 1023) // 1024))
 
 
-_MSE_COUNTER = {}
+_MSE_COUNTER = None     # the caller-owned completion counter (loss_counter), or None
 _UNIT_SEED = None       # the constant 1.0 a caller seeds backward() with (unit_seed)
 
 
@@ -1888,16 +1913,30 @@ def unit_seed(one: torch.Tensor):
         _UNIT_SEED = prev
 
 
+@contextlib.contextmanager
+def loss_counter(counter: torch.Tensor):
+    """Within this context the fused MSE forward uses ``counter`` (one int32, zero; the
+    launch's last workgroup resets it) as its completion counter instead of a fresh zeroed one.
+    For a caller that owns one counter per captured graph (GraphedBagStep: the last slot of a
+    key's index blob, zeroed before capture), so a replay needs no memset node.  The counter
+    must not be shared by launches that may run concurrently (two streams)."""
+    global _MSE_COUNTER
+    if counter.dtype != torch.int32 or counter.numel() != 1 or not counter.is_cuda:
+        raise BlindnoError("loss_counter: one int32 device element")
+    prev, _MSE_COUNTER = _MSE_COUNTER, counter
+    try:
+        yield
+    finally:
+        _MSE_COUNTER = prev
+
+
 def _mse_counter(dev):
-    """The fused MSE forward's completion counter (one per device, zero between launches;
-    created outside stream capture by the eager warm-up, so graphs reference ordinary memory)."""
-    key = str(dev)
-    c = _MSE_COUNTER.get(key)
-    if c is None:
-        c = torch.zeros(1, dtype=torch.int32, device=dev)
-        if not torch.cuda.is_current_stream_capturing():
-            _MSE_COUNTER[key] = c
-    return c
+    """The fused MSE forward's completion counter: the caller's (loss_counter), or a fresh
+    zeroed one per launch -- never one shared across launches that could overlap on different
+    streams (their workgroups would count into each other's finish)."""
+    if _MSE_COUNTER is not None:
+        return _MSE_COUNTER
+    return torch.zeros(1, dtype=torch.int32, device=dev)
 
 
 class MSEFn(torch.autograd.Function):

@@ -249,6 +249,7 @@ class GraphedBagStep:
         self.graphs = {}
         self.idx = {}
         self.lw = {}
+        self.ctr = {}
         self.out = {}
         self.loss = {}
         self.T = x.shape[1]
@@ -260,9 +261,24 @@ class GraphedBagStep:
         self._ev = [None] * len(self._ring)
         self._k = 0
 
-    def _seeded(self):
-        """The loss's gradient for the unit seed formed in its forward pass (ops.unit_seed)."""
-        return ops.unit_seed(self._one) if UNIT_SEED_LOSS else contextlib.nullcontext()
+    def _new_blob(self, L):
+        """The key's static device buffer: [idx (L) | weights (L, float32 bits) | the fused
+        MSE's completion counter (1, ops.loss_counter)], zeroed before the capture."""
+        blob = torch.zeros(2 * L + 1, dtype=torch.int32, device=self.x.device)
+        self.blob = getattr(self, "blob", {})
+        self.blob[L] = blob
+        self.idx[L] = blob[:L]
+        self.lw[L] = blob[L:2 * L].view(torch.float32)
+        self.ctr[L] = blob[2 * L:]
+
+    def _seeded(self, L):
+        """The loss's gradient for the unit seed formed in its forward pass (ops.unit_seed),
+        and the key's own loss completion counter (ops.loss_counter)."""
+        st = contextlib.ExitStack()
+        st.enter_context(ops.loss_counter(self.ctr[L]))
+        if UNIT_SEED_LOSS:
+            st.enter_context(ops.unit_seed(self._one))
+        return st
 
     def _loss(self, out, accumulate):
         """The step's loss; with the fused MSE the running loss sum is accumulated by the loss
@@ -276,7 +292,7 @@ class GraphedBagStep:
     def _body(self, L, accumulate=True):
         bag = (self.idx[L], self.lw[L]) if self.dedup else self.idx[L]
         out = self.model(self.x, self.grid, bag_idx=bag)
-        with self._seeded():                          # backward is seeded with self._one
+        with self._seeded(L):                         # backward is seeded with self._one
             loss, add = self._loss(out, accumulate)
         with ops.deferred_reductions() as fin:        # one batched gradient finalisation,
             loss.backward(self._one)
@@ -294,7 +310,7 @@ class GraphedBagStep:
         h = self.model.forward_encoder(self.x, self.grid, bag_idx=bag)
         hd = h.detach().requires_grad_(True)
         out = self.model.forward_heads(hd)
-        with self._seeded():
+        with self._seeded(L):
             loss, add = self._loss(out, accumulate)
         with ops.deferred_reductions() as fin:
             loss.backward(self._one)
@@ -330,11 +346,7 @@ class GraphedBagStep:
             return
         if self.overlap:
             return self._capture_split(L)
-        blob = torch.zeros(2 * L, dtype=torch.int32, device=self.x.device)
-        self.blob = getattr(self, "blob", {})
-        self.blob[L] = blob
-        self.idx[L] = blob[:L]
-        self.lw[L] = blob[L:].view(torch.float32)
+        self._new_blob(L)
         saved = self._buffers()
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream())
@@ -351,11 +363,7 @@ class GraphedBagStep:
         self.graphs[L] = g
 
     def _capture_split(self, L: int):
-        blob = torch.zeros(2 * L, dtype=torch.int32, device=self.x.device)
-        self.blob = getattr(self, "blob", {})
-        self.blob[L] = blob
-        self.idx[L] = blob[:L]
-        self.lw[L] = blob[L:].view(torch.float32)
+        self._new_blob(L)
         saved = self._buffers()
         side = torch.cuda.Stream(self.x.device)
         side.wait_stream(torch.cuda.current_stream())
@@ -386,6 +394,7 @@ class GraphedBagStep:
         self.loss.clear()
         self.idx.clear()
         self.lw.clear()
+        self.ctr.clear()
         getattr(self, "blob", {}).clear()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()

@@ -248,3 +248,68 @@ def test_grid_spectrum_cache_follows_fc0_and_grid():
         c2 = m2(x, grid.clone())          # fresh grid storage: computed from scratch
     assert not torch.equal(a, b) and not torch.equal(b, c)
     assert rel_l2(c.cpu().numpy(), c2.cpu().numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("width,B", [(12, 2), (16, 10)])
+@pytest.mark.parametrize("toggle", ["default", "HEAD_BWD_MERGED", "UNPACK_FOLD", "HOST_ENC_MIX",
+                                    "REDIRECT_GRADS"])
+def test_deferred_finalisation_toggles_match_eager(toggle, width, B, monkeypatch):
+    """The batched gradient finalisation (ops.deferred_reductions, which every graphed step
+    takes) with each of its A/B switches turned off, against eager backward.  Width
+    16 is outside the range the heads' merged weight-gradient kernel takes (5..15) and B = 10
+    splits the weight gradient over samples: the grouped heads' (G, ...) reduction is then read
+    slice-wise by the unpacks, which must not share a launch with it."""
+    import blindno
+    from blindno import ops, train
+    from blindno.train import DataParallel, FlatAdam, GraphedBagStep, grid2d, trained_parameters
+    if toggle != "default":
+        mod = train if toggle == "REDIRECT_GRADS" else ops
+        monkeypatch.setattr(mod, toggle, False)
+    T, N = 60, 32
+    g = torch.Generator(device="cuda").manual_seed(21)
+    x = torch.randn(B, T, N, N, device="cuda", generator=g)
+    y = torch.randn(B, N, N, 2, device="cuda", generator=g)
+    grid = grid2d(N, N, "cuda")
+    rs = np.random.RandomState(2)
+    draws = [rs.choice(T, rs.randint(50, T)) for _ in range(2)]
+    finals = []
+    for graphed in (False, True):
+        torch.manual_seed(13)
+        m = blindno.NIOFP2D_FNO(2, 3, 100, 25, 3, width, 6, 2).cuda().train()
+        opt = FlatAdam(trained_parameters(m), lr=1e-3)
+        if graphed:
+            gs = GraphedBagStep(m, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+            for idx in draws:
+                gs.step(idx)
+        else:
+            for idx in draws:
+                blindno.mse_loss(m(x, grid, bag_idx=idx), y).backward()
+                opt.step()
+                opt.zero_grad()
+        torch.cuda.synchronize()
+        finals.append(opt.flat.cpu().numpy().copy())
+    assert np.isfinite(finals[1]).all()
+    assert rel_l2(finals[1], finals[0]) <= 1e-6
+
+
+def test_mse_counter_per_launch_streams():
+    """The fused MSE forward's completion counter is per launch (or the caller's, per graph):
+    two losses enqueued on two streams at once each return their own value."""
+    import blindno
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = [torch.randn(4, 128, 128, 2, device="cuda", generator=g) for _ in range(4)]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1.wait_stream(torch.cuda.current_stream())
+    s2.wait_stream(torch.cuda.current_stream())
+    outs = []
+    for _ in range(20):
+        with torch.cuda.stream(s1):
+            l1 = blindno.mse_loss(a[0], a[1])
+        with torch.cuda.stream(s2):
+            l2 = blindno.mse_loss(a[2], a[3])
+        outs.append((l1, l2))
+    torch.cuda.synchronize()
+    r1 = torch.mean((a[0].double() - a[1].double()) ** 2).item()
+    r2 = torch.mean((a[2].double() - a[3].double()) ** 2).item()
+    for l1, l2 in outs:
+        assert abs(l1.item() - r1) <= 1e-5 * r1 and abs(l2.item() - r2) <= 1e-5 * r2
