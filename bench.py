@@ -346,11 +346,14 @@ def main():
         if timer:
             # the limiter: the bag-level projection is fp32 VALU-issue-bound (PMC valu_issue_util);
             # the conv family runs on the fp32 matrix cores
+            # PMC records of this config's shapes (profiles/pmc_traffic.json: config C unprefixed,
+            # config E as "E:<entry>", tools/pmc_traffic.py --prefix)
+            pre = {"C": "", "E": "E:"}.get(a.config)
             res["roofline"] = timer.roofline(HBM_PEAK_GBS, FP32_PEAK_TFLOPS,
                                              bound="valu" if timer.name == timing.DOMINANT else None,
-                                             traffic_per_point=timing.pmc_traffic(ROOT, timing.DOMINANT)
-                                             if a.config == "C" else None)
-            rec = timing.pmc_record(ROOT, timing.DOMINANT) if a.config == "C" else None
+                                             traffic_per_point=timing.pmc_traffic(ROOT, pre + timing.DOMINANT)
+                                             if pre is not None else None)
+            rec = timing.pmc_record(ROOT, pre + timing.DOMINANT) if pre is not None else None
             if res["roofline"] and rec and "valu_issue_util" in rec:
                 # the limiter of this kernel (profiles/pmc_traffic.json, tools/pmc_traffic.py)
                 res["roofline"]["valu_issue_util"] = rec["valu_issue_util"]
@@ -366,7 +369,7 @@ def main():
                     res["roofline"]["valu_issue_util_benched_step"] = sb["valu_issue_util"]
                     res["roofline"]["valu_issue_util_benched_step_source"] = sb.get("source")
             if a.config in ("C", "E"):
-                res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev)
+                res["roofline_spectral"] = spectral_roofline(model, grid, B, T, N, dev, pmc_prefix=pre)
         if world == 1 and a.config in ("A", "B", "C", "D", "E"):
             # the reference's CPU path on the same weights / inputs: accuracy parity of the
             # benched step (the "rel-L2 drift error" half of BASELINE's metric), then its timing
@@ -394,7 +397,7 @@ SPECTRAL_PMC_KERNELS = ("colfuse (blindno_colpass, FNO_input)", "blindno_rowidft
 SPECTRAL_PMC_KERNELS_FOLDED = ("blindno_colmix", "blindno_rowidft_epi_zc")
 
 
-def spectral_roofline(model, grid, B, T, N, dev):
+def spectral_roofline(model, grid, B, T, N, dev, pmc_prefix=""):
     """HBM roofline of one FNO_input spectral layer (the north star's 'spectral-conv kernel') at
     the mean bag size (L = 75), timed with HIP events on the launch stream; algorithmic bytes per
     SURVEY.md 8d: 4 Bn Ci P^2 (read x) + 4 Bn Co P^2 (write y) + 16 Ci Co m1 m2 (weights).
@@ -442,13 +445,29 @@ def spectral_roofline(model, grid, B, T, N, dev):
             call("blindno_rowidft_epi_zc", ptr(Y), ptr(x), ptr(cw), ptr(cb), ptr(z), ptr(cs.tb), ptr(cs.tab),
                  ptr(p_out), ptr(cs.Tp), Bn, C, P, P, m, m, 1, 1, P, P, stream_ptr())
 
-    def timed(layer):
-        # the best of three 10-launch trials: one trial of a round-5 run read 2x the others
-        # (gpurun_out/bench_r05z_C.json), a host or scheduling stall inside the event pair
+        # the same layer's adjoint as the step chains it: colmix (direction 1) + the adjoint row
+        # inverse with GELU' of the layer input, the 1x1-conv weight gradient and the previous
+        # layer's column-DFT partials (blindno_rowidft_bwd_zc); dz given as a field
+        dzt, dxt = torch.randn_like(x), torch.empty_like(x)
+        pa_in, pa_out = cs.part(C, x), cs.part(C, x)
+        call("blindno_rowdft_cd", ptr(dzt), ptr(pa_in), ptr(cs.Tp), ptr(cs.tab), Bn, C, P, P, m, 0, P, P,
+             stream_ptr())
+        pw = torch.empty(ops.query("blindno_colspec_bwd_nchunk", Bn, P), C * C + C, device=dev)
+
+        def adjoint():
+            _, Yb = cs.mix(pa_in, cs.nb, Wt, 1)
+            call("blindno_rowidft_bwd_zc", ptr(Yb), ptr(dzt), ptr(cw), ptr(x), ptr(dxt), ptr(cs.tb), ptr(cs.tab),
+                 ptr(pa_out), ptr(cs.Tp), ptr(pw), Bn, C, P, P, m, m, 1, P, P, stream_ptr())
+
+    trials = {}
+
+    def timed(layer, name=None):
+        # the best of five 10-launch trials, with min / median / max kept for the line: one trial
+        # of a round-5 run read 2x the others (gpurun_out/bench_r05z_C.json)
         for _ in range(3):
             layer()
-        best = None
-        for _ in range(3):
+        ts = []
+        for _ in range(5):
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             reps = 10
             ev0.record()
@@ -456,9 +475,11 @@ def spectral_roofline(model, grid, B, T, N, dev):
                 layer()
             ev1.record()
             torch.cuda.synchronize()
-            ms = ev0.elapsed_time(ev1) / reps
-            best = ms if best is None else min(best, ms)
-        return best
+            ts.append(ev0.elapsed_time(ev1) / reps)
+        if name is not None:
+            trials[name] = {"min": round(min(ts), 4), "median": round(sorted(ts)[len(ts) // 2], 4),
+                            "max": round(max(ts), 4)}
+        return min(ts)
 
     nbytes = 4 * Bn * C * P * P * 2 + 16 * C * C * m * m
     gb = lambda ms: nbytes / (ms * 1e-3) / 1e9
@@ -469,8 +490,14 @@ def spectral_roofline(model, grid, B, T, N, dev):
             "unchained": {"kernels": "blindno_rowdft + blindno_colpass + blindno_rowidft_epi",
                           "achieved": round(gb(ms_u), 1), "frac": round(gb(ms_u) / HBM_PEAK_GBS, 4),
                           "ms_per_layer": round(ms_u, 4)}}
+    adj = None
     if folded is not None:
-        ms = timed(folded)
+        ms = timed(folded, "forward")
+        ms_a = timed(adjoint, "adjoint")
+        ab = 4 * Bn * C * P * P * 3 + 16 * C * C * m * m      # read dz, x; write dx
+        adj = {"kernels": "blindno_colmix (direction 1) + blindno_rowidft_bwd_zc", "bytes": int(ab),
+               "achieved": round(ab / (ms_a * 1e-3) / 1e9, 1),
+               "frac": round(ab / (ms_a * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms_per_layer": round(ms_a, 4)}
         kern = ("blindno_colmix + blindno_rowidft_epi_zc (one chained FNO_input layer with the column pass "
                 "folded into the row kernels: the mixed spectrum in, the next layer's column-DFT partials out)")
         pmc_keys = SPECTRAL_PMC_KERNELS_FOLDED
@@ -483,11 +510,16 @@ def spectral_roofline(model, grid, B, T, N, dev):
     res = {"kernels": kern, "bound": "hbm", "achieved": round(gb(ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(gb(ms) / HBM_PEAK_GBS, 4), "ms_per_layer": round(ms, 4),
            "algorithmic_bytes": int(nbytes), "snapshots": Bn, "traffic": None, **side}
+    if adj is not None:
+        res["adjoint"] = adj
+    res["trials_ms"] = trials
     # measured HBM bytes of the same layer shape (Bn = 300: tools/kbench.py "[input]" under
     # tools/pmc_kbench.sh -> profiles/pmc_traffic.json)
     from blindno import timing
-    parts = {k: timing.pmc_record(ROOT, k) for k in pmc_keys}
-    if Bn == 300 and all(v is not None for v in parts.values()):
+    parts = {k: timing.pmc_record(ROOT, pmc_prefix + k) for k in pmc_keys}
+    # only records of this very shape: Bn = 300 snapshots at this grid (a record without "N" is
+    # from the 128^2 runs of rounds 4-5)
+    if Bn == 300 and all(v is not None and v.get("N", 128) == N for v in parts.values()):
         res["traffic"] = int(sum(v["hbm_bytes_per_dispatch"] for v in parts.values()))
         res["traffic_by_kernel"] = {k: v["hbm_bytes_per_dispatch"] for k, v in parts.items()}
         res["traffic_source"] = sorted({v.get("source") for v in parts.values()})

@@ -411,3 +411,57 @@ def test_config_c_after_training_steps():
     ((ref - y.double()) ** 2).mean().backward()
     worst = _check_grads(m, opt, p64, 40)
     print("config C trained: fwd", e, "worst grad", worst)
+
+
+def test_config_c_channel_margins_across_draws():
+    """Config C's benched step (B = 4), after 40 training steps, on five recorded draws: every
+    output channel's forward
+    error against fp64 must stay within the 1e-5 bar AND within 2x (+ 1e-6) of what a plain fp32
+    evaluation of the same graph reaches against fp64 on that draw (the conditioning floor; the
+    diffusion channel's floor is close to the bar).  The per-channel
+    margins are printed, so a regression toward the floor shows before it fails."""
+    import oracle
+    from oracle import fno_ref
+    import blindno
+    from blindno import Encoder2D, NIOFP2D_FNO
+    from blindno.train import DataParallel, FlatAdam, GraphedBagStep, trained_parameters
+    torch.manual_seed(0)
+    B = 4
+    m = NIOFP2D_FNO(2, 3, 100, 25, 3, 12, 32, 2,
+                    branch_last_kernel=Encoder2D.kernel_for_grid(128)).cuda().train()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(B, 100, 128, 128, device="cuda", generator=g)
+    y = torch.randn(B, 128, 128, 2, device="cuda", generator=g)
+    grid = _grid2d(128)
+    opt = FlatAdam(trained_parameters(m), lr=5e-4)
+    gs = GraphedBagStep(m, blindno.mse_loss, opt, DataParallel(opt), x, y, grid)
+    # trained as bench.py trains before its parity leg (40 Adam steps at config C's lr): the
+    # diffusion channel's conditioning is that of a trained model, not of the initial weights
+    for idx in _draws(100, 5, k=40):
+        gs.step(idx)
+    torch.cuda.synchronize()
+    p64 = _oracle_params(m)
+    p32 = {k: v.detach().float() if not v.is_complex() else v.detach().to(torch.complex64)
+           for k, v in p64.items()}
+    worst = []
+    for idx in _draws(100, 23, k=5):
+        key = gs.replay(idx)
+        torch.cuda.synchronize()
+        out = gs.out[key].double()
+        with torch.no_grad():
+            ref = oracle.niofp2d_fno(p64, x.double(), grid.double(), idx=idx.tolist())
+            fno_ref.set_precision("fp32")
+            try:
+                r32 = oracle.niofp2d_fno(p32, x, grid, idx=idx.tolist()).double()
+            finally:
+                fno_ref.set_precision("fp64")
+        line = []
+        for c in range(out.shape[-1]):
+            e = rel_l2(out[..., c].cpu().numpy(), ref[..., c].cpu().numpy())
+            f = rel_l2(r32[..., c].cpu().numpy(), ref[..., c].cpu().numpy())
+            line.append(f"ch{c} gpu {e:.2e} fp32-floor {f:.2e} ({e / FWD_TOL:.2f} of bar)")
+            worst.append(e / FWD_TOL)
+            assert e <= FWD_TOL, (len(idx), c, e)
+            assert e <= 2 * f + 1e-6, (len(idx), c, e, f)
+        print(f"  L={len(idx)} key={key}: " + "; ".join(line))
+    print(f"  worst channel at {max(worst):.2f} of the bar")

@@ -2,6 +2,7 @@
 """Kernel micro-benchmarks at config-C shapes (HIP events on the launch stream).
 
     python tools/kbench.py [filter-regex]
+    KBENCH_N=256 KBENCH_MIX=fp16 python tools/kbench.py [filter-regex]     (config E's shapes)
 
 Times the C-ABI entry points of the FNO_input body (Bn = 4 * 75 snapshots, width 4,
 P = 160, m = 12) and of one head layer (Bn = 4, width 12, m = 32) in isolation, so kernel
@@ -38,6 +39,10 @@ def timeit(fn, iters=20, warm=3):
 def main():
     pat = sys.argv[1] if len(sys.argv) > 1 else ""
     blindno.load_library()
+    # KBENCH_N: the encoder grid (128: config C; 256: config E), KBENCH_MIX=fp16: config E's mix
+    NG = int(os.environ.get("KBENCH_N", "128"))
+    if os.environ.get("KBENCH_MIX"):
+        ops.set_mix_precision(os.environ["KBENCH_MIX"])
     dev = torch.device("cuda")
     torch.manual_seed(0)
     res = []
@@ -55,7 +60,8 @@ def main():
     extra = [(f"bn{b}", int(b), 4, 12, 1) for b in os.environ.get("KBENCH_BN", "").split(",") if b]
     for tag, Bn, C, m, Cout in [("input", 300, 4, 12, 1), ("u52", 208, 4, 12, 1), ("u50", 200, 4, 12, 1),
                                 *extra, ("head", 4, 12, 32, 1), ("head2", 8, 12, 32, 1)]:
-        P, N = 160, 128
+        N = NG
+        P = N + ops.pad_amount(N)
         z = torch.randn(Bn, C, P, P, device=dev)
         w1 = torch.randn(128, C, device=dev) * 0.3
         b1 = torch.randn(128, device=dev) * 0.1

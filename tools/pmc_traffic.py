@@ -2,7 +2,10 @@
 """Write profiles/pmc_traffic.json from a tools/pmc_kbench.sh run over kbench's "[input]" cases
 (config C's snapshot encoder at the mean bag size: Bn = 4 * 75 snapshots, P = 160, 128^2 crop).
 
-    python tools/pmc_traffic.py gpurun_out/pmck_TAG [profiles/rNN/TAG_pmc_summary.json]
+    python tools/pmc_traffic.py gpurun_out/pmck_TAG [profiles/rNN/TAG_pmc_summary.json] [--n 256 --prefix E:]
+
+--n / --prefix: the kbench run was at another encoder grid (KBENCH_N; config E: 256, its records
+are stored as "E:<entry>"); records are merged into the existing file (other prefixes kept).
 
 The optional second argument names the committed per-kernel summary of the same passes
 (tools/pmc_summary.py --json), recorded as each entry's "source".
@@ -27,7 +30,6 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NPTS = 300 * 128 * 128
 # ABI entry -> kernel-name pattern of its [input] kbench case (grid-size filter below)
 KERNELS = {
     "blindno_project_bag_fwd": r"bagproj_fwd_kernel",
@@ -51,8 +53,19 @@ KERNELS = {
 
 
 def main():
-    root = sys.argv[1]
-    src = sys.argv[2] if len(sys.argv) > 2 else os.path.relpath(root, ROOT)
+    args = sys.argv[1:]
+    n_grid, prefix = 128, ""
+    if "--n" in args:
+        i = args.index("--n")
+        n_grid = int(args[i + 1])
+        del args[i:i + 2]
+    if "--prefix" in args:
+        i = args.index("--prefix")
+        prefix = args[i + 1]
+        del args[i:i + 2]
+    root = args[0]
+    src = args[1] if len(args) > 1 else os.path.relpath(root, ROOT)
+    npts = 300 * n_grid * n_grid
     acc = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
     for f in glob.glob(os.path.join(root, "p*", "run_counter_collection.csv")):
@@ -76,10 +89,10 @@ def main():
         write = 1024 * a.get("WRITE_SIZE", 0.0)
         rec = {"fetch_bytes_x2": int(fetch), "write_bytes": int(write),
                "hbm_bytes_per_dispatch": int(fetch + write), "us_per_dispatch_profiled": round(t * 1e6, 2),
-               "grid": key[1], "source": src}
+               "grid": key[1], "source": src, "N": n_grid}
         if abi.startswith("blindno_project"):
-            rec["bytes_per_point"] = round((fetch + write) / NPTS, 3)
-            rec["points"] = NPTS
+            rec["bytes_per_point"] = round((fetch + write) / npts, 3)
+            rec["points"] = npts
         if "SQ_INSTS_VALU" in a and "GRBM_GUI_ACTIVE" in a:
             valu, trans = a["SQ_INSTS_VALU"], a.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
             mfma = a.get("SQ_INSTS_MFMA", 0.0)
@@ -88,9 +101,13 @@ def main():
             rec.update({"SQ_INSTS_VALU": int(valu), "SQ_INSTS_VALU_TRANS_F32": int(trans),
                         "SQ_INSTS_MFMA": int(mfma), "clock_GHz": round(clk / 1e9, 3),
                         "valu_issue_util": round(cyc / (1024 * clk * t), 3)})
-        out[abi] = rec
+        out[prefix + abi] = rec
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    json.dump(out, open(path, "w"), indent=1)
+    old = json.load(open(path)) if os.path.exists(path) else {}
+    # replace this prefix's records, keep the others
+    merged = {k: v for k, v in old.items() if not (k.startswith(prefix) and (prefix or ":" not in k))}
+    merged.update(out)
+    json.dump(merged, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
