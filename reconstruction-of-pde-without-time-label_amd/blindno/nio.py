@@ -11,7 +11,6 @@ seeded run sees the same bags.  ``bag_idx=`` overrides the draw (parity harness)
 """
 from __future__ import annotations
 
-import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -59,12 +58,9 @@ _SIDE = {}
 
 
 HEAD_STREAMS = True     # fork the two heads over two streams (ops.HeadPairFn)
-# the grouped heads' spectral weights packed by the encoder's pack launch (BLINDNO_PACK_AHEAD=0:
-# their own launch)
-PACK_HEADS_AHEAD = os.environ.get("BLINDNO_PACK_AHEAD", "1") != "0"
 # the encoder hands the grouped heads the bag mean ubar, the heads' lift forms their input
-# (BLINDNO_BAG_HEADS=0: the (B, N, N, width) field between them and two bag-mean launches)
-BAG_INPUT_HEADS = os.environ.get("BLINDNO_BAG_HEADS", "1") != "0"
+# (False, tests only: the (B, N, N, width) field between them and two bag-mean launches)
+BAG_INPUT_HEADS = True
 DEDUP_BAGS = True       # run the snapshot encoder once per distinct snapshot of a bag
 
 
@@ -146,7 +142,7 @@ class NIOFP2D_FNO(nn.Module):
         (ops.BagEncoderFn: snapshots read from x through the bag's indices); otherwise as the
         generic composition below (same numerics, gradients for x and grid)."""
         # the grouped heads' spectral weights are packed by the encoder's pack launch
-        if PACK_HEADS_AHEAD and x.is_cuda and HEAD_STREAMS and len(self._heads) == 2 and x.dim() == 4:
+        if x.is_cuda and HEAD_STREAMS and len(self._heads) == 2 and x.dim() == 4:
             hs = [getattr(self, nm) for nm in self._heads]
             w = self.fc0.out_features
             if all(isinstance(hd, FNO2d) for hd in hs) and hs[0].meta(w).__dict__ == hs[1].meta(w).__dict__:

@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -45,22 +44,25 @@ BAG_STATS_MAX_BYTES = 4 << 30
 # mix on the partials, the row coefficients rebuilt from the mixed spectrum in the next row
 # inverse's prologue): FNO_input at C = 4, m1 = m2 = 12 with the fp32 mix.  False: the fused
 # column pass (blindno_colpass) between the row kernels, as before.
-COLSPEC = os.environ.get("BLINDNO_COLSPEC", "1") != "0"
-# ... with the bag-level projection, the last layer's gradient dz = lw_l ghat v formed on load by
-# its readers instead of written by the projection backward (BLINDNO_BAGDZ=0: written)
-BAG_DZ_ON_LOAD = os.environ.get("BLINDNO_BAGDZ", "1") != "0"
+# (Kept as a module flag, not an environment switch: tests/test_gpu_colspec.py compares the two.)
+# With the bag-level projection, the last layer's gradient dz = lw_l ghat v is always formed on
+# load by its readers (the projection backward writes no dz field).
+COLSPEC = True
+# The flags below select between a fused launch and its general fallback, which other shapes
+# take anyway; the tests turn them off to check both forms (tests/test_gpu_graphs.py,
+# test_gpu_parity.py).  Settled defaults, no environment switches.
 # the grouped heads' backward: row DFT + conv gradient + the previous layer's mix gradient in
-# one launch per layer (BLINDNO_HEADBWD_MERGED=0: three launches)
-HEAD_BWD_MERGED = os.environ.get("BLINDNO_HEADBWD_MERGED", "1") != "0"
+# one launch per layer (False: three launches)
+HEAD_BWD_MERGED = True
 # the deferred finalisation stores the spectral weight gradients unpacked from the kernel that
-# finishes them (BLINDNO_UNPACK_FOLD=0: a separate unpack launch)
-UNPACK_FOLD = os.environ.get("BLINDNO_UNPACK_FOLD", "1") != "0"
+# finishes them (False: a separate unpack launch)
+UNPACK_FOLD = True
 # the encoder's spectral weight gradients hosted by its first layer's adjoint launch
-# (BLINDNO_HOST_ENC_MIX=0: the deferred finalisation's mix launch)
-HOST_ENC_MIX = os.environ.get("BLINDNO_HOST_ENC_MIX", "1") != "0"
+# (False: the deferred finalisation's mix launch)
+HOST_ENC_MIX = True
 # the bag encoder's spectral-weight pack (with the heads' pack_ahead requests) hosted by its
-# first row-DFT launch (BLINDNO_HOST_PACK=0: a pack launch of its own)
-HOST_PACK = os.environ.get("BLINDNO_HOST_PACK", "1") != "0"
+# first row-DFT launch (False: a pack launch of its own)
+HOST_PACK = True
 
 
 def set_mix_precision(name: str) -> None:
@@ -1003,9 +1005,6 @@ def _sub(buf, off):
     return buf[off:] if off else buf
 
 
-HEAD_WEIGHTS_IN_PLACE = os.environ.get("BLINDNO_HEAD_INPLACE", "1") != "0"
-
-
 class _GroupWeights:
     """The grouped heads' small weights: ``p(i)`` = the device pointer of head 0's tensor i,
     head g's at + g * S floats."""
@@ -1020,7 +1019,7 @@ class _GroupWeights:
                     direct = False
                     break
                 d = diff // g
-        if direct and d and HEAD_WEIGHTS_IN_PLACE:
+        if direct and d:
             self.base, self.buf, self.S = list(smalls[0]), None, d // 4
         else:
             self.offs, self.S = _offsets(smalls[0])
@@ -1641,7 +1640,7 @@ class BagEncoderFn(torch.autograd.Function):
         # the folded column pass with the bag-level projection: dz = lw_l ghat v is formed on load
         # by its two readers (the last layer's row DFT and row-inverse adjoint), so the projection
         # backward neither writes dz nor reads v (a field write and read less per step)
-        bagdz = cs is not None and bag is not None and crop is not None and BAG_DZ_ON_LOAD
+        bagdz = cs is not None and bag is not None and crop is not None
         dz = None if bagdz else (_empty(Bn, C, P1, P2, like=gh) if crop else
                                  torch.zeros(Bn, C, P1, P2, dtype=F32, device=gh.device))
         np_p = Hd * C + Hd + Cout * Hd + Cout

@@ -17,7 +17,6 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
-import os
 import time
 from typing import Iterable, List, Optional
 
@@ -30,11 +29,8 @@ from ._lib import call, ptr, stream_ptr
 
 
 # the graphed step's deferred finalisation writes the gradients straight into the flat buffer
-# (BLINDNO_REDIRECT=0: into their own tensors, then one gather copy)
-REDIRECT_GRADS = os.environ.get("BLINDNO_REDIRECT", "1") != "0"
-# the loss's gradient for the step's unit seed formed in the loss's forward pass
-# (BLINDNO_UNIT_SEED=0: its own launch in backward)
-UNIT_SEED_LOSS = os.environ.get("BLINDNO_UNIT_SEED", "1") != "0"
+# (False, tests only: into their own tensors, then one gather copy)
+REDIRECT_GRADS = True
 
 
 def _real(t: torch.Tensor) -> torch.Tensor:
@@ -276,8 +272,7 @@ class GraphedBagStep:
         and the key's own loss completion counter (ops.loss_counter)."""
         st = contextlib.ExitStack()
         st.enter_context(ops.loss_counter(self.ctr[L]))
-        if UNIT_SEED_LOSS:
-            st.enter_context(ops.unit_seed(self._one))
+        st.enter_context(ops.unit_seed(self._one))
         return st
 
     def _loss(self, out, accumulate):

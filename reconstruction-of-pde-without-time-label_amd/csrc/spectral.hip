@@ -1157,26 +1157,6 @@ bool colfuse_on() {
   return g_colfuse != 0;
 }
 
-// the fused pass also for the fp16-operand mix (config E); BLINDNO_COLFUSE16=0: the split kernels
-int g_colfuse16 = -1;
-bool colfuse16_on() {
-  if (g_colfuse16 < 0) {
-    const char* e = getenv("BLINDNO_COLFUSE16");
-    g_colfuse16 = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_colfuse16 != 0;
-}
-
-// colfuse workgroup size: 0 = by launch size (default), 4 or 8 waves forced (BLINDNO_COLFUSE_WAVES)
-int g_colfuse_waves = -1;
-int colfuse_waves() {
-  if (g_colfuse_waves < 0) {
-    const char* e = getenv("BLINDNO_COLFUSE_WAVES");
-    g_colfuse_waves = e ? atoi(e) : 0;
-  }
-  return g_colfuse_waves;
-}
-
 BLINDNO_API int blindno_set_colfuse(int on) {
   const int prev = colfuse_on() ? 1 : 0;
   g_colfuse = on ? 1 : 0;
@@ -1207,9 +1187,9 @@ BLINDNO_API int blindno_colpass_g(const float* At, const float* Wt, float* Xs, f
   // at most 64 kept rows, at most 10 row blocks per K chunk
   // workgroups of 8 waves when the launch has fewer than two workgroups per CU (the heads)
   const int G16 = 16 / cin;
-  const int NWf = (colfuse_waves() == 8 || (colfuse_waves() == 0 && cdiv(npairs, G16 > 0 ? G16 : 1) < 512)) ? 8 : 4;
+  const int NWf = cdiv(npairs, G16 > 0 ? G16 : 1) < 512 ? 8 : 4;
   const int KSf = Jt >= NWf ? 1 : NWf / Jt;      // K chunks so that the waves have units
-  if (colfuse_on() && (!h16 || colfuse16_on()) && Ci == Co && Ci <= 16 && K1p <= 64 &&
+  if (colfuse_on() && Ci == Co && Ci <= 16 && K1p <= 64 &&
       (HB + KSf - 1) / KSf <= 10) {
     const int tiled = rowinv_tile_layout(Bn, cout, P1, P2, m2) ? 1 : 0;
     const int G = G16;
