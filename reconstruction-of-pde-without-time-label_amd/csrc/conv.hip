@@ -74,6 +74,8 @@ struct ConvArgs {
   int nph;                      // BWD_D: stride-phase classes (blockIdx.z = class + nph split)
   int64_t slab;                 // FWD / BWD_D split: floats per partial output slab
   int wt;                       // BWD_D tap-major: the weights come as Wt[tap][ci][co]
+  int bsep;                     // BWD_W: the bias column (the last of Ncol) is not a GEMM column;
+                                // the first column tile's workgroups form it as row sums of dy
   FastDiv dKHW, dKW, dHoWo, dWo, dHiWi, dWi;
   Phase phase[kMaxPhases];      // BWD_D
 };
@@ -173,7 +175,7 @@ __device__ __forceinline__ Tap decode_tap(const ConvArgs& g, int ng) {
     t.kw = khw - t.kh * g.KW;
     t.coff = (int64_t)ci * g.Hi * g.Wi;
     t.kind = 1;
-  } else if (ng == g.Ci * KHW) {
+  } else if (ng == g.Ci * KHW && !g.bsep) {
     t.kind = 2;
   }
   return t;
@@ -256,6 +258,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
   // register staging: loads run one K-step ahead of the MFMAs (two steps ahead, with two
   // register sets, costs the 128 x 128 kernels an occupancy step: 3-8 % slower, r03t)
   float ra[EA], rb[EB];
+  // BWD_W with g.bsep: db[co] = sum dy[co] over this split's pixels, summed on the A loads by
+  // the first column tile's workgroups (the GEMM then has exactly Ci KH KW columns: a tile
+  // holding only the bias column cost up to 10 % of the MFMAs, e.g. 1153 = 9 x 128 + 1)
+  constexpr int EA4 = (TM && MODE == BWD_W) ? EA / 4 : 1;
+  float bsum[EA4];
+#pragma unroll
+  for (int e = 0; e < EA4; ++e) bsum[e] = 0.f;
+  const bool bcol = MODE == BWD_W && TM && g.bsep && blockIdx.x == 0;
   auto gload = [&](int kt) {
     const int k0 = kbeg + kt * BK;
     if constexpr (TM && MODE != BWD_W) {
@@ -312,6 +322,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
                              : (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < 4; ++r) ra[4 * e + r] = a4[r];
+        if (bcol) bsum[e] += (a4[0] + a4[1]) + (a4[2] + a4[3]);
       }
     } else {
 #pragma unroll
@@ -416,11 +427,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const float* __restrict
     }
   }
 
+  if constexpr (MODE == BWD_W && TM) {
+    if (bcol) {
+      // the 4 threads of a row (tid & 3: adjacent lanes) in a fixed butterfly order
+#pragma unroll
+      for (int e = 0; e < EA4; ++e) {
+        float v = bsum[e];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        const int mg = m0 + (tid >> 2) + 64 * e;
+        if ((tid & 3) == 0 && mg < g.M) out[((int64_t)blockIdx.z * g.M + mg) * g.Ncol + g.Ncol - 1] = v;
+      }
+    }
+  }
+
   // epilogue: lane holds rows acc_row(r, gm) of column cm of each MF x MF block
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int ng = n0 + wn * (BN / 2) + j * MF + cm;
-    if (ng >= g.Ncol) continue;
+    if (ng >= g.Ncol - (MODE == BWD_W ? g.bsep : 0)) continue;
     if (MODE == BWD_W) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -495,6 +520,7 @@ bool make_args(ConvArgs& g, int N, int Ci, int Hi, int Wi, int Co, int KH, int K
   g.nph = 1;
   g.slab = 0;
   g.wt = 0;
+  g.bsep = 0;
   g.dKHW = FastDiv::make((unsigned)(KH * KW));
   g.dKW = FastDiv::make((unsigned)KW);
   g.dHoWo = FastDiv::make((unsigned)(Ho * Wo));
@@ -812,6 +838,9 @@ BLINDNO_API int blindno_conv2d_wgrad_nsplit(int N, int Ci, int Hi, int Wi, int C
   return wgrad_splits(g);
 }
 
+#ifndef CONV_BSEP
+#define CONV_BSEP 1
+#endif
 BLINDNO_API int blindno_conv2d_bwd_weight(const float* dy, const float* x, float* dwb,
                                           float* partial, int nsplit, int N, int Ci, int Hi, int Wi,
                                           int Co, int KH, int KW, int sh, int sw, int ph, int pw,
@@ -827,7 +856,12 @@ BLINDNO_API int blindno_conv2d_bwd_weight(const float* dy, const float* x, float
   const int nz = cdiv(g.K, g.kchunk);
   if ((int64_t)g.M * g.Ncol >= INT32_MAX / (nz > 0 ? nz : 1)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  launch_igemm<BWD_W>(dim3(1, 1, nz), g.M, g.Ncol, dy, x, nullptr, nz > 1 ? partial : dwb, g, st);
+  // the vectorised (tap-major) loaders form the bias column from dy's row sums (bsep); the
+  // column grid then covers the Ci KH KW weight columns only (launch_igemm takes the TM form
+  // under exactly this condition)
+  g.bsep = (CONV_BSEP && ((uintptr_t)dy & 15) == 0 && use_tm(BWD_W, g)) ? 1 : 0;
+  launch_igemm<BWD_W>(dim3(1, 1, nz), g.M, g.Ncol - g.bsep, dy, x, nullptr, nz > 1 ? partial : dwb, g,
+                      st);
   if (nz > 1) {
     const int e = (int)hipGetLastError();
     if (e) return e;
