@@ -62,6 +62,70 @@ __device__ __forceinline__ f32x2 norm_cdf_pair_pdf(f32x2 hk, f32x2& ep) {
 }
 
 
+// norm_cdf_pair / norm_cdf_pair_pdf on N pairs in lockstep (every step issued for all N pairs
+// before the next step): the same operations per value in the same order (bit-identical), but
+// consecutive packed ops are independent.  One pair at a time, every Horner step read the
+// previous packed result and hipcc put an s_nop between them: 766 of them per 16-row item of
+// the encoder's forward row kernel (profiles/r06/r06_issue_budget_rowfuse_fwd_zc_item.txt).
+template <int N>
+__device__ __forceinline__ void norm_cdf_pairs(const f32x2 (&hk)[N], f32x2 (&cdf)[N]) {
+  f32x2 t[N], e[N], q[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    t[j] = (f32x2){__builtin_amdgcn_rcpf(fmaf(fabsf(hk[j].x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk[j].y), kT, 1.0f))};
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 sq = hk[j] * hk[j];
+    e[j] = (f32x2){__builtin_amdgcn_exp2f(-sq.x), __builtin_amdgcn_exp2f(-sq.y)};
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], splat2(0.5307027145f), splat2(-0.7265760135f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], q[j], splat2(0.7107068705f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], q[j], splat2(-0.142248368f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], q[j], splat2(0.127414796f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = -(q[j] * t[j]);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 m = pk_fma(q[j], e[j], splat2(0.5f));          // 1/2 - half
+    cdf[j] = (f32x2){copysignf(m.x, hk[j].x), copysignf(m.y, hk[j].y)} + splat2(0.5f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void norm_cdf_pdf_pairs(const f32x2 (&hk)[N], f32x2 (&cdf)[N],
+                                                   f32x2 (&ep)[N]) {
+  f32x2 t[N], q[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    t[j] = (f32x2){__builtin_amdgcn_rcpf(fmaf(fabsf(hk[j].x), kT, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(hk[j].y), kT, 1.0f))};
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 ea = pk_fma(-hk[j], hk[j], splat2(kLog2Kp));
+    ep[j] = (f32x2){__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], splat2(1.129831073415752f), splat2(-1.5468324069611348f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], q[j], splat2(1.513048048260859f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], q[j], splat2(-0.3028373926078324f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], q[j], splat2(0.27125769625911544f));
+#pragma unroll
+  for (int j = 0; j < N; ++j) q[j] = -(q[j] * t[j]);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 m = pk_fma(q[j], ep[j], splat2(0.5f));         // 1/2 - half
+    cdf[j] = (f32x2){copysignf(m.x, hk[j].x), copysignf(m.y, hk[j].y)} + splat2(0.5f);
+  }
+}
+
 // norm_cdf_pair_pdf without the final + 1/2: Phi(h) - 1/2 (the bag-level projection adds the
 // halves back once per point, csrc/bagproj.hip)
 __device__ __forceinline__ f32x2 norm_cdf_pair_pdf_centered(f32x2 hk, f32x2& ep) {

@@ -196,10 +196,11 @@ __global__ __launch_bounds__(256) void project_fwd_mfma_kernel(
         f32x4 d = {bb, bb, bb, bb};
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x4f32(az[np][kk], bw[kk], d, 0, 0, 0);
-        const f32x2 h01 = {d[0], d[1]}, h23 = {d[2], d[3]};
-        f32x2 e01, e23;
-        const f32x2 g01 = h01 * norm_cdf_pair(h01, e01);          // k GELU
-        const f32x2 g23 = h23 * norm_cdf_pair(h23, e23);
+        const f32x2 hh[2] = {{d[0], d[1]}, {d[2], d[3]}};
+        f32x2 cdf[2];
+        norm_cdf_pairs<2>(hh, cdf);                                 // both pairs in lockstep
+        const f32x2 g01 = hh[0] * cdf[0];                           // k GELU
+        const f32x2 g23 = hh[1] * cdf[1];
 #pragma unroll
         for (int c = 0; c < COM; ++c) {
           const f32x2 wv = splat2(w2v[c]);
@@ -393,8 +394,10 @@ __global__ __launch_bounds__(256) void project_bwd_mfma_kernel(
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x4f32(az[np][kk], bw[kk], d, 0, 0, 0);
         const f32x2 h01 = {d[0], d[1]}, h23 = {d[2], d[3]};
-        f32x2 ep01, ep23;
-        const f32x2 cdf01 = norm_cdf_pair_pdf(h01, ep01), cdf23 = norm_cdf_pair_pdf(h23, ep23);
+        const f32x2 hh[2] = {h01, h23};
+        f32x2 cdfv[2], epv[2];
+        norm_cdf_pdf_pairs<2>(hh, cdfv, epv);                       // both pairs in lockstep
+        const f32x2 cdf01 = cdfv[0], cdf23 = cdfv[1], ep01 = epv[0], ep23 = epv[1];
         f32x2 da01 = {0.f, 0.f}, da23 = {0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < COM; ++c) {

@@ -475,17 +475,13 @@ __global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
 __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
 #if ROWFUSE_PKGELU
   using namespace blindno::gelu_pk;
-  f32x4 y;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const f32x2 v = {x[2 * i], x[2 * i + 1]};
-    f32x2 e;
-    const f32x2 cdf = norm_cdf_pair(v * splat2(kK), e);
-    const f32x2 g = v * cdf;
-    y[2 * i] = g.x;
-    y[2 * i + 1] = g.y;
-  }
-  return y;
+  // both pairs in lockstep (norm_cdf_pairs): no wait state between dependent packed steps
+  const f32x2 v[2] = {{x[0], x[1]}, {x[2], x[3]}};
+  const f32x2 hk[2] = {v[0] * splat2(kK), v[1] * splat2(kK)};
+  f32x2 cdf[2];
+  norm_cdf_pairs<2>(hk, cdf);
+  const f32x2 g0 = v[0] * cdf[0], g1 = v[1] * cdf[1];
+  return (f32x4){g0.x, g0.y, g1.x, g1.y};
 #else
   return (f32x4){gelu_f(x[0]), gelu_f(x[1]), gelu_f(x[2]), gelu_f(x[3])};
 #endif
@@ -494,14 +490,14 @@ __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
 __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 #if ROWFUSE_PKGELU
   using namespace blindno::gelu_pk;
+  const f32x2 v[2] = {{x[0], x[1]}, {x[2], x[3]}};
+  const f32x2 hk[2] = {v[0] * splat2(kK), v[1] * splat2(kK)};
+  f32x2 cdf[2], ep[2];
+  norm_cdf_pdf_pairs<2>(hk, cdf, ep);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const f32x2 v = {x[2 * i], x[2 * i + 1]};
-    const f32x2 hk = v * splat2(kK);
-    f32x2 ep;
-    const f32x2 cdf = norm_cdf_pair_pdf(hk, ep);
-    const f32x2 gv = v * cdf;
-    const f32x2 dv = pk_fma(hk, ep, cdf);          // Phi + h phi(h)
+    const f32x2 gv = v[i] * cdf[i];
+    const f32x2 dv = pk_fma(hk[i], ep[i], cdf[i]);    // Phi + h phi(h)
     a[2 * i] = gv.x;
     a[2 * i + 1] = gv.y;
     dg[2 * i] = dv.x;
