@@ -483,7 +483,7 @@ def spectral_roofline(model, grid, B, T, N, dev, pmc_prefix=""):
 
     nbytes = 4 * Bn * C * P * P * 2 + 16 * C * C * m * m
     gb = lambda ms: nbytes / (ms * 1e-3) / 1e9
-    ms_c, ms_u = timed(colpass_chained), timed(unchained)
+    ms_c, ms_u = timed(colpass_chained, "column_pass_chained"), timed(unchained, "unchained")
     side = {"column_pass_chained": {"kernels": "blindno_colpass + blindno_rowidft_epi_rd",
                                     "achieved": round(gb(ms_c), 1), "frac": round(gb(ms_c) / HBM_PEAK_GBS, 4),
                                     "ms_per_layer": round(ms_c, 4)},
