@@ -189,6 +189,45 @@ def test_conv2d_split_k(case):
     print(f"splits {splits}, weight scratch {nwf} / {nwd} floats")
 
 
+WGRAD_CASES = [
+    (5, 128, 64, 32, 128, 3, 3, 1, 1, 1, 1),   # N = 1152 + 1: the bias column outside the GEMM tiles
+    (4, 64, 32, 16, 128, 3, 3, 2, 2, 1, 1),    # 576 + 1: a ragged last column tile
+    (6, 1, 32, 32, 64, 1, 7, 1, 2, 0, 3),      # 7 + 1, 64 x 64 tiles
+    (3, 5, 13, 11, 7, 3, 2, 3, 2, 2, 1),       # odd output plane: the scalar loaders, bias as a column
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_CASES)
+def test_conv2d_wgrad_bias_column_split(case):
+    """blindno_conv2d_bwd_weight at split counts 1, 2, 7 and the default: the weight and bias
+    gradient (Co, Ci KH KW + 1) against fp64, deterministic, and with the vectorised loaders the
+    bias column formed from dy's row sums (ConvArgs::bsep) rather than a GEMM column."""
+    from blindno._lib import call, ptr, query, stream_ptr
+    N, Ci, Hi, Wi, Co, KH, KW, sh, sw, ph, pw = case
+    torch.manual_seed(sum(case) + 7)
+    x = torch.randn(N, Ci, Hi, Wi, device="cuda", dtype=torch.float64)
+    w = torch.randn(Co, Ci, KH, KW, device="cuda", dtype=torch.float64, requires_grad=True)
+    b = torch.randn(Co, device="cuda", dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, w, b, stride=(sh, sw), padding=(ph, pw))
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref = torch.cat([w.grad.reshape(Co, -1), b.grad[:, None]], 1)
+    xs, dys = x.float().contiguous(), dy.float().contiguous()
+    g = case
+    for ns in sorted({1, 2, 7, query("blindno_conv2d_wgrad_nsplit", *g)}):
+        outs = []
+        for _ in range(2):
+            dwb = torch.full((Co, Ci * KH * KW + 1), float("nan"), device="cuda")
+            part = torch.full((ns, dwb.numel()), float("nan"), device="cuda")
+            call("blindno_conv2d_bwd_weight", ptr(dys), ptr(xs), ptr(dwb), ptr(part), ns, *g, stream_ptr())
+            outs.append(dwb)
+        torch.cuda.synchronize()
+        assert torch.isfinite(outs[0]).all(), ns
+        assert rel_l2(outs[0][:, :-1].cpu().numpy(), ref[:, :-1].cpu().numpy()) <= 1e-5, ns
+        assert rel_l2(outs[0][:, -1].cpu().numpy(), ref[:, -1].cpu().numpy()) <= 1e-5, ns
+        assert torch.equal(outs[0], outs[1]), ns
+
+
 def _branch_masks(enc):
     """Forward hooks recording each ConvBlock's LeakyReLU branch (output > 0 <=> pre-activation > 0)."""
     masks, hooks = [], []
