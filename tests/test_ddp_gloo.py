@@ -102,7 +102,7 @@ def test_synthetic_bag_set_is_keyed_by_bag_id():
             assert torch.equal(xr, X[ids]) and torch.equal(yr, Y[ids])
 
 
-def _shard_worker(rank, world, port, q):
+def _shard_worker(rank, world, port, q, n_bags=22):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -111,7 +111,7 @@ def _shard_worker(rank, world, port, q):
             root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
             sys.path.insert(0, os.path.join(root, "reconstruction-of-pde-without-time-label_amd"))
             from blindno.train import shard_bag_ids, synthetic_bags
-            n_bags, B = 22, 4
+            B = 4
             ids = shard_bag_ids(n_bags, B, rank, world)
             X, Y = synthetic_bags(len(ids), 3, (4, 5), 2, seed=1234, device="cpu", bag_ids=ids)
             # every rank's ids and per-bag checksums, gathered over the process group
@@ -135,15 +135,16 @@ def _shard_worker(rank, world, port, q):
         raise
 
 
-def test_bag_sharding_gloo_world4():
-    """bench.py's bag-keyed sharding at world 4 (gloo, CPU): the ranks' shards are disjoint,
-    their union is the N = 1 bag set, and every bag's content equals the N = 1 set's."""
+@pytest.mark.parametrize("world,n_bags", [(4, 22), (8, 42)])
+def test_bag_sharding_gloo(world, n_bags):
+    """bench.py's bag-keyed sharding at world 4 and at the driver's world 8 (gloo, CPU): the
+    ranks' shards are disjoint, their union is the N = 1 bag set, and every bag's content equals
+    the N = 1 set's."""
     from blindno.train import shard_bag_ids, synthetic_bags
-    world = 4
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q, n_bags)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -155,7 +156,7 @@ def test_bag_sharding_gloo_world4():
     gi, gc = res[0][1], res[0][2]
     ids = [int(i) for a in gi for i in a if i >= 0]
     sums = {int(i): float(c) for a, b in zip(gi, gc) for i, c in zip(a, b) if i >= 0}
-    full = shard_bag_ids(22, 4, 0, 1)
+    full = shard_bag_ids(n_bags, 4, 0, 1)
     assert sorted(ids) == full and len(ids) == len(set(ids))
     X, Y = synthetic_bags(len(full), 3, (4, 5), 2, seed=1234, device="cpu")
     ref = X.double().sum(dim=(1, 2, 3)) + Y.double().sum(dim=(1, 2, 3))
