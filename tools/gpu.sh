@@ -12,7 +12,7 @@
 #   ab:VARS[:REGEX]   A/B of library variants (variants/<v>/libblindno.so, comma separated)
 #                     against the in-tree library: 3 alternations of the config-C bench
 #   abenv:VAR=a,b     the config-C bench under VAR=a, VAR=b, ... (3 alternations), e.g.
-#                     abenv:BLINDNO_COLSPEC=1,0
+#                     abenv:BLINDNO_BENCH_BACKEND=nccl,gloo (any environment variable bench.py reads)
 #   pmc:KERNEL        PMC counters over the benched step for KERNEL (tools/pmc_bench.sh)
 #   pmck:REGEX        PMC HBM traffic of kbench kernels (tools/pmc_kbench.sh -> pmc_traffic)
 # Index of the round-by-round evidence these produce: DESIGN.md section 8.
