@@ -503,6 +503,26 @@ __global__ __launch_bounds__(256) void coldft_mix_kernel(const float2* __restric
 // NW waves per workgroup: 8 for the small head launches (one (sample, mode) pair of 12 channels
 // per workgroup and only Bn m2 of them: with 4 waves the chip runs one wave per SIMD)
 // H16: the fp16-operand mix of coldft_mix (config E), block-scaled over this workgroup's rows
+#ifndef COLFUSE_PROBE
+#define COLFUSE_PROBE 0
+#endif
+#ifndef COLFUSE_PREFETCH
+#define COLFUSE_PREFETCH 1
+#endif
+#if COLFUSE_PROBE
+// diagnostic build only (tools/probe_colfuse.py): per-wave realtime stamps at the phase edges
+__device__ unsigned long long g_colfuse_probe[4096 * 8];
+#define CF_MARK(i)                                                                          \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
+    const int slot_ = blockIdx.x * NW + (threadIdx.x >> 6);                                 \
+    if ((threadIdx.x & 63) == 0 && slot_ < 4096) g_colfuse_probe[slot_ * 8 + (i)] = t_;     \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+  } while (0)
+#else
+#define CF_MARK(i) do {} while (0)
+#endif
 template <int DIR, int HBC, int NW = 4, bool H16 = false>
 __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restrict__ At,
                                                       const float2* __restrict__ Wt,
@@ -516,6 +536,7 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
   constexpr int kLd = 65;                          // LDS row stride (float2) for K1p <= 64
   constexpr int kLdP = 16 * NW + 1;                 // DFT partials: KS K1p <= 16 NW
   constexpr int kT = 64 * NW;
+  CF_MARK(7);
   // DFT partials, chunk kc in columns [kc K1p, (kc + 1) K1p), then Y
   __shared__ float2 sP[16][kLdP];
   __shared__ float2 sX[16][kLd];
@@ -531,6 +552,52 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
   const int wave = uniform_int(threadIdx.x >> 6);
   const int r16 = lane & 15, kq = lane >> 4;
   const float inv = 1.0f / ((float)P1 * (float)P2);
+  CF_MARK(0);
+
+  // PF (the 8-wave head launches): the mix weights and the column inverse's twiddles are
+  // loaded here, in flight together with the column DFT's operands.  Each phase otherwise
+  // opened with its own round trip to L2 / MALL at the start of the kernel (per-wave phase
+  // stamps, tools/probe_colfuse.py: mix 1.8 us, inverse 4-5.7 us of a 13 us wave)
+  constexpr bool PF = COLFUSE_PREFETCH && NW == 8 && HBC <= 5 && !H16;   // 239 VGPRs at HBC 5
+  const bool c12 = COLFUSE_C12 && !H16 && Cin == 12 && Cout == 12 && 16 * K1p <= 2 * kT && np == 1;
+  constexpr int kC = 12;
+  float2 wv[2][kC];
+  int jv[2], ov[2];
+  bool live[2];
+  auto load_mix_weights = [&]() {
+    const int k = q0 % m2;
+    const float2* wg = wtgs ? reinterpret_cast<const float2*>(
+                                  reinterpret_cast<const float*>(Wt) + (q0 / m2 / Bg) * wtgs)
+                            : Wt;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + i * kT;
+      ov[i] = e % kC;
+      const int t = e / kC;
+      jv[i] = t % K1p;
+      live[i] = e < 16 * K1p && t < K1p && jv[i] < K1;      // p == 0 (one pair)
+      const float2* wj = wg + ((int64_t)k * K1 + (live[i] ? jv[i] : 0)) * kC * kC;
+#pragma unroll
+      for (int c = 0; c < kC; ++c) wv[i][c] = DIR == 0 ? wj[c * kC + ov[i]] : wj[ov[i] * kC + c];
+    }
+  };
+  f32x4 pg0[2][4], pg1[2][4];
+  if constexpr (PF) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ht = wave + t * NW;
+      if (ht < HB) {
+        const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          if (jb < Jt) {
+            pg0[t][jb] = gb[jb * 128];
+            pg1[t][jb] = gb[jb * 128 + 1];
+          }
+      }
+    }
+    if (c12) load_mix_weights();
+  }
 
   // ---- 1. column DFT: unit u = (tile jt, chunk kc), u = wave, wave + 4, ...
   const int HBc = (HB + KS - 1) / KS;
@@ -561,7 +628,9 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
       for (int r = 0; r < 4; ++r) sP[kq * 4 + r][kc * K1p + jt * 16 + r16] = make_float2(dr[r], di[r]);
     }
   }
+  CF_MARK(1);
   __syncthreads();
+  CF_MARK(2);
   // chunk sum in order, the adjoint's c_k / (P1 P2) scale, the saved spectrum
   for (int e = threadIdx.x; e < 16 * K1p; e += kT) {
     const int row = e / K1p, j = e - row * K1p;
@@ -582,6 +651,7 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
     sX[row][j] = v;
   }
   __syncthreads();
+  CF_MARK(3);
 
   // H16: block scale 2^e with max |component| * 2^e in [2^14, 2^15) over the spectra rows
   float hs = 1.0f, hinv = 1.0f;
@@ -612,26 +682,9 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
   // waves): every weight load of the thread's outputs issued before the first multiply (with
   // the generic 4-unrolled loop each output waited on three L2 round trips in turn); same
   // summation order
-  if (COLFUSE_C12 && !H16 && Cin == 12 && Cout == 12 && 16 * K1p <= 2 * kT && np == 1) {
-    constexpr int kC = 12;
-    float2 wv[2][kC];
-    int jv[2], ov[2];
-    bool live[2];
+  if (c12) {
     const int k = q0 % m2;
-    const float2* wg = wtgs ? reinterpret_cast<const float2*>(
-                                  reinterpret_cast<const float*>(Wt) + (q0 / m2 / Bg) * wtgs)
-                            : Wt;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = threadIdx.x + i * kT;
-      ov[i] = e % kC;
-      const int t = e / kC;
-      jv[i] = t % K1p;
-      live[i] = e < 16 * K1p && t < K1p && jv[i] < K1;      // p == 0 (one pair)
-      const float2* wj = wg + ((int64_t)k * K1 + (live[i] ? jv[i] : 0)) * kC * kC;
-#pragma unroll
-      for (int c = 0; c < kC; ++c) wv[i][c] = DIR == 0 ? wj[c * kC + ov[i]] : wj[ov[i] * kC + c];
-    }
+    if constexpr (!PF) load_mix_weights();
     const float sc = DIR == 0 ? c2r_weight(k, P2) * inv : 1.0f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -718,22 +771,15 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
     const int row = e / K1p;
     if (row >= min(16, (16 / Cout) * Cout)) sP[row][e - row * K1p] = make_float2(0.f, 0.f);
   }
+  CF_MARK(4);
   __syncthreads();
+  CF_MARK(5);
 
   // ---- 3. column inverse: D[orow][h] = sum_j Y[orow][j] conj F[h][j], h tiles over the waves
   const int Ht = HB;
   const int R = m2 * Cout;
-  for (int ht = wave; ht < Ht; ht += NW) {
-    const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
+  auto inv_tile = [&](const int ht, const f32x4 (&g0)[4], const f32x4 (&g1)[4]) {
     f32x4 dr = {0.f, 0.f, 0.f, 0.f}, di = {0.f, 0.f, 0.f, 0.f};
-    // every j block's twiddles in flight before the first MFMA (Jt <= 4)
-    f32x4 g0[4], g1[4];
-#pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
-      if (jb < Jt) {
-        g0[jb] = gb[jb * 128];
-        g1[jb] = gb[jb * 128 + 1];
-      }
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) {
       if (jb >= Jt) break;
@@ -747,7 +793,7 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
       cmfma4(re, im, g0[jb], g1[jb], dr, di);
     }
     const int h = ht * 16 + r16;
-    if (h >= P1) continue;
+    if (h >= P1) return;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int orow = kq * 4 + r;
@@ -766,8 +812,37 @@ __global__ __launch_bounds__(64 * NW) void colfuse_kernel(const float2* __restri
         zt[32 * (k & 1) + 16 + c16] = v.y;
       }
     }
+  };
+  // every j block's twiddles in flight before the first MFMA (Jt <= 4)
+  auto load_inv_twiddles = [&](const int ht, f32x4 (&g0)[4], f32x4 (&g1)[4]) {
+    const f32x4* gb = GB + ((int64_t)ht * Jt * 64 + lane) * 2;
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+      if (jb < Jt) {
+        g0[jb] = gb[jb * 128];
+        g1[jb] = gb[jb * 128 + 1];
+      }
+  };
+  int ht0 = wave;
+  if constexpr (PF) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      if (wave + t * NW < Ht) inv_tile(wave + t * NW, pg0[t], pg1[t]);
+    ht0 = wave + 2 * NW;
   }
+  for (int ht = ht0; ht < Ht; ht += NW) {
+    f32x4 g0[4], g1[4];
+    load_inv_twiddles(ht, g0, g1);
+    inv_tile(ht, g0, g1);
+  }
+  CF_MARK(6);
 }
+#if COLFUSE_PROBE
+BLINDNO_API int blindno_colfuse_probe_read(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_colfuse_probe),
+                                  sizeof(unsigned long long) * (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // Z[n][h][k][o] = sum_j Y[n m2 + k][o][j] conj(F[h][j]).  Workgroup = (sample, 16-row h
 // tile, 64 spectrum rows (k, o)); one 16-row MFMA tile per wave; the result is transposed
