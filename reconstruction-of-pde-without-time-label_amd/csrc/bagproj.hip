@@ -46,6 +46,13 @@ constexpr int kMaxU = 1024;
 #ifndef BAGPROJ_FWD_WAVES
 #define BAGPROJ_FWD_WAVES 3
 #endif
+// 1: the workgroup set-up off the critical path -- the first tile's first z chunk is loaded
+// before the weights, and sum_l lw_l is accumulated in the snapshot loop (same order) instead
+// of a U-step LDS chain of its own (per-wave phase stamps, tools/probe_bagproj.py: the set-up
+// took ~13 us of a one-tile workgroup's ~70 us)
+#ifndef BAGPROJ_SETUP2
+#define BAGPROJ_SETUP2 1
+#endif
 
 // point f of the flattened (bag, crop point) space -> offset of (bag b, snapshot 0, channel 0,
 // row h, column w) in z (B U, C, P1, P2); 32-bit (the launchers bound the field below 2^31)
@@ -87,6 +94,23 @@ __device__ __forceinline__ float swap_sum16(float a, float b) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+#ifndef BAGPROJ_PROBE
+#define BAGPROJ_PROBE 0
+#endif
+#if BAGPROJ_PROBE
+// diagnostic build only (tools/probe_bagproj.py): per-wave realtime stamps at the phase edges
+__device__ unsigned long long g_bagproj_probe[32768 * 8];
+#define BP_MARK(i)                                                                          \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
+    const int slot_ = blockIdx.x * 4 + (threadIdx.x >> 6);                                  \
+    if ((threadIdx.x & 63) == 0 && slot_ < 32768) g_bagproj_probe[slot_ * 8 + (i)] = t_;    \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+  } while (0)
+#else
+#define BP_MARK(i) do {} while (0)
+#endif
 __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
     const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ lw,
@@ -104,8 +128,85 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
   const int wave = uniform_int(tid >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
   const int C = (int)g.C, U = (int)g.U;
-  for (int l = tid; l < U; l += 256) slw[l] = lw ? lw[l] : 1.0f / (float)U;
+  BP_MARK(0);
+  // staging / v-output role of this thread: point tid & 15 (= the compute lane's c16),
+  // channel (tid >> 4) & 3, snapshots (tid >> 6) + 4 i of each chunk
+  const int cs = (tid >> 4) & 3, ls = tid >> 6;
+  const unsigned ntiles = (g.npts + 15) / 16;
+  auto zload = [&](unsigned bo, bool ok, int ch, float (&zr)[kSC2 / 4]) {
+#pragma unroll
+    for (int i = 0; i < kSC2 / 4; ++i) {
+      const int lg = ch * kSC2 + ls + 4 * i;
+#if BAGPROJ_SETUP2
+      // unconditional loads from clamped offsets (bo is a valid point), then a select: a
+      // guarded load is a branch the compiler will not hoist the load out of
+      const int lc = lg < U ? lg : U - 1, cc = cs < C ? cs : C - 1;
+      const float zv = z[bo + (unsigned)(lc * C + cc) * g.HW];
+      zr[i] = (ok && lg < U && cs < C) ? zv : 0.f;
+#else
+      zr[i] = (ok && lg < U && cs < C) ? z[bo + (unsigned)(lg * C + cs) * g.HW] : 0.f;
+#endif
+    }
+  };
   float wa[2], bb[2][4], vloc[4] = {0.f, 0.f, 0.f, 0.f};
+#if BAGPROJ_SETUP2
+  // the weights staged through LDS by coalesced loads (one round trip) before the per-lane
+  // set-up reads them: as global loads inside per-channel branches, each (w2[k], w1[k][c])
+  // pair was its own L2 round trip.  Their loads go out before the first z chunk's, so that
+  // the LDS stores wait for them alone (vector-memory counts retire in order)
+  __shared__ float sw1[kHd * 4], sb1[kHd], sw2[kHd];
+  constexpr int kLwIt = kMaxU / 256;
+  float lwv[kLwIt], w1v[2], b1v = 0.f, w2v = 0.f;
+#pragma unroll
+  for (int i = 0; i < kLwIt; ++i) {
+    const int l = tid + 256 * i;
+    lwv[i] = l < U ? (lw ? lw[l] : 1.0f / (float)U) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) w1v[i] = tid + 256 * i < kHd * C ? w1[tid + 256 * i] : 0.f;
+  if (tid < kHd) {
+    b1v = b1[tid];
+    w2v = w2[tid];
+  }
+  float zfirst[kSC2 / 4];
+  {
+    const unsigned f = blockIdx.x * 16 + (unsigned)c16;
+    const bool ok = f < g.npts;
+    zload(g.base(ok ? f : 0u), ok, 0, zfirst);
+  }
+#pragma unroll
+  for (int i = 0; i < kLwIt; ++i)
+    if (tid + 256 * i < U) slw[tid + 256 * i] = lwv[i];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (tid + 256 * i < kHd * C) sw1[tid + 256 * i] = w1v[i];
+  if (tid < kHd) {
+    sb1[tid] = b1v;
+    sw2[tid] = w2v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int k0 = 16 * (2 * wave + tt);
+    wa[tt] = g4 < C ? kK * sw1[(k0 + c16) * C + g4] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 4 * g4 + r;
+      bb[tt][r] = kK * sb1[k];
+      if (c16 == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float wrv = c < C ? sw2[k] * sw1[k * C + c] : 0.f;
+          vloc[c] += wrv;
+          float2& e = swr[wave][g4][tt][r >> 1][c];
+          if (r & 1) e.y = wrv; else e.x = wrv;
+        }
+      }
+    }
+  }
+#else
+  float zfirst[kSC2 / 4];
+  for (int l = tid; l < U; l += 256) slw[l] = lw ? lw[l] : 1.0f / (float)U;
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int k0 = 16 * (2 * wave + tt);
@@ -125,6 +226,7 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
       }
     }
   }
+#endif
   if (c16 == 0) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) vpart[4 * wave + g4][c] = 0.5f * vloc[c];
@@ -135,15 +237,14 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
     for (int j = 0; j < 16; ++j) acc += vpart[j][tid];
     vhalf[tid] = acc;                          // read after the first chunk's barrier
   }
+#if !BAGPROJ_SETUP2
   float lsum = 0.f;                            // sum_l lw_l, same order in every thread
   for (int l = 0; l < U; ++l) lsum += slw[l];
   const float b2l = b2[0] * lsum;
+#endif
+  BP_MARK(1);
 
-  // staging / v-output role of this thread: point tid & 15 (= the compute lane's c16),
-  // channel (tid >> 4) & 3, snapshots (tid >> 6) + 4 i of each chunk
-  const int cs = (tid >> 4) & 3, ls = tid >> 6;
   const int nch = (U + kSC2 - 1) / kSC2;
-  const unsigned ntiles = (g.npts + 15) / 16;
   for (unsigned tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const unsigned f = tile * 16 + (unsigned)c16;
     const bool ok = f < g.npts;
@@ -152,13 +253,7 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
     // staging is split so that the next chunk's global loads are in flight during this
     // chunk's compute: load() into registers, store() into the LDS buffer after the compute
     float zn[kSC2 / 4];
-    auto load = [&](int ch) {
-#pragma unroll
-      for (int i = 0; i < kSC2 / 4; ++i) {
-        const int lg = ch * kSC2 + ls + 4 * i;
-        zn[i] = (ok && lg < U && cs < C) ? z[bo + (unsigned)(lg * C + cs) * g.HW] : 0.f;
-      }
-    };
+    auto load = [&](int ch) { zload(bo, ok, ch, zn); };
     auto store = [&](int ch, int buf) {
 #pragma unroll
       for (int i = 0; i < kSC2 / 4; ++i) {
@@ -188,10 +283,19 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
 #pragma unroll
         for (int c = 0; c < 4; ++c) Q[tt][c][i] = (f32x2){0.f, 0.f};
       }
-    load(0);
+    if (BAGPROJ_SETUP2 && tile == blockIdx.x) {
+#pragma unroll
+      for (int i = 0; i < kSC2 / 4; ++i) zn[i] = zfirst[i];
+    } else {
+      load(0);
+    }
     store(0, 0);
     if (nch > 1) load(1);
+#if BAGPROJ_SETUP2
+    float lsum = 0.f;                          // sum_l lw_l in l order, as the stand-alone loop
+#endif
     __syncthreads();
+    BP_MARK(2);
     for (int ch = 0; ch < nch; ++ch) {
       const int buf = ch & 1, l0 = ch * kSC2;
       const int nl = U - l0 < kSC2 ? U - l0 : kSC2;
@@ -200,7 +304,11 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
         asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
         const float4 zc = *reinterpret_cast<const float4*>(&zw[buf][l][c16][0]);
         const float az = zs[buf][l][c16][g4];
-        const f32x2 wl = splat2(slw[l0 + l]);
+        const float lwl = slw[l0 + l];
+        const f32x2 wl = splat2(lwl);
+#if BAGPROJ_SETUP2
+        lsum += lwl;
+#endif
         f32x2 vp[4];
 #if BAGPROJ_QUAD
         // both tiles' pre-activations first, then the four pairs' GELU / GELU' in lockstep
@@ -266,7 +374,11 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
       __syncthreads();
     }
     vwrite(nch - 1, (nch - 1) & 1);
+#if BAGPROJ_SETUP2
+    const float b2l = b2[0] * lsum;
+#endif
     zbr[ls][lane] = zbp;
+    BP_MARK(3);
     __syncthreads();
     // statistics of this tile: slot ((t 6 + comp) 64 + lane) holds hidden 16 t + 4 g4 + r
     // (r = the float4 component) of point c16
@@ -283,15 +395,25 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int k = 16 * t + 4 * g4 + r;
+#if BAGPROJ_SETUP2
+        float hb = sb1[k] * lsum;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hb = c < C ? fmaf(sw1[k * C + c], zb[c], hb) : hb;
+#else
         float hb = b1[k] * lsum;
 #pragma unroll
         for (int c = 0; c < 4; ++c) hb = c < C ? fmaf(w1[k * C + c], zb[c], hb) : hb;
+#endif
         const float acc = r == 0 ? A[tt][0].x : (r == 1 ? A[tt][0].y : (r == 2 ? A[tt][1].x : A[tt][1].y));
         av[r] = fmaf(kInvK, acc, 0.5f * hb);
       }
       const float4 a4 = {av[0], av[1], av[2], av[3]};
       const int kb = 16 * t + 4 * g4;
+#if BAGPROJ_SETUP2
+      up += (sw2[kb] * a4.x + sw2[kb + 1] * a4.y) + (sw2[kb + 2] * a4.z + sw2[kb + 3] * a4.w);
+#else
       up += (w2[kb] * a4.x + w2[kb + 1] * a4.y) + (w2[kb + 2] * a4.z + w2[kb + 3] * a4.w);
+#endif
       st[(t * kNStat + 0) * 64] = a4;
       const float hs = 0.5f * lsum;
       st[(t * kNStat + 1) * 64] = (float4){S[tt][0].x + hs, S[tt][0].y + hs, S[tt][1].x + hs, S[tt][1].y + hs};
@@ -308,7 +430,23 @@ __global__ __launch_bounds__(256, BAGPROJ_FWD_WAVES) void bagproj_fwd_kernel(
     __syncthreads();
     if (tid < 16 && ok) ubar[f] = (((ured[0][tid] + ured[1][tid]) + ured[2][tid]) + ured[3][tid]) + b2l;
   }
+  BP_MARK(4);
+#if BAGPROJ_PROBE
+  if ((threadIdx.x & 63) == 0) {
+    const int slot_ = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (slot_ < 32768) {
+      g_bagproj_probe[slot_ * 8 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+      g_bagproj_probe[slot_ * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+    }
+  }
+#endif
 }
+#if BAGPROJ_PROBE
+BLINDNO_API int blindno_bagproj_probe_read(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_bagproj_probe),
+                                  sizeof(unsigned long long) * (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // Backward: ghat-weighted reduction of the statistics (thread tid owns float4 slots tid + 256 j
 // of every tile, all of point tid & 15) into one partial per workgroup
