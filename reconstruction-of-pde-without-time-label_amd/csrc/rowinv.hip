@@ -527,6 +527,9 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 #ifndef ROWFUSE_ZPRE
 #define ROWFUSE_ZPRE 0
 #endif
+#ifndef ROWFUSE_STAGE4
+#define ROWFUSE_STAGE4 1
+#endif
 // operand prefetch (ping-pong buffers) in the adjoint
 #ifndef ROWFUSE_PF1
 #define ROWFUSE_PF1 1
@@ -594,12 +597,28 @@ void rowfuse_kernel(
   float* sA = lds;                                  // [NT][64 lanes][S]
   float* sT = lds + NT * 64 * S;                    // RD: [NT][4][Npad][4] (rowdft's image)
 
-  for (int e = threadIdx.x; e < NT * 64 * S; e += blockDim.x) {
+  auto tb_at = [&](int e) {
     const int t = e / (64 * S), rem = e - t * (64 * S);
     const int ln = rem / S, sp = rem - ln * S;
     const int kk = S * (ln >> 4) + sp;
     const int w = 16 * NH * (t / NH) + 4 * NH * ((ln & 15) >> 2) + 4 * (t % NH) + (ln & 3);
-    sA[e] = TB[((kk >> 2) * NT + (w >> 4)) * 64 + (kk & 3) * 16 + (w & 15)];
+    return TB[((kk >> 2) * NT + (w >> 4)) * 64 + (kk & 3) * 16 + (w & 15)];
+  };
+  {
+    // the twiddle image gathered four loads at a time (a loop of single load -> LDS store
+    // steps waits one L2 round trip per step: 15 of them per workgroup at P2 = 160)
+    const int n = NT * 64 * S, st = blockDim.x;
+    int e = threadIdx.x;
+#if ROWFUSE_STAGE4
+    for (; e + 3 * st < n; e += 4 * st) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = tb_at(e + j * st);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sA[e + j * st] = v[j];
+    }
+#endif
+    for (; e < n; e += st) sA[e] = tb_at(e);
   }
   if (RD) stage_to_lds(sT, rd.Tp, NT * 16 * Npad);
   __syncthreads();
