@@ -532,7 +532,8 @@ __global__ __launch_bounds__(256) void bagproj_bwd_kernel(
     if (tid == 0) sgs = s;
   }
   __syncthreads();
-  float lsum = 0.f;
+  float lsum = 0.f;                          // in l order; the LDS reads eight at a time
+#pragma unroll 8
   for (int l = 0; l < U; ++l) lsum += slw[l];
   const int np_ = kHd * C + 2 * kHd + 1;
   float* pp = partial + (size_t)blockIdx.x * np_;

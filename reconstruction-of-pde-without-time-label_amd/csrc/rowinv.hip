@@ -328,9 +328,15 @@ constexpr int kWideMaxG = 4;
 #ifndef ROWINV_WIDE_WAVES
 #define ROWINV_WIDE_WAVES 2
 #endif
+// EX (the heads' m2 = 32): budgeted for 4 waves per SIMD (128 VGPRs, a few spilled).  At 3
+// waves (136-146 VGPRs) the grouped heads' 3200 one-tile items took 800 workgroups for 768
+// resident slots, and the last 32 ran as a second round (bench +1.9 %, r06y)
+#ifndef ROWINV_WIDE_WAVES_EX
+#define ROWINV_WIDE_WAVES_EX 4
+#endif
 // EX: m2 == 2 KSM (the heads: m2 = 32), every mode bound a compile-time constant
 template <int CM, int KSM, int MODE, int ACT, bool EX>
-__global__ __launch_bounds__(256, ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
+__global__ __launch_bounds__(256, EX ? ROWINV_WIDE_WAVES_EX : ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
     const float* __restrict__ Z, const float* __restrict__ xs, const float* __restrict__ dz,
     const float* __restrict__ wc, const float* __restrict__ bc, float* __restrict__ out,
     const float* __restrict__ TB, int Bn, int P1, int P2, int m2_, int TPW, int Bg,

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Per-kernel register / occupancy summary of one HIP source (compiler remarks).
-# usage: bash tools/res_usage.sh csrc/FILE.hip [kernel-name-regex]
+# usage: [RES_FLAGS="-DMACRO=1"] bash tools/res_usage.sh csrc/FILE.hip [kernel-name-regex]
 cd "$(dirname "$0")/../reconstruction-of-pde-without-time-label_amd" || exit 1
 /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I ../include -I csrc -fvisibility=hidden \
-  -Wno-unused-function -c "$1" -o /tmp/res_usage.o -Rpass-analysis=kernel-resource-usage 2>&1 |
+  -Wno-unused-function $RES_FLAGS -c "$1" -o /tmp/res_usage.o -Rpass-analysis=kernel-resource-usage 2>&1 |
 python3 -c '
 import re, sys, subprocess
 pat = sys.argv[1] if len(sys.argv) > 1 else ""
