@@ -533,8 +533,8 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 #ifndef ROWFUSE_ZPRE
 #define ROWFUSE_ZPRE 0
 #endif
-#ifndef ROWFUSE_STAGE4
-#define ROWFUSE_STAGE4 1
+#ifndef ROWFUSE_STAGE_N
+#define ROWFUSE_STAGE_N 16
 #endif
 // operand prefetch (ping-pong buffers) in the adjoint
 #ifndef ROWFUSE_PF1
@@ -557,6 +557,23 @@ __device__ __forceinline__ void gelu_both4(f32x4 x, f32x4& a, f32x4& dg) {
 #define ROWFUSE_NH0_NORD 2
 #endif
 
+#ifndef ROWFUSE_PROBE
+#define ROWFUSE_PROBE 0
+#endif
+#if ROWFUSE_PROBE
+// diagnostic build only (tools/kbench.py with KBENCH_PROBE=1): per-wave realtime stamps
+__device__ unsigned long long g_rowfuse_probe[8192 * 8];
+#define RF_MARK(i)                                                                          \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
+    const int slot_ = blockIdx.x * 4 + (threadIdx.x >> 6);                                  \
+    if ((threadIdx.x & 63) == 0 && slot_ < 8192) g_rowfuse_probe[slot_ * 8 + (i)] = t_;     \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+  } while (0)
+#else
+#define RF_MARK(i) do {} while (0)
+#endif
 // HW: the layer has its 1x1 conv (wc != NULL) -- a compile-time flag: a runtime test around each
 // operand load made hipcc branch around the loads and count their waits conservatively.
 // NSC: steps per row block as a compile-time constant (P2 / (16 NH)), 0 = a runtime loop.
@@ -598,6 +615,12 @@ void rowfuse_kernel(
     }
   }
   const int gxm = (kHost && sc.nmixb > 0) ? sc.nmain : (int)gridDim.x;   // the row kernel's grid
+  RF_MARK(0);
+#if ROWFUSE_PROBE
+  if ((threadIdx.x & 63) == 0 && blockIdx.x * 4 + (threadIdx.x >> 6) < 8192)
+    for (int i = 2; i < 7; ++i) g_rowfuse_probe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + i] = 0;
+  int it_probe = 0;
+#endif
   const int NT = P2 >> 4;                           // MFMA column tiles (NT % NH == 0)
   extern __shared__ float lds[];
   float* sA = lds;                                  // [NT][64 lanes][S]
@@ -611,11 +634,42 @@ void rowfuse_kernel(
     return TB[((kk >> 2) * NT + (w >> 4)) * 64 + (kk & 3) * 16 + (w & 15)];
   };
   {
-    // the twiddle image gathered four loads at a time (a loop of single load -> LDS store
-    // steps waits one L2 round trip per step: 15 of them per workgroup at P2 = 160)
+    // the twiddle image, read in TB order (coalesced) and scattered into LDS: sA[tb_slot(q)] =
+    // TB[q] (the inverse of tb_at, a bijection of the NT 64 S slots).  Gathered in sA order, every
+    // wave load touched up to 64 cache lines and the staging took ~4.5 us per workgroup
+    // (per-wave stamps, kbench KBENCH_PROBE); the first ROWFUSE_STAGE_N values per thread are
+    // loaded together, the next row DFT's image staged while they are in flight
+    static_assert(NH == 1 || NH == 2, "column tiles per step");
     const int n = NT * 64 * S, st = blockDim.x;
+    auto tb_slot = [&](int q) {
+      const int s4 = q / (NT * 64), r = q - s4 * (NT * 64);
+      const int l64 = r & 63, w = 16 * (r >> 6) + (l64 & 15);
+      const int kk = 4 * s4 + (l64 >> 4), lg = kk / S, sp = kk - lg * S;
+      int t, lo;
+      if (NH == 1) {
+        t = w >> 4;
+        lo = w & 15;
+      } else {
+        t = 2 * (w >> 5) + ((w >> 2) & 1);
+        lo = 4 * ((w & 31) >> 3) + (w & 3);
+      }
+      return (t * 64 + 16 * lg + lo) * S + sp;
+    };
     int e = threadIdx.x;
-#if ROWFUSE_STAGE4
+#if ROWFUSE_STAGE_N > 0
+    float v0[ROWFUSE_STAGE_N];
+#pragma unroll
+    for (int j = 0; j < ROWFUSE_STAGE_N; ++j) {
+      const int ej = e + j * st;
+      v0[j] = TB[ej < n ? ej : n - 1];
+    }
+    if (RD) stage_to_lds(sT, rd.Tp, NT * 16 * Npad);
+#pragma unroll
+    for (int j = 0; j < ROWFUSE_STAGE_N; ++j)
+      if (e + j * st < n) sA[tb_slot(e + j * st)] = v0[j];
+    e += ROWFUSE_STAGE_N * st;
+    for (; e < n; e += st) sA[tb_slot(e)] = TB[e];
+#else
     for (; e + 3 * st < n; e += 4 * st) {
       float v[4];
 #pragma unroll
@@ -623,11 +677,12 @@ void rowfuse_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) sA[e + j * st] = v[j];
     }
-#endif
     for (; e < n; e += st) sA[e] = tb_at(e);
+    if (RD) stage_to_lds(sT, rd.Tp, NT * 16 * Npad);
+#endif
   }
-  if (RD) stage_to_lds(sT, rd.Tp, NT * 16 * Npad);
   __syncthreads();
+  RF_MARK(1);
   const int lane = threadIdx.x & 63;
   const int wave = uniform_int(threadIdx.x >> 6);
   const int c16 = lane & 15, g = lane >> 4;
@@ -945,6 +1000,10 @@ void rowfuse_kernel(
                   make_float2(racc[c][nt][2 * rp], racc[c][nt][2 * rp + 1]);
           }
     }
+#if ROWFUSE_PROBE
+    if (it_probe < 5) RF_MARK(2 + it_probe);
+    ++it_probe;
+#endif
   }
   if (WG || NWL) {
     // block reduction of the per-lane partials -> partial[blockIdx.x][np] (np = C*C + C, + 4 C
@@ -965,7 +1024,19 @@ void rowfuse_kernel(
       partial[(int64_t)blockIdx.x * np + p] = s;
     }
   }
+  RF_MARK(7);
 }
+#if ROWFUSE_PROBE
+BLINDNO_API int blindno_rowfuse_probe_reset() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_rowfuse_probe)) != hipSuccess) return 1;
+  return (int)hipMemset(p, 0, sizeof(g_rowfuse_probe));
+}
+BLINDNO_API int blindno_rowfuse_probe_read(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rowfuse_probe),
+                                  sizeof(unsigned long long) * (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // namespace
 

@@ -3,6 +3,8 @@
 
     python tools/kbench.py [filter-regex]
     KBENCH_N=256 KBENCH_MIX=fp16 python tools/kbench.py [filter-regex]     (config E's shapes)
+    KBENCH_PROBE=1 BLINDNO_LIB=variants/rfprobe/libblindno.so python tools/kbench.py REGEX
+        (a ROWFUSE_PROBE=1 build: per-wave staging / item times of the row kernels)
 
 Times the C-ABI entry points of the FNO_input body (Bn = 4 * 75 snapshots, width 4,
 P = 160, m = 12) and of one head layer (Bn = 4, width 12, m = 32) in isolation, so kernel
@@ -53,6 +55,42 @@ def main():
         us = timeit(fn)
         res.append((name, us, nbytes / (us * 1e-6) / 1e9))
         print(f"{name:40s} {us:9.1f} us  {nbytes / (us * 1e-6) / 1e9:8.0f} GB/s", flush=True)
+        if probe is not None:
+            probe_report(fn)
+
+    # KBENCH_PROBE=1 with a ROWFUSE_PROBE=1 build: per-wave phase stamps of the row kernels
+    probe = None
+    if os.environ.get("KBENCH_PROBE"):
+        import ctypes
+        import numpy as np
+        from blindno import _lib
+        lib = _lib.load()
+        probe = (lib.blindno_rowfuse_probe_reset, lib.blindno_rowfuse_probe_read)
+        probe[1].argtypes = [ctypes.c_void_p, ctypes.c_int]
+
+    def probe_report(fn):
+        torch.cuda.synchronize()
+        probe[0]()
+        fn()
+        torch.cuda.synchronize()
+        buf = np.zeros(8192 * 8, dtype=np.uint64)
+        probe[1](buf.ctypes.data, buf.size)
+        t = buf.reshape(8192, 8).astype(np.int64)
+        t = t[t[:, 0] > 0]
+        if not len(t):
+            print("    (no row-kernel stamps)")
+            return
+        t0 = t[:, 0].min()
+        us_ = lambda a: (a - t0) * 0.01
+        stage = us_(t[:, 1]) - us_(t[:, 0])
+        nit = (t[:, 2:7] > 0).sum(axis=1)
+        first = us_(t[:, 2]) - us_(t[:, 1])
+        later = [us_(t[i, 2 + k]) - us_(t[i, 1 + k]) for i in range(len(t)) for k in range(1, 5) if t[i, 2 + k] > 0]
+        end = us_(t[:, 7])
+        print(f"    waves {len(t)}  items/wave {np.bincount(nit).tolist()}  start spread {us_(t[:, 0]).max():5.2f}"
+              f"  staging {np.median(stage):5.2f}/{stage.max():5.2f}  first item {np.median(first):6.2f}/{first.max():6.2f}"
+              f"  later items {np.median(later) if later else 0:6.2f}  wave end med {np.median(end):6.2f} max {end.max():6.2f} us",
+              flush=True)
 
     # "u52": the encoder at the step's mean bag size (4 bags x ~52 distinct snapshots)
     # "u50": 200 snapshots, 2000 16-row items (< the 2048 resident waves of the row kernels)
