@@ -76,6 +76,7 @@ def main():
         buf = np.zeros(8192 * 8, dtype=np.uint64)
         probe[1](buf.ctypes.data, buf.size)
         t = buf.reshape(8192, 8).astype(np.int64)
+        slot = np.nonzero(t[:, 0] > 0)[0]
         t = t[t[:, 0] > 0]
         if not len(t):
             print("    (no row-kernel stamps)")
@@ -91,6 +92,10 @@ def main():
               f"  staging {np.median(stage):5.2f}/{stage.max():5.2f}  first item {np.median(first):6.2f}/{first.max():6.2f}"
               f"  later items {np.median(later) if later else 0:6.2f}  wave end med {np.median(end):6.2f} max {end.max():6.2f} us",
               flush=True)
+        # a wave's first item is its slot (blockIdx 4 + wave): its 16-row block is slot % 10 at P1 = 160
+        blk = slot % 10
+        print("    first item by 16-row block (median us):",
+              " ".join(f"{b}:{np.median(first[blk == b]):5.1f}" for b in range(10) if (blk == b).any()), flush=True)
 
     # "u52": the encoder at the step's mean bag size (4 bags x ~52 distinct snapshots)
     # "u50": 200 snapshots, 2000 16-row items (< the 2048 resident waves of the row kernels)
