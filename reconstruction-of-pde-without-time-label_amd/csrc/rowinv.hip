@@ -334,6 +334,23 @@ constexpr int kWideMaxG = 4;
 #ifndef ROWINV_WIDE_WAVES_EX
 #define ROWINV_WIDE_WAVES_EX 4
 #endif
+#ifndef ROWINV_WIDE_PROBE
+#define ROWINV_WIDE_PROBE 0
+#endif
+#if ROWINV_WIDE_PROBE
+// diagnostic build only (tools/kbench.py with KBENCH_PROBE=2): per-wave realtime stamps
+__device__ unsigned long long g_rowinv_wide_probe[8192 * 8];
+#define RW_MARK(i)                                                                          \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
+    const int slot_ = blockIdx.x * 4 + (threadIdx.x >> 6);                                  \
+    if ((threadIdx.x & 63) == 0 && slot_ < 8192) g_rowinv_wide_probe[slot_ * 8 + (i)] = t_; \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+  } while (0)
+#else
+#define RW_MARK(i) do {} while (0)
+#endif
 // EX: m2 == 2 KSM (the heads: m2 = 32), every mode bound a compile-time constant
 template <int CM, int KSM, int MODE, int ACT, bool EX>
 __global__ __launch_bounds__(256, EX ? ROWINV_WIDE_WAVES_EX : ROWINV_WIDE_WAVES) void rowinv_wide_kernel(
@@ -360,6 +377,7 @@ __global__ __launch_bounds__(256, EX ? ROWINV_WIDE_WAVES_EX : ROWINV_WIDE_WAVES)
   constexpr int per = CM * CM + CM;
   __shared__ float swc[kWideMaxG][per];
   const int ngw = wgs ? Bn / Bg : 1;
+  RW_MARK(0);
   if (has_wc) {
     for (int e = threadIdx.x; e < ngw * per; e += blockDim.x) {
       const int g = e / per, q = e - g * per;
@@ -375,6 +393,7 @@ __global__ __launch_bounds__(256, EX ? ROWINV_WIDE_WAVES_EX : ROWINV_WIDE_WAVES)
     __syncthreads();
   }
   const int vb = xcd_block(blockIdx.x, gridDim.x);
+  RW_MARK(1);
   for (int item = vb * kW + wave; item < nitems; item += gridDim.x * kW) {
     const int chunk = item % NC, quad = item / NC;
     // A operands of every group: one coalesced load per (group, K step), tile order
@@ -421,6 +440,14 @@ __global__ __launch_bounds__(256, EX ? ROWINV_WIDE_WAVES_EX : ROWINV_WIDE_WAVES)
 #pragma unroll
         for (int i = 0; i < CM; ++i) sv[i] = gelu_grad_f(sv[i]);
       }
+#if ROWINV_WIDE_PROBE
+      if (tile == t0) {
+        // the operands are in registers once every load has returned
+        float s_ = fv[0] + sv[0] + bv[0] + av[0][0] + av[NGM - 1][KSM - 1];
+        asm volatile("" :: "v"(s_));
+        RW_MARK(2);
+      }
+#endif
 #pragma unroll
       for (int g = 0; g < NGM; ++g) {
         f32x4 d = {0.f, 0.f, 0.f, 0.f};
@@ -449,8 +476,23 @@ __global__ __launch_bounds__(256, EX ? ROWINV_WIDE_WAVES_EX : ROWINV_WIDE_WAVES)
         }
       }
     }
+#if ROWINV_WIDE_PROBE
+    if (item == vb * kW + wave) RW_MARK(3);
+#endif
   }
+  RW_MARK(4);
 }
+#if ROWINV_WIDE_PROBE
+BLINDNO_API int blindno_rowinv_wide_probe_reset() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_rowinv_wide_probe)) != hipSuccess) return 1;
+  return (int)hipMemset(p, 0, sizeof(g_rowinv_wide_probe));
+}
+BLINDNO_API int blindno_rowinv_wide_probe_read(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rowinv_wide_probe),
+                                  sizeof(unsigned long long) * (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // ------------------------------------------------------------ transposed row inverse (C = 4)
 // The snapshot encoder's layers (FNO_input: C = 4, m2 = 12, P2 = 160 at 128^2), whole rows per

@@ -4,7 +4,8 @@
     python tools/kbench.py [filter-regex]
     KBENCH_N=256 KBENCH_MIX=fp16 python tools/kbench.py [filter-regex]     (config E's shapes)
     KBENCH_PROBE=1 BLINDNO_LIB=variants/rfprobe/libblindno.so python tools/kbench.py REGEX
-        (a ROWFUSE_PROBE=1 build: per-wave staging / item times of the row kernels)
+        (a ROWFUSE_PROBE=1 build: per-wave staging / item times of the row kernels;
+         KBENCH_PROBE=2 with a ROWINV_WIDE_PROBE=1 build: the heads' wide row inverse)
 
 Times the C-ABI entry points of the FNO_input body (Bn = 4 * 75 snapshots, width 4,
 P = 160, m = 12) and of one head layer (Bn = 4, width 12, m = 32) in isolation, so kernel
@@ -65,7 +66,10 @@ def main():
         import numpy as np
         from blindno import _lib
         lib = _lib.load()
-        probe = (lib.blindno_rowfuse_probe_reset, lib.blindno_rowfuse_probe_read)
+        if os.environ["KBENCH_PROBE"] == "2":      # the heads' wide row inverse (ROWINV_WIDE_PROBE=1)
+            probe = (lib.blindno_rowinv_wide_probe_reset, lib.blindno_rowinv_wide_probe_read, 2)
+        else:
+            probe = (lib.blindno_rowfuse_probe_reset, lib.blindno_rowfuse_probe_read, 1)
         probe[1].argtypes = [ctypes.c_void_p, ctypes.c_int]
 
     def probe_report(fn):
@@ -83,6 +87,13 @@ def main():
             return
         t0 = t[:, 0].min()
         us_ = lambda a: (a - t0) * 0.01
+        if probe[2] == 2:
+            ready = us_(t[:, 2]) - us_(t[:, 1])
+            rest = us_(t[:, 3]) - us_(t[:, 2])
+            print(f"    waves {len(t)}  start spread {us_(t[:, 0]).max():5.2f}  weights {np.median(us_(t[:, 1]) - us_(t[:, 0])):5.2f}"
+                  f"  operands ready {np.median(ready):5.2f}/{ready.max():5.2f}  MFMA+epilogue+stores {np.median(rest):5.2f}/{rest.max():5.2f}"
+                  f"  wave end med {np.median(us_(t[:, 4])):6.2f} max {us_(t[:, 4]).max():6.2f} us", flush=True)
+            return
         stage = us_(t[:, 1]) - us_(t[:, 0])
         nit = (t[:, 2:7] > 0).sum(axis=1)
         first = us_(t[:, 2]) - us_(t[:, 1])
